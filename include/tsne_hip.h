@@ -1,0 +1,179 @@
+/*
+ * tsne_hip.h -- C ABI of libtsne_hip, the MI355X-native hot path of
+ * tsne-flink (ChristophAl/tsne-flink): brute-force kNN, perplexity-calibrated
+ * affinities, and the Barnes-Hut gradient / optimizer loop.
+ *
+ * The reference exposes this path as Scala object methods over Flink
+ * DataSets (TsneHelpers.scala).  Each entry point below replaces exactly one
+ * of them; a JNI shim turns the DataSet partition into the
+ * flat arrays used here.  Conventions:
+ *   - point ids are dense 0..n-1 (the host mirror remaps arbitrary int ids);
+ *   - sparse matrices are CSR: row_ptr[n+1] (int64), col[nnz] (int32),
+ *     val[nnz] (double);
+ *   - embeddings are row-major n x n_components doubles;
+ *   - every call returns a tsne_status; on error tsne_last_error() holds a
+ *     thread-local message.  No C++ exception crosses this boundary.
+ *   - tsne_* functions take HOST buffers (caller-owned); tsne_dev_* take
+ *     DEVICE buffers on the context's device and enqueue on its stream.
+ * Numerics are fp64 everywhere except the kNN candidate filter, which runs on
+ * fp32 MFMA with a rigorous error bound and an exact fp64 re-rank.
+ */
+#ifndef TSNE_HIP_H
+#define TSNE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSNE_HIP_ABI_VERSION 1
+#define TSNE_UNIQUE_ID_BYTES 128
+
+typedef enum {
+    TSNE_OK = 0,
+    TSNE_ERR_ARG = -1,          /* IllegalArgumentException in the reference */
+    TSNE_ERR_HIP = -2,          /* HIP runtime / kernel launch failure */
+    TSNE_ERR_NOMEM = -3,
+    TSNE_ERR_UNSUPPORTED = -4,  /* e.g. n_components != 2 (Cell.scala:32 require) */
+    TSNE_ERR_CAPACITY = -5,     /* caller buffer too small; required size reported */
+    TSNE_ERR_COMM = -6,         /* RCCL failure */
+    TSNE_ERR_NO_DEVICE = -7
+} tsne_status;
+
+/* Tsne.getMetric (Tsne.scala:161-168) */
+typedef enum {
+    TSNE_METRIC_SQEUCLIDEAN = 0,
+    TSNE_METRIC_EUCLIDEAN = 1,
+    TSNE_METRIC_COSINE = 2
+} tsne_metric;
+
+/* Optimizer parameters; defaults = Tsne.scala:47-63 + TsneHelpers.scala:386. */
+typedef struct {
+    int32_t n_components;       /* --nComponents, 2 */
+    int32_t metric;             /* --metric, sqeuclidean (used for the attractive q) */
+    double learning_rate;       /* --learningRate, 1000 */
+    int32_t iterations;         /* --iterations, 300 */
+    double early_exaggeration;  /* --earlyExaggeration, 4 */
+    double initial_momentum;    /* --initialMomentum, 0.5 */
+    double final_momentum;      /* --finalMomentum, 0.8 */
+    double theta;               /* --theta, 0.25 */
+    double min_gain;            /* hard-coded 0.01 (TsneHelpers.scala:386) */
+} tsne_params;
+
+typedef struct tsne_ctx tsne_ctx;
+
+/* ---------------------------------------------------------------- basics */
+int tsne_abi_version(void);
+const char *tsne_last_error(void);
+void tsne_params_default(tsne_params *p);
+/* Tsne.getMetric (Tsne.scala:161-168): unknown name -> TSNE_ERR_ARG. */
+int tsne_metric_from_name(const char *name, int32_t *metric_out);
+/* Row shard [r0, r1) of rank `rank` out of `world` (contiguous, balanced). */
+int tsne_shard_rows(int64_t n, int32_t world, int32_t rank, int64_t *r0, int64_t *r1);
+
+/* ---------------------------------------------------------------- context */
+int tsne_ctx_create(int32_t device, tsne_ctx **out);
+int tsne_ctx_destroy(tsne_ctx *ctx);
+/* Enqueue on a caller-owned hipStream_t (e.g. torch's current stream). NULL = own stream. */
+int tsne_ctx_set_stream(tsne_ctx *ctx, void *hip_stream);
+void *tsne_ctx_stream(tsne_ctx *ctx);
+int tsne_ctx_synchronize(tsne_ctx *ctx);
+
+/* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls
+ * tsne_comm_unique_id and ships the bytes to the other ranks out of band
+ * (torch.distributed / MPI / a file); every rank then calls
+ * tsne_ctx_init_comm.  Afterwards tsne_knn shards query rows and
+ * tsne_optimize / tsne_dev_opt_* shard P rows and BH queries; results are
+ * replicated on every rank. */
+int tsne_comm_unique_id(uint8_t id_out[TSNE_UNIQUE_ID_BYTES]);
+int tsne_ctx_init_comm(tsne_ctx *ctx, int32_t rank, int32_t world,
+                       const uint8_t id[TSNE_UNIQUE_ID_BYTES]);
+int tsne_ctx_rank(tsne_ctx *ctx, int32_t *rank, int32_t *world);
+
+/* ------------------------------------------------- host-buffer operators */
+
+/* kNearestNeighbors (TsneHelpers.scala:41-59).  X: n x d row-major.
+ * For query rows [q0, q1): the kk = min(k, n-1) nearest j != i, ascending by
+ * (metric value, j).  idx_out / dist_out: (q1-q0) x kk.  Distances are the
+ * exact fp64 breeze metric values (sequential sums). */
+int tsne_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metric,
+             int32_t k, int64_t q0, int64_t q1, int32_t *idx_out, double *dist_out);
+
+/* pairwiseAffinities (TsneHelpers.scala:162-180 + 434-504): per CSR row the
+ * beta binary search to entropy ln(perplexity); p_out has the layout of dist. */
+int tsne_pairwise_affinities(tsne_ctx *ctx, const int64_t *row_ptr, const double *dist,
+                             int64_t nrows, double perplexity, double *p_out);
+
+/* jointDistribution (TsneHelpers.scala:182-196): P = (C + C^T) / sum over the
+ * union pattern (explicit zeros kept); output rows sorted by column.  If
+ * cap < nnz returns TSNE_ERR_CAPACITY with *nnz_out set (cap = 2*nnz_in
+ * always suffices). */
+int tsne_joint_distribution(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col,
+                            const double *p, int64_t n, int64_t cap, int64_t *out_row_ptr,
+                            int32_t *out_col, double *out_val, int64_t *nnz_out);
+
+/* gradient (TsneHelpers.scala:221-318): Barnes-Hut with the reference
+ * quadtree semantics and opening criterion.  P values are multiplied by
+ * `exaggeration`.  Y, grad_out: n x 2.  sumq_out (Z) and loss_out (KL term
+ * of TsneHelpers.scala:297-299) are optional (NULL). */
+int tsne_gradient(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *P,
+                  int64_t n, const double *Y, int32_t metric, double theta, double exaggeration,
+                  double *grad_out, double *sumq_out, double *loss_out);
+
+/* updateEmbedding (TsneHelpers.scala:341-369), in place on Y, upd, gains. */
+int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *grad, double *Y,
+                          double *upd, double *gains, double min_gain, double momentum,
+                          double learning_rate);
+
+/* centerEmbedding (TsneHelpers.scala:320-329), in place. */
+int tsne_center_embedding(tsne_ctx *ctx, int64_t n, int32_t c, double *Y);
+
+/* initWorkingSet (TsneHelpers.scala:198-219): Y ~ N(0, 1e-4^2) from a
+ * counter-based generator keyed by `seed` (the reference ignores
+ * --randomState; this build honours it), upd = 0, gains = 1. */
+int tsne_init_working_set(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed, double *Y,
+                          double *upd, double *gains);
+
+/* optimize (TsneHelpers.scala:396-430): all iterations on the device; Y,
+ * upd and gains (n x 2) are read and written back.  loss_keys / loss_vals
+ * receive (t, KL) for every t % 10 == 0 (the "loss" accumulator,
+ * TsneHelpers.scala:297-300), at most loss_cap entries. */
+int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_ptr,
+                  const int32_t *col, const double *P, int64_t n, double *Y, double *upd,
+                  double *gains, int32_t *loss_keys, double *loss_vals, int32_t loss_cap,
+                  int32_t *n_loss);
+
+/* ----------------------------------------------------- device-buffer API */
+/* Same operators, pointers on the context's device, enqueued on its stream.
+ * They do not synchronise unless a result size must reach the host. */
+int tsne_dev_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric,
+                 int32_t k, int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist);
+int tsne_dev_pairwise_affinities(tsne_ctx *ctx, const int64_t *d_row_ptr, const double *d_dist,
+                                 int64_t nrows, double perplexity, double *d_p);
+/* Fixed-k conditional rows (row i = entries [i*k, (i+1)*k)), symmetrised into
+ * caller-allocated CSR (capacity 2*n*k); *nnz_out is synchronised to host. */
+int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
+                                const double *d_p, int64_t n, int64_t cap, int64_t *d_out_row_ptr,
+                                int32_t *d_out_col, double *d_out_val, int64_t *nnz_out);
+
+/* Device-resident optimizer.  setup binds device buffers (rows of P for this
+ * rank's shard, full Y/upd/gains) and allocates the workspace; step runs
+ * global iteration t (1-based) with the reference phase schedule; losses for
+ * t % 10 == 0 are kept on the device and read by tsne_dev_opt_losses. */
+int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *d_row_ptr,
+                       const int32_t *d_col, const double *d_P, int64_t n, double *d_Y,
+                       double *d_upd, double *d_gains);
+int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t);
+int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap,
+                        int32_t *n_loss);
+/* Per-kernel timing of the last step (HIP events on the ctx stream), in ms:
+ * [0] tree build, [1] BH repulsion, [2] attraction+update, [3] centre/exchange.
+ * Also the number of BH node visits of the last step (device counter). */
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out4, int64_t *visits_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSNE_HIP_H */

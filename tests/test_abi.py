@@ -1,0 +1,71 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports
+every symbol include/tsne_hip.h declares, and its host-only logic (metric
+names, shard arithmetic, error reporting) behaves like the reference."""
+import re
+from pathlib import Path
+
+import pytest
+
+import tsne_amd as T
+from tsne_amd._lib import SIGNATURES
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def declared_symbols():
+    text = (ROOT / "include" / "tsne_hip.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tsne_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    L = T.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(SIGNATURES), set(syms) ^ set(SIGNATURES)
+
+
+def test_abi_version():
+    assert T.lib().tsne_abi_version() == 1
+
+
+@pytest.mark.parametrize("name,val", [("sqeuclidean", 0), ("euclidean", 1), ("cosine", 2)])
+def test_metric_names(name, val):
+    # Tsne.getMetric (Tsne.scala:161-168)
+    assert T.metric_from_name(name) == val
+
+
+def test_unknown_metric_is_illegal_argument():
+    with pytest.raises(T.TsneError) as e:
+        T.metric_from_name("manhattan")
+    assert e.value.status == -1 and "not defined" in str(e.value)
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (1_000_000, 8), (7, 8), (0, 2), (129, 2)])
+def test_shard_rows_partition(n, world):
+    got = [T.shard_rows(n, world, r) for r in range(world)]
+    assert got[0][0] == 0 and got[-1][1] == n
+    for (a, b), (c, d) in zip(got, got[1:]):
+        assert b == c and a <= b
+    chunk = -(-n // world)
+    assert all(b - a <= chunk for a, b in got)
+
+
+def test_default_params_match_reference_flags():
+    # Tsne.scala:47-63 defaults; minGain TsneHelpers.scala:386
+    from tsne_amd.api import default_params
+    p = default_params()
+    assert (p.n_components, p.metric, p.learning_rate, p.iterations) == (2, 0, 1000.0, 300)
+    assert (p.early_exaggeration, p.initial_momentum, p.final_momentum) == (4.0, 0.5, 0.8)
+    assert (p.theta, p.min_gain) == (0.25, 0.01)
+
+
+def test_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(T.TsneError) as e:
+        T.Context(0)
+    assert e.value.status == -7

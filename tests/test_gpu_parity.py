@@ -1,0 +1,268 @@
+"""GPU parity: libtsne_hip (through the C ABI) against the CPU oracle and the
+reference goldens.  Tolerances: kNN indices bit-exact (ties ordered by
+(d, j)), kNN distances bit-exact fp64; goldens at the reference suite's own
+tolerances; BH gradients at 1e-4 relative to max|grad| (north_star)."""
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import tsne_amd as T
+from golden_data import csr_to_dict, dense_input, goldens, triples_to_csr
+from tsne_amd.api import default_params
+
+pytestmark = pytest.mark.gpu
+G = goldens()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+def knn_csr(idx, dist):
+    n, k = idx.shape
+    return np.arange(0, n * k + 1, k, dtype=np.int64), idx.ravel(), dist.ravel()
+
+
+# ------------------------------------------------------------------ kNN
+def test_knn_golden(ctx):
+    X = np.array([v for _, v in G["knnInput"]])
+    idx, dist = ctx.kNearestNeighbors(X, 2)
+    got = {(i, int(idx[i, t]), float(dist[i, t])) for i in range(9) for t in range(2)}
+    assert got == {tuple(t) for t in G["knnResults"]}
+
+
+def gmm(n, d, k=5, seed=0, scale=10.0):
+    rng = np.random.default_rng(seed)
+    centers = rng.normal(size=(k, d)) * scale
+    return centers[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+
+
+@pytest.mark.parametrize("n,d,k,metric", [
+    (300, 4, 5, "sqeuclidean"), (1000, 50, 90, "sqeuclidean"), (777, 33, 30, "euclidean"),
+    (640, 784, 90, "sqeuclidean"), (500, 20, 10, "cosine"), (2000, 50, 90, "sqeuclidean"),
+    (100, 3, 99, "sqeuclidean"), (129, 7, 200, "sqeuclidean")])
+def test_knn_matches_oracle(ctx, n, d, k, metric):
+    X = gmm(n, d, seed=n + d)
+    gi, gd = ctx.kNearestNeighbors(X, k, metric)
+    oi, od = O.knn(X, k, metric)
+    assert np.array_equal(gi, oi)
+    assert np.array_equal(gd, od)
+
+
+def test_knn_ties_and_duplicates(ctx):
+    # integer grid with many exact distance ties, plus 40 copies of one point
+    rng = np.random.default_rng(3)
+    X = rng.integers(0, 4, size=(600, 6)).astype(np.float64)
+    X[100:140] = X[5]
+    gi, gd = ctx.kNearestNeighbors(X, 25)
+    oi, od = O.knn(X, 25)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+def test_knn_query_range(ctx):
+    X = gmm(900, 16, seed=9)
+    gi, gd = ctx.kNearestNeighbors(X, 12, q0=333, q1=701)
+    oi, od = O.knn(X, 12, q0=333, q1=701)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+def test_knn_large_norm_offset(ctx):
+    # far from the origin: exercises the centring + error bound of the fp32 filter
+    X = gmm(1500, 64, seed=5) + 1e4
+    gi, gd = ctx.kNearestNeighbors(X, 40)
+    oi, od = O.knn(X, 40)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+
+
+def test_knn_cosine_zero_rows(ctx):
+    X = gmm(400, 12, seed=2)
+    X[7] = 0.0
+    X[200] = 0.0
+    gi, gd = ctx.kNearestNeighbors(X, 15, "cosine")
+    oi, od = O.knn(X, 15, "cosine")
+    assert np.array_equal(gi, oi)
+    assert np.array_equal(np.isnan(gd), np.isnan(od))
+    assert np.array_equal(gd[~np.isnan(gd)], od[~np.isnan(od)])
+
+
+# ----------------------------------------------------------- affinities
+def test_pairwise_affinities_golden(ctx):
+    ids, X = dense_input()
+    idx, dist = ctx.kNearestNeighbors(X, 10)
+    rp, col, d = knn_csr(idx, dist)
+    p = ctx.pairwiseAffinities(rp, d, 2.0)
+    want = {(a, b): c for a, b, c in G["densePairwiseAffinitiesResults"]}
+    got = {(i, int(col[e])): p[e] for i in range(10) for e in range(rp[i], rp[i + 1])}
+    assert set(got) == set(want)
+    assert max(abs(got[k] - v) for k, v in want.items()) <= 1e-12
+
+
+def test_affinities_match_oracle(ctx):
+    X = gmm(3000, 30, seed=1)
+    oi, od = O.knn(X, 90)
+    rp, col, d = knn_csr(oi, od)
+    p = ctx.pairwiseAffinities(rp, d, 30.0)
+    po, _ = O.affinities(rp, d, 30.0)
+    assert np.abs(p - po).max() <= 1e-12
+
+
+def test_affinities_long_rows(ctx):
+    # distance-matrix mode: one row holds every other point (> 128 entries)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 700, size=40)
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    d = rng.uniform(0, 50, size=rp[-1])
+    p = ctx.pairwiseAffinities(rp, d, 20.0)
+    po, _ = O.affinities(rp, d, 20.0)
+    assert np.abs(p - po).max() <= 1e-12
+
+
+# ---------------------------------------------------------------- joint
+@pytest.mark.parametrize("name,n,tol", [("dense", 10, 1e-12), ("sparse", 12, 1e-6)])
+def test_joint_goldens(ctx, name, n, tol):
+    src = G["densePairwiseAffinitiesResults" if name == "dense" else "sparsePairwiseAffinitiesResults"]
+    want = G["denseJointProbabilitiesResults" if name == "dense" else "sparseJointProbabilitiesResults"]
+    rp, col, val = triples_to_csr(src, n)
+    orp, oc, ov = ctx.jointDistribution(rp, col, val, n)
+    got = csr_to_dict(orp, oc, ov)
+    w = {(a, b): c for a, b, c in want}
+    assert set(got) == set(w)
+    assert max(abs(got[k] - v) for k, v in w.items()) <= tol
+    assert abs(ov.sum() - 1.0) <= 1e-12
+
+
+def test_joint_matches_oracle(ctx):
+    X = gmm(2500, 20, seed=8)
+    oi, od = O.knn(X, 30)
+    rp, col, d = knn_csr(oi, od)
+    p, _ = O.affinities(rp, d, 10.0)
+    a = ctx.jointDistribution(rp, col, p, 2500)
+    b = O.joint(rp, col, p, 2500)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert np.abs(a[2] - b[2]).max() <= 1e-15
+
+
+# ------------------------------------------------------------- gradient
+def _emb():
+    return np.array([v for _, v in sorted(G["initialEmbedding"])])
+
+
+def test_gradient_golden(ctx):
+    rp, col, val = triples_to_csr(G["denseJointProbabilitiesResults"], 10)
+    grad, Z, _ = ctx.gradient(rp, col, val, _emb(), theta=0.0)
+    want = np.array([v for _, v in sorted(G["denseGradientResults"])])
+    assert np.abs(grad - want).max() <= 1e-12
+    assert abs(Z - G["denseSumQ"]) <= 1e-9
+
+
+def random_problem(n, k, seed):
+    X = gmm(n, 10, seed=seed)
+    oi, od = O.knn(X, k)
+    rp, col, d = knn_csr(oi, od)
+    p, _ = O.affinities(rp, d, k / 3)
+    return O.joint(rp, col, p, n)
+
+
+@pytest.mark.parametrize("scale,theta,metric", [
+    (1e-4, 0.5, "sqeuclidean"), (1.0, 0.25, "sqeuclidean"), (30.0, 0.5, "sqeuclidean"),
+    (5.0, 0.5, "euclidean"), (5.0, 0.25, "cosine"), (20.0, 0.0, "sqeuclidean")])
+def test_gradient_matches_oracle(ctx, scale, theta, metric):
+    n = 1500
+    rp, col, val = random_problem(n, 30, seed=int(scale * 10) + 1)
+    Y = np.random.default_rng(1).normal(size=(n, 2)) * scale
+    g, Z, loss = ctx.gradient(rp, col, val, Y, theta, metric, exaggeration=4.0, want_loss=True)
+    r = O.gradient(rp, col, val, Y, theta, metric, exaggeration=4.0, want_loss=True)
+    scale_g = np.abs(r["grad"]).max()
+    assert np.abs(g - r["grad"]).max() <= 1e-4 * scale_g
+    assert abs(Z - r["Z"]) <= 1e-9 * r["Z"]
+    assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
+
+
+def test_gradient_points_outside_root_and_duplicates(ctx):
+    # n = 2 on one side: W = range < |x| drops points from the reference tree
+    n = 400
+    rp, col, val = random_problem(n, 10, seed=11)
+    Y = np.random.default_rng(2).normal(size=(n, 2)) + np.array([5.0, 3.0])
+    g, Z, _ = ctx.gradient(rp, col, val, Y, 0.5)
+    r = O.gradient(rp, col, val, Y, 0.5)
+    assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
+    assert abs(Z - r["Z"]) <= 1e-9 * r["Z"]
+
+
+# ---------------------------------------------------------- update / centre
+def test_update_and_center_goldens(ctx):
+    Y = _emb().copy()
+    g = np.array([v for _, v in sorted(G["denseGradientResults"])])
+    upd, gains = np.zeros_like(Y), np.ones_like(Y)
+    ctx.updateEmbedding(g, Y, upd, gains, 0.01, 0.5, 300.0)
+    assert np.abs(Y - np.array([v for _, v in sorted(G["updatedEmbeddingResults"])])).max() <= 1e-9
+    assert np.abs(gains - np.array([v for _, v in sorted(G["updatedGainsResults"])])).max() <= 1e-12
+    ctx.centerEmbedding(Y)
+    assert np.abs(Y - np.array([v for _, v in sorted(G["updatedAndCentredEmbeddingResults"])])).max() <= 1e-9
+    C = np.array([v for _, v in sorted(G["centeringInput"])])
+    ctx.centerEmbedding(C)
+    assert np.array_equal(C, np.array([v for _, v in sorted(G["centeringResults"])]))
+
+
+def test_iteration_golden_via_optimize(ctx):
+    # iterationComputation, 1 iteration, theta 0, lr 300, momentum 0.5
+    rp, col, val = triples_to_csr(G["denseJointProbabilitiesResults"], 10)
+    Y = _emb().copy()
+    upd, gains = np.zeros_like(Y), np.ones_like(Y)
+    p = default_params(iterations=1, learning_rate=300.0, theta=0.0, early_exaggeration=1.0)
+    ctx.optimize(rp, col, val, Y, upd, gains, p)
+    want = np.array([v for _, v in sorted(G["updatedAndCentredEmbeddingResults"])])
+    assert np.abs(Y - want).max() <= 1e-9
+
+
+def test_init_working_set(ctx):
+    Y, upd, gains = ctx.initWorkingSet(5000, 2, seed=7)
+    assert np.all(upd == 0) and np.all(gains == 1)
+    assert abs(Y.std() - 1e-4) < 5e-6 and abs(Y.mean()) < 5e-6
+    Y2, _, _ = ctx.initWorkingSet(5000, 2, seed=7)
+    assert np.array_equal(Y, Y2)
+
+
+def test_optimize_per_iteration_gradients(ctx):
+    """Per-iteration parity: drive the GPU loop one step at a time and check
+    each step's embedding against the oracle's step from the same state."""
+    n = 800
+    rp, col, val = random_problem(n, 30, seed=21)
+    Y = np.random.default_rng(5).normal(size=(n, 2)) * 1e-2
+    upd, gains = np.zeros_like(Y), np.ones_like(Y)
+    T_ = 130
+    for t in range(1, T_ + 1):
+        p = default_params(iterations=T_, theta=0.5, learning_rate=200.0)
+        ex = 4.0 if t <= 101 else 1.0
+        mom = 0.5 if t <= 20 else 0.8
+        g, Z, _ = ctx.gradient(rp, col, val, Y, 0.5, exaggeration=ex)
+        r = O.gradient(rp, col, val, Y, 0.5, exaggeration=ex)
+        assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max(), t
+        ctx.updateEmbedding(r["grad"], Y, upd, gains, 0.01, mom, 200.0)
+        ctx.centerEmbedding(Y)
+        del p
+
+
+def test_optimize_loss_matches_oracle(ctx):
+    n = 600
+    rp, col, val = random_problem(n, 30, seed=31)
+    Y0 = np.random.default_rng(6).normal(size=(n, 2)) * 1e-4
+    p = default_params(iterations=200, theta=0.5)
+    Yg, ug, gg = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lg = ctx.optimize(rp, col, val, Yg, ug, gg, p)
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lo = O.optimize(rp, col, val, Yo, uo, go, iterations=200, theta=0.5)
+    assert sorted(lg) == sorted(lo) == list(range(10, 201, 10))
+    assert abs(lg[200] - lo[200]) <= 0.01 * abs(lo[200])
+
+
+def test_unsupported_components(ctx):
+    rp, col, val = triples_to_csr(G["denseJointProbabilitiesResults"], 10)
+    Y = np.zeros((10, 3))
+    p = default_params(n_components=3)
+    with pytest.raises(T.TsneError) as e:
+        ctx.optimize(rp, col, val, Y, np.zeros_like(Y), np.ones_like(Y), p)
+    assert e.value.status == -4

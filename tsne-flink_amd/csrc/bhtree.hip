@@ -1,0 +1,348 @@
+// bhtree.hip -- Barnes-Hut quadtree build + traversal (TsneHelpers.scala:227-264,
+// QuadTree.scala:38-152, Cell.scala:31-36) on gfx950.
+//
+// Equivalence with the reference pointer quadtree (capacity 1, root
+// Cell(0, 0, W) with W = max(dX, dY)):
+//  * a point's Morton digits are computed by replaying the reference's own
+//    fp64 cell arithmetic (child centres x -/+ 0.5*hW, closed containment
+//    tests tried in the order NW, NE, SW, SE), so boundary ties and the
+//    rounding of non-dyadic W land in the same cell as in the reference;
+//  * the reference tree only splits cells holding >= 2 distinct points.
+//    Cells with a single occupied child form chains with identical
+//    (count, centre of mass); because the criterion max(hW,hH)/D < theta is
+//    monotone along such a chain (h halves, D fixed), summarising the chain
+//    at its deepest cell gives the same contribution as the reference's
+//    walk down it.  The binary radix tree (Karras) over the sorted keys has
+//    exactly one node per split; nodes that split inside a quad level are
+//    transparent (always opened);
+//  * leaves always interact directly; a leaf equal to the query contributes
+//    nothing (QuadTree.scala:128); points outside the root cell are not in
+//    the tree but still get a force (they are queries).
+// Known deviations (documented in DESIGN.md): exact duplicate embedding
+// points are counted with full multiplicity (the reference resets the
+// multiplicity to 1 each time a duplicate's leaf is split); cells deeper
+// than 31 levels are not split further (keys tie: all points interact
+// directly); centres of mass are summed in tree order, not insertion order.
+#include <hipcub/hipcub.hpp>
+
+#include "bhtree.hpp"
+
+namespace tsne {
+namespace {
+
+constexpr int LEVELS = 31;                 // 62 key bits
+constexpr uint64_t OUT_KEY = 1ull << 63;   // outside the root cell: sorts last
+constexpr int STACK = 128;                 // >= max tree depth (62 + 32) + 1
+
+__global__ void bbox_partial(const double *__restrict__ Y, int64_t n, double *__restrict__ part) {
+    __shared__ double sm[4][4];
+    double mnx = __builtin_inf(), mxx = -__builtin_inf(), mny = __builtin_inf(), mxy = -__builtin_inf();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double x = Y[2 * i], y = Y[2 * i + 1];
+        mnx = fmin(mnx, x); mxx = fmax(mxx, x);
+        mny = fmin(mny, y); mxy = fmax(mxy, y);
+    }
+    mnx = wave_min(mnx); mxx = wave_max(mxx); mny = wave_min(mny); mxy = wave_max(mxy);
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) { sm[w][0] = mnx; sm[w][1] = mxx; sm[w][2] = mny; sm[w][3] = mxy; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; ++k) {
+            sm[0][0] = fmin(sm[0][0], sm[k][0]); sm[0][1] = fmax(sm[0][1], sm[k][1]);
+            sm[0][2] = fmin(sm[0][2], sm[k][2]); sm[0][3] = fmax(sm[0][3], sm[k][3]);
+        }
+        for (int k = 0; k < 4; ++k) part[blockIdx.x * 4 + k] = sm[0][k];
+    }
+}
+
+__global__ void bbox_final(const double *__restrict__ part, int nb, double *__restrict__ W,
+                           int32_t *__restrict__ meta) {
+    if (threadIdx.x != 0) return;
+    double mnx = part[0], mxx = part[1], mny = part[2], mxy = part[3];
+    for (int b = 1; b < nb; ++b) {
+        mnx = fmin(mnx, part[4 * b]); mxx = fmax(mxx, part[4 * b + 1]);
+        mny = fmin(mny, part[4 * b + 2]); mxy = fmax(mxy, part[4 * b + 3]);
+    }
+    double a = mxx - mnx, c = mxy - mny;
+    *W = a > c ? a : c;  // scala.math.max(maxX - minX, maxY - minY)
+    meta[0] = 0;
+}
+
+// Morton key by replaying the reference cell arithmetic (no FMA contraction).
+__global__ void morton_keys(const double *__restrict__ Y, int64_t n, const double *__restrict__ Wp,
+                            uint64_t *__restrict__ keys, int32_t *__restrict__ idx,
+                            int32_t *__restrict__ meta) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double W = *Wp;
+    const double px = Y[2 * i], py = Y[2 * i + 1];
+    double x = 0.0, y = 0.0, hw = W, hh = W;
+    bool in = (__dsub_rn(x, hw) <= px) && (__dadd_rn(x, hw) >= px) && (__dsub_rn(y, hh) <= py) &&
+              (__dadd_rn(y, hh) >= py);
+    uint64_t key = 0;
+    if (in) {
+        for (int l = 0; l < LEVELS; ++l) {
+            const double nw = __dmul_rn(0.5, hw), nh = __dmul_rn(0.5, hw);
+            const double xw = __dsub_rn(x, nw), xe = __dadd_rn(x, nw);
+            const double yn = __dadd_rn(y, nh), ys = __dsub_rn(y, nh);
+            const bool inW = (__dsub_rn(xw, nw) <= px) && (__dadd_rn(xw, nw) >= px);
+            const bool inE = (__dsub_rn(xe, nw) <= px) && (__dadd_rn(xe, nw) >= px);
+            const bool inN = (__dsub_rn(yn, nh) <= py) && (__dadd_rn(yn, nh) >= py);
+            const bool inS = (__dsub_rn(ys, nh) <= py) && (__dadd_rn(ys, nh) >= py);
+            int q;
+            if (inN && inW) q = 0;        // NW
+            else if (inN && inE) q = 1;   // NE
+            else if (inS && inW) q = 2;   // SW
+            else q = 3;                   // SE (or a rounding gap: see header)
+            x = (q & 1) ? xe : xw;
+            y = (q & 2) ? ys : yn;
+            hw = nw;
+            hh = nh;
+            key = (key << 2) | (uint64_t)q;
+        }
+        atomicAdd(&meta[0], 1);
+    } else {
+        key = OUT_KEY;
+    }
+    keys[i] = key;
+    idx[i] = (int32_t)i;
+}
+
+__global__ void gather_sorted(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted,
+                              int64_t n, double2 *__restrict__ pos, int32_t *__restrict__ inv) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    int32_t i = idx_sorted[s];
+    pos[s] = make_double2(Y[2 * i], Y[2 * i + 1]);
+    inv[i] = (int32_t)s;
+}
+
+// delta between sorted keys i and j (bits of common prefix of the 62-bit
+// Morton field; ties extend with the index bits); -1 out of range.
+__device__ __forceinline__ int kdelta(const uint64_t *__restrict__ k, int m, int i, int j) {
+    if (j < 0 || j >= m) return -1;
+    uint64_t a = k[i], b = k[j];
+    if (a == b) return 62 + __clz((unsigned)(i ^ j));
+    return __clzll((long long)(a ^ b)) - 2;
+}
+
+// Karras (2012) binary radix tree over the m in-root points.
+__global__ void karras_build(const uint64_t *__restrict__ k, int64_t n, const int32_t *__restrict__ meta,
+                             BHNode *__restrict__ nodes, int32_t *__restrict__ parent_leaf,
+                             int32_t *__restrict__ parent_node, int32_t *__restrict__ arrive) {
+    const int m = meta[0];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m - 1) return;
+    arrive[i] = 0;
+    const int dr = kdelta(k, m, i, i + 1), dl = kdelta(k, m, i, i - 1);
+    const int d = (dr > dl) ? 1 : -1;
+    const int dmin = d > 0 ? dl : dr;
+    int lmax = 2;
+    while (kdelta(k, m, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (kdelta(k, m, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = kdelta(k, m, i, j);
+    int s = 0;
+    int t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (kdelta(k, m, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int lo = min(i, j), hi = max(i, j);
+    int left, right;
+    if (lo == gamma) { left = ~gamma; parent_leaf[gamma] = i; }
+    else { left = gamma; parent_node[gamma] = i; }
+    if (hi == gamma + 1) { right = ~(gamma + 1); parent_leaf[gamma + 1] = i; }
+    else { right = gamma + 1; parent_node[gamma + 1] = i; }
+    nodes[i].left = left;
+    nodes[i].right = right;
+    nodes[i].delta = dnode;
+    if (i == 0) parent_node[0] = -1;
+}
+
+// Bottom-up count / centre of mass.  The second thread to reach a node
+// computes it from its two children (fixed order: deterministic sums).
+// Hand-off across workgroups: agent-scope fences around the arrival atomic.
+__global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
+                          const double *__restrict__ Wp, BHNode *nodes, double2 *sums,
+                          const int32_t *__restrict__ parent_leaf,
+                          const int32_t *__restrict__ parent_node, int32_t *arrive) {
+    const int m = meta[0];
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= m || m < 2) return;
+    const double W = *Wp;
+    int p = parent_leaf[s];
+    while (p >= 0) {
+        __threadfence();                                 // release this thread's node writes
+        if (atomicAdd(&arrive[p], 1) == 0) return;       // first arriver stops
+        __threadfence();                                 // acquire the sibling's writes
+        const int32_t l = nodes[p].left, r = nodes[p].right, dl = nodes[p].delta;
+        double2 ls, rs;
+        int lc, rc;
+        if (l < 0) { ls = pos[~l]; lc = 1; } else { ls = sums[l]; lc = nodes[l].cnt; }
+        if (r < 0) { rs = pos[~r]; rc = 1; } else { rs = sums[r]; rc = nodes[r].cnt; }
+        const int cnt = lc + rc;
+        const double sx = ls.x + rs.x, sy = ls.y + rs.y;
+        const int par = parent_node[p];
+        const int dlev = dl >> 1;
+        bool real;
+        if (dl >= 62) real = false;                      // keys tie below 31 levels
+        else if (par < 0) real = true;                   // root cell chain
+        else real = (nodes[par].delta >> 1) < dlev;      // first node of its quad level
+        sums[p] = make_double2(sx, sy);
+        nodes[p].cx = sx / (double)cnt;                  // centerOfMass = sum / cumSize
+        nodes[p].cy = sy / (double)cnt;
+        nodes[p].cnt = cnt;
+        nodes[p].h = real ? ldexp(W, -dlev) : 0.0;
+        p = par;
+    }
+}
+
+__global__ void set_root(int32_t *meta) {
+    const int m = meta[0];
+    meta[1] = (m >= 2) ? 0 : (m == 1 ? ~0 : INT32_MIN);
+}
+
+// Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
+// (node, lane mask).  Every lane takes exactly its own reference decision;
+// the wave visits the union of the lanes' opened nodes.
+__global__ __launch_bounds__(256) void bh_traverse(
+    const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+    const int32_t *__restrict__ meta, double theta, int64_t s0, int64_t s1,
+    double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
+    __shared__ int32_t sref[4][STACK];
+    __shared__ uint64_t smask[4][STACK];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t s = s0 + ((int64_t)blockIdx.x * 4 + w) * 64 + lane;
+    const bool valid = s < s1;
+    if (__ballot(valid) == 0) return;
+    const int root = meta[1];
+    double qx = 0.0, qy = 0.0;
+    if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    unsigned long long nvis = 0;
+    int sp = 0;
+    const uint64_t vmask = __ballot(valid);
+    if (root != INT32_MIN) {
+        if (lane == 0) { sref[w][0] = root; smask[w][0] = vmask; }
+        sp = 1;
+    }
+    while (sp > 0) {
+        --sp;
+        const int ref = __builtin_amdgcn_readfirstlane(sref[w][sp]);
+        const uint64_t msk = smask[w][sp];
+        const bool act = (msk >> lane) & 1ull;
+        if (ref < 0) {
+            const double2 p = pos[~ref];
+            if (act) {
+                ++nvis;
+                if (!(p.x == qx && p.y == qy)) {
+                    const double dx = __dsub_rn(qx, p.x), dy = __dsub_rn(qy, p.y);
+                    const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+                    const double Q = 1.0 / (1.0 + D);
+                    const double sc = __dmul_rn(Q, Q);
+                    fx = __dadd_rn(fx, __dmul_rn(sc, dx));
+                    fy = __dadd_rn(fy, __dmul_rn(sc, dy));
+                    zs = __dadd_rn(zs, Q);
+                }
+            }
+        } else {
+            const BHNode nd = nodes[ref];
+            bool open = false;
+            if (nd.h == 0.0) {
+                open = act;
+            } else if (act) {
+                ++nvis;
+                const double dx = __dsub_rn(qx, nd.cx), dy = __dsub_rn(qy, nd.cy);
+                const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+                if (nd.h / D < theta) {
+                    const double Q = 1.0 / (1.0 + D);
+                    const double mult = __dmul_rn((double)nd.cnt, Q);
+                    const double sc = __dmul_rn(mult, Q);
+                    fx = __dadd_rn(fx, __dmul_rn(sc, dx));
+                    fy = __dadd_rn(fy, __dmul_rn(sc, dy));
+                    zs = __dadd_rn(zs, mult);
+                } else {
+                    open = true;
+                }
+            }
+            const uint64_t om = __ballot(open);
+            if (om) {
+                if (lane == 0) {
+                    sref[w][sp] = nd.right; smask[w][sp] = om;
+                    sref[w][sp + 1] = nd.left; smask[w][sp + 1] = om;
+                }
+                sp += 2;
+            }
+        }
+    }
+    if (valid) {
+        F[s] = make_double2(fx, fy);
+        Z[s] = zs;
+    }
+    if (visits) {
+        unsigned long long tot = wave_sum(nvis);
+        if (lane == 0) atomicAdd(visits, tot);
+    }
+}
+
+}  // namespace
+
+void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
+    Workspace &ws = ctx->ws;
+    t.n = n;
+    t.keys = ws.get<uint64_t>("bh.keys", n);
+    t.keys_sorted = ws.get<uint64_t>("bh.keys_sorted", n);
+    t.idx = ws.get<int32_t>("bh.idx", n);
+    t.idx_sorted = ws.get<int32_t>("bh.idx_sorted", n);
+    t.inv = ws.get<int32_t>("bh.inv", n);
+    t.pos = ws.get<double2>("bh.pos", n);
+    t.nodes = ws.get<BHNode>("bh.nodes", n);
+    t.sums = ws.get<double2>("bh.sums", n);
+    t.parent_leaf = ws.get<int32_t>("bh.parent_leaf", n);
+    t.parent_node = ws.get<int32_t>("bh.parent_node", n);
+    t.arrive = ws.get<int32_t>("bh.arrive", n);
+    t.meta = ws.get<int32_t>("bh.meta", 4);
+    t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
+    t.bbox_part = ws.get<double>("bh.bbox_part", 4 * (size_t)t.bbox_blocks);
+    t.W = ws.get<double>("bh.W", 1);
+    size_t tb = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
+                                               (int)n, 0, 64, ctx->stream));
+    t.sort_tmp_bytes = tb;
+    t.sort_tmp = ws.get<uint8_t>("bh.sort_tmp", tb);
+}
+
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY) {
+    hipStream_t st = ctx->stream;
+    const int64_t n = t.n;
+    hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
+    hipLaunchKernelGGL(bbox_final, dim3(1), dim3(64), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
+    hipLaunchKernelGGL(morton_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
+    TSNE_LAUNCH_CHECK();
+    size_t tb = t.sort_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
+                                               (int)n, 0, 64, st));
+    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
+    hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
+                       t.nodes, t.parent_leaf, t.parent_node, t.arrive);
+    hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, t.nodes,
+                       t.sums, t.parent_leaf, t.parent_node, t.arrive);
+    hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
+    TSNE_LAUNCH_CHECK();
+}
+
+void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
+                  double2 *dF, double *dz, unsigned long long *visits) {
+    if (s1 <= s0) return;
+    const int64_t waves = ceil_div(s1 - s0, 64);
+    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes,
+                       t.meta, theta, s0, s1, dF, dz, visits);
+    TSNE_LAUNCH_CHECK();
+}
+
+}  // namespace tsne

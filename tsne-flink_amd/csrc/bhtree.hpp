@@ -1,0 +1,47 @@
+// bhtree.hpp -- GPU Barnes-Hut quadtree with the reference's semantics.
+#pragma once
+#include "common.hpp"
+
+namespace tsne {
+
+// Internal node of the binary radix tree over sorted Morton keys.  A node
+// whose common prefix ends inside a quad level is "transparent" (h == 0:
+// always opened); otherwise it IS the reference quadtree cell of half width
+// h = W / 2^level (QuadTree.scala subDivide halves hWidth per level).
+struct __attribute__((aligned(16))) BHNode {
+    double cx, cy;    // centre of mass (sum / count)
+    double h;         // half width of the quad cell, 0 = transparent
+    int32_t cnt;      // cumSize
+    int32_t left;     // child refs: >= 0 internal node, < 0 leaf ~ref
+    int32_t right;
+    int32_t delta;    // common-prefix length in bits (62+ = key tie)
+};
+
+struct BHTree {
+    int64_t n = 0;           // points (queries)
+    // device arrays (ctx workspace)
+    uint64_t *keys = nullptr, *keys_sorted = nullptr;
+    int32_t *idx = nullptr, *idx_sorted = nullptr;  // sorted position -> original row
+    int32_t *inv = nullptr;                         // original row -> sorted position
+    double2 *pos = nullptr;                         // sorted positions (leaves + queries)
+    BHNode *nodes = nullptr;
+    double2 *sums = nullptr;
+    int32_t *parent_leaf = nullptr, *parent_node = nullptr;
+    int32_t *arrive = nullptr;
+    int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref
+    double *bbox_part = nullptr, *W = nullptr;
+    void *sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    int bbox_blocks = 0;
+};
+
+// Allocate (from ctx->ws) for n points.
+void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
+// Build the tree of all n points of Y (n x 2, device).
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY);
+// Repulsion for sorted positions [s0, s1): F (double2) and z (sum of Q)
+// written at the sorted position; visits (nullable) += node evaluations.
+void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
+                  double2 *dF, double *dz, unsigned long long *visits);
+
+}  // namespace tsne

@@ -1,0 +1,439 @@
+// capi.cpp -- the extern "C" boundary of libtsne_hip (include/tsne_hip.h).
+// Every entry point converts internal tsne::Error exceptions into a status
+// code plus a thread-local message; nothing throws across the ABI.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "common.hpp"
+
+namespace tsne {
+
+static thread_local std::string g_last_error;
+
+[[noreturn]] void fail(int status, const std::string &msg) { throw Error(status, msg); }
+
+template <class Fn> static int guard(Fn &&fn) {
+    try {
+        fn();
+        return TSNE_OK;
+    } catch (const Error &e) {
+        g_last_error = e.what();
+        return e.status;
+    } catch (const std::bad_alloc &) {
+        g_last_error = "host allocation failed";
+        return TSNE_ERR_NOMEM;
+    } catch (const std::exception &e) {
+        g_last_error = e.what();
+        return TSNE_ERR_HIP;
+    } catch (...) {
+        g_last_error = "unknown error";
+        return TSNE_ERR_HIP;
+    }
+}
+
+static void check_ctx(tsne_ctx *ctx) {
+    if (!ctx) fail(TSNE_ERR_ARG, "context is NULL");
+}
+
+template <class T> static T *upload(tsne_ctx *ctx, const std::string &name, const T *h, size_t count) {
+    T *d = ctx->ws.get<T>(name, count ? count : 1);
+    if (count) TSNE_HIP(hipMemcpyAsync(d, h, sizeof(T) * count, hipMemcpyHostToDevice, ctx->stream));
+    return d;
+}
+
+template <class T> static void download(tsne_ctx *ctx, T *h, const T *d, size_t count) {
+    if (count) TSNE_HIP(hipMemcpyAsync(h, d, sizeof(T) * count, hipMemcpyDeviceToHost, ctx->stream));
+}
+
+static void sync(tsne_ctx *ctx) { TSNE_HIP(hipStreamSynchronize(ctx->stream)); }
+
+}  // namespace tsne
+
+using namespace tsne;
+
+extern "C" {
+
+int tsne_abi_version(void) { return TSNE_HIP_ABI_VERSION; }
+
+const char *tsne_last_error(void) { return g_last_error.c_str(); }
+
+void tsne_params_default(tsne_params *p) {
+    if (!p) return;
+    p->n_components = 2;
+    p->metric = TSNE_METRIC_SQEUCLIDEAN;
+    p->learning_rate = 1000.0;
+    p->iterations = 300;
+    p->early_exaggeration = 4.0;
+    p->initial_momentum = 0.5;
+    p->final_momentum = 0.8;
+    p->theta = 0.25;
+    p->min_gain = 0.01;
+}
+
+int tsne_metric_from_name(const char *name, int32_t *metric_out) {
+    return guard([&] {
+        std::string m = name ? name : "";
+        int32_t v;
+        if (m == "sqeuclidean") v = TSNE_METRIC_SQEUCLIDEAN;
+        else if (m == "euclidean") v = TSNE_METRIC_EUCLIDEAN;
+        else if (m == "cosine") v = TSNE_METRIC_COSINE;
+        else fail(TSNE_ERR_ARG, "Metric '" + m + "' not defined");  // Tsne.scala:166
+        if (metric_out) *metric_out = v;
+    });
+}
+
+int tsne_shard_rows(int64_t n, int32_t world, int32_t rank, int64_t *r0, int64_t *r1) {
+    return guard([&] {
+        TSNE_REQUIRE(n >= 0 && world >= 1 && rank >= 0 && rank < world, "bad shard arguments");
+        const int64_t chunk = ceil_div(n, world);
+        const int64_t a = std::min<int64_t>(n, chunk * rank);
+        if (r0) *r0 = a;
+        if (r1) *r1 = std::min<int64_t>(n, a + chunk);
+    });
+}
+
+int tsne_ctx_create(int32_t device, tsne_ctx **out) {
+    return guard([&] {
+        TSNE_REQUIRE(out != nullptr, "out is NULL");
+        *out = nullptr;
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+            fail(TSNE_ERR_NO_DEVICE, "no HIP device visible");
+        TSNE_REQUIRE(device >= 0 && device < count, "device index out of range");
+        TSNE_HIP(hipSetDevice(device));
+        hipDeviceProp_t prop;
+        TSNE_HIP(hipGetDeviceProperties(&prop, device));
+        std::unique_ptr<tsne_ctx> c(new tsne_ctx());
+        c->device = device;
+        c->cu_count = prop.multiProcessorCount;
+        TSNE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+        *out = c.release();
+    });
+}
+
+int tsne_ctx_destroy(tsne_ctx *ctx) {
+    if (!ctx) return TSNE_OK;
+    int rc = guard([&] {
+        DeviceGuard g(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+        opt_destroy(ctx);
+        comm_destroy(ctx);
+        ctx->ws.clear();
+        if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    });
+    delete ctx;
+    return rc;
+}
+
+int tsne_ctx_set_stream(tsne_ctx *ctx, void *hip_stream) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        if (ctx->own_stream && ctx->stream) {
+            TSNE_HIP(hipStreamSynchronize(ctx->stream));
+            TSNE_HIP(hipStreamDestroy(ctx->stream));
+        }
+        if (hip_stream) {
+            ctx->stream = static_cast<hipStream_t>(hip_stream);
+            ctx->own_stream = false;
+        } else {
+            TSNE_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+            ctx->own_stream = true;
+        }
+    });
+}
+
+void *tsne_ctx_stream(tsne_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int tsne_ctx_synchronize(tsne_ctx *ctx) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        sync(ctx);
+    });
+}
+
+int tsne_comm_unique_id(uint8_t id_out[TSNE_UNIQUE_ID_BYTES]) {
+    return guard([&] {
+        TSNE_REQUIRE(id_out != nullptr, "id_out is NULL");
+        comm_unique_id(id_out);
+    });
+}
+
+int tsne_ctx_init_comm(tsne_ctx *ctx, int32_t rank, int32_t world, const uint8_t id[TSNE_UNIQUE_ID_BYTES]) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(world == 1 || id != nullptr, "unique id is NULL");
+        comm_init(ctx, rank, world, id);
+    });
+}
+
+int tsne_ctx_rank(tsne_ctx *ctx, int32_t *rank, int32_t *world) {
+    return guard([&] {
+        check_ctx(ctx);
+        if (rank) *rank = ctx->rank;
+        if (world) *world = ctx->world;
+    });
+}
+
+// ------------------------------------------------------------ device API
+
+int tsne_dev_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t k,
+                 int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        knn_device(ctx, dX, n, d, metric, k, q0, q1, d_idx, d_dist);
+    });
+}
+
+int tsne_dev_pairwise_affinities(tsne_ctx *ctx, const int64_t *d_row_ptr, const double *d_dist,
+                                 int64_t nrows, double perplexity, double *d_p) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        affinities_device(ctx, d_row_ptr, d_dist, nrows, perplexity, d_p);
+    });
+}
+
+int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
+                                const double *d_p, int64_t n, int64_t cap, int64_t *d_out_row_ptr,
+                                int32_t *d_out_col, double *d_out_val, int64_t *nnz_out) {
+    int64_t nnz = -1;
+    int rc = guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(n >= 1, "empty matrix");
+        nnz = joint_device(ctx, d_row_ptr, d_col, d_p, n, cap, d_out_row_ptr, d_out_col, d_out_val);
+    });
+    if (nnz_out) *nnz_out = nnz;
+    if (rc == TSNE_OK && nnz > cap) {
+        g_last_error = "joint distribution needs " + std::to_string(nnz) + " entries, cap is " + std::to_string(cap);
+        return TSNE_ERR_CAPACITY;
+    }
+    return rc;
+}
+
+int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *d_row_ptr,
+                       const int32_t *d_col, const double *d_P, int64_t n, double *d_Y,
+                       double *d_upd, double *d_gains) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        opt_setup(ctx, params, d_row_ptr, d_col, d_P, n, d_Y, d_upd, d_gains);
+    });
+}
+
+int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        opt_step(ctx, t);
+    });
+}
+
+int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap, int32_t *n_loss) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        int32_t k = opt_losses(ctx, loss_keys, loss_vals, cap);
+        if (n_loss) *n_loss = k;
+    });
+}
+
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out4, int64_t *visits_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        opt_profile(ctx, enable, ms_out4, visits_out);
+    });
+}
+
+// ------------------------------------------------------------ host API
+
+int tsne_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metric, int32_t k,
+             int64_t q0, int64_t q1, int32_t *idx_out, double *dist_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(X && idx_out && dist_out, "NULL buffer");
+        TSNE_REQUIRE(n >= 2 && d >= 1 && k >= 1, "bad sizes");
+        TSNE_REQUIRE(q0 >= 0 && q1 <= n && q0 <= q1, "query range out of bounds");
+        const int64_t kk = std::min<int64_t>(k, n - 1);
+        double *dX = upload(ctx, "h.X", X, (size_t)(n * d));
+        int32_t *di = ctx->ws.get<int32_t>("h.knn_idx", (size_t)std::max<int64_t>(1, (q1 - q0) * kk));
+        double *dd = ctx->ws.get<double>("h.knn_dist", (size_t)std::max<int64_t>(1, (q1 - q0) * kk));
+        knn_device(ctx, dX, n, d, metric, k, q0, q1, di, dd);
+        download(ctx, idx_out, di, (size_t)((q1 - q0) * kk));
+        download(ctx, dist_out, dd, (size_t)((q1 - q0) * kk));
+        sync(ctx);
+    });
+}
+
+int tsne_pairwise_affinities(tsne_ctx *ctx, const int64_t *row_ptr, const double *dist, int64_t nrows,
+                             double perplexity, double *p_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(row_ptr && nrows >= 0, "bad CSR");
+        const int64_t nnz = row_ptr[nrows] - row_ptr[0];
+        TSNE_REQUIRE(row_ptr[0] == 0, "row_ptr[0] must be 0");
+        TSNE_REQUIRE(nnz == 0 || (dist && p_out), "NULL buffer");
+        int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)nrows + 1);
+        double *dd = upload(ctx, "h.dist", dist, (size_t)nnz);
+        double *dp = ctx->ws.get<double>("h.p", (size_t)nnz + 1);
+        affinities_device(ctx, drp, dd, nrows, perplexity, dp);
+        download(ctx, p_out, dp, (size_t)nnz);
+        sync(ctx);
+    });
+}
+
+int tsne_joint_distribution(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *p,
+                            int64_t n, int64_t cap, int64_t *out_row_ptr, int32_t *out_col,
+                            double *out_val, int64_t *nnz_out) {
+    int64_t nnz = -1;
+    int rc = guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(row_ptr && n >= 1 && row_ptr[0] == 0, "bad CSR");
+        const int64_t nin = row_ptr[n];
+        for (int64_t e = 0; e < nin; ++e)
+            if (col[e] < 0 || col[e] >= n) fail(TSNE_ERR_ARG, "column index out of range");
+        int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)n + 1);
+        int32_t *dc = upload(ctx, "h.col", col, (size_t)nin);
+        double *dp = upload(ctx, "h.p", p, (size_t)nin);
+        const int64_t dcap = 2 * nin + 1;
+        int64_t *orp = ctx->ws.get<int64_t>("h.orp", (size_t)n + 1);
+        int32_t *oc = ctx->ws.get<int32_t>("h.ocol", (size_t)dcap);
+        double *ov = ctx->ws.get<double>("h.oval", (size_t)dcap);
+        nnz = joint_device(ctx, drp, dc, dp, n, dcap, orp, oc, ov);
+        if (nnz <= cap) {
+            download(ctx, out_row_ptr, orp, (size_t)n + 1);
+            download(ctx, out_col, oc, (size_t)nnz);
+            download(ctx, out_val, ov, (size_t)nnz);
+            sync(ctx);
+        }
+    });
+    if (nnz_out) *nnz_out = nnz;
+    if (rc == TSNE_OK && nnz > cap) {
+        g_last_error = "joint distribution needs " + std::to_string(nnz) + " entries, cap is " + std::to_string(cap);
+        return TSNE_ERR_CAPACITY;
+    }
+    return rc;
+}
+
+int tsne_gradient(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *P, int64_t n,
+                  const double *Y, int32_t metric, double theta, double exaggeration, double *grad_out,
+                  double *sumq_out, double *loss_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(row_ptr && Y && grad_out && n >= 1 && row_ptr[0] == 0, "bad arguments");
+        TSNE_REQUIRE(metric >= 0 && metric <= 2, "unknown metric");
+        const int64_t nnz = row_ptr[n];
+        int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)n + 1);
+        int32_t *dc = upload(ctx, "h.col", col, (size_t)nnz);
+        double *dp = upload(ctx, "h.p", P, (size_t)nnz);
+        double *dY = upload(ctx, "h.Y", Y, (size_t)n * 2);
+        double *dg = ctx->ws.get<double>("h.grad", (size_t)n * 2);
+        gradient_device(ctx, drp, dc, dp, n, dY, metric, theta, exaggeration, dg, sumq_out, loss_out);
+        download(ctx, grad_out, dg, (size_t)n * 2);
+        sync(ctx);
+    });
+}
+
+int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *grad, double *Y, double *upd,
+                          double *gains, double min_gain, double momentum, double learning_rate) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(grad && Y && upd && gains && n >= 0 && c >= 1, "bad arguments");
+        const size_t ne = (size_t)(n * c);
+        double *dg = upload(ctx, "h.grad", grad, ne);
+        double *dY = upload(ctx, "h.Y", Y, ne);
+        double *du = upload(ctx, "h.upd", upd, ne);
+        double *dn = upload(ctx, "h.gains", gains, ne);
+        update_device(ctx, n, c, dg, dY, du, dn, min_gain, momentum, learning_rate);
+        download(ctx, Y, dY, ne);
+        download(ctx, upd, du, ne);
+        download(ctx, gains, dn, ne);
+        sync(ctx);
+    });
+}
+
+int tsne_center_embedding(tsne_ctx *ctx, int64_t n, int32_t c, double *Y) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(Y && n >= 1 && c >= 1 && c <= 8, "bad arguments");
+        double *dY = upload(ctx, "h.Y", Y, (size_t)(n * c));
+        center_device(ctx, n, c, dY);
+        download(ctx, Y, dY, (size_t)(n * c));
+        sync(ctx);
+    });
+}
+
+int tsne_init_working_set(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed, double *Y, double *upd,
+                          double *gains) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(Y && upd && gains && n >= 0 && c >= 1, "bad arguments");
+        const size_t ne = (size_t)(n * c);
+        double *dY = ctx->ws.get<double>("h.Y", ne + 1);
+        double *du = ctx->ws.get<double>("h.upd", ne + 1);
+        double *dn = ctx->ws.get<double>("h.gains", ne + 1);
+        init_working_set_device(ctx, n, c, seed, dY, du, dn);
+        download(ctx, Y, dY, ne);
+        download(ctx, upd, du, ne);
+        download(ctx, gains, dn, ne);
+        sync(ctx);
+    });
+}
+
+int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_ptr, const int32_t *col,
+                  const double *P, int64_t n, double *Y, double *upd, double *gains, int32_t *loss_keys,
+                  double *loss_vals, int32_t loss_cap, int32_t *n_loss) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(params && row_ptr && Y && upd && gains && n >= 1 && row_ptr[0] == 0, "bad arguments");
+        if (params->n_components != 2)
+            fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (Cell.contains requires 2-D points)");
+        const int64_t chunk = ceil_div(n, ctx->world);
+        const int64_t npad = chunk * ctx->world;
+        const int64_t r0 = std::min<int64_t>(n, chunk * ctx->rank);
+        const int64_t r1 = std::min<int64_t>(n, r0 + chunk);
+        // this rank's rows of P, rebased
+        std::vector<int64_t> lrp((size_t)(r1 - r0) + 1);
+        for (int64_t i = r0; i <= r1; ++i) lrp[(size_t)(i - r0)] = row_ptr[i] - row_ptr[r0];
+        const int64_t lnnz = lrp.back();
+        int64_t *drp = upload(ctx, "h.rp", lrp.data(), lrp.size());
+        int32_t *dc = upload(ctx, "h.col", col + row_ptr[r0], (size_t)lnnz);
+        double *dp = upload(ctx, "h.p", P + row_ptr[r0], (size_t)lnnz);
+        double *dY = ctx->ws.get<double>("h.Yopt", (size_t)npad * 2);
+        double *du = ctx->ws.get<double>("h.updopt", (size_t)npad * 2);
+        double *dn = ctx->ws.get<double>("h.gainsopt", (size_t)npad * 2);
+        TSNE_HIP(hipMemcpyAsync(dY, Y, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        TSNE_HIP(hipMemcpyAsync(du, upd, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        TSNE_HIP(hipMemcpyAsync(dn, gains, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        opt_setup(ctx, params, drp, dc, dp, n, dY, du, dn);
+        for (int32_t t = 1; t <= params->iterations; ++t) opt_step(ctx, t);
+        if (ctx->world > 1) {  // each rank updated only its own rows of upd / gains
+            comm_allgather_bytes(ctx, du + 2 * r0, du, sizeof(double) * 2 * chunk);
+            comm_allgather_bytes(ctx, dn + 2 * r0, dn, sizeof(double) * 2 * chunk);
+        }
+        download(ctx, Y, dY, (size_t)n * 2);
+        download(ctx, upd, du, (size_t)n * 2);
+        download(ctx, gains, dn, (size_t)n * 2);
+        sync(ctx);
+        int32_t k = opt_losses(ctx, loss_keys, loss_vals, loss_cap);
+        if (n_loss) *n_loss = k;
+    });
+}
+
+}  // extern "C"

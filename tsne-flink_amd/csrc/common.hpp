@@ -1,0 +1,201 @@
+// common.hpp -- shared plumbing for libtsne_hip (gfx950 / MI355X only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tsne_hip.h"
+
+namespace tsne {
+
+// Internal error type; converted to a tsne_status at the C ABI boundary.
+struct Error : std::runtime_error {
+    int status;
+    Error(int s, const std::string &m) : std::runtime_error(m), status(s) {}
+};
+
+[[noreturn]] void fail(int status, const std::string &msg);
+
+#define TSNE_HIP(expr)                                                                     \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            ::tsne::fail(TSNE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define TSNE_LAUNCH_CHECK() TSNE_HIP(hipGetLastError())
+
+#define TSNE_REQUIRE(cond, msg)                                         \
+    do {                                                                \
+        if (!(cond)) ::tsne::fail(TSNE_ERR_ARG, std::string(msg));     \
+    } while (0)
+
+// Growable device allocation owned by the context.
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    void *ensure(size_t b) {
+        if (b > bytes) {
+            release();
+            size_t want = b < 256 ? 256 : b;
+            hipError_t e = hipMalloc(&p, want);
+            if (e != hipSuccess) {
+                p = nullptr;
+                fail(TSNE_ERR_NOMEM, "hipMalloc(" + std::to_string(want) + ") failed: " + hipGetErrorString(e));
+            }
+            bytes = want;
+        }
+        return p;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// Named workspace: each stage grabs buffers by name; they persist across calls.
+struct Workspace {
+    std::map<std::string, std::unique_ptr<DevBuf>> bufs;
+    template <class T> T *get(const std::string &name, size_t count) {
+        auto &b = bufs[name];
+        if (!b) b.reset(new DevBuf());
+        return static_cast<T *>(b->ensure(count * sizeof(T)));
+    }
+    void clear() { bufs.clear(); }
+};
+
+struct Comm;      // RCCL communicator (comm.cpp)
+struct OptState;  // device-resident optimizer state (optimize.hip)
+
+}  // namespace tsne
+
+struct tsne_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int rank = 0, world = 1;
+    tsne::Comm *comm = nullptr;
+    tsne::Workspace ws;
+    tsne::OptState *opt = nullptr;
+    int cu_count = 256;
+};
+
+namespace tsne {
+
+// RAII guard that makes ctx->device current for the calling thread.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) TSNE_HIP(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+
+// ---- stage entry points (device pointers, enqueue on ctx->stream) ----
+void knn_device(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric,
+                int32_t k, int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist);
+void affinities_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const double *d_dist,
+                       int64_t nrows, double perplexity, double *d_p);
+int64_t joint_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
+                     const double *d_p, int64_t n, int64_t cap, int64_t *d_out_row_ptr,
+                     int32_t *d_out_col, double *d_out_val);
+void init_working_set_device(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed, double *dY,
+                             double *dupd, double *dgains);
+void update_device(tsne_ctx *ctx, int64_t n, int32_t c, const double *dgrad, double *dY,
+                   double *dupd, double *dgains, double min_gain, double momentum, double lr);
+void center_device(tsne_ctx *ctx, int64_t n, int32_t c, double *dY);
+// single gradient evaluation (whole problem on this device)
+void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
+                     const double *d_P, int64_t n, const double *dY, int32_t metric,
+                     double theta, double exaggeration, double *d_grad, double *h_sumq,
+                     double *h_loss);
+
+void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr,
+               const int32_t *d_col, const double *d_P, int64_t n, double *dY, double *dupd,
+               double *dgains);
+void opt_step(tsne_ctx *ctx, int32_t t);
+int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap);
+void opt_profile(tsne_ctx *ctx, int enable, double *ms4, int64_t *visits);
+void opt_destroy(tsne_ctx *ctx);
+
+// comm.cpp
+void comm_unique_id(uint8_t *out);
+void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id);
+void comm_destroy(tsne_ctx *ctx);
+void comm_allgather_bytes(tsne_ctx *ctx, const void *send, void *recv, size_t bytes_per_rank);
+void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count);
+
+}  // namespace tsne
+
+// ---------------------------------------------------------------- device helpers
+namespace tsne {
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <class T> __device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <class T> __device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        T w = __shfl_xor(v, o, 64);
+        v = v > w ? v : w;
+    }
+    return v;
+}
+
+template <class T> __device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        T w = __shfl_xor(v, o, 64);
+        v = v < w ? v : w;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// Order-preserving map of a double to uint64 (NaN canonicalised, sorts last).
+__device__ __forceinline__ uint64_t dkey(double d) {
+    uint64_t u = __double_as_longlong(d);
+    if (d != d) u = 0x7FF8000000000000ull;
+    return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ uint32_t fkey(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (f != f) return 0xFFFFFFFFu;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+    uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    return __uint_as_float(u);
+}
+
+}  // namespace tsne

@@ -1,0 +1,543 @@
+// knn.hip -- brute-force kNN (TsneHelpers.scala:41-59) on gfx950.
+//
+// The reference crosses all N^2 pairs, filters i != j, sorts each group by
+// the fp64 breeze metric and keeps the first k.  Here:
+//   1. prep:   centre X (or L2-normalise for cosine) and round to fp32, with
+//              fp32 squared norms; rows padded to a multiple of 32 columns.
+//   2. filter: MFMA fp32 tiles (v_mfma_f32_32x32x2_f32) compute
+//              d32 = |q|^2 + |c|^2 - 2 q.c for a 128x128 (query x candidate)
+//              tile staged through LDS; every pair with d32 <= tau_q (the
+//              query's running threshold) is appended to the query's
+//              candidate buffer.  The N x N matrix is never materialised.
+//              Candidates are swept in doubling ranges; after each range a
+//   3. compact kernel (one wave per query) radix-selects the kk-th smallest
+//              d32, sets tau_q = kth + 2*delta_q and drops everything above.
+//              delta_q is a rigorous bound on |d32 - d64| (fp32 rounding of
+//              the inputs, the K-term fp32 FMA chain, the final add), so the
+//              buffer always holds every j whose exact distance can be in the
+//              top kk -- including exact ties at the k-th distance.
+//   4. rerank: one wave per query recomputes the surviving candidates with
+//              the exact breeze fp64 metric (sequential sum, no FMA
+//              contraction) and bitonic-sorts them by (d, j) in LDS.
+//   5. fallback: a query whose buffer overflows (only pathological crowds of
+//              near-equal distances, e.g. many duplicate points) is redone by
+//              an exact fp64 scan + stable radix sort.
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace tsne {
+namespace {
+
+constexpr int TQ = 128;   // queries per workgroup tile
+constexpr int TC = 128;   // candidates per workgroup tile
+constexpr int KC = 32;    // k-chunk staged in LDS
+constexpr int LDSW = KC + 1;  // padded LDS row (bank-conflict free column reads)
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------- prep
+// Column partial sums for the mean (deterministic two-level reduction).
+__global__ void colsum_partial(const double *__restrict__ X, int64_t n, int32_t d,
+                               int64_t rows_per_block, double *__restrict__ part) {
+    const int64_t r0 = blockIdx.x * rows_per_block;
+    const int64_t r1 = min(n, r0 + rows_per_block);
+    for (int32_t c = threadIdx.x; c < d; c += blockDim.x) {
+        double s = 0.0;
+        for (int64_t r = r0; r < r1; ++r) s += X[r * d + c];
+        part[(int64_t)blockIdx.x * d + c] = s;
+    }
+}
+
+__global__ void colsum_final(const double *__restrict__ part, int64_t nblocks, int32_t d,
+                             int64_t n, double *__restrict__ mean) {
+    for (int32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < d; c += gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int64_t b = 0; b < nblocks; ++b) s += part[b * d + c];
+        mean[c] = s / (double)n;
+    }
+}
+
+// One wave per row: X32 = fp32(x - mean) (or fp32(x / |x|) for cosine),
+// norm32 = fp32(sum X32^2) (0.5 for cosine), norm64 = sqrt(sum x^2) fp64
+// sequential (cosine rerank).  Rows >= n are zero.
+__global__ void prep_rows(const double *__restrict__ X, int64_t n, int32_t d, int32_t dpad,
+                          int64_t npad, int32_t metric, const double *__restrict__ mean,
+                          float *__restrict__ X32, float *__restrict__ norm32,
+                          double *__restrict__ norm64, unsigned int *__restrict__ nmax_bits) {
+    const int64_t row = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x / 64);
+    const int lane = lane_id();
+    if (row >= npad) return;
+    float *out = X32 + row * dpad;
+    if (row >= n) {
+        for (int c = lane; c < dpad; c += 64) out[c] = 0.f;
+        if (lane == 0) { norm32[row] = 0.f; norm64[row] = 0.0; }
+        return;
+    }
+    const double *x = X + row * d;
+    double scale = 1.0;
+    if (metric == TSNE_METRIC_COSINE) {
+        if (lane == 0) {  // exact sequential norm, as breeze norm()
+            double s = 0.0;
+            for (int c = 0; c < d; ++c) s = __dadd_rn(s, __dmul_rn(x[c], x[c]));
+            norm64[row] = sqrt(s);
+        }
+        double s = 0.0;
+        for (int c = lane; c < d; c += 64) s += x[c] * x[c];
+        s = wave_sum(s);
+        scale = s > 0.0 ? 1.0 / sqrt(s) : 0.0;
+    }
+    double acc = 0.0;
+    for (int c = lane; c < dpad; c += 64) {
+        float v = 0.f;
+        if (c < d) v = (metric == TSNE_METRIC_COSINE) ? (float)(x[c] * scale) : (float)(x[c] - mean[c]);
+        out[c] = v;
+        acc += (double)v * (double)v;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+        float nv = (metric == TSNE_METRIC_COSINE) ? 0.5f : (float)acc;
+        norm32[row] = nv;
+        if (metric != TSNE_METRIC_COSINE) norm64[row] = 0.0;
+        atomicMax(nmax_bits, __float_as_uint(nv));  // non-negative floats order as uints
+    }
+}
+
+// ------------------------------------------------------------- filter
+// Workgroup = 4 waves in a 2x2 arrangement; wave tile 64x64 = 2x2 MFMA
+// 32x32 tiles (64 accumulators per lane).  MODE 0 = dense first pass
+// (every candidate written at slot c - c0, self = +inf); MODE 1 = threshold
+// filter with wave-aggregated atomic appends.
+template <int MODE>
+__global__ __launch_bounds__(256) void knn_filter(
+    const float *__restrict__ X32, const float *__restrict__ norm32, int32_t dpad,
+    int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale,
+    const float *__restrict__ tau, int32_t *__restrict__ cnt, float *__restrict__ cand_d,
+    int32_t *__restrict__ cand_j, int32_t *__restrict__ flags, int32_t cap) {
+    __shared__ float Qs[TQ * LDSW];
+    __shared__ float Cs[TC * LDSW];
+    __shared__ float nq_s[TQ], tau_s[TQ], nc_s[TC];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int64_t qb = q0 + (int64_t)blockIdx.y * TQ;   // query tile base (global row)
+    const int64_t cb = c0 + (int64_t)blockIdx.x * TC;   // candidate tile base
+
+    if (tid < TQ) {
+        int64_t q = qb + tid;
+        nq_s[tid] = norm32[q];  // padded arrays: q < npad always
+        tau_s[tid] = (MODE == 1 && q < q1) ? tau[q - q0] : 0.f;
+    } else {
+        int64_t c = cb + (tid - TQ);
+        nc_s[tid - TQ] = norm32[c];
+    }
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    for (int k0 = 0; k0 < dpad; k0 += KC) {
+        // stage 128 x 32 of queries and of candidates: 1024 float4 each, 4 per thread
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            int idx = tid + it * 256;
+            int r = idx >> 3, c4 = (idx & 7) * 4;
+            float4 vq = *reinterpret_cast<const float4 *>(X32 + (qb + r) * dpad + k0 + c4);
+            float4 vc = *reinterpret_cast<const float4 *>(X32 + (cb + r) * dpad + k0 + c4);
+            float *dq = Qs + r * LDSW + c4;
+            float *dc = Cs + r * LDSW + c4;
+            dq[0] = vq.x; dq[1] = vq.y; dq[2] = vq.z; dq[3] = vq.w;
+            dc[0] = vc.x; dc[1] = vc.y; dc[2] = vc.z; dc[3] = vc.w;
+        }
+        __syncthreads();
+        const int lr = lane & 31, lk = lane >> 5;
+#pragma unroll
+        for (int s = 0; s < KC / 2; ++s) {
+            const int kk = 2 * s + lk;
+            float a0 = Qs[(wr * 64 + lr) * LDSW + kk];
+            float a1 = Qs[(wr * 64 + 32 + lr) * LDSW + kk];
+            float b0 = Cs[(wc * 64 + lr) * LDSW + kk];
+            float b1 = Cs[(wc * 64 + 32 + lr) * LDSW + kk];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+    // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    const int half = lane >> 5, lcol = lane & 31;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+            const int lc = wc * 64 + tj * 32 + lcol;
+            const int64_t c = cb + lc;
+            const float ncv = nc_s[lc];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lrow = wr * 64 + ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+                const int64_t q = qb + lrow;
+                float dv = nq_s[lrow] + ncv - dot_scale * acc[ti][tj][r];
+                if (MODE == 0) {
+                    if (q < q1 && c < c1) {
+                        float w = (c == q) ? __builtin_inff() : dv;
+                        int64_t o = (q - q0) * (int64_t)cap + (c - c0);
+                        cand_d[o] = w;
+                        cand_j[o] = (int32_t)c;
+                    }
+                } else {
+                    bool ok = (q < q1) && (c < c1) && (c != q) && (dv <= tau_s[lrow]);
+                    uint64_t m = __ballot(ok);
+                    if (m) {
+                        uint32_t mine = half ? (uint32_t)(m >> 32) : (uint32_t)m;
+                        int leader = __ffs(mine) - 1;  // -1 if none in this half
+                        int base = 0;
+                        if (ok && lcol == leader) base = atomicAdd(&cnt[q - q0], __popc(mine));
+                        base = __shfl(base, (half << 5) + (leader < 0 ? 0 : leader), 64);
+                        if (ok) {
+                            int slot = base + __popc(mine & ((1u << lcol) - 1u));
+                            if (slot < cap) {
+                                int64_t o = (q - q0) * (int64_t)cap + slot;
+                                cand_d[o] = dv;
+                                cand_j[o] = (int32_t)c;
+                            } else {
+                                flags[q - q0] = 1;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- compact
+// One wave per query: radix-select the kk-th smallest d32 among the first
+// min(cnt, CAP) entries, tau = kth + 2 delta, keep entries <= tau in place.
+template <int CAP>
+__global__ __launch_bounds__(256) void knn_compact(
+    int64_t nq, int32_t kk, const float *__restrict__ norm32, int64_t q0, float nmax,
+    float delta_coef, float *__restrict__ tau, int32_t *__restrict__ cnt,
+    float *__restrict__ cand_d, int32_t *__restrict__ cand_j, int32_t *__restrict__ flags) {
+    constexpr int R = CAP / 64;
+    __shared__ unsigned int hist_s[4][256];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + w;
+    if (qi >= nq) return;
+    unsigned int *hist = hist_s[w];
+    if (flags[qi]) { if (lane == 0) tau[qi] = -__builtin_inff(); return; }
+    const int m = min(cnt[qi], CAP);
+    float *bd = cand_d + qi * CAP;
+    int32_t *bj = cand_j + qi * CAP;
+    float dv[R];
+    int32_t jv[R];
+    uint32_t key[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int e = r * 64 + lane;
+        dv[r] = e < m ? bd[e] : __builtin_inff();
+        jv[r] = e < m ? bj[e] : 0;
+        key[r] = e < m ? fkey(dv[r]) : 0xFFFFFFFFu;
+    }
+    float t;
+    if (m < kk) {
+        t = __builtin_inff();
+    } else {
+        uint32_t prefix = 0, pmask = 0;
+        int rank = kk;  // 1-based rank of the wanted element
+        for (int shift = 24; shift >= 0; shift -= 8) {
+            for (int b = lane; b < 256; b += 64) hist[b] = 0;
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if ((key[r] & pmask) == prefix && (r * 64 + lane) < m)
+                    atomicAdd(&hist[(key[r] >> shift) & 255u], 1u);
+            __builtin_amdgcn_wave_barrier();
+            unsigned int h0 = hist[lane * 4], h1 = hist[lane * 4 + 1], h2 = hist[lane * 4 + 2],
+                         h3 = hist[lane * 4 + 3];
+            unsigned int s = h0 + h1 + h2 + h3, incl = s;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                unsigned int y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            unsigned int excl = incl - s;
+            // the lane whose [excl, incl) covers rank
+            bool here = (excl < (unsigned)rank) && ((unsigned)rank <= incl);
+            uint64_t hm = __ballot(here);
+            int src = __ffsll((unsigned long long)hm) - 1;
+            int bin = 0;
+            unsigned int below = excl;
+            if (here) {
+                unsigned int acc2 = excl;
+                if ((unsigned)rank <= acc2 + h0) { bin = lane * 4; }
+                else if ((unsigned)rank <= acc2 + h0 + h1) { bin = lane * 4 + 1; below = acc2 + h0; }
+                else if ((unsigned)rank <= acc2 + h0 + h1 + h2) { bin = lane * 4 + 2; below = acc2 + h0 + h1; }
+                else { bin = lane * 4 + 3; below = acc2 + h0 + h1 + h2; }
+            }
+            bin = __shfl(bin, src, 64);
+            below = __shfl(below, src, 64);
+            prefix |= (uint32_t)bin << shift;
+            pmask |= 255u << shift;
+            rank -= (int)below;
+            __builtin_amdgcn_wave_barrier();
+        }
+        float kth = fkey_inv(prefix);
+        float delta = delta_coef * (norm32[q0 + qi] + nmax);
+        t = (kth + 2.0f * delta) * 1.000001f + 1e-30f;
+        if (!(t == t)) t = __builtin_inff();
+    }
+    // compaction in place (all reads are in registers already)
+    int out = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        bool keep = (r * 64 + lane) < m && dv[r] <= t;
+        uint64_t km = __ballot(keep);
+        if (keep) {
+            int pos = out + __popcll(km & lanemask_lt());
+            bd[pos] = dv[r];
+            bj[pos] = jv[r];
+        }
+        out += __popcll(km);
+    }
+    if (lane == 0) {
+        cnt[qi] = out;
+        tau[qi] = t;
+        if (out > CAP / 2) { flags[qi] = 1; tau[qi] = -__builtin_inff(); }
+    }
+}
+
+// -------------------------------------------------------------- rerank
+// Exact breeze metric in fp64, sequential over the coordinates (no FMA).
+__device__ __forceinline__ double exact_metric(const double *__restrict__ a,
+                                               const double *__restrict__ b, int32_t d,
+                                               int32_t metric, double na, double nb) {
+    if (metric == TSNE_METRIC_COSINE) {
+        double s = 0.0;
+        for (int32_t t = 0; t < d; ++t) s = __dadd_rn(s, __dmul_rn(a[t], b[t]));
+        return 1.0 - s / (na * nb);
+    }
+    double s = 0.0;
+    for (int32_t t = 0; t < d; ++t) {
+        double df = __dsub_rn(a[t], b[t]);
+        s = __dadd_rn(s, __dmul_rn(df, df));
+    }
+    return metric == TSNE_METRIC_EUCLIDEAN ? sqrt(s) : s;
+}
+
+// One wave per query (WG of 64 threads), bitonic sort of (key(d), j) in LDS.
+template <int CAP>
+__global__ __launch_bounds__(64) void knn_rerank(
+    const double *__restrict__ X, int32_t d, int32_t metric, const double *__restrict__ norm64,
+    int64_t q0, int64_t nq, int32_t kk, const int32_t *__restrict__ cnt,
+    const float *__restrict__ cand_d, const int32_t *__restrict__ cand_j,
+    int32_t *__restrict__ flags, int32_t *__restrict__ out_idx, double *__restrict__ out_dist) {
+    __shared__ uint64_t ks[CAP];
+    __shared__ int32_t js[CAP];
+    __shared__ double ds[CAP];
+    const int lane = threadIdx.x;
+    const int64_t qi = blockIdx.x;
+    if (qi >= nq || flags[qi]) return;
+    const int m = min(cnt[qi], CAP);
+    if (m < kk) { if (lane == 0) flags[qi] = 1; return; }
+    int P = 64;
+    while (P < m) P <<= 1;
+    const int64_t q = q0 + qi;
+    const double *xq = X + q * d;
+    const double nqv = norm64[q];
+    for (int e = lane; e < P; e += 64) {
+        if (e < m) {
+            int32_t j = cand_j[qi * CAP + e];
+            double dv = exact_metric(xq, X + (int64_t)j * d, d, metric, nqv, norm64[j]);
+            ks[e] = dkey(dv);
+            js[e] = j;
+            ds[e] = dv;
+        } else {
+            ks[e] = ~0ull;
+            js[e] = 0x7FFFFFFF;
+            ds[e] = 0.0;
+        }
+    }
+    __syncthreads();
+    for (int size = 2; size <= P; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int e = lane; e < P / 2; e += 64) {
+                int lo = 2 * e - (e & (stride - 1));
+                int hi = lo + stride;
+                bool up = ((lo & size) == 0);
+                uint64_t ka = ks[lo], kb = ks[hi];
+                int32_t ja = js[lo], jb = js[hi];
+                bool gt = (ka > kb) || (ka == kb && ja > jb);
+                if (gt == up) {
+                    ks[lo] = kb; ks[hi] = ka;
+                    js[lo] = jb; js[hi] = ja;
+                    double t = ds[lo]; ds[lo] = ds[hi]; ds[hi] = t;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int t = lane; t < kk; t += 64) {
+        out_idx[qi * kk + t] = js[t];
+        out_dist[qi * kk + t] = ds[t];
+    }
+}
+
+// ------------------------------------------------------------ fallback
+__global__ void fallback_dist(const double *__restrict__ X, int64_t n, int32_t d, int32_t metric,
+                              const double *__restrict__ norm64, int64_t q,
+                              uint64_t *__restrict__ keys, int32_t *__restrict__ vals,
+                              double *__restrict__ dist) {
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    double dv = exact_metric(X + q * d, X + j * d, d, metric, norm64[q], norm64[j]);
+    keys[j] = (j == q) ? ~0ull : dkey(dv);
+    vals[j] = (int32_t)j;
+    dist[j] = dv;
+}
+
+__global__ void fallback_emit(const uint64_t *__restrict__ keys, const int32_t *__restrict__ vals,
+                              const double *__restrict__ dist, int32_t kk,
+                              int32_t *__restrict__ out_idx, double *__restrict__ out_dist) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= kk) return;
+    int32_t j = vals[t];
+    out_idx[t] = j;
+    out_dist[t] = dist[j];
+}
+
+__global__ void fill_i32(int32_t *p, int64_t n, int32_t v) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void fill_f32(float *p, int64_t n, float v) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+template <int CAP>
+void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t kk,
+             int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist) {
+    hipStream_t st = ctx->stream;
+    Workspace &ws = ctx->ws;
+    const int64_t nq = q1 - q0;
+    const int32_t dpad = (int32_t)round_up(d, KC);
+    const int64_t npad = round_up(n, 128);
+
+    // --- prep
+    double *mean = ws.get<double>("knn.mean", d);
+    if (metric != TSNE_METRIC_COSINE) {
+        const int64_t rpb = 2048;
+        const int64_t nb = ceil_div(n, rpb);
+        double *part = ws.get<double>("knn.colpart", (size_t)nb * d);
+        hipLaunchKernelGGL(colsum_partial, dim3(nb), dim3(256), 0, st, dX, n, d, rpb, part);
+        hipLaunchKernelGGL(colsum_final, dim3(ceil_div(d, 256)), dim3(256), 0, st, part, nb, d, n, mean);
+        TSNE_LAUNCH_CHECK();
+    }
+    float *X32 = ws.get<float>("knn.x32", (size_t)npad * dpad);
+    float *norm32 = ws.get<float>("knn.norm32", npad);
+    double *norm64 = ws.get<double>("knn.norm64", npad);
+    unsigned int *nmax_bits = ws.get<unsigned int>("knn.nmax", 1);
+    TSNE_HIP(hipMemsetAsync(nmax_bits, 0, sizeof(unsigned int), st));
+    hipLaunchKernelGGL(prep_rows, dim3(ceil_div(npad, 4)), dim3(256), 0, st, dX, n, d, dpad, npad,
+                       metric, mean, X32, norm32, norm64, nmax_bits);
+    TSNE_LAUNCH_CHECK();
+    unsigned int nmax_h = 0;
+    TSNE_HIP(hipMemcpyAsync(&nmax_h, nmax_bits, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    float nmax;
+    std::memcpy(&nmax, &nmax_h, sizeof(float));
+    // |d32 - d64| <= (K + 8) u (|a|^2 + |b|^2) (see header); use K + 32 for slack.
+    const float delta_coef = (float)((dpad + 32) * 5.9604644775390625e-8);
+    const float dot_scale = metric == TSNE_METRIC_COSINE ? 1.0f : 2.0f;
+
+    // --- per-query state
+    float *tau = ws.get<float>("knn.tau", nq);
+    int32_t *cnt = ws.get<int32_t>("knn.cnt", nq);
+    int32_t *flags = ws.get<int32_t>("knn.flags", nq);
+    float *cand_d = ws.get<float>("knn.cand_d", (size_t)nq * CAP);
+    int32_t *cand_j = ws.get<int32_t>("knn.cand_j", (size_t)nq * CAP);
+    TSNE_HIP(hipMemsetAsync(flags, 0, nq * sizeof(int32_t), st));
+
+    const int64_t qtiles = ceil_div(nq, TQ);
+    // dense first range
+    int64_t s0 = round_up(std::max<int64_t>(kk + 1, 256), TC);
+    s0 = std::min<int64_t>(std::min<int64_t>(s0, CAP), n);
+    hipLaunchKernelGGL(fill_i32, dim3(ceil_div(nq, 256)), dim3(256), 0, st, cnt, nq, (int32_t)s0);
+    hipLaunchKernelGGL(knn_filter<0>, dim3(ceil_div(s0, TC), qtiles), dim3(256), 0, st, X32, norm32,
+                       dpad, q0, q1, (int64_t)0, s0, dot_scale, tau, cnt, cand_d, cand_j, flags,
+                       (int32_t)CAP);
+    TSNE_LAUNCH_CHECK();
+    auto compact = [&]() {
+        hipLaunchKernelGGL(knn_compact<CAP>, dim3(ceil_div(nq, 4)), dim3(256), 0, st, nq, kk, norm32,
+                           q0, nmax, delta_coef, tau, cnt, cand_d, cand_j, flags);
+        TSNE_LAUNCH_CHECK();
+    };
+    compact();
+    int64_t seen = s0;
+    while (seen < n) {
+        int64_t r = std::min<int64_t>(seen, n - seen);
+        hipLaunchKernelGGL(knn_filter<1>, dim3(ceil_div(r, TC), qtiles), dim3(256), 0, st, X32,
+                           norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d,
+                           cand_j, flags, (int32_t)CAP);
+        TSNE_LAUNCH_CHECK();
+        compact();
+        seen += r;
+    }
+    hipLaunchKernelGGL(knn_rerank<CAP>, dim3(nq), dim3(64), 0, st, dX, d, metric, norm64, q0, nq,
+                       kk, cnt, cand_d, cand_j, flags, d_idx, d_dist);
+    TSNE_LAUNCH_CHECK();
+
+    // --- exact fallback for flagged queries
+    std::vector<int32_t> hflags(nq);
+    TSNE_HIP(hipMemcpyAsync(hflags.data(), flags, nq * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    bool any = false;
+    for (int64_t i = 0; i < nq && !any; ++i) any = hflags[i] != 0;
+    if (!any) return;
+    uint64_t *keys = ws.get<uint64_t>("knn.fb_keys", n);
+    uint64_t *keys2 = ws.get<uint64_t>("knn.fb_keys2", n);
+    int32_t *vals = ws.get<int32_t>("knn.fb_vals", n);
+    int32_t *vals2 = ws.get<int32_t>("knn.fb_vals2", n);
+    double *dist = ws.get<double>("knn.fb_dist", n);
+    size_t tmp_bytes = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, keys, keys2, vals, vals2, (int)n, 0, 64, st));
+    void *tmp = ws.get<uint8_t>("knn.fb_tmp", tmp_bytes);
+    for (int64_t i = 0; i < nq; ++i) {
+        if (!hflags[i]) continue;
+        hipLaunchKernelGGL(fallback_dist, dim3(ceil_div(n, 256)), dim3(256), 0, st, dX, n, d, metric,
+                           norm64, q0 + i, keys, vals, dist);
+        TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys2, vals, vals2, (int)n, 0, 64, st));
+        hipLaunchKernelGGL(fallback_emit, dim3(ceil_div(kk, 256)), dim3(256), 0, st, keys2, vals2, dist,
+                           kk, d_idx + i * kk, d_dist + i * kk);
+        TSNE_LAUNCH_CHECK();
+    }
+}
+
+}  // namespace
+
+void knn_device(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t k,
+                int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist) {
+    TSNE_REQUIRE(n >= 2, "kNN needs at least two points");
+    TSNE_REQUIRE(d >= 1, "dimension must be positive");
+    TSNE_REQUIRE(k >= 1, "k must be positive");
+    TSNE_REQUIRE(metric >= 0 && metric <= 2, "unknown metric");
+    TSNE_REQUIRE(q0 >= 0 && q1 <= n && q0 <= q1, "query range out of bounds");
+    TSNE_REQUIRE(n < (int64_t)INT32_MAX, "n must fit int32 point ids");
+    const int32_t kk = (int32_t)std::min<int64_t>(k, n - 1);
+    if (q1 == q0) return;
+    if (4 * kk + 256 <= 1024)
+        knn_run<1024>(ctx, dX, n, d, metric, kk, q0, q1, d_idx, d_dist);
+    else if (4 * kk + 512 <= 4096)
+        knn_run<4096>(ctx, dX, n, d, metric, kk, q0, q1, d_idx, d_dist);
+    else
+        fail(TSNE_ERR_UNSUPPORTED, "k too large (max 896)");
+}
+
+}  // namespace tsne

@@ -1,0 +1,411 @@
+// optimize.hip -- gradient combine, updateEmbedding, centerEmbedding and the
+// device-resident optimize loop (TsneHelpers.scala:221-430) on gfx950.
+//
+// Per global iteration t (1-based, TsneHelpers.scala:403-427 phases):
+//   ex  = earlyExaggeration if t <= min(T,20) + min(T-20, 81) else 1
+//   mom = initialMomentum if t <= min(T,20) else finalMomentum
+//   1. quadtree of the full Y (every rank builds the identical tree)
+//   2. BH repulsion for this rank's slice of the Morton-sorted points
+//   3. [multi-GPU] all-gather of (F, z) slices;  Z = sum z  (TsneHelpers.scala:266)
+//   4. fused kernel per owned row of P: attraction over the CSR row
+//      (q = 1/(1+metric(y_i, y_j)), TsneHelpers.scala:290-302), loss term
+//      every 10th iteration, grad = attr - F/Z (:311-317), gains/momentum/
+//      step (:341-369) -> Ynew
+//   5. [multi-GPU] all-gather of Ynew slices
+//   6. centre: Y = Ynew - mean(Ynew) (:320-329)
+#include "bhtree.hpp"
+
+namespace tsne {
+
+struct OptState {
+    tsne_params p{};
+    int64_t n = 0, chunk = 0, npad = 0, r0 = 0, r1 = 0;
+    const int64_t *row_ptr = nullptr;  // local rows [r0, r1)
+    const int32_t *col = nullptr;
+    const double *val = nullptr;
+    double *Y = nullptr, *upd = nullptr, *gains = nullptr;  // full n x 2
+    double *Ynew = nullptr;   // npad x 2
+    double2 *F = nullptr;     // npad, sorted order
+    double *z = nullptr;      // npad, sorted order
+    double *scal = nullptr;   // [0] Z, [1] loss, [2..3] mean
+    double *part = nullptr;   // reduction partials
+    double *loss = nullptr;   // per loss slot
+    int32_t loss_slots = 0;
+    std::vector<int32_t> loss_written;
+    unsigned long long *visits = nullptr;
+    BHTree tree;
+    bool profile = false;
+    hipEvent_t ev[5] = {};
+    double last_ms[4] = {0, 0, 0, 0};
+    int64_t last_visits = 0;
+};
+
+namespace {
+
+constexpr int NPART = 512;
+
+__device__ __forceinline__ double jmax(double a, double b) {  // java.lang.Math.max
+    if (a != a) return a;
+    if (b != b) return b;
+    return a >= b ? a : b;
+}
+
+__device__ __forceinline__ double metric2(double ax, double ay, double bx, double by, int metric) {
+    if (metric == TSNE_METRIC_COSINE) {
+        const double dt = __dadd_rn(__dmul_rn(ax, bx), __dmul_rn(ay, by));
+        const double na = sqrt(__dadd_rn(__dmul_rn(ax, ax), __dmul_rn(ay, ay)));
+        const double nb = sqrt(__dadd_rn(__dmul_rn(bx, bx), __dmul_rn(by, by)));
+        return 1.0 - dt / (na * nb);
+    }
+    const double dx = __dsub_rn(ax, bx), dy = __dsub_rn(ay, by);
+    const double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+    return metric == TSNE_METRIC_EUCLIDEAN ? sqrt(s) : s;
+}
+
+// Deterministic sum of v[0..n) (stride elements, component c) into part[block].
+__global__ void reduce_partial(const double *__restrict__ v, int64_t n, int stride, int c,
+                               double *__restrict__ part) {
+    __shared__ double sw[4];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        s += v[i * stride + c];
+    s = wave_sum(s);
+    if (lane_id() == 0) sw[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (sw[0] + sw[1]) + (sw[2] + sw[3]);
+}
+
+__global__ void reduce_final(const double *__restrict__ part, int np, double *__restrict__ out,
+                             double scale_div) {
+    __shared__ double sw[4];
+    double s = 0.0;
+    for (int b = threadIdx.x; b < np; b += blockDim.x) s += part[b];
+    s = wave_sum(s);
+    if (lane_id() == 0) sw[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = (sw[0] + sw[1]) + (sw[2] + sw[3]);
+        *out = scale_div > 0.0 ? t / scale_div : t;
+    }
+}
+
+// MODE 0: grad only.  MODE 1: grad + updateEmbedding -> Ynew.
+// 16 lanes per CSR row, 4 rows per wave.
+template <int MODE>
+__global__ __launch_bounds__(256) void attract_kernel(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+    const double *__restrict__ val, int64_t r0, int64_t r1, const double *__restrict__ Y,
+    const int32_t *__restrict__ inv, const double2 *__restrict__ F, const double *__restrict__ scal,
+    int metric, double ex, int want_loss, double *__restrict__ grad, double *__restrict__ Ynew,
+    double *__restrict__ upd, double *__restrict__ gains, double min_gain, double mom, double lr,
+    double *__restrict__ lpart) {
+    __shared__ double sl[4];
+    const int sub = threadIdx.x & 15;
+    const int64_t li = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const int64_t i = r0 + li;
+    const double Z = scal[0];
+    double lsum = 0.0;
+    if (i < r1) {
+        const double yx = Y[2 * i], yy = Y[2 * i + 1];
+        double fx = 0.0, fy = 0.0;
+        const int64_t e1 = row_ptr[li + 1];
+        for (int64_t e = row_ptr[li] + sub; e < e1; e += 16) {
+            const int32_t j = col[e];
+            const double pij = __dmul_rn(val[e], ex);
+            const double jx = Y[2 * (int64_t)j], jy = Y[2 * (int64_t)j + 1];
+            const double q = 1.0 / (1.0 + metric2(yx, yy, jx, jy, metric));
+            const double s = __dmul_rn(pij, q);
+            fx = __dadd_rn(fx, __dmul_rn(s, __dsub_rn(yx, jx)));
+            fy = __dadd_rn(fy, __dmul_rn(s, __dsub_rn(yy, jy)));
+            if (want_loss) lsum += pij * log(pij / (q / Z));
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            fx += __shfl_xor(fx, o, 16);
+            fy += __shfl_xor(fy, o, 16);
+        }
+        if (sub == 0) {
+            const double2 f = F[inv[i]];
+            const double gx = fx - f.x / Z, gy = fy - f.y / Z;  // attrForce - repForce / sumQ
+            if (MODE == 0) {
+                grad[2 * i] = gx;
+                grad[2 * i + 1] = gy;
+            } else {
+                const double g[2] = {gx, gy};
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int64_t o = 2 * i + c;
+                    const double u = upd[o], gn0 = gains[o];
+                    const double gn = ((g[c] > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain)
+                                                                  : jmax(gn0 + 0.2, min_gain);
+                    const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g[c]));
+                    gains[o] = gn;
+                    upd[o] = un;
+                    Ynew[o] = __dadd_rn(un, Y[o]);
+                }
+            }
+        }
+    }
+    if (want_loss) {
+        lsum = wave_sum(lsum);
+        if (lane_id() == 0) sl[threadIdx.x >> 6] = lsum;
+        __syncthreads();
+        if (threadIdx.x == 0) lpart[blockIdx.x] = (sl[0] + sl[1]) + (sl[2] + sl[3]);
+    }
+}
+
+__global__ void center_apply(const double *__restrict__ src, int64_t n, int32_t c,
+                             const double *__restrict__ mean, double *__restrict__ dst) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * c) return;
+    dst[e] = src[e] - mean[e % c];
+}
+
+__global__ void update_kernel(int64_t ne, const double *__restrict__ grad, double *__restrict__ Y,
+                              double *__restrict__ upd, double *__restrict__ gains, double min_gain,
+                              double mom, double lr) {
+    int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= ne) return;
+    const double g = grad[o], u = upd[o], gn0 = gains[o];
+    const double gn = ((g > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain) : jmax(gn0 + 0.2, min_gain);
+    const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g));
+    gains[o] = gn;
+    upd[o] = un;
+    Y[o] = __dadd_rn(un, Y[o]);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// N(0, 1e-4^2) by Box-Muller on a counter-based stream keyed by seed.
+__global__ void init_ws_kernel(int64_t ne, uint64_t seed, double *__restrict__ Y,
+                               double *__restrict__ upd, double *__restrict__ gains) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint64_t a = splitmix64(seed ^ splitmix64(2 * (uint64_t)e));
+    const uint64_t b = splitmix64(seed ^ splitmix64(2 * (uint64_t)e + 1));
+    const double u1 = ((double)(a >> 11) + 1.0) * 0x1.0p-53;
+    const double u2 = (double)(b >> 11) * 0x1.0p-53;
+    Y[e] = 1e-4 * sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+    upd[e] = 0.0;
+    gains[e] = 1.0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ single ops
+
+void update_device(tsne_ctx *ctx, int64_t n, int32_t c, const double *dgrad, double *dY,
+                   double *dupd, double *dgains, double min_gain, double momentum, double lr) {
+    const int64_t ne = n * c;
+    if (ne <= 0) return;
+    hipLaunchKernelGGL(update_kernel, dim3(ceil_div(ne, 256)), dim3(256), 0, ctx->stream, ne, dgrad,
+                       dY, dupd, dgains, min_gain, momentum, lr);
+    TSNE_LAUNCH_CHECK();
+}
+
+void center_device(tsne_ctx *ctx, int64_t n, int32_t c, double *dY) {
+    if (n <= 0) return;
+    TSNE_REQUIRE(c >= 1 && c <= 8, "n_components out of range");
+    double *part = ctx->ws.get<double>("ctr.part", NPART);
+    double *mean = ctx->ws.get<double>("ctr.mean", 8);
+    double *tmp = ctx->ws.get<double>("ctr.tmp", (size_t)n * c);
+    for (int k = 0; k < c; ++k) {
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, ctx->stream, dY, n, c, k, part);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, ctx->stream, part, NPART, mean + k, (double)n);
+    }
+    TSNE_HIP(hipMemcpyAsync(tmp, dY, sizeof(double) * n * c, hipMemcpyDeviceToDevice, ctx->stream));
+    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * c, 256)), dim3(256), 0, ctx->stream, tmp, n, c, mean, dY);
+    TSNE_LAUNCH_CHECK();
+}
+
+void init_working_set_device(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed, double *dY,
+                             double *dupd, double *dgains) {
+    const int64_t ne = n * c;
+    if (ne <= 0) return;
+    hipLaunchKernelGGL(init_ws_kernel, dim3(ceil_div(ne, 256)), dim3(256), 0, ctx->stream, ne, seed, dY,
+                       dupd, dgains);
+    TSNE_LAUNCH_CHECK();
+}
+
+void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
+                     const double *d_P, int64_t n, const double *dY, int32_t metric, double theta,
+                     double exaggeration, double *d_grad, double *h_sumq, double *h_loss) {
+    TSNE_REQUIRE(n >= 1, "empty embedding");
+    hipStream_t st = ctx->stream;
+    BHTree t;
+    bh_alloc(ctx, t, n);
+    bh_build(ctx, t, dY);
+    double2 *F = ctx->ws.get<double2>("grad.F", n);
+    double *z = ctx->ws.get<double>("grad.z", n);
+    double *part = ctx->ws.get<double>("grad.part", NPART);
+    double *scal = ctx->ws.get<double>("grad.scal", 4);
+    bh_repulsion(ctx, t, theta, 0, n, F, z, nullptr);
+    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, z, n, 1, 0, part);
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, part, NPART, scal, 0.0);
+    const int64_t blocks = ceil_div(n * 16, 256);
+    double *lpart = ctx->ws.get<double>("grad.lpart", blocks);
+    const int want_loss = h_loss != nullptr;
+    hipLaunchKernelGGL(attract_kernel<0>, dim3(blocks), dim3(256), 0, st, d_row_ptr, d_col, d_P,
+                       (int64_t)0, n, dY, t.inv, F, scal, metric, exaggeration, want_loss, d_grad,
+                       nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, lpart);
+    TSNE_LAUNCH_CHECK();
+    if (want_loss) hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, lpart, (int)blocks, scal + 1, 0.0);
+    double hs[2] = {0, 0};
+    TSNE_HIP(hipMemcpyAsync(hs, scal, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    if (h_sumq) *h_sumq = hs[0];
+    if (h_loss) *h_loss = hs[1];
+}
+
+// ------------------------------------------------------------ optimizer
+
+void opt_destroy(tsne_ctx *ctx) {
+    if (!ctx->opt) return;
+    for (auto &e : ctx->opt->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete ctx->opt;
+    ctx->opt = nullptr;
+}
+
+void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, const int32_t *d_col,
+               const double *d_P, int64_t n, double *dY, double *dupd, double *dgains) {
+    TSNE_REQUIRE(p != nullptr, "params is NULL");
+    if (p->n_components != 2)
+        fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (Cell.contains requires 2-D points)");
+    TSNE_REQUIRE(n >= 1, "empty embedding");
+    TSNE_REQUIRE(p->metric >= 0 && p->metric <= 2, "unknown metric");
+    opt_destroy(ctx);
+    OptState *s = new OptState();
+    ctx->opt = s;
+    s->p = *p;
+    s->n = n;
+    s->chunk = ceil_div(n, ctx->world);
+    s->npad = s->chunk * ctx->world;
+    s->r0 = std::min<int64_t>(n, s->chunk * ctx->rank);
+    s->r1 = std::min<int64_t>(n, s->r0 + s->chunk);
+    s->row_ptr = d_row_ptr;
+    s->col = d_col;
+    s->val = d_P;
+    s->Y = dY;
+    s->upd = dupd;
+    s->gains = dgains;
+    Workspace &ws = ctx->ws;
+    s->Ynew = ws.get<double>("opt.Ynew", 2 * s->npad);
+    s->F = ws.get<double2>("opt.F", s->npad);
+    s->z = ws.get<double>("opt.z", s->npad);
+    s->scal = ws.get<double>("opt.scal", 8);
+    s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, ceil_div(s->chunk * 16, 256)));
+    s->loss_slots = std::max(1, p->iterations / 10 + 1);
+    s->loss = ws.get<double>("opt.loss", s->loss_slots);
+    s->loss_written.assign(s->loss_slots, 0);
+    s->visits = ws.get<unsigned long long>("opt.visits", 1);
+    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, ctx->stream));
+    TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, ctx->stream));
+    TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, ctx->stream));
+    bh_alloc(ctx, s->tree, n);
+    for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
+}
+
+void opt_step(tsne_ctx *ctx, int32_t t) {
+    OptState *s = ctx->opt;
+    TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    TSNE_REQUIRE(t >= 1, "iteration numbers start at 1");
+    hipStream_t st = ctx->stream;
+    const tsne_params &p = s->p;
+    const int32_t T = p.iterations;
+    const int32_t n1 = std::min(T, 20);
+    const int32_t n2 = std::min(T - n1, 81);
+    const double ex = (t <= n1 + n2) ? p.early_exaggeration : 1.0;
+    const double mom = (t <= n1) ? p.initial_momentum : p.final_momentum;
+    const int want_loss = (t % 10 == 0);
+    const int64_t n = s->n;
+    if (s->profile) {
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, sizeof(unsigned long long), st));
+        TSNE_HIP(hipEventRecord(s->ev[0], st));
+    }
+    // 1. tree
+    bh_build(ctx, s->tree, s->Y);
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
+    // 2. repulsion for this rank's slice of sorted points
+    bh_repulsion(ctx, s->tree, p.theta, s->r0, s->r1, s->F, s->z, s->profile ? s->visits : nullptr);
+    // 3. exchange + Z
+    if (ctx->world > 1) {
+        comm_allgather_bytes(ctx, s->F + s->r0, s->F, sizeof(double2) * s->chunk);
+        comm_allgather_bytes(ctx, s->z + s->r0, s->z, sizeof(double) * s->chunk);
+    }
+    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
+    // 4. attraction + update for owned rows
+    const int64_t rows = s->r1 - s->r0;
+    const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * 16, 256));
+    hipLaunchKernelGGL(attract_kernel<1>, dim3(blocks), dim3(256), 0, st, s->row_ptr, s->col, s->val,
+                       s->r0, s->r1, s->Y, s->tree.inv, s->F, s->scal, p.metric, ex, want_loss,
+                       nullptr, s->Ynew, s->upd, s->gains, p.min_gain, mom, p.learning_rate, s->part);
+    TSNE_LAUNCH_CHECK();
+    if (want_loss) {
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, (int)blocks, s->scal + 1, 0.0);
+        if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
+        const int slot = t / 10 - 1;
+        if (slot >= 0 && slot < s->loss_slots) {
+            TSNE_HIP(hipMemcpyAsync(s->loss + slot, s->scal + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
+            s->loss_written[slot] = t;
+        }
+    }
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
+    // 5. exchange + 6. centre
+    if (ctx->world > 1) comm_allgather_bytes(ctx, s->Ynew + 2 * s->r0, s->Ynew, sizeof(double) * 2 * s->chunk);
+    for (int k = 0; k < 2; ++k) {
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 2, k, s->part);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
+    }
+    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 2, 256)), dim3(256), 0, st, s->Ynew, n, 2, s->scal + 2, s->Y);
+    TSNE_LAUNCH_CHECK();
+    if (s->profile) {
+        TSNE_HIP(hipEventRecord(s->ev[4], st));
+        TSNE_HIP(hipEventSynchronize(s->ev[4]));
+        for (int k = 0; k < 4; ++k) {
+            float ms = 0.f;
+            TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+            s->last_ms[k] = ms;
+        }
+        unsigned long long v = 0;
+        TSNE_HIP(hipMemcpy(&v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
+        s->last_visits = (int64_t)v;
+    }
+}
+
+int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap) {
+    OptState *s = ctx->opt;
+    TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    std::vector<double> h(s->loss_slots);
+    TSNE_HIP(hipMemcpyAsync(h.data(), s->loss, sizeof(double) * s->loss_slots, hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    int32_t k = 0;
+    for (int32_t i = 0; i < s->loss_slots; ++i) {
+        if (!s->loss_written[i]) continue;
+        if (k < cap) {
+            if (keys) keys[k] = s->loss_written[i];
+            if (vals) vals[k] = h[i];
+        }
+        ++k;
+    }
+    return k;
+}
+
+void opt_profile(tsne_ctx *ctx, int enable, double *ms4, int64_t *visits) {
+    OptState *s = ctx->opt;
+    TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    if (enable >= 0) s->profile = enable != 0;
+    if (ms4)
+        for (int k = 0; k < 4; ++k) ms4[k] = s->last_ms[k];
+    if (visits) *visits = s->last_visits;
+}
+
+}  // namespace tsne

@@ -1,0 +1,196 @@
+"""Host-side operators mirroring TsneHelpers (TsneHelpers.scala), over the C ABI.
+
+Arguments are numpy arrays (host) or torch CUDA tensors (device API).  Names
+and argument meaning follow the reference's Scala methods.
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import METRICS, UNIQUE_ID_BYTES, Params, check, lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):       # torch tensor (device API)
+        return C.c_void_p(a.data_ptr())
+    return C.c_void_p(a.ctypes.data)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def default_params(**kw):
+    p = Params()
+    lib().tsne_params_default(C.byref(p))
+    for k, v in kw.items():
+        if k == "metric" and isinstance(v, str):
+            v = METRICS[v]
+        setattr(p, k, v)
+    return p
+
+
+class Context:
+    """One tsne_ctx (one GPU, optionally one rank of an RCCL communicator)."""
+
+    def __init__(self, device=0):
+        self._h = C.c_void_p()
+        check(lib().tsne_ctx_create(device, C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            lib().tsne_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- multi-GPU
+    @staticmethod
+    def unique_id():
+        buf = C.create_string_buffer(UNIQUE_ID_BYTES)
+        check(lib().tsne_comm_unique_id(buf))
+        return buf.raw
+
+    def init_comm(self, rank, world, uid):
+        check(lib().tsne_ctx_init_comm(self._h, rank, world, uid))
+
+    def set_stream(self, stream_ptr):
+        check(lib().tsne_ctx_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def synchronize(self):
+        check(lib().tsne_ctx_synchronize(self._h))
+
+    # ---- host operators (TsneHelpers names)
+    def kNearestNeighbors(self, X, k, metric="sqeuclidean", q0=0, q1=None):
+        """TsneHelpers.scala:41-59 -> (idx[nq, kk] int32, dist[nq, kk] f64)."""
+        X = _f64(X)
+        n, d = X.shape
+        q1 = n if q1 is None else q1
+        kk = min(k, n - 1)
+        idx = np.zeros((q1 - q0, kk), dtype=np.int32)
+        dist = np.zeros((q1 - q0, kk), dtype=np.float64)
+        check(lib().tsne_knn(self._h, _ptr(X), n, d, METRICS[metric], k, q0, q1, _ptr(idx), _ptr(dist)))
+        return idx, dist
+
+    def pairwiseAffinities(self, row_ptr, dist, perplexity):
+        """TsneHelpers.scala:162-180 on CSR rows of distances."""
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        dist = _f64(dist).ravel()
+        p = np.zeros_like(dist)
+        check(lib().tsne_pairwise_affinities(self._h, _ptr(row_ptr), _ptr(dist), len(row_ptr) - 1,
+                                             perplexity, _ptr(p)))
+        return p
+
+    def jointDistribution(self, row_ptr, col, p, n):
+        """TsneHelpers.scala:182-196 -> symmetric CSR (rows sorted by column)."""
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        p = _f64(p)
+        cap = 2 * len(col) + 1
+        orp = np.zeros(n + 1, dtype=np.int64)
+        oc = np.zeros(cap, dtype=np.int32)
+        ov = np.zeros(cap, dtype=np.float64)
+        nnz = C.c_int64()
+        check(lib().tsne_joint_distribution(self._h, _ptr(row_ptr), _ptr(col), _ptr(p), n, cap,
+                                            _ptr(orp), _ptr(oc), _ptr(ov), C.byref(nnz)))
+        return orp, oc[:nnz.value].copy(), ov[:nnz.value].copy()
+
+    def gradient(self, row_ptr, col, P, Y, theta, metric="sqeuclidean", exaggeration=1.0,
+                 want_loss=False):
+        """TsneHelpers.scala:221-318 -> (grad[n,2], Z, loss or None)."""
+        Y = _f64(Y)
+        n = Y.shape[0]
+        grad = np.zeros((n, 2))
+        z = C.c_double()
+        loss = C.c_double()
+        check(lib().tsne_gradient(self._h, _ptr(np.ascontiguousarray(row_ptr, np.int64)),
+                                  _ptr(np.ascontiguousarray(col, np.int32)), _ptr(_f64(P)), n,
+                                  _ptr(Y), METRICS[metric], theta, exaggeration, _ptr(grad),
+                                  C.byref(z), C.byref(loss) if want_loss else None))
+        return grad, z.value, (loss.value if want_loss else None)
+
+    def updateEmbedding(self, grad, Y, upd, gains, min_gain, momentum, learning_rate):
+        """TsneHelpers.scala:341-369, in place on Y / upd / gains."""
+        n, c = Y.shape
+        g = _f64(grad)
+        for a in (Y, upd, gains):
+            assert a.dtype == np.float64 and a.flags.c_contiguous
+        check(lib().tsne_update_embedding(self._h, n, c, _ptr(g), _ptr(Y), _ptr(upd), _ptr(gains),
+                                          min_gain, momentum, learning_rate))
+
+    def centerEmbedding(self, Y):
+        """TsneHelpers.scala:320-329, in place."""
+        assert Y.dtype == np.float64 and Y.flags.c_contiguous
+        n, c = Y.shape
+        check(lib().tsne_center_embedding(self._h, n, c, _ptr(Y)))
+
+    def initWorkingSet(self, n, n_components=2, seed=0):
+        """TsneHelpers.scala:198-219 (seeded) -> (Y, upd, gains)."""
+        Y = np.zeros((n, n_components))
+        upd = np.zeros_like(Y)
+        gains = np.zeros_like(Y)
+        check(lib().tsne_init_working_set(self._h, n, n_components, seed, _ptr(Y), _ptr(upd), _ptr(gains)))
+        return Y, upd, gains
+
+    def optimize(self, row_ptr, col, P, Y, upd, gains, params):
+        """TsneHelpers.scala:396-430, in place; returns {iteration: loss}."""
+        n = Y.shape[0]
+        cap = params.iterations // 10 + 1
+        keys = np.zeros(cap, dtype=np.int32)
+        vals = np.zeros(cap)
+        nl = C.c_int32()
+        check(lib().tsne_optimize(self._h, C.byref(params), _ptr(np.ascontiguousarray(row_ptr, np.int64)),
+                                  _ptr(np.ascontiguousarray(col, np.int32)), _ptr(_f64(P)), n, _ptr(Y),
+                                  _ptr(upd), _ptr(gains), _ptr(keys), _ptr(vals), cap, C.byref(nl)))
+        return dict(zip(keys[:nl.value].tolist(), vals[:nl.value].tolist()))
+
+    # ---- device operators (torch CUDA tensors)
+    def dev_knn(self, dX, k, metric, q0, q1, d_idx, d_dist):
+        n, d = dX.shape
+        check(lib().tsne_dev_knn(self._h, _ptr(dX), n, d, METRICS[metric], k, q0, q1, _ptr(d_idx), _ptr(d_dist)))
+
+    def dev_affinities(self, d_row_ptr, d_dist, nrows, perplexity, d_p):
+        check(lib().tsne_dev_pairwise_affinities(self._h, _ptr(d_row_ptr), _ptr(d_dist), nrows, perplexity, _ptr(d_p)))
+
+    def dev_joint(self, d_row_ptr, d_col, d_p, n, cap, d_orp, d_oc, d_ov):
+        nnz = C.c_int64()
+        check(lib().tsne_dev_joint_distribution(self._h, _ptr(d_row_ptr), _ptr(d_col), _ptr(d_p), n, cap,
+                                                _ptr(d_orp), _ptr(d_oc), _ptr(d_ov), C.byref(nnz)))
+        return nnz.value
+
+    def dev_opt_setup(self, params, d_row_ptr, d_col, d_P, n, dY, dupd, dgains):
+        check(lib().tsne_dev_opt_setup(self._h, C.byref(params), _ptr(d_row_ptr), _ptr(d_col), _ptr(d_P), n,
+                                       _ptr(dY), _ptr(dupd), _ptr(dgains)))
+
+    def dev_opt_step(self, t):
+        check(lib().tsne_dev_opt_step(self._h, t))
+
+    def dev_opt_losses(self, cap=1024):
+        keys = np.zeros(cap, dtype=np.int32)
+        vals = np.zeros(cap)
+        nl = C.c_int32()
+        check(lib().tsne_dev_opt_losses(self._h, _ptr(keys), _ptr(vals), cap, C.byref(nl)))
+        k = min(nl.value, cap)
+        return dict(zip(keys[:k].tolist(), vals[:k].tolist()))
+
+    def dev_opt_profile(self, enable=-1):
+        ms = np.zeros(4)
+        visits = C.c_int64()
+        check(lib().tsne_dev_opt_profile(self._h, enable, _ptr(ms), C.byref(visits)))
+        return ms, visits.value
