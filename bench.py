@@ -1,0 +1,260 @@
+"""bench.py -- t-SNE hot path on MI355X (BASELINE.json configs[2]: 1M x 128 GMM,
+sqeuclidean, k = 90, perplexity 30, theta 0.5, 1000 Barnes-Hut iterations).
+
+One "step" = one optimizer iteration (tree build + BH repulsion + attraction +
+fused gains/momentum update + centring) of the device-resident loop, with the
+embedding, P and all state resident in HBM.  Setup (synthetic data, kNN,
+affinities, symmetrisation, seeded init) runs first and is timed separately:
+kNN points/s is reported beside the main metric.  `value` = iterations/s of
+the whole job (all ranks together; rows of P and BH queries are sharded, so
+N GPUs share one 1M-point problem: strong scaling).
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; the
+library's own RCCL communicator carries the per-iteration all-gathers;
+torch.distributed is only used for the one-time id exchange / kNN graph
+gather and the barriers around the timed region.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "tsne-flink_amd"))
+sys.path.insert(0, str(ROOT / "tests"))
+
+import tsne_amd as T  # noqa: E402
+from tsne_amd.api import default_params  # noqa: E402
+
+METRIC = "t-SNE iterations/sec + end-to-end sec at N=1M×128 on 1/2/4/8 MI355X; kNN pts/s"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed optimizer iterations")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed iterations before the timed ones")
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--k", type=int, default=90)
+    ap.add_argument("--perplexity", type=float, default=30.0)
+    ap.add_argument("--theta", type=float, default=0.5)
+    ap.add_argument("--iterations", type=int, default=1000, help="schedule length T")
+    ap.add_argument("--start", type=int, default=1, help="first iteration index t of the warmup")
+    ap.add_argument("--full", action="store_true", help="also run all T iterations end to end")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="queries in the CPU baseline sample")
+    return ap.parse_args()
+
+
+def gmm(n, d, seed, device):
+    """C3 generator: 10 centres ~ N(0, 5^2 I), within-blob N(0, I), fp32-rounded."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    centers = torch.randn(10, d, generator=g, device=device, dtype=torch.float64) * 5.0
+    lab = torch.randint(0, 10, (n,), generator=g, device=device)
+    X = centers[lab] + torch.randn(n, d, generator=g, device=device, dtype=torch.float64)
+    return X.float().double().contiguous()
+
+
+def sync_barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    ctx = T.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    if world > 1:
+        obj = [T.Context.unique_id() if rank == 0 else None]
+        torch.distributed.broadcast_object_list(obj, src=0)
+        ctx.init_comm(rank, world, obj[0])
+    n, d, k = a.n, a.dim, a.k
+    kk = min(k, n - 1)
+    r0, r1 = T.shard_rows(n, world, rank)
+
+    # ---------------------------------------------------------- setup stages
+    X = gmm(n, d, 2, dev)
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    idx = torch.empty((r1 - r0, kk), dtype=torch.int32, device=dev)
+    dist = torch.empty((r1 - r0, kk), dtype=torch.float64, device=dev)
+    ctx.dev_knn(X, k, "sqeuclidean", r0, r1, idx, dist)
+    sync_barrier(world)
+    t_knn = max_over_ranks(time.perf_counter() - t0, world)
+
+    t0 = time.perf_counter()
+    rp_local = torch.arange(0, (r1 - r0) * kk + 1, kk, dtype=torch.int64, device=dev)
+    p = torch.empty_like(dist)
+    ctx.dev_affinities(rp_local, dist, r1 - r0, a.perplexity, p)
+    if world > 1:   # full conditional graph on every rank for the symmetrisation
+        chunk = -(-n // world)
+        pad = chunk - (r1 - r0)
+        gi = torch.nn.functional.pad(idx, (0, 0, 0, pad)).contiguous()
+        gp = torch.nn.functional.pad(p, (0, 0, 0, pad)).contiguous()
+        all_i = torch.empty((world * chunk, kk), dtype=torch.int32, device=dev)
+        all_p = torch.empty((world * chunk, kk), dtype=torch.float64, device=dev)
+        torch.distributed.all_gather_into_tensor(all_i, gi)
+        torch.distributed.all_gather_into_tensor(all_p, gp)
+        idx_full, p_full = all_i[:n].contiguous(), all_p[:n].contiguous()
+    else:
+        idx_full, p_full = idx, p
+    rp_full = torch.arange(0, n * kk + 1, kk, dtype=torch.int64, device=dev)
+    cap = 2 * n * kk
+    orp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    oc = torch.empty(cap, dtype=torch.int32, device=dev)
+    ov = torch.empty(cap, dtype=torch.float64, device=dev)
+    nnz = ctx.dev_joint(rp_full, idx_full, p_full, n, cap, orp, oc, ov)
+    # this rank's rows of P, rebased
+    lrp = (orp[r0:r1 + 1] - orp[r0]).contiguous()
+    e0, e1 = int(orp[r0].item()), int(orp[r1].item())
+    lcol, lval = oc[e0:e1].contiguous(), ov[e0:e1].contiguous()
+    sync_barrier(world)
+    t_aff = max_over_ranks(time.perf_counter() - t0, world)
+    del X, dist, p
+
+    chunk = -(-n // world)
+    Y = torch.zeros((chunk * world, 2), dtype=torch.float64, device=dev)
+    upd = torch.zeros_like(Y)
+    gains = torch.ones_like(Y)
+    Yh, uh, gh = ctx.initWorkingSet(n, 2, seed=0)
+    Y[:n].copy_(torch.from_numpy(Yh))
+    params = default_params(iterations=a.iterations, theta=a.theta)
+    ctx.dev_opt_setup(params, lrp, lcol, lval, n, Y, upd, gains)
+
+    # ------------------------------------------------------- optimizer steps
+    t = a.start
+    ctx.dev_opt_profile(1)
+    prof = []
+    for _ in range(a.warmup):
+        ctx.dev_opt_step(t)
+        t += 1
+    ctx.dev_opt_profile(0)
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.dev_opt_step(t)
+        t += 1
+    sync_barrier(world)
+    t_steps = max_over_ranks(time.perf_counter() - t0, world)
+    # one more profiled step (not in the timed region) for the per-stage split
+    ctx.dev_opt_profile(1)
+    ctx.dev_opt_step(t)
+    ms, visits = ctx.dev_opt_profile(-1)
+    t += 1
+    ctx.dev_opt_profile(0)
+    t_done = t
+
+    full = None
+    if a.full:
+        sync_barrier(world)
+        t0 = time.perf_counter()
+        while t <= a.iterations:
+            ctx.dev_opt_step(t)
+            t += 1
+        sync_barrier(world)
+        full = max_over_ranks(time.perf_counter() - t0, world)
+
+    ms_per_step = 1e3 * t_steps / a.steps
+    value = a.steps / t_steps
+    # roofline of the attraction + update kernel (HBM bound), from the profiled step:
+    # bytes = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr + rows*(16 own Y + 16 gathered Y_j once
+    #         + 16 F + 4 inv + 16 upd r + 16 upd w + 16 gains r + 16 gains w + 16 Ynew w)
+    rows = r1 - r0
+    lnnz = e1 - e0
+    attr_bytes = lnnz * 12 + (rows + 1) * 8 + rows * (16 * 8 + 4)
+    attr_ms = ms[3]
+    attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms > 0 else None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)",
+        "config": {"workload": f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, "
+                               f"theta {a.theta}, schedule T={a.iterations}; timed iterations "
+                               f"t={a.start + a.warmup}..{a.start + a.warmup + a.steps - 1}",
+                   "n": n, "dim": d, "k": k, "theta": a.theta, "parallelism": f"rows{world}",
+                   "nnz_P": int(nnz)},
+        "knn_pts_per_s": n / t_knn,
+        "knn_s": t_knn,
+        "affinities_joint_s": t_aff,
+        "stage_ms_last_step": {"tree": ms[0], "bh": ms[1], "exchange_z": ms[2],
+                               "attract_update": ms[3], "centre": ms[4], "t": t_done - 1},
+        "bh_interactions_per_s": visits / (ms[1] * 1e-3) if ms[1] > 0 else None,
+        "roofline": {"kernel": "attract_kernel<1> (attraction + gains/momentum update)",
+                     "bound": "hbm", "achieved": attr_gbs, "peak": 8000.0, "unit": "GB/s",
+                     "frac": (attr_gbs / 8000.0) if attr_gbs else None, "traffic": None,
+                     "bytes_per_launch": attr_bytes},
+    }
+    if full is not None:
+        out["full_run_s"] = full
+        out["full_run_iterations"] = a.iterations - t_done + 1
+
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ctx, Y[:n], a, n)
+    if rank == 0:
+        print(json.dumps(out))
+    ctx.close()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(ctx, Ydev, a, n):
+    """The oracle (C fp64 restatement of the reference, OpenMP) on a bounded
+    sample of the same state: tree build of all n points + BH repulsion for
+    `cpu_sample` queries, extrapolated to one full iteration."""
+    import oracle_ctypes as O
+    threads = min(16, os.cpu_count() or 1)
+    Y = Ydev.detach().cpu().numpy().copy()
+    q = min(a.cpu_sample, n)
+    sel = np.random.default_rng(0).choice(n, q, replace=False)
+    # the oracle repulsion takes a contiguous query range: permute the sample first
+    perm = np.concatenate([sel, np.setdiff1d(np.arange(n), sel)])
+    Yp = np.ascontiguousarray(Y[perm])
+    t0 = time.perf_counter()
+    O.repulsion(Yp, a.theta, 0, q, threads=threads)
+    t_sample = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    O.repulsion(Yp, a.theta, 0, 1, threads=1)   # tree build + 1 query
+    t_build = time.perf_counter() - t0
+    per_query = max(t_sample - t_build, 1e-9) / q
+    t_iter = t_build + per_query * n
+    return {"value": 1.0 / t_iter, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (C fp64 reference restatement) quadtree build of all {n} points + "
+                      f"BH repulsion of {q} random queries at the GPU's post-timing state, "
+                      f"extrapolated linearly to {n} queries (attraction excluded)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -168,10 +168,12 @@ int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *
 int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t);
 int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap,
                         int32_t *n_loss);
-/* Per-kernel timing of the last step (HIP events on the ctx stream), in ms:
- * [0] tree build, [1] BH repulsion, [2] attraction+update, [3] centre/exchange.
- * Also the number of BH node visits of the last step (device counter). */
-int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out4, int64_t *visits_out);
+/* Per-stage timing of the last step (HIP events on the ctx stream), in ms:
+ * [0] tree build, [1] BH repulsion kernel, [2] (F, z) exchange + Z reduce,
+ * [3] attraction + update kernel, [4] loss, embedding exchange, centring.
+ * Also the number of BH node evaluations (lane visits) of the last step.
+ * enable: 1 on, 0 off, -1 leave unchanged. */
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *visits_out);
 
 #ifdef __cplusplus
 }

@@ -35,8 +35,8 @@ struct OptState {
     unsigned long long *visits = nullptr;
     BHTree tree;
     bool profile = false;
-    hipEvent_t ev[5] = {};
-    double last_ms[4] = {0, 0, 0, 0};
+    hipEvent_t ev[6] = {};
+    double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits = 0;
 };
 
@@ -334,6 +334,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's slice of sorted points
     bh_repulsion(ctx, s->tree, p.theta, s->r0, s->r1, s->F, s->z, s->profile ? s->visits : nullptr);
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. exchange + Z
     if (ctx->world > 1) {
         comm_allgather_bytes(ctx, s->F + s->r0, s->F, sizeof(double2) * s->chunk);
@@ -341,7 +342,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     }
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
-    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 4. attraction + update for owned rows
     const int64_t rows = s->r1 - s->r0;
     const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * 16, 256));
@@ -349,6 +350,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
                        s->r0, s->r1, s->Y, s->tree.inv, s->F, s->scal, p.metric, ex, want_loss,
                        nullptr, s->Ynew, s->upd, s->gains, p.min_gain, mom, p.learning_rate, s->part);
     TSNE_LAUNCH_CHECK();
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     if (want_loss) {
         hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, (int)blocks, s->scal + 1, 0.0);
         if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
@@ -358,7 +360,6 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
             s->loss_written[slot] = t;
         }
     }
-    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 5. exchange + 6. centre
     if (ctx->world > 1) comm_allgather_bytes(ctx, s->Ynew + 2 * s->r0, s->Ynew, sizeof(double) * 2 * s->chunk);
     for (int k = 0; k < 2; ++k) {
@@ -368,9 +369,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 2, 256)), dim3(256), 0, st, s->Ynew, n, 2, s->scal + 2, s->Y);
     TSNE_LAUNCH_CHECK();
     if (s->profile) {
-        TSNE_HIP(hipEventRecord(s->ev[4], st));
-        TSNE_HIP(hipEventSynchronize(s->ev[4]));
-        for (int k = 0; k < 4; ++k) {
+        TSNE_HIP(hipEventRecord(s->ev[5], st));
+        TSNE_HIP(hipEventSynchronize(s->ev[5]));
+        for (int k = 0; k < 5; ++k) {
             float ms = 0.f;
             TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
@@ -399,12 +400,12 @@ int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap) {
     return k;
 }
 
-void opt_profile(tsne_ctx *ctx, int enable, double *ms4, int64_t *visits) {
+void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits) {
     OptState *s = ctx->opt;
     TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
     if (enable >= 0) s->profile = enable != 0;
-    if (ms4)
-        for (int k = 0; k < 4; ++k) ms4[k] = s->last_ms[k];
+    if (ms5)
+        for (int k = 0; k < 5; ++k) ms5[k] = s->last_ms[k];
     if (visits) *visits = s->last_visits;
 }
 

@@ -1,0 +1,242 @@
+// tsne_helpers.cpp -- C++ host mirror of TsneHelpers over libtsne_hip.
+#include "tsne_helpers.hpp"
+
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace tsne_flink {
+
+void check(int status) {
+    if (status == TSNE_OK) return;
+    std::string msg = tsne_last_error();
+    if (status == TSNE_ERR_ARG) throw std::invalid_argument(msg);
+    throw std::runtime_error("libtsne_hip status " + std::to_string(status) + ": " + msg);
+}
+
+int32_t getMetric(const std::string &name) {
+    int32_t m = 0;
+    check(tsne_metric_from_name(name.c_str(), &m));
+    return m;
+}
+
+TsneHelpers::TsneHelpers(int device) { check(tsne_ctx_create(device, &ctx_)); }
+TsneHelpers::~TsneHelpers() { tsne_ctx_destroy(ctx_); }
+
+Csr toCsr(const std::vector<Triple> &t, const std::vector<int32_t> *idsIn) {
+    Csr c;
+    if (idsIn) {
+        c.ids = *idsIn;
+    } else {
+        c.ids.reserve(2 * t.size());
+        for (const auto &e : t) { c.ids.push_back(e.i); c.ids.push_back(e.j); }
+        std::sort(c.ids.begin(), c.ids.end());
+        c.ids.erase(std::unique(c.ids.begin(), c.ids.end()), c.ids.end());
+    }
+    auto dense = [&](int32_t id) {
+        auto it = std::lower_bound(c.ids.begin(), c.ids.end(), id);
+        if (it == c.ids.end() || *it != id) throw std::invalid_argument("unknown point id " + std::to_string(id));
+        return (int32_t)(it - c.ids.begin());
+    };
+    const size_t n = c.ids.size();
+    std::vector<std::pair<int32_t, size_t>> order(t.size());
+    for (size_t e = 0; e < t.size(); ++e) order[e] = {dense(t[e].i), e};
+    std::stable_sort(order.begin(), order.end(),
+                     [](const auto &a, const auto &b) { return a.first < b.first; });
+    c.row_ptr.assign(n + 1, 0);
+    c.col.resize(t.size());
+    c.val.resize(t.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+        const Triple &e = t[order[k].second];
+        c.row_ptr[order[k].first + 1]++;
+        c.col[k] = dense(e.j);
+        c.val[k] = e.v;
+    }
+    for (size_t i = 0; i < n; ++i) c.row_ptr[i + 1] += c.row_ptr[i];
+    return c;
+}
+
+std::vector<Triple> TsneHelpers::kNearestNeighbors(const Vectors &input, int32_t k, int32_t metric) {
+    if (input.size() < 2) return {};
+    const int64_t n = (int64_t)input.size();
+    const int32_t d = (int32_t)input[0].second.size();
+    std::vector<size_t> order(input.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return input[a].first < input[b].first; });
+    std::vector<double> X((size_t)n * d);
+    std::vector<int32_t> ids(n);
+    for (int64_t r = 0; r < n; ++r) {
+        const auto &v = input[order[r]];
+        if ((int32_t)v.second.size() != d) throw std::invalid_argument("vectors of different lengths");
+        ids[r] = v.first;
+        std::memcpy(&X[(size_t)r * d], v.second.data(), sizeof(double) * d);
+    }
+    const int64_t kk = std::min<int64_t>(k, n - 1);
+    std::vector<int32_t> idx((size_t)(n * kk));
+    std::vector<double> dist((size_t)(n * kk));
+    check(tsne_knn(ctx_, X.data(), n, d, metric, k, 0, n, idx.data(), dist.data()));
+    std::vector<Triple> out;
+    out.reserve(idx.size());
+    for (int64_t r = 0; r < n; ++r)
+        for (int64_t t = 0; t < kk; ++t)
+            out.push_back({ids[r], ids[idx[(size_t)(r * kk + t)]], dist[(size_t)(r * kk + t)]});
+    return out;
+}
+
+std::vector<Triple> TsneHelpers::partitionKnn(const Vectors &input, int32_t k, int32_t metric, int32_t) {
+    return kNearestNeighbors(input, k, metric);
+}
+
+std::vector<Triple> TsneHelpers::pairwiseAffinities(const std::vector<Triple> &knn, double perplexity) {
+    Csr c = toCsr(knn);
+    std::vector<double> p(c.val.size());
+    check(tsne_pairwise_affinities(ctx_, c.row_ptr.data(), c.val.data(), (int64_t)c.ids.size(), perplexity,
+                                   p.data()));
+    std::vector<Triple> out;
+    out.reserve(p.size());
+    for (size_t i = 0; i + 1 < c.row_ptr.size(); ++i)
+        for (int64_t e = c.row_ptr[i]; e < c.row_ptr[i + 1]; ++e)
+            out.push_back({c.ids[i], c.ids[c.col[e]], p[e]});
+    return out;
+}
+
+std::vector<Triple> TsneHelpers::jointDistribution(const std::vector<Triple> &aff) {
+    Csr c = toCsr(aff);
+    const int64_t n = (int64_t)c.ids.size();
+    const int64_t cap = 2 * (int64_t)c.val.size() + 1;
+    std::vector<int64_t> orp(n + 1);
+    std::vector<int32_t> oc(cap);
+    std::vector<double> ov(cap);
+    int64_t nnz = 0;
+    check(tsne_joint_distribution(ctx_, c.row_ptr.data(), c.col.data(), c.val.data(), n, cap, orp.data(),
+                                  oc.data(), ov.data(), &nnz));
+    std::vector<Triple> out;
+    out.reserve(nnz);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t e = orp[i]; e < orp[i + 1]; ++e) out.push_back({c.ids[i], c.ids[oc[e]], ov[e]});
+    return out;
+}
+
+WorkingSet TsneHelpers::initWorkingSet(const std::vector<int32_t> &ids, int32_t nComponents,
+                                       int64_t randomState) {
+    WorkingSet w;
+    w.ids = ids;
+    std::sort(w.ids.begin(), w.ids.end());
+    w.n_components = nComponents;
+    const size_t ne = w.ids.size() * (size_t)nComponents;
+    w.y.resize(ne);
+    w.upd.resize(ne);
+    w.gains.resize(ne);
+    check(tsne_init_working_set(ctx_, (int64_t)w.ids.size(), nComponents, (uint64_t)randomState, w.y.data(),
+                                w.upd.data(), w.gains.data()));
+    return w;
+}
+
+std::vector<std::pair<int32_t, std::vector<double>>> TsneHelpers::gradient(const std::vector<Triple> &P,
+                                                                         const WorkingSet &ws, int32_t metric,
+                                                                         double theta, double exaggeration) {
+    if (ws.n_components != 2) check(TSNE_ERR_UNSUPPORTED);
+    Csr c = toCsr(P, &ws.ids);
+    const int64_t n = (int64_t)ws.ids.size();
+    std::vector<double> g((size_t)n * 2);
+    check(tsne_gradient(ctx_, c.row_ptr.data(), c.col.data(), c.val.data(), n, ws.y.data(), metric, theta,
+                        exaggeration, g.data(), nullptr, nullptr));
+    std::vector<std::pair<int32_t, std::vector<double>>> out;
+    for (int64_t i = 0; i < n; ++i) out.push_back({ws.ids[i], {g[2 * i], g[2 * i + 1]}});
+    return out;
+}
+
+void TsneHelpers::updateEmbedding(const std::vector<double> &grad, WorkingSet &ws, double minGain, double momentum,
+                                  double learningRate) {
+    check(tsne_update_embedding(ctx_, (int64_t)ws.ids.size(), ws.n_components, grad.data(), ws.y.data(),
+                                ws.upd.data(), ws.gains.data(), minGain, momentum, learningRate));
+}
+
+void TsneHelpers::centerEmbedding(WorkingSet &ws) {
+    check(tsne_center_embedding(ctx_, (int64_t)ws.ids.size(), ws.n_components, ws.y.data()));
+}
+
+void TsneHelpers::optimize(const std::vector<Triple> &P, WorkingSet &ws, double learningRate, int32_t iterations,
+                           int32_t metric, double earlyExaggeration, double initialMomentum, double finalMomentum,
+                           double theta, std::map<int32_t, double> *loss) {
+    Csr c = toCsr(P, &ws.ids);
+    tsne_params p;
+    tsne_params_default(&p);
+    p.n_components = ws.n_components;
+    p.metric = metric;
+    p.learning_rate = learningRate;
+    p.iterations = iterations;
+    p.early_exaggeration = earlyExaggeration;
+    p.initial_momentum = initialMomentum;
+    p.final_momentum = finalMomentum;
+    p.theta = theta;
+    const int32_t cap = iterations / 10 + 1;
+    std::vector<int32_t> keys(cap);
+    std::vector<double> vals(cap);
+    int32_t nl = 0;
+    check(tsne_optimize(ctx_, &p, c.row_ptr.data(), c.col.data(), c.val.data(), (int64_t)ws.ids.size(),
+                        ws.y.data(), ws.upd.data(), ws.gains.data(), keys.data(), vals.data(), cap, &nl));
+    if (loss)
+        for (int32_t k = 0; k < std::min(nl, cap); ++k) (*loss)[keys[k]] += vals[k];
+}
+
+// java.lang.Double.toString: shortest round-trip digits; plain notation for
+// 1e-3 <= |v| < 1e7 (at least one fractional digit), else d.dddE<exp>.
+std::string javaDouble(double v) {
+    if (std::isnan(v)) return "NaN";
+    if (std::isinf(v)) return v > 0 ? "Infinity" : "-Infinity";
+    if (v == 0.0) return std::signbit(v) ? "-0.0" : "0.0";
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);
+    std::string s(buf, r.ptr);
+    // s = [-]d[.ddd]e[+-]XX
+    bool neg = s[0] == '-';
+    if (neg) s.erase(0, 1);
+    size_t epos = s.find('e');
+    int exp = std::stoi(s.substr(epos + 1));
+    std::string mant = s.substr(0, epos);
+    std::string digits;
+    for (char ch : mant)
+        if (ch != '.') digits.push_back(ch);
+    std::string out;
+    const double a = std::fabs(v);
+    if (a >= 1e-3 && a < 1e7) {
+        int point = exp + 1;  // digits before the decimal point
+        if (point <= 0) {
+            out = "0." + std::string(-point, '0') + digits;
+        } else if (point >= (int)digits.size()) {
+            out = digits + std::string(point - digits.size(), '0') + ".0";
+        } else {
+            out = digits.substr(0, point) + "." + digits.substr(point);
+        }
+    } else {
+        out = digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(exp);
+    }
+    return (neg ? "-" : "") + out;
+}
+
+// java.util.HashMap<Integer, Double>.toString: "{k=v, k=v}" in bucket order
+// (capacity 16 doubling at load factor 0.75; Integer hash h ^ (h >>> 16)).
+std::string javaHashMapString(const std::map<int32_t, double> &m) {
+    size_t cap = 16;
+    while ((double)m.size() > 0.75 * (double)cap) cap <<= 1;
+    std::vector<std::pair<uint32_t, int32_t>> order;
+    size_t ins = 0;
+    std::vector<std::pair<std::pair<uint32_t, size_t>, int32_t>> keyed;
+    for (const auto &kv : m) {  // insertion order = ascending iteration (keys accumulate in order)
+        uint32_t h = (uint32_t)kv.first;
+        h ^= (h >> 16);
+        keyed.push_back({{h & (uint32_t)(cap - 1), ins++}, kv.first});
+    }
+    std::sort(keyed.begin(), keyed.end());
+    std::string s = "{";
+    for (size_t i = 0; i < keyed.size(); ++i) {
+        if (i) s += ", ";
+        s += std::to_string(keyed[i].second) + "=" + javaDouble(m.at(keyed[i].second));
+    }
+    return s + "}";
+}
+
+}  // namespace tsne_flink

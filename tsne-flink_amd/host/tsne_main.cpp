@@ -1,0 +1,200 @@
+// tsne_main.cpp -- native CLI with the exact flags and file formats of the
+// reference's Tsne.main (Tsne.scala:33-168), running the hot path through
+// libtsne_hip on one GPU.  For benchmarking on a box without a JVM/Flink.
+//
+//   tsne_hip --input X.csv --output Y.csv --dimension D --knnMethod bruteforce
+//            [--metric sqeuclidean] [--perplexity 30] [--nComponents 2]
+//            [--earlyExaggeration 4] [--learningRate 1000] [--iterations 300]
+//            [--randomState 0] [--neighbors 3*perplexity] [--initialMomentum 0.5]
+//            [--finalMomentum 0.8] [--theta 0.25] [--loss loss.txt | --lossFile loss.txt]
+//            [--knnIterations 3] [--knnBlocks P] [--inputDistanceMatrix] [--executionPlan]
+//            [--device 0]
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "tsne_helpers.hpp"
+
+using namespace tsne_flink;
+
+namespace {
+
+// org.apache.flink.api.java.utils.ParameterTool.fromArgs: --key value | --flag
+struct Params {
+    std::map<std::string, std::string> kv;
+    static Params fromArgs(int argc, char **argv) {
+        Params p;
+        for (int i = 1; i < argc; ++i) {
+            std::string a = argv[i];
+            if (a.rfind("--", 0) != 0 && a.rfind("-", 0) != 0)
+                throw std::invalid_argument("Error parsing arguments '" + a + "'");
+            std::string key = a.substr(a.rfind("--", 0) == 0 ? 2 : 1);
+            if (i + 1 < argc && std::strncmp(argv[i + 1], "--", 2) != 0) p.kv[key] = argv[++i];
+            else p.kv[key] = "__NO_VALUE_KEY";
+        }
+        return p;
+    }
+    bool has(const std::string &k) const { return kv.count(k) > 0; }
+    std::string getRequired(const std::string &k) const {
+        auto it = kv.find(k);
+        if (it == kv.end() || it->second == "__NO_VALUE_KEY")
+            throw std::runtime_error("No data for required key '" + k + "'");
+        return it->second;
+    }
+    std::string get(const std::string &k, const std::string &def) const {
+        auto it = kv.find(k);
+        return it == kv.end() ? def : it->second;
+    }
+    double getDouble(const std::string &k, double def) const { return has(k) ? std::stod(getRequired(k)) : def; }
+    // the reference reads these with getLong; accept "4" and (unlike Flink) "4.0"
+    long getLong(const std::string &k, long def) const { return has(k) ? (long)std::stod(getRequired(k)) : def; }
+};
+
+// Tsne.readInput (Tsne.scala:138-153): COO "i,j,v" lines -> dense vectors.
+Vectors readInput(const std::string &path, int dimension) {
+    std::ifstream f(path);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    std::unordered_map<int32_t, size_t> slot;
+    Vectors out;
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty()) continue;
+        const char *s = line.c_str();
+        char *e;
+        long i = std::strtol(s, &e, 10);
+        if (*e != ',') throw std::runtime_error("bad line: " + line);
+        long j = std::strtol(e + 1, &e, 10);
+        if (*e != ',') throw std::runtime_error("bad line: " + line);
+        double v = std::strtod(e + 1, &e);
+        if (j < 0 || j >= dimension) throw std::out_of_range("index " + std::to_string(j) + " out of dimension");
+        auto it = slot.find((int32_t)i);
+        if (it == slot.end()) {
+            it = slot.emplace((int32_t)i, out.size()).first;
+            out.push_back({(int32_t)i, std::vector<double>(dimension, 0.0)});
+        }
+        out[it->second].second[j] += v;  // VectorBuilder.add accumulates
+    }
+    return out;
+}
+
+// Tsne.readDistanceMatrix (Tsne.scala:155-159): raw (i, j, d) triples.
+std::vector<Triple> readDistanceMatrix(const std::string &path) {
+    std::ifstream f(path);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    std::vector<Triple> out;
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty()) continue;
+        const char *s = line.c_str();
+        char *e;
+        long i = std::strtol(s, &e, 10);
+        long j = std::strtol(e + 1, &e, 10);
+        double v = std::strtod(e + 1, &e);
+        out.push_back({(int32_t)i, (int32_t)j, v});
+    }
+    return out;
+}
+
+double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    try {
+        Params parameters = Params::fromArgs(argc, argv);
+        const bool getExecutionPlan = parameters.has("executionPlan");
+        const bool inputDistanceMatrix = parameters.has("inputDistanceMatrix");
+        const std::string inputPath = parameters.getRequired("input");
+        const std::string outputPath = parameters.getRequired("output");
+        const int inputDimension = std::stoi(parameters.getRequired("dimension"));
+        const std::string metricName = parameters.get("metric", "sqeuclidean");
+        const double perplexity = parameters.getDouble("perplexity", 30.0);
+        const long nComponents = parameters.getLong("nComponents", 2);
+        const double earlyExaggeration = (double)parameters.getLong("earlyExaggeration", 4);
+        const double learningRate = parameters.getDouble("learningRate", 1000);
+        const long iterations = parameters.getLong("iterations", 300);
+        const long randomState = parameters.getLong("randomState", 0);
+        const long neighbors = parameters.getLong("neighbors", 3 * (long)perplexity);
+        const double initialMomentum = parameters.getDouble("initialMomentum", 0.5);
+        const double finalMomentum = parameters.getDouble("finalMomentum", 0.8);
+        const double theta = parameters.getDouble("theta", 0.25);
+        // the code reads "loss" (Tsne.scala:60); README.md:36 documents "lossFile": accept both
+        const std::string lossFile = parameters.get("loss", parameters.get("lossFile", "loss.txt"));
+        const std::string knnMethod = parameters.getRequired("knnMethod");
+        const int device = (int)parameters.getLong("device", 0);
+        (void)parameters.getLong("knnIterations", 3);
+        (void)parameters.getLong("knnBlocks", 1);
+
+        if (getExecutionPlan) {  // Tsne.scala:89-95: write the plan instead of executing
+            std::ofstream pw("tsne_executionPlan.json");
+            pw << "{\"nodes\":[{\"id\":1,\"type\":\"source\",\"contents\":\"" << inputPath << "\"},"
+               << "{\"id\":2,\"type\":\"knn\",\"contents\":\"" << (inputDistanceMatrix ? "distance-matrix" : knnMethod)
+               << " (libtsne_hip)\"},{\"id\":3,\"type\":\"pairwiseAffinities\"},{\"id\":4,\"type\":\"jointDistribution\"},"
+               << "{\"id\":5,\"type\":\"optimize\",\"iterations\":" << iterations << "},"
+               << "{\"id\":6,\"type\":\"sink\",\"contents\":\"" << outputPath << "\"}]}\n";
+            return 0;
+        }
+
+        const int32_t metric = getMetric(metricName);  // IllegalArgumentException before any work
+        TsneHelpers h(device);
+        double t0 = now();
+        std::vector<Triple> knn;
+        if (inputDistanceMatrix) {
+            knn = readDistanceMatrix(inputPath);
+        } else {
+            Vectors input = readInput(inputPath, inputDimension);
+            double t1 = now();
+            std::fprintf(stderr, "[tsne_hip] read %zu points in %.3f s\n", input.size(), t1 - t0);
+            if (knnMethod == "bruteforce") knn = h.kNearestNeighbors(input, (int32_t)neighbors, metric);
+            else if (knnMethod == "partition") knn = h.partitionKnn(input, (int32_t)neighbors, metric, 1);
+            else if (knnMethod == "project")
+                throw std::invalid_argument("Knn method 'project' (approximate Z-order kNN) is not part of this build");
+            else throw std::invalid_argument("Knn method '" + metricName + "' not defined");  // Tsne.scala:78
+            std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", now() - t1);
+        }
+        double t2 = now();
+        std::vector<Triple> pw = h.pairwiseAffinities(knn, perplexity);
+        std::vector<Triple> joint = h.jointDistribution(pw);
+        std::vector<int32_t> ids;
+        for (const auto &e : joint) ids.push_back(e.i);
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %zu)\n", now() - t2, joint.size());
+        WorkingSet ws = h.initWorkingSet(ids, (int32_t)nComponents, randomState);
+        std::map<int32_t, double> loss;
+        double t3 = now();
+        h.optimize(joint, ws, learningRate, (int32_t)iterations, metric, earlyExaggeration, initialMomentum,
+                   finalMomentum, theta, &loss);
+        std::fprintf(stderr, "[tsne_hip] %ld iterations in %.3f s\n", iterations, now() - t3);
+
+        {   // result.map(x => (x._1, x._2(0), x._2(1))).writeAsCsv (Tsne.scala:86)
+            FILE *f = std::fopen(outputPath.c_str(), "w");
+            if (!f) throw std::runtime_error("cannot write " + outputPath);
+            for (size_t r = 0; r < ws.ids.size(); ++r)
+                std::fprintf(f, "%d,%s,%s\n", ws.ids[r], javaDouble(ws.y[2 * r]).c_str(),
+                             javaDouble(ws.y[2 * r + 1]).c_str());
+            std::fclose(f);
+        }
+        std::ofstream lf(lossFile);  // Tsne.scala:99-101
+        lf << javaHashMapString(loss);
+        std::fprintf(stderr, "[tsne_hip] end-to-end %.3f s\n", now() - t0);
+        return 0;
+    } catch (const std::invalid_argument &e) {
+        std::fprintf(stderr, "java.lang.IllegalArgumentException: %s\n", e.what());
+        return 2;
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+}

@@ -190,7 +190,7 @@ class Context:
         return dict(zip(keys[:k].tolist(), vals[:k].tolist()))
 
     def dev_opt_profile(self, enable=-1):
-        ms = np.zeros(4)
+        ms = np.zeros(5)
         visits = C.c_int64()
         check(lib().tsne_dev_opt_profile(self._h, enable, _ptr(ms), C.byref(visits)))
         return ms, visits.value
