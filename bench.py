@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--iterations", type=int, default=1000, help="schedule length T")
     ap.add_argument("--start", type=int, default=1, help="first iteration index t of the warmup")
     ap.add_argument("--full", action="store_true", help="also run all T iterations end to end")
+    ap.add_argument("--trace", type=int, default=0, help="with --full: profile every N-th iteration")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=256, help="queries in the CPU baseline sample")
     return ap.parse_args()
@@ -168,11 +169,26 @@ def main():
     t_done = t
 
     full = None
+    timeline = []
     if a.full:
         sync_barrier(world)
         t0 = time.perf_counter()
+        tl_last = t0
         while t <= a.iterations:
+            traced = a.trace and t % a.trace == 0
+            if traced:
+                ctx.dev_opt_profile(1)
             ctx.dev_opt_step(t)
+            if traced:
+                ms_t, vis_t = ctx.dev_opt_profile(0)
+                ext = (Y[:n].max(0).values - Y[:n].min(0).values).max().item()
+                now = time.perf_counter()
+                timeline.append({"t": t, "extent": ext, "bh_ms": round(ms_t[1], 3),
+                                 "tree_ms": round(ms_t[0], 3), "attr_ms": round(ms_t[3], 3),
+                                 "visits_per_point": vis_t / max(1, r1 - r0),
+                                 "wall_s": round(now - t0, 3)})
+                if rank == 0:
+                    print(json.dumps(timeline[-1]), file=sys.stderr, flush=True)
             t += 1
         sync_barrier(world)
         full = max_over_ranks(time.perf_counter() - t0, world)
@@ -220,6 +236,9 @@ def main():
     if full is not None:
         out["full_run_s"] = full
         out["full_run_iterations"] = a.iterations - t_done + 1
+        out["end_to_end_s_estimate"] = t_knn + t_aff + full + t_steps
+        if timeline:
+            out["timeline"] = timeline
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, Y[:n], a, n)

@@ -456,3 +456,52 @@ int oracle_optimize(const int64_t *row_ptr, const int32_t *col, const double *va
     free(grad);
     return 0;
 }
+
+/* ------------------------------------------------ sharded-path helpers */
+
+/* Repulsion of an arbitrary query list against the tree of all n points. */
+int oracle_repulsion_queries(const double *Y, int64_t n, double theta, const double *Q, int64_t nq,
+                             double *rep, double *zi, int threads) {
+    if (!Y || n < 1 || nq < 0) return -1;
+    qtree_t t;
+    build_tree(&t, Y, n);
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+#endif
+    for (int64_t i = 0; i < nq; ++i) {
+        double fx, fy, s;
+        int64_t v = 0;
+        qt_repulsive(&t, 0, Q[2 * i], Q[2 * i + 1], theta, &fx, &fy, &s, &v);
+        rep[2 * i] = fx; rep[2 * i + 1] = fy; zi[i] = s;
+    }
+    free(t.v);
+    return 0;
+}
+
+/* Attraction + combine for rows [r0, r1) given the full repulsion and Z
+ * (TsneHelpers.scala:269-317).  grad is (r1-r0) x 2; loss (nullable) is the
+ * partial KL sum of these rows. */
+int oracle_attraction_rows(const int64_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                           const double *Y, int metric, double exaggeration, const double *rep,
+                           double Z, int64_t r0, int64_t r1, double *grad, double *loss) {
+    if (!row_ptr || !Y || r0 < 0 || r1 > n || r0 > r1) return -1;
+    double l = 0.0;
+    for (int64_t i = r0; i < r1; ++i) {
+        double gx = 0.0, gy = 0.0;
+        const double *yi = Y + 2 * i;
+        for (int64_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+            const double *yj = Y + 2 * (int64_t)col[e];
+            double pij = val[e] * exaggeration;
+            double qij = 1.0 / (1.0 + oracle_metric(yi, yj, 2, metric));
+            double s = pij * qij;
+            gx = gx + s * (yi[0] - yj[0]);
+            gy = gy + s * (yi[1] - yj[1]);
+            if (loss) l += pij * log(pij / (qij / Z));
+        }
+        grad[2 * (i - r0)] = gx - rep[2 * i] / Z;
+        grad[2 * (i - r0) + 1] = gy - rep[2 * i + 1] / Z;
+    }
+    if (loss) *loss = l;
+    return 0;
+}

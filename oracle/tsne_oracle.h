@@ -75,6 +75,15 @@ int oracle_gradient(const int64_t *row_ptr, const int32_t *col, const double *va
 int oracle_repulsion(const double *Y, int64_t n, double theta, int64_t q0, int64_t q1,
                      double *rep, double *zi, int threads);
 
+/* Repulsion of an arbitrary query list Q (nq x 2) against the tree of Y. */
+int oracle_repulsion_queries(const double *Y, int64_t n, double theta, const double *Q, int64_t nq,
+                             double *rep, double *zi, int threads);
+
+/* Attraction + combine for rows [r0, r1) given full rep (n x 2) and Z. */
+int oracle_attraction_rows(const int64_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                           const double *Y, int metric, double exaggeration, const double *rep,
+                           double Z, int64_t r0, int64_t r1, double *grad, double *loss);
+
 /* updateEmbedding (TsneHelpers.scala:341-369), in place. */
 int oracle_update(int64_t n, int32_t c, const double *grad, double *Y, double *upd,
                   double *gains, double min_gain, double momentum, double lr);

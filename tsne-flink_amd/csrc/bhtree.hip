@@ -161,6 +161,8 @@ __global__ void karras_build(const uint64_t *__restrict__ k, int64_t n, const in
     nodes[i].left = left;
     nodes[i].right = right;
     nodes[i].delta = dnode;
+    nodes[i].first = lo;
+    nodes[i].last = hi;
     if (i == 0) parent_node[0] = -1;
 }
 
@@ -183,8 +185,25 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
         const int32_t l = nodes[p].left, r = nodes[p].right, dl = nodes[p].delta;
         double2 ls, rs;
         int lc, rc;
-        if (l < 0) { ls = pos[~l]; lc = 1; } else { ls = sums[l]; lc = nodes[l].cnt; }
-        if (r < 0) { rs = pos[~r]; rc = 1; } else { rs = sums[r]; rc = nodes[r].cnt; }
+        double lx0, lx1, ly0, ly1, lh, rx0, rx1, ry0, ry1, rh;
+        if (l < 0) {
+            ls = pos[~l]; lc = 1;
+            lx0 = lx1 = ls.x; ly0 = ly1 = ls.y; lh = __builtin_inf();
+        } else {
+            ls = sums[l]; lc = nodes[l].cnt;
+            lx0 = nodes[l].bx0; lx1 = nodes[l].bx1; ly0 = nodes[l].by0; ly1 = nodes[l].by1; lh = nodes[l].hmin;
+        }
+        if (r < 0) {
+            rs = pos[~r]; rc = 1;
+            rx0 = rx1 = rs.x; ry0 = ry1 = rs.y; rh = __builtin_inf();
+        } else {
+            rs = sums[r]; rc = nodes[r].cnt;
+            rx0 = nodes[r].bx0; rx1 = nodes[r].bx1; ry0 = nodes[r].by0; ry1 = nodes[r].by1; rh = nodes[r].hmin;
+        }
+        nodes[p].bx0 = fmin(lx0, rx0);
+        nodes[p].bx1 = fmax(lx1, rx1);
+        nodes[p].by0 = fmin(ly0, ry0);
+        nodes[p].by1 = fmax(ly1, ry1);
         const int cnt = lc + rc;
         const double sx = ls.x + rs.x, sy = ls.y + rs.y;
         const int par = parent_node[p];
@@ -197,7 +216,9 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
         nodes[p].cx = sx / (double)cnt;                  // centerOfMass = sum / cumSize
         nodes[p].cy = sy / (double)cnt;
         nodes[p].cnt = cnt;
-        nodes[p].h = real ? ldexp(W, -dlev) : 0.0;
+        const double h = real ? ldexp(W, -dlev) : -1.0;  // -1 = transparent
+        nodes[p].h = h;
+        nodes[p].hmin = fmin(real ? h : __builtin_inf(), fmin(lh, rh));
         p = par;
     }
 }
@@ -207,9 +228,33 @@ __global__ void set_root(int32_t *meta) {
     meta[1] = (m >= 2) ? 0 : (m == 1 ? ~0 : INT32_MIN);
 }
 
+// Direct interaction of one lane's query with one leaf point (QuadTree.scala:
+// 128-142 at a leaf: cumSize 1, com = the point; zero if equal to the query).
+__device__ __forceinline__ void leaf_force(double qx, double qy, double px, double py, double &fx,
+                                           double &fy, double &zs) {
+    if (px == qx && py == qy) return;
+    const double dx = qx - px, dy = qy - py;
+    const double D = __fma_rn(dx, dx, dy * dy);
+    const double x = 1.0 + D;
+    double r = __builtin_amdgcn_rcp(x);          // v_rcp_f64 + two Newton steps
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    const double sc = r * r;
+    fx = __fma_rn(sc, dx, fx);
+    fy = __fma_rn(sc, dy, fy);
+    zs += r;
+}
+
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
 // (node, lane mask).  Every lane takes exactly its own reference decision;
-// the wave visits the union of the lanes' opened nodes.
+// the wave visits the union of the lanes' opened nodes.  Fast path: if for a
+// lane EVERY real cell of a subtree would be opened (the largest squared
+// distance from the query to the subtree's bounding box is below
+// hmin/theta, with a rounding margin), the reference would reach every leaf
+// of that subtree, so the lane sums the subtree's leaves directly -- a dense
+// N-body tile over a contiguous range of sorted points, with no criterion
+// evaluations and no stack traffic.  That is the near-exact regime of a
+// small embedding.
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
     const int32_t *__restrict__ meta, double theta, int64_t s0, int64_t s1,
@@ -221,8 +266,10 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const bool valid = s < s1;
     if (__ballot(valid) == 0) return;
     const int root = meta[1];
+    const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
+    const double qmag = fabs(qx) + fabs(qy);
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0;
     int sp = 0;
@@ -235,49 +282,71 @@ __global__ __launch_bounds__(256) void bh_traverse(
         --sp;
         const int ref = __builtin_amdgcn_readfirstlane(sref[w][sp]);
         const uint64_t msk = smask[w][sp];
-        const bool act = (msk >> lane) & 1ull;
+        bool act = (msk >> lane) & 1ull;
         if (ref < 0) {
             const double2 p = pos[~ref];
             if (act) {
                 ++nvis;
-                if (!(p.x == qx && p.y == qy)) {
-                    const double dx = __dsub_rn(qx, p.x), dy = __dsub_rn(qy, p.y);
-                    const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-                    const double Q = 1.0 / (1.0 + D);
-                    const double sc = __dmul_rn(Q, Q);
-                    fx = __dadd_rn(fx, __dmul_rn(sc, dx));
-                    fy = __dadd_rn(fy, __dmul_rn(sc, dy));
-                    zs = __dadd_rn(zs, Q);
+                leaf_force(qx, qy, p.x, p.y, fx, fy, zs);
+            }
+            continue;
+        }
+        const BHNode nd = nodes[ref];
+        // all-open test (per lane) -> direct tile over the subtree's leaves
+        bool tile = false;
+        if (act) {
+            const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+            const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+            const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+            const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
+            tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12);
+        }
+        const uint64_t tm = __ballot(tile);
+        if (tm) {
+            const int a = nd.first, b = nd.last;
+            if (tile) nvis += (unsigned long long)(b - a + 1);
+            int p = a;
+            for (; p + 3 <= b; p += 4) {
+                const double2 p0 = pos[p], p1 = pos[p + 1], p2 = pos[p + 2], p3 = pos[p + 3];
+                if (tile) {
+                    leaf_force(qx, qy, p0.x, p0.y, fx, fy, zs);
+                    leaf_force(qx, qy, p1.x, p1.y, fx, fy, zs);
+                    leaf_force(qx, qy, p2.x, p2.y, fx, fy, zs);
+                    leaf_force(qx, qy, p3.x, p3.y, fx, fy, zs);
                 }
             }
-        } else {
-            const BHNode nd = nodes[ref];
-            bool open = false;
-            if (nd.h == 0.0) {
-                open = act;
-            } else if (act) {
-                ++nvis;
-                const double dx = __dsub_rn(qx, nd.cx), dy = __dsub_rn(qy, nd.cy);
-                const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-                if (nd.h / D < theta) {
-                    const double Q = 1.0 / (1.0 + D);
-                    const double mult = __dmul_rn((double)nd.cnt, Q);
-                    const double sc = __dmul_rn(mult, Q);
-                    fx = __dadd_rn(fx, __dmul_rn(sc, dx));
-                    fy = __dadd_rn(fy, __dmul_rn(sc, dy));
-                    zs = __dadd_rn(zs, mult);
-                } else {
-                    open = true;
-                }
+            for (; p <= b; ++p) {
+                const double2 p0 = pos[p];
+                if (tile) leaf_force(qx, qy, p0.x, p0.y, fx, fy, zs);
             }
-            const uint64_t om = __ballot(open);
-            if (om) {
-                if (lane == 0) {
-                    sref[w][sp] = nd.right; smask[w][sp] = om;
-                    sref[w][sp + 1] = nd.left; smask[w][sp + 1] = om;
-                }
-                sp += 2;
+            act = act && !tile;
+        }
+        if (__ballot(act) == 0) continue;
+        bool open = false;
+        if (nd.h < 0.0) {
+            open = act;                       // transparent: split inside a quad level
+        } else if (act) {
+            ++nvis;
+            const double dx = __dsub_rn(qx, nd.cx), dy = __dsub_rn(qy, nd.cy);
+            const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+            if (nd.h / D < theta) {           // max(hHeigth, hWidth) / D < theta
+                const double Q = 1.0 / (1.0 + D);
+                const double mult = __dmul_rn((double)nd.cnt, Q);
+                const double sc = __dmul_rn(mult, Q);
+                fx = __dadd_rn(fx, __dmul_rn(sc, dx));
+                fy = __dadd_rn(fy, __dmul_rn(sc, dy));
+                zs = __dadd_rn(zs, mult);
+            } else {
+                open = true;
             }
+        }
+        const uint64_t om = __ballot(open);
+        if (om) {
+            if (lane == 0) {
+                sref[w][sp] = nd.right; smask[w][sp] = om;
+                sref[w][sp + 1] = nd.left; smask[w][sp + 1] = om;
+            }
+            sp += 2;
         }
     }
     if (valid) {

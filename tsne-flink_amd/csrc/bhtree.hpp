@@ -11,10 +11,14 @@ namespace tsne {
 struct __attribute__((aligned(16))) BHNode {
     double cx, cy;    // centre of mass (sum / count)
     double h;         // half width of the quad cell, 0 = transparent
+    double hmin;      // min h over the real internal nodes of this subtree (+inf if none)
+    double bx0, bx1, by0, by1;  // bounding box of the subtree's points
     int32_t cnt;      // cumSize
     int32_t left;     // child refs: >= 0 internal node, < 0 leaf ~ref
     int32_t right;
     int32_t delta;    // common-prefix length in bits (62+ = key tie)
+    int32_t first, last;  // leaf range [first, last] in sorted order
+    int32_t pad0, pad1;
 };
 
 struct BHTree {
