@@ -1,18 +1,22 @@
 """bench.py -- t-SNE hot path on MI355X (BASELINE.json configs[2]: 1M x 128 GMM,
 sqeuclidean, k = 90, perplexity 30, theta 0.5, 1000 Barnes-Hut iterations).
 
-One "step" = one optimizer iteration (tree build + BH repulsion + attraction +
-fused gains/momentum update + centring) of the device-resident loop, with the
-embedding, P and all state resident in HBM.  Setup (synthetic data, kNN,
-affinities, symmetrisation, seeded init) runs first and is timed separately:
-kNN points/s is reported beside the main metric.  `value` = iterations/s of
-the whole job (all ranks together; rows of P and BH queries are sharded, so
-N GPUs share one 1M-point problem: strong scaling).
+One "step" = one optimizer iteration t of the reference schedule (tree build +
+BH repulsion + attraction + fused gains/momentum update + centring) of the
+device-resident loop; the embedding, P and all state stay in HBM.  By default
+the timed steps are the WHOLE schedule t = 1..T (T = 1000): per-iteration cost
+varies by >1000x over a run (near-exact O(N^2) BH while the embedding is tiny,
+~2 node visits per point once it has expanded: SURVEY.md section 8a row A15),
+so `value` = T / (time of the full loop) is the honest iterations/s.  Warmup
+iterations run on a snapshot of the initial state, which is restored before
+timing.  Setup (synthetic data, kNN, affinities, symmetrisation, seeded init)
+is timed separately; kNN points/s and end-to-end seconds are reported beside.
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; the
 library's own RCCL communicator carries the per-iteration all-gathers;
-torch.distributed is only used for the one-time id exchange / kNN graph
-gather and the barriers around the timed region.
+torch.distributed is used only for the one-time id exchange / kNN graph
+gather and for the barriers around the timed region.  Rows of P and BH
+queries are sharded, so N GPUs share one problem (strong scaling).
 """
 import argparse
 import json
@@ -32,24 +36,24 @@ import tsne_amd as T  # noqa: E402
 from tsne_amd.api import default_params  # noqa: E402
 
 METRIC = "t-SNE iterations/sec + end-to-end sec at N=1M×128 on 1/2/4/8 MI355X; kNN pts/s"
+FP32_MFMA_PEAK_TF = 157.3
+HBM_PEAK_GBS = 8000.0
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed optimizer iterations")
-    ap.add_argument("--warmup", type=int, default=5, help="untimed iterations before the timed ones")
+    ap.add_argument("--steps", type=int, default=0, help="timed iterations (0 = the whole schedule T)")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed iterations on a restored snapshot")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=90)
     ap.add_argument("--perplexity", type=float, default=30.0)
     ap.add_argument("--theta", type=float, default=0.5)
     ap.add_argument("--iterations", type=int, default=1000, help="schedule length T")
-    ap.add_argument("--start", type=int, default=1, help="first iteration index t of the warmup")
-    ap.add_argument("--full", action="store_true", help="also run all T iterations end to end")
-    ap.add_argument("--trace", type=int, default=0, help="with --full: profile every N-th iteration")
+    ap.add_argument("--trace", type=int, default=50, help="profile every N-th timed iteration (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=256, help="queries in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
     return ap.parse_args()
 
 
@@ -95,6 +99,7 @@ def main():
     n, d, k = a.n, a.dim, a.k
     kk = min(k, n - 1)
     r0, r1 = T.shard_rows(n, world, rank)
+    steps = a.steps if a.steps > 0 else a.iterations
 
     # ---------------------------------------------------------- setup stages
     X = gmm(n, d, 2, dev)
@@ -110,8 +115,8 @@ def main():
     rp_local = torch.arange(0, (r1 - r0) * kk + 1, kk, dtype=torch.int64, device=dev)
     p = torch.empty_like(dist)
     ctx.dev_affinities(rp_local, dist, r1 - r0, a.perplexity, p)
+    chunk = -(-n // world)
     if world > 1:   # full conditional graph on every rank for the symmetrisation
-        chunk = -(-n // world)
         pad = chunk - (r1 - r0)
         gi = torch.nn.functional.pad(idx, (0, 0, 0, pad)).contiguous()
         gp = torch.nn.functional.pad(p, (0, 0, 0, pad)).contiguous()
@@ -128,120 +133,93 @@ def main():
     oc = torch.empty(cap, dtype=torch.int32, device=dev)
     ov = torch.empty(cap, dtype=torch.float64, device=dev)
     nnz = ctx.dev_joint(rp_full, idx_full, p_full, n, cap, orp, oc, ov)
-    # this rank's rows of P, rebased
-    lrp = (orp[r0:r1 + 1] - orp[r0]).contiguous()
-    e0, e1 = int(orp[r0].item()), int(orp[r1].item())
-    lcol, lval = oc[e0:e1].contiguous(), ov[e0:e1].contiguous()
+    e0, e1 = int(orp[r0].item()), int(orp[r1].item())      # this rank's rows of P
     sync_barrier(world)
     t_aff = max_over_ranks(time.perf_counter() - t0, world)
     del X, dist, p
 
-    chunk = -(-n // world)
-    Y = torch.zeros((chunk * world, 2), dtype=torch.float64, device=dev)
+    Y = torch.zeros((n, 2), dtype=torch.float64, device=dev)
     upd = torch.zeros_like(Y)
     gains = torch.ones_like(Y)
-    Yh, uh, gh = ctx.initWorkingSet(n, 2, seed=0)
+    Yh, _, _ = ctx.initWorkingSet(n, 2, seed=0)
     Y[:n].copy_(torch.from_numpy(Yh))
+    snap = (Y.clone(), upd.clone(), gains.clone())
     params = default_params(iterations=a.iterations, theta=a.theta)
-    ctx.dev_opt_setup(params, lrp, lcol, lval, n, Y, upd, gains)
+    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)
 
-    # ------------------------------------------------------- optimizer steps
-    t = a.start
-    ctx.dev_opt_profile(1)
-    prof = []
-    for _ in range(a.warmup):
+    # ----------------------------------------------- warmup on a snapshot
+    for t in range(1, a.warmup + 1):
         ctx.dev_opt_step(t)
-        t += 1
-    ctx.dev_opt_profile(0)
+    torch.cuda.synchronize()
+    Y.copy_(snap[0]); upd.copy_(snap[1]); gains.copy_(snap[2])
+    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)   # fresh loss slots
+
+    # ------------------------------------------------------- timed steps
+    timeline = []
+    snap_at = {1, max(1, steps // 10), max(1, steps // 5), max(1, 2 * steps // 5), steps}
+    snaps = {}
     sync_barrier(world)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for t in range(1, steps + 1):
+        traced = a.trace and (t % a.trace == 0 or t == 1)
+        if traced:
+            ctx.dev_opt_profile(1)
         ctx.dev_opt_step(t)
-        t += 1
+        if traced:
+            ms_t, vis_t = ctx.dev_opt_profile(0)
+            timeline.append({"t": t, "tree_ms": ms_t[0], "bh_ms": ms_t[1], "exchange_ms": ms_t[2],
+                             "attract_ms": ms_t[3], "centre_ms": ms_t[4],
+                             "visits_per_point": vis_t / max(1, r1 - r0),
+                             "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
+        if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
+            snaps[t] = Y[:n].cpu().numpy().copy()
     sync_barrier(world)
-    t_steps = max_over_ranks(time.perf_counter() - t0, world)
-    # one more profiled step (not in the timed region) for the per-stage split
-    ctx.dev_opt_profile(1)
-    ctx.dev_opt_step(t)
-    ms, visits = ctx.dev_opt_profile(-1)
-    t += 1
-    ctx.dev_opt_profile(0)
-    t_done = t
+    t_loop = max_over_ranks(time.perf_counter() - t0, world)
+    losses = ctx.dev_opt_losses()
 
-    full = None
-    timeline = []
-    if a.full:
-        sync_barrier(world)
-        t0 = time.perf_counter()
-        tl_last = t0
-        while t <= a.iterations:
-            traced = a.trace and t % a.trace == 0
-            if traced:
-                ctx.dev_opt_profile(1)
-            ctx.dev_opt_step(t)
-            if traced:
-                ms_t, vis_t = ctx.dev_opt_profile(0)
-                ext = (Y[:n].max(0).values - Y[:n].min(0).values).max().item()
-                now = time.perf_counter()
-                timeline.append({"t": t, "extent": ext, "bh_ms": round(ms_t[1], 3),
-                                 "tree_ms": round(ms_t[0], 3), "attr_ms": round(ms_t[3], 3),
-                                 "visits_per_point": vis_t / max(1, r1 - r0),
-                                 "wall_s": round(now - t0, 3)})
-                if rank == 0:
-                    print(json.dumps(timeline[-1]), file=sys.stderr, flush=True)
-            t += 1
-        sync_barrier(world)
-        full = max_over_ranks(time.perf_counter() - t0, world)
-
-    ms_per_step = 1e3 * t_steps / a.steps
-    value = a.steps / t_steps
-    # roofline of the attraction + update kernel (HBM bound), from the profiled step:
-    # bytes = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr + rows*(16 own Y + 16 gathered Y_j once
-    #         + 16 F + 4 inv + 16 upd r + 16 upd w + 16 gains r + 16 gains w + 16 Ynew w)
+    value = steps / t_loop
+    # ---- roofline of the HBM-bound gradient kernel (attraction + fused update)
+    # bytes per launch = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr
+    #   + rows*(16 own Y + 16 gathered Y_j once + 16 F + 4 inv + 32 upd r/w + 32 gains r/w + 16 Ynew)
     rows = r1 - r0
-    lnnz = e1 - e0
-    attr_bytes = lnnz * 12 + (rows + 1) * 8 + rows * (16 * 8 + 4)
-    attr_ms = ms[3]
-    attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms > 0 else None
+    attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 132
+    attr_ms = float(np.median([e["attract_ms"] for e in timeline])) if timeline else None
+    attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
+    knn_flops = 2.0 * (r1 - r0) * n * d
 
     out = {
         "metric": METRIC,
         "value": value,
         "unit": "iterations/s",
         "n_gpus": world,
-        "steps": a.steps,
+        "steps": steps,
         "warmup": a.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": 1e3 * t_loop / steps,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)",
         "config": {"workload": f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, "
-                               f"theta {a.theta}, schedule T={a.iterations}; timed iterations "
-                               f"t={a.start + a.warmup}..{a.start + a.warmup + a.steps - 1}",
+                               f"theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}",
                    "n": n, "dim": d, "k": k, "theta": a.theta, "parallelism": f"rows{world}",
                    "nnz_P": int(nnz)},
-        "knn_pts_per_s": n / t_knn,
+        "end_to_end_s": t_knn + t_aff + t_loop,
+        "loop_s": t_loop,
         "knn_s": t_knn,
+        "knn_pts_per_s": n / t_knn,
+        "knn_mfma_tflops": knn_flops / t_knn / 1e12,
+        "knn_mfma_frac_of_peak": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF,
         "affinities_joint_s": t_aff,
-        "stage_ms_last_step": {"tree": ms[0], "bh": ms[1], "exchange_z": ms[2],
-                               "attract_update": ms[3], "centre": ms[4], "t": t_done - 1},
-        "bh_interactions_per_s": visits / (ms[1] * 1e-3) if ms[1] > 0 else None,
-        "roofline": {"kernel": "attract_kernel<1> (attraction + gains/momentum update)",
-                     "bound": "hbm", "achieved": attr_gbs, "peak": 8000.0, "unit": "GB/s",
-                     "frac": (attr_gbs / 8000.0) if attr_gbs else None, "traffic": None,
-                     "bytes_per_launch": attr_bytes},
+        "final_loss": losses.get(max(losses)) if losses else None,
+        "roofline": {"kernel": "attract_kernel<1> (CSR attraction + gains/momentum update)",
+                     "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
+                     "bytes_per_launch": attr_bytes, "avg_ms": attr_ms},
+        "timeline": timeline,
     }
-    if full is not None:
-        out["full_run_s"] = full
-        out["full_run_iterations"] = a.iterations - t_done + 1
-        out["end_to_end_s_estimate"] = t_knn + t_aff + full + t_steps
-        if timeline:
-            out["timeline"] = timeline
-
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(ctx, Y[:n], a, n)
+        out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps)
     if rank == 0:
         print(json.dumps(out))
     ctx.close()
@@ -249,30 +227,37 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(ctx, Ydev, a, n):
-    """The oracle (C fp64 restatement of the reference, OpenMP) on a bounded
-    sample of the same state: tree build of all n points + BH repulsion for
-    `cpu_sample` queries, extrapolated to one full iteration."""
+def cpu_baseline(snaps, a, n, steps):
+    """The oracle (C fp64 restatement of the reference, OpenMP) timed on a
+    bounded sample of the same run: at each embedding snapshot taken from the
+    GPU trajectory (t in snaps), the reference quadtree build of all n points
+    + BH repulsion of `cpu_sample` random queries, extrapolated to n queries;
+    the per-iteration cost is held piecewise constant between snapshots and
+    integrated over the timed schedule -> iterations/s."""
     import oracle_ctypes as O
     threads = min(16, os.cpu_count() or 1)
-    Y = Ydev.detach().cpu().numpy().copy()
     q = min(a.cpu_sample, n)
     sel = np.random.default_rng(0).choice(n, q, replace=False)
-    # the oracle repulsion takes a contiguous query range: permute the sample first
-    perm = np.concatenate([sel, np.setdiff1d(np.arange(n), sel)])
-    Yp = np.ascontiguousarray(Y[perm])
-    t0 = time.perf_counter()
-    O.repulsion(Yp, a.theta, 0, q, threads=threads)
-    t_sample = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    O.repulsion(Yp, a.theta, 0, 1, threads=1)   # tree build + 1 query
-    t_build = time.perf_counter() - t0
-    per_query = max(t_sample - t_build, 1e-9) / q
-    t_iter = t_build + per_query * n
-    return {"value": 1.0 / t_iter, "unit": "iterations/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (C fp64 reference restatement) quadtree build of all {n} points + "
-                      f"BH repulsion of {q} random queries at the GPU's post-timing state, "
-                      f"extrapolated linearly to {n} queries (attraction excluded)"}
+    per_t = {}
+    for t, Ys in sorted(snaps.items()):
+        t0 = time.perf_counter()
+        O.repulsion_queries(Ys, a.theta, Ys[sel], threads=threads)
+        t_sample = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        O.repulsion_queries(Ys, a.theta, Ys[sel[:1]], threads=1)
+        t_build = time.perf_counter() - t0
+        per_t[t] = t_build + max(t_sample - t_build, 1e-9) / q * n
+    ts = sorted(per_t)
+    total = 0.0
+    for it in range(1, steps + 1):
+        nearest = min(ts, key=lambda s: abs(s - it))
+        total += per_t[nearest]
+    return {"value": steps / total, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "per_iteration_s_at": {str(t): per_t[t] for t in ts},
+            "sample": f"oracle (C fp64 reference restatement, OpenMP {threads} threads): at GPU-trajectory "
+                      f"snapshots t={ts}, reference quadtree build of all {n} points + BH repulsion of {q} "
+                      f"random queries extrapolated to {n}; piecewise-constant over t=1..{steps}; "
+                      f"attraction/update excluded (so the CPU figure is optimistic)"}
 
 
 if __name__ == "__main__":

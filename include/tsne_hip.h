@@ -158,14 +158,20 @@ int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const i
                                 const double *d_p, int64_t n, int64_t cap, int64_t *d_out_row_ptr,
                                 int32_t *d_out_col, double *d_out_val, int64_t *nnz_out);
 
-/* Device-resident optimizer.  setup binds device buffers (rows of P for this
- * rank's shard, full Y/upd/gains) and allocates the workspace; step runs
- * global iteration t (1-based) with the reference phase schedule; losses for
- * t % 10 == 0 are kept on the device and read by tsne_dev_opt_losses. */
+/* Device-resident optimizer.  setup copies the FULL P (every rank holds it;
+ * rank r computes rows [r*ceil(n/world), ...) of the optimizer's internal
+ * point labels) and the working set (Y, upd, gains: n x 2, original point
+ * order) into its own state and allocates the workspace; step runs global
+ * iteration t (1-based) with the reference phase schedule and rewrites the
+ * caller's Y (original order) at the end of every step; sync also writes
+ * back upd and gains.  Losses for t % 10 == 0 stay on the device and are read
+ * by tsne_dev_opt_losses.  Internally the points are relabelled into Morton
+ * order every 25 iterations (cache locality of the CSR attraction). */
 int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *d_row_ptr,
                        const int32_t *d_col, const double *d_P, int64_t n, double *d_Y,
                        double *d_upd, double *d_gains);
 int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t);
+int tsne_dev_opt_sync(tsne_ctx *ctx);
 int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap,
                         int32_t *n_loss);
 /* Per-stage timing of the last step (HIP events on the ctx stream), in ms:

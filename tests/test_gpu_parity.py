@@ -281,3 +281,27 @@ def test_unsupported_components(ctx):
     with pytest.raises(T.TsneError) as e:
         ctx.optimize(rp, col, val, Y, np.zeros_like(Y), np.ones_like(Y), p)
     assert e.value.status == -4
+
+
+def test_device_optimizer_matches_host_path(ctx):
+    """tsne_dev_opt_* on torch device tensors (with the internal Morton
+    relabelling every 25 iterations) == tsne_optimize on host buffers."""
+    import torch
+    n = 700
+    rp, col, val = random_problem(n, 20, seed=41)
+    Y0 = np.random.default_rng(8).normal(size=(n, 2)) * 1e-3
+    p = default_params(iterations=80, theta=0.5)
+    Yh, uh, gh = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lh = ctx.optimize(rp, col, val, Yh, uh, gh, p)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    dY, du, dg = t(Y0, torch.float64), torch.zeros((n, 2), dtype=torch.float64, device=dev), \
+        torch.ones((n, 2), dtype=torch.float64, device=dev)
+    ctx.dev_opt_setup(p, t(rp, torch.int64), t(col, torch.int32), t(val, torch.float64), n, dY, du, dg)
+    for it in range(1, 81):
+        ctx.dev_opt_step(it)
+    ctx.dev_opt_sync()
+    ctx.synchronize()
+    assert np.array_equal(dY.cpu().numpy(), Yh)
+    assert np.array_equal(du.cpu().numpy(), uh) and np.array_equal(dg.cpu().numpy(), gh)
+    assert ctx.dev_opt_losses() == lh

@@ -1,0 +1,86 @@
+"""Host C++ layer (tsne-flink_amd/host): the Tsne.main-compatible CLI and the
+Java formatting used by the output / loss files.  CPU only: no GPU is touched
+(argument errors and --executionPlan return before any device work)."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "tsne-flink_amd"
+CLI = PKG / "tsne_hip"
+
+HARNESS = r'''
+#include <cstdio>
+#include <map>
+#include "tsne_helpers.hpp"
+using namespace tsne_flink;
+int main() {
+    double v[] = {1.0, 21.25, 1e-5, 12345678.0, 0.001, 1e7, 123456.789, -0.5, 0.1, 2.0 / 3.0,
+                  9.999999e6, 1e-3 * 0.999, 0.0, -0.0, 1e300, 2.5e-7};
+    for (double x : v) std::printf("%s\n", javaDouble(x).c_str());
+    std::map<int32_t, double> m;
+    for (int t = 10; t <= 300; t += 10) m[t] = t / 4.0;
+    std::printf("%s\n", javaHashMapString(m).c_str());
+    std::map<int32_t, double> m2 = {{10, 1.5}, {20, 2.5}};
+    std::printf("%s\n", javaHashMapString(m2).c_str());
+    return 0;
+}
+'''
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    d = tmp_path_factory.mktemp("fmt")
+    src = d / "h.cpp"
+    src.write_text(HARNESS)
+    exe = d / "h"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", f"-I{ROOT / 'include'}", f"-I{PKG / 'host'}",
+                           str(src), str(PKG / "host" / "tsne_helpers.cpp"), f"-L{PKG}", "-ltsne_hip",
+                           f"-Wl,-rpath,{PKG}", "-o", str(exe)])
+    return subprocess.check_output([str(exe)], text=True).splitlines()
+
+
+def test_java_double_format(harness):
+    # java.lang.Double.toString
+    assert harness[:16] == ["1.0", "21.25", "1.0E-5", "1.2345678E7", "0.001", "1.0E7", "123456.789",
+                            "-0.5", "0.1", "0.6666666666666666", "9999999.0", "9.99E-4", "0.0",
+                            "-0.0", "1.0E300", "2.5E-7"]
+
+
+def java_hashmap_order(keys):
+    cap = 16
+    while len(keys) > 0.75 * cap:
+        cap *= 2
+    return sorted(keys, key=lambda k: (((k ^ (k >> 16)) & (cap - 1)), keys.index(k)))
+
+
+def test_loss_file_is_java_hashmap_tostring(harness):
+    keys = list(range(10, 301, 10))
+    order = java_hashmap_order(keys)
+    want = "{" + ", ".join(f"{k}={k / 4.0!r}" for k in order) + "}"
+    assert harness[16] == want
+    assert harness[17] == "{20=2.5, 10=1.5}" or harness[17] == "{10=1.5, 20=2.5}"
+
+
+def run(*args, cwd=None):
+    return subprocess.run([str(CLI), *args], capture_output=True, text=True, cwd=cwd)
+
+
+def test_cli_unknown_metric_is_illegal_argument():
+    r = run("--input", "x", "--output", "y", "--dimension", "4", "--knnMethod", "bruteforce",
+            "--metric", "manhattan")
+    assert r.returncode == 2 and "IllegalArgumentException" in r.stderr
+
+
+def test_cli_required_keys():
+    r = run("--input", "x", "--dimension", "4", "--knnMethod", "bruteforce")
+    assert r.returncode != 0 and "output" in r.stderr
+
+
+def test_cli_execution_plan(tmp_path):
+    r = run("--input", "in.csv", "--output", "out.csv", "--dimension", "4", "--knnMethod",
+            "bruteforce", "--executionPlan", cwd=tmp_path)
+    assert r.returncode == 0
+    plan = (tmp_path / "tsne_executionPlan.json").read_text()
+    assert "pairwiseAffinities" in plan and "optimize" in plan

@@ -56,17 +56,28 @@ __global__ void bbox_partial(const double *__restrict__ Y, int64_t n, double *__
     }
 }
 
+// One 256-thread block folds the per-block partials.
 __global__ void bbox_final(const double *__restrict__ part, int nb, double *__restrict__ W,
                            int32_t *__restrict__ meta) {
-    if (threadIdx.x != 0) return;
-    double mnx = part[0], mxx = part[1], mny = part[2], mxy = part[3];
-    for (int b = 1; b < nb; ++b) {
+    __shared__ double sm[4][4];
+    double mnx = __builtin_inf(), mxx = -__builtin_inf(), mny = __builtin_inf(), mxy = -__builtin_inf();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
         mnx = fmin(mnx, part[4 * b]); mxx = fmax(mxx, part[4 * b + 1]);
         mny = fmin(mny, part[4 * b + 2]); mxy = fmax(mxy, part[4 * b + 3]);
     }
-    double a = mxx - mnx, c = mxy - mny;
-    *W = a > c ? a : c;  // scala.math.max(maxX - minX, maxY - minY)
-    meta[0] = 0;
+    mnx = wave_min(mnx); mxx = wave_max(mxx); mny = wave_min(mny); mxy = wave_max(mxy);
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 0) { sm[w][0] = mnx; sm[w][1] = mxx; sm[w][2] = mny; sm[w][3] = mxy; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; ++k) {
+            sm[0][0] = fmin(sm[0][0], sm[k][0]); sm[0][1] = fmax(sm[0][1], sm[k][1]);
+            sm[0][2] = fmin(sm[0][2], sm[k][2]); sm[0][3] = fmax(sm[0][3], sm[k][3]);
+        }
+        const double a = sm[0][1] - sm[0][0], c = sm[0][3] - sm[0][2];
+        *W = a > c ? a : c;  // scala.math.max(maxX - minX, maxY - minY)
+        meta[0] = 0;
+    }
 }
 
 // Morton key by replaying the reference cell arithmetic (no FMA contraction).
@@ -110,11 +121,14 @@ __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const doubl
 }
 
 __global__ void gather_sorted(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted,
-                              int64_t n, double2 *__restrict__ pos, int32_t *__restrict__ inv) {
+                              int64_t n, double2 *__restrict__ pos, float2 *__restrict__ pos32,
+                              int32_t *__restrict__ inv) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     int32_t i = idx_sorted[s];
-    pos[s] = make_double2(Y[2 * i], Y[2 * i + 1]);
+    const double x = Y[2 * i], y = Y[2 * i + 1];
+    pos[s] = make_double2(x, y);
+    pos32[s] = make_float2((float)x, (float)y);
     inv[i] = (int32_t)s;
 }
 
@@ -166,11 +180,23 @@ __global__ void karras_build(const uint64_t *__restrict__ k, int64_t n, const in
     if (i == 0) parent_node[0] = -1;
 }
 
-// Bottom-up count / centre of mass.  The second thread to reach a node
-// computes it from its two children (fixed order: deterministic sums).
-// Hand-off across workgroups: agent-scope fences around the arrival atomic.
+// Bottom-up count / sums / bounding box / hmin.  The second thread to reach a
+// node computes it from its two children (fixed order: deterministic sums).
+// Cross-workgroup hand-off without fences (MI355X_MICROARCH.md, "Valid forms"):
+// the per-node aggregates that a sibling thread reads are written and read
+// with system-scope (sc0 sc1, write-through / cache-bypassing) 8-byte
+// accesses; every thread drains its stores (s_waitcnt vmcnt(0)) before its
+// relaxed arrival atomic.  Agent-scope __threadfence() here wrote back the
+// whole XCD L2 per wave and cost ~8 ms per build at 1M points.
+__device__ __forceinline__ void st_sys(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
-                          const double *__restrict__ Wp, BHNode *nodes, double2 *sums,
+                          const double *__restrict__ Wp, BHNode *nodes, double *agg,
                           const int32_t *__restrict__ parent_leaf,
                           const int32_t *__restrict__ parent_node, int32_t *arrive) {
     const int m = meta[0];
@@ -179,49 +205,54 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
     const double W = *Wp;
     int p = parent_leaf[s];
     while (p >= 0) {
-        __threadfence();                                 // release this thread's node writes
-        if (atomicAdd(&arrive[p], 1) == 0) return;       // first arriver stops
-        __threadfence();                                 // acquire the sibling's writes
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            return;                                      // first arriver stops
         const int32_t l = nodes[p].left, r = nodes[p].right, dl = nodes[p].delta;
-        double2 ls, rs;
-        int lc, rc;
-        double lx0, lx1, ly0, ly1, lh, rx0, rx1, ry0, ry1, rh;
-        if (l < 0) {
-            ls = pos[~l]; lc = 1;
-            lx0 = lx1 = ls.x; ly0 = ly1 = ls.y; lh = __builtin_inf();
-        } else {
-            ls = sums[l]; lc = nodes[l].cnt;
-            lx0 = nodes[l].bx0; lx1 = nodes[l].bx1; ly0 = nodes[l].by0; ly1 = nodes[l].by1; lh = nodes[l].hmin;
+        double a[2][7];                                  // sx, sy, x0, x1, y0, y1, hmin
+        double c[2];
+        const int32_t ch[2] = {l, r};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (ch[k] < 0) {
+                const double2 q = pos[~ch[k]];
+                a[k][0] = q.x; a[k][1] = q.y; a[k][2] = q.x; a[k][3] = q.x; a[k][4] = q.y; a[k][5] = q.y;
+                a[k][6] = __builtin_inf();
+                c[k] = 1.0;
+            } else {
+                const double *g = agg + 8 * (int64_t)ch[k];
+#pragma unroll
+                for (int f = 0; f < 7; ++f) a[k][f] = ld_sys(g + f);
+                c[k] = ld_sys(g + 7);
+            }
         }
-        if (r < 0) {
-            rs = pos[~r]; rc = 1;
-            rx0 = rx1 = rs.x; ry0 = ry1 = rs.y; rh = __builtin_inf();
-        } else {
-            rs = sums[r]; rc = nodes[r].cnt;
-            rx0 = nodes[r].bx0; rx1 = nodes[r].bx1; ry0 = nodes[r].by0; ry1 = nodes[r].by1; rh = nodes[r].hmin;
-        }
-        nodes[p].bx0 = fmin(lx0, rx0);
-        nodes[p].bx1 = fmax(lx1, rx1);
-        nodes[p].by0 = fmin(ly0, ry0);
-        nodes[p].by1 = fmax(ly1, ry1);
-        const int cnt = lc + rc;
-        const double sx = ls.x + rs.x, sy = ls.y + rs.y;
+        const double cnt = c[0] + c[1];
+        const double sx = a[0][0] + a[1][0], sy = a[0][1] + a[1][1];
+        const double x0 = fmin(a[0][2], a[1][2]), x1 = fmax(a[0][3], a[1][3]);
+        const double y0 = fmin(a[0][4], a[1][4]), y1 = fmax(a[0][5], a[1][5]);
         const int par = parent_node[p];
         const int dlev = dl >> 1;
         bool real;
         if (dl >= 62) real = false;                      // keys tie below 31 levels
         else if (par < 0) real = true;                   // root cell chain
         else real = (nodes[par].delta >> 1) < dlev;      // first node of its quad level
-        sums[p] = make_double2(sx, sy);
-        nodes[p].cx = sx / (double)cnt;                  // centerOfMass = sum / cumSize
-        nodes[p].cy = sy / (double)cnt;
-        nodes[p].cnt = cnt;
         const double h = real ? ldexp(W, -dlev) : -1.0;  // -1 = transparent
-        nodes[p].h = h;
-        nodes[p].hmin = fmin(real ? h : __builtin_inf(), fmin(lh, rh));
+        const double hmin = fmin(real ? h : __builtin_inf(), fmin(a[0][6], a[1][6]));
+        double *g = agg + 8 * (int64_t)p;
+        st_sys(g + 0, sx); st_sys(g + 1, sy);
+        st_sys(g + 2, x0); st_sys(g + 3, x1); st_sys(g + 4, y0); st_sys(g + 5, y1);
+        st_sys(g + 6, hmin); st_sys(g + 7, cnt);
+        BHNode &nd = nodes[p];                           // read by the traversal (next launch)
+        nd.cx = sx / cnt;                                // centerOfMass = sum / cumSize
+        nd.cy = sy / cnt;
+        nd.cnt = (int32_t)cnt;
+        nd.h = h;
+        nd.hmin = hmin;
+        nd.bx0 = x0; nd.bx1 = x1; nd.by0 = y0; nd.by1 = y1;
         p = par;
     }
 }
+
 
 __global__ void set_root(int32_t *meta) {
     const int m = meta[0];
@@ -245,6 +276,22 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
     zs += r;
 }
 
+// The same pair term in fp32 for dense leaf tiles (pair terms only; the
+// per-chunk sums are accumulated in fp64 by the caller).  A pair whose fp32
+// squared distance is 0 (the query itself, exact duplicates, and points equal
+// to it within fp32 rounding) contributes nothing.
+__device__ __forceinline__ void leaf_force32(float qx, float qy, float px, float py, float &fx,
+                                             float &fy, float &zs) {
+    const float dx = qx - px, dy = qy - py;
+    const float D = __fmaf_rn(dx, dx, dy * dy);
+    float r = __builtin_amdgcn_rcpf(1.0f + D);
+    r = (D == 0.0f) ? 0.0f : r;
+    const float sc = r * r;
+    fx = __fmaf_rn(sc, dx, fx);
+    fy = __fmaf_rn(sc, dy, fy);
+    zs += r;
+}
+
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
 // (node, lane mask).  Every lane takes exactly its own reference decision;
 // the wave visits the union of the lanes' opened nodes.  Fast path: if for a
@@ -256,7 +303,7 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
 // evaluations and no stack traffic.  That is the near-exact regime of a
 // small embedding.
 __global__ __launch_bounds__(256) void bh_traverse(
-    const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+    const double2 *__restrict__ pos, const float2 *__restrict__ pos32, const BHNode *__restrict__ nodes,
     const int32_t *__restrict__ meta, double theta, int64_t s0, int64_t s1,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
@@ -270,6 +317,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
+    const float qxf = (float)qx, qyf = (float)qy;
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0;
     int sp = 0;
@@ -303,21 +351,29 @@ __global__ __launch_bounds__(256) void bh_traverse(
         }
         const uint64_t tm = __ballot(tile);
         if (tm) {
+            // fp32 pair terms over 64-point chunks, chunk sums accumulated in fp64
             const int a = nd.first, b = nd.last;
             if (tile) nvis += (unsigned long long)(b - a + 1);
-            int p = a;
-            for (; p + 3 <= b; p += 4) {
-                const double2 p0 = pos[p], p1 = pos[p + 1], p2 = pos[p + 2], p3 = pos[p + 3];
-                if (tile) {
-                    leaf_force(qx, qy, p0.x, p0.y, fx, fy, zs);
-                    leaf_force(qx, qy, p1.x, p1.y, fx, fy, zs);
-                    leaf_force(qx, qy, p2.x, p2.y, fx, fy, zs);
-                    leaf_force(qx, qy, p3.x, p3.y, fx, fy, zs);
+            for (int c0 = a; c0 <= b; c0 += 64) {
+                const int c1 = min(b + 1, c0 + 64);
+                float ax = 0.f, ay = 0.f, az = 0.f;
+                int p = c0;
+                for (; p + 8 <= c1; p += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const float2 pp = pos32[p + u];
+                        leaf_force32(qxf, qyf, pp.x, pp.y, ax, ay, az);
+                    }
                 }
-            }
-            for (; p <= b; ++p) {
-                const double2 p0 = pos[p];
-                if (tile) leaf_force(qx, qy, p0.x, p0.y, fx, fy, zs);
+                for (; p < c1; ++p) {
+                    const float2 pp = pos32[p];
+                    leaf_force32(qxf, qyf, pp.x, pp.y, ax, ay, az);
+                }
+                if (tile) {
+                    fx += (double)ax;
+                    fy += (double)ay;
+                    zs += (double)az;
+                }
             }
             act = act && !tile;
         }
@@ -370,8 +426,9 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.idx_sorted = ws.get<int32_t>("bh.idx_sorted", n);
     t.inv = ws.get<int32_t>("bh.inv", n);
     t.pos = ws.get<double2>("bh.pos", n);
+    t.pos32 = ws.get<float2>("bh.pos32", n + 64);
     t.nodes = ws.get<BHNode>("bh.nodes", n);
-    t.sums = ws.get<double2>("bh.sums", n);
+    t.agg = ws.get<double>("bh.agg", 8 * (size_t)n);
     t.parent_leaf = ws.get<int32_t>("bh.parent_leaf", n);
     t.parent_node = ws.get<int32_t>("bh.parent_node", n);
     t.arrive = ws.get<int32_t>("bh.arrive", n);
@@ -390,17 +447,17 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY) {
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
     hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
-    hipLaunchKernelGGL(bbox_final, dim3(1), dim3(64), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
+    hipLaunchKernelGGL(bbox_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
     hipLaunchKernelGGL(morton_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
     TSNE_LAUNCH_CHECK();
     size_t tb = t.sort_tmp_bytes;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
                                                (int)n, 0, 64, st));
-    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
+    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.pos32, t.inv);
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
                        t.nodes, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, t.nodes,
-                       t.sums, t.parent_leaf, t.parent_node, t.arrive);
+                       t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
     TSNE_LAUNCH_CHECK();
 }
@@ -409,7 +466,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                   double2 *dF, double *dz, unsigned long long *visits) {
     if (s1 <= s0) return;
     const int64_t waves = ceil_div(s1 - s0, 64);
-    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes,
+    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.pos32, t.nodes,
                        t.meta, theta, s0, s1, dF, dz, visits);
     TSNE_LAUNCH_CHECK();
 }

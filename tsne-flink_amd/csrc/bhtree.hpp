@@ -28,8 +28,9 @@ struct BHTree {
     int32_t *idx = nullptr, *idx_sorted = nullptr;  // sorted position -> original row
     int32_t *inv = nullptr;                         // original row -> sorted position
     double2 *pos = nullptr;                         // sorted positions (leaves + queries)
+    float2 *pos32 = nullptr;                        // the same rounded to fp32 (dense tiles)
     BHNode *nodes = nullptr;
-    double2 *sums = nullptr;
+    double *agg = nullptr;      // per-node bottom-up aggregates (8 doubles)
     int32_t *parent_leaf = nullptr, *parent_node = nullptr;
     int32_t *arrive = nullptr;
     int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref

@@ -404,35 +404,33 @@ int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_p
         TSNE_REQUIRE(params && row_ptr && Y && upd && gains && n >= 1 && row_ptr[0] == 0, "bad arguments");
         if (params->n_components != 2)
             fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (Cell.contains requires 2-D points)");
-        const int64_t chunk = ceil_div(n, ctx->world);
-        const int64_t npad = chunk * ctx->world;
-        const int64_t r0 = std::min<int64_t>(n, chunk * ctx->rank);
-        const int64_t r1 = std::min<int64_t>(n, r0 + chunk);
-        // this rank's rows of P, rebased
-        std::vector<int64_t> lrp((size_t)(r1 - r0) + 1);
-        for (int64_t i = r0; i <= r1; ++i) lrp[(size_t)(i - r0)] = row_ptr[i] - row_ptr[r0];
-        const int64_t lnnz = lrp.back();
-        int64_t *drp = upload(ctx, "h.rp", lrp.data(), lrp.size());
-        int32_t *dc = upload(ctx, "h.col", col + row_ptr[r0], (size_t)lnnz);
-        double *dp = upload(ctx, "h.p", P + row_ptr[r0], (size_t)lnnz);
-        double *dY = ctx->ws.get<double>("h.Yopt", (size_t)npad * 2);
-        double *du = ctx->ws.get<double>("h.updopt", (size_t)npad * 2);
-        double *dn = ctx->ws.get<double>("h.gainsopt", (size_t)npad * 2);
-        TSNE_HIP(hipMemcpyAsync(dY, Y, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
-        TSNE_HIP(hipMemcpyAsync(du, upd, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
-        TSNE_HIP(hipMemcpyAsync(dn, gains, sizeof(double) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        const int64_t nnz = row_ptr[n];
+        for (int64_t e = 0; e < nnz; ++e)
+            if (col[e] < 0 || col[e] >= n) fail(TSNE_ERR_ARG, "column index out of range");
+        // the full P on every rank; each rank computes its own label slice
+        int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)n + 1);
+        int32_t *dc = upload(ctx, "h.col", col, (size_t)nnz);
+        double *dp = upload(ctx, "h.p", P, (size_t)nnz);
+        double *dY = upload(ctx, "h.Yopt", Y, (size_t)n * 2);
+        double *du = upload(ctx, "h.updopt", upd, (size_t)n * 2);
+        double *dn = upload(ctx, "h.gainsopt", gains, (size_t)n * 2);
         opt_setup(ctx, params, drp, dc, dp, n, dY, du, dn);
         for (int32_t t = 1; t <= params->iterations; ++t) opt_step(ctx, t);
-        if (ctx->world > 1) {  // each rank updated only its own rows of upd / gains
-            comm_allgather_bytes(ctx, du + 2 * r0, du, sizeof(double) * 2 * chunk);
-            comm_allgather_bytes(ctx, dn + 2 * r0, dn, sizeof(double) * 2 * chunk);
-        }
+        opt_sync(ctx);
         download(ctx, Y, dY, (size_t)n * 2);
         download(ctx, upd, du, (size_t)n * 2);
         download(ctx, gains, dn, (size_t)n * 2);
         sync(ctx);
         int32_t k = opt_losses(ctx, loss_keys, loss_vals, loss_cap);
         if (n_loss) *n_loss = k;
+    });
+}
+
+int tsne_dev_opt_sync(tsne_ctx *ctx) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        opt_sync(ctx);
     });
 }
 

@@ -135,6 +135,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr,
                const int32_t *d_col, const double *d_P, int64_t n, double *dY, double *dupd,
                double *dgains);
 void opt_step(tsne_ctx *ctx, int32_t t);
+void opt_sync(tsne_ctx *ctx);
 int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap);
 void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits);
 void opt_destroy(tsne_ctx *ctx);

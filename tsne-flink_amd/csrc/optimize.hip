@@ -13,17 +13,36 @@
 //      step (:341-369) -> Ynew
 //   5. [multi-GPU] all-gather of Ynew slices
 //   6. centre: Y = Ynew - mean(Ynew) (:320-329)
+//
+// Internal labels.  The optimizer keeps its own copy of P (full, every rank)
+// and of the working set, indexed by internal point labels.  Every
+// RELABEL_EVERY iterations the labels are renumbered into the current Morton
+// order of the embedding (which the tree build computes anyway), so rows that
+// are consecutive in memory are spatial neighbours and the CSR attraction's
+// gathers of Y_j hit the L2 instead of streaming random lines from the MALL.
+// Rank r owns labels [r*chunk, (r+1)*chunk).  The caller's Y is rewritten in
+// the original order after every step; upd / gains on tsne_dev_opt_sync.
+#include <hipcub/hipcub.hpp>
+
 #include "bhtree.hpp"
 
 namespace tsne {
 
 struct OptState {
     tsne_params p{};
-    int64_t n = 0, chunk = 0, npad = 0, r0 = 0, r1 = 0;
-    const int64_t *row_ptr = nullptr;  // local rows [r0, r1)
-    const int32_t *col = nullptr;
-    const double *val = nullptr;
-    double *Y = nullptr, *upd = nullptr, *gains = nullptr;  // full n x 2
+    int64_t n = 0, chunk = 0, npad = 0, r0 = 0, r1 = 0, nnz = 0;
+    // caller buffers (original order, n x 2)
+    double *Yu = nullptr, *updu = nullptr, *gainsu = nullptr;
+    // internal (label order): full CSR P and working set, double-buffered for relabeling
+    int64_t *rp[2] = {nullptr, nullptr};
+    int32_t *col[2] = {nullptr, nullptr};
+    double *val[2] = {nullptr, nullptr};
+    double *Y[2] = {nullptr, nullptr}, *upd[2] = {nullptr, nullptr}, *gains[2] = {nullptr, nullptr};
+    int32_t *orig[2] = {nullptr, nullptr};   // label -> original index
+    int64_t *rowlen = nullptr;
+    void *scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    int cur = 0;
     double *Ynew = nullptr;   // npad x 2
     double2 *F = nullptr;     // npad, sorted order
     double *z = nullptr;      // npad, sorted order
@@ -43,6 +62,7 @@ struct OptState {
 namespace {
 
 constexpr int NPART = 512;
+constexpr int RELABEL_EVERY = 25;
 
 __device__ __forceinline__ double jmax(double a, double b) {  // java.lang.Math.max
     if (a != a) return a;
@@ -50,16 +70,25 @@ __device__ __forceinline__ double jmax(double a, double b) {  // java.lang.Math.
     return a >= b ? a : b;
 }
 
-__device__ __forceinline__ double metric2(double ax, double ay, double bx, double by, int metric) {
+// q = 1 / (1 + metric(y_i, y_j)) with the input metric on 2-D points
+// (TsneHelpers.scala:293); v_rcp_f64 + two Newton steps.
+__device__ __forceinline__ double qterm(double ax, double ay, double bx, double by, int metric) {
+    double m;
     if (metric == TSNE_METRIC_COSINE) {
         const double dt = __dadd_rn(__dmul_rn(ax, bx), __dmul_rn(ay, by));
         const double na = sqrt(__dadd_rn(__dmul_rn(ax, ax), __dmul_rn(ay, ay)));
         const double nb = sqrt(__dadd_rn(__dmul_rn(bx, bx), __dmul_rn(by, by)));
-        return 1.0 - dt / (na * nb);
+        m = 1.0 - dt / (na * nb);
+    } else {
+        const double dx = __dsub_rn(ax, bx), dy = __dsub_rn(ay, by);
+        const double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+        m = metric == TSNE_METRIC_EUCLIDEAN ? sqrt(s) : s;
     }
-    const double dx = __dsub_rn(ax, bx), dy = __dsub_rn(ay, by);
-    const double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-    return metric == TSNE_METRIC_EUCLIDEAN ? sqrt(s) : s;
+    const double x = 1.0 + m;
+    double r = __builtin_amdgcn_rcp(x);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    return r;
 }
 
 // Deterministic sum of v[0..n) (stride elements, component c) into part[block].
@@ -91,7 +120,8 @@ __global__ void reduce_final(const double *__restrict__ part, int np, double *__
 }
 
 // MODE 0: grad only.  MODE 1: grad + updateEmbedding -> Ynew.
-// 16 lanes per CSR row, 4 rows per wave.
+// 16 lanes per CSR row (row_ptr indexed by the global row), 4 rows per wave;
+// each lane keeps 4 (col, val, Y_j) gathers in flight.
 template <int MODE>
 __global__ __launch_bounds__(256) void attract_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
@@ -102,19 +132,37 @@ __global__ __launch_bounds__(256) void attract_kernel(
     double *__restrict__ lpart) {
     __shared__ double sl[4];
     const int sub = threadIdx.x & 15;
-    const int64_t li = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const int64_t i = r0 + li;
+    const int64_t i = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);
     const double Z = scal[0];
     double lsum = 0.0;
     if (i < r1) {
         const double yx = Y[2 * i], yy = Y[2 * i + 1];
         double fx = 0.0, fy = 0.0;
-        const int64_t e1 = row_ptr[li + 1];
-        for (int64_t e = row_ptr[li] + sub; e < e1; e += 16) {
+        const int64_t e1 = row_ptr[i + 1];
+        int64_t e = row_ptr[i] + sub;
+        for (; e + 48 < e1; e += 64) {
+            int32_t j[4];
+            double pv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { j[u] = col[e + 16 * u]; pv[u] = val[e + 16 * u]; }
+            double jx[4], jy[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { jx[u] = Y[2 * (int64_t)j[u]]; jy[u] = Y[2 * (int64_t)j[u] + 1]; }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double pij = __dmul_rn(pv[u], ex);
+                const double q = qterm(yx, yy, jx[u], jy[u], metric);
+                const double s = __dmul_rn(pij, q);
+                fx = __dadd_rn(fx, __dmul_rn(s, __dsub_rn(yx, jx[u])));
+                fy = __dadd_rn(fy, __dmul_rn(s, __dsub_rn(yy, jy[u])));
+                if (want_loss) lsum += pij * log(pij / (q / Z));
+            }
+        }
+        for (; e < e1; e += 16) {
             const int32_t j = col[e];
             const double pij = __dmul_rn(val[e], ex);
             const double jx = Y[2 * (int64_t)j], jy = Y[2 * (int64_t)j + 1];
-            const double q = 1.0 / (1.0 + metric2(yx, yy, jx, jy, metric));
+            const double q = qterm(yx, yy, jx, jy, metric);
             const double s = __dmul_rn(pij, q);
             fx = __dadd_rn(fx, __dmul_rn(s, __dsub_rn(yx, jx)));
             fy = __dadd_rn(fy, __dmul_rn(s, __dsub_rn(yy, jy)));
@@ -194,6 +242,55 @@ __global__ void init_ws_kernel(int64_t ne, uint64_t seed, double *__restrict__ Y
     Y[e] = 1e-4 * sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
     upd[e] = 0.0;
     gains[e] = 1.0;
+}
+
+// ---- internal labels
+__global__ void iota_i32(int32_t *p, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = (int32_t)i;
+}
+
+// dst[orig[i]] = src[i] (2 components)
+__global__ void scatter_to_user(const double *__restrict__ src, const int32_t *__restrict__ orig,
+                                int64_t n, double *__restrict__ dst) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = orig[i];
+    dst[2 * o] = src[2 * i];
+    dst[2 * o + 1] = src[2 * i + 1];
+}
+
+// new label s <- old label idx_sorted[s]: working set, label map, row lengths
+__global__ void relabel_state(const int32_t *__restrict__ order, int64_t n,
+                              const double *__restrict__ Y0, const double *__restrict__ u0,
+                              const double *__restrict__ g0, const int32_t *__restrict__ o0,
+                              const int64_t *__restrict__ rp0, double *__restrict__ Y1,
+                              double *__restrict__ u1, double *__restrict__ g1, int32_t *__restrict__ o1,
+                              int64_t *__restrict__ len) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > n) return;
+    if (s == n) { len[n] = 0; return; }
+    const int64_t i = order[s];
+    Y1[2 * s] = Y0[2 * i]; Y1[2 * s + 1] = Y0[2 * i + 1];
+    u1[2 * s] = u0[2 * i]; u1[2 * s + 1] = u0[2 * i + 1];
+    g1[2 * s] = g0[2 * i]; g1[2 * s + 1] = g0[2 * i + 1];
+    o1[s] = o0[i];
+    len[s] = rp0[i + 1] - rp0[i];
+}
+
+// one wave per new row: copy the old row, columns renamed old -> new label
+__global__ void relabel_rows(const int32_t *__restrict__ order, const int32_t *__restrict__ inv, int64_t n,
+                             const int64_t *__restrict__ rp0, const int32_t *__restrict__ c0,
+                             const double *__restrict__ v0, const int64_t *__restrict__ rp1,
+                             int32_t *__restrict__ c1, double *__restrict__ v1) {
+    const int64_t s = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (s >= n) return;
+    const int64_t i = order[s];
+    const int64_t a = rp0[i], len = rp0[i + 1] - a, b = rp1[s];
+    for (int64_t e = lane_id(); e < len; e += 64) {
+        c1[b + e] = inv[c0[a + e]];
+        v1[b + e] = v0[a + e];
+    }
 }
 
 }  // namespace
@@ -280,6 +377,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (Cell.contains requires 2-D points)");
     TSNE_REQUIRE(n >= 1, "empty embedding");
     TSNE_REQUIRE(p->metric >= 0 && p->metric <= 2, "unknown metric");
+    hipStream_t st = ctx->stream;
     opt_destroy(ctx);
     OptState *s = new OptState();
     ctx->opt = s;
@@ -289,13 +387,38 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->npad = s->chunk * ctx->world;
     s->r0 = std::min<int64_t>(n, s->chunk * ctx->rank);
     s->r1 = std::min<int64_t>(n, s->r0 + s->chunk);
-    s->row_ptr = d_row_ptr;
-    s->col = d_col;
-    s->val = d_P;
-    s->Y = dY;
-    s->upd = dupd;
-    s->gains = dgains;
+    s->Yu = dY;
+    s->updu = dupd;
+    s->gainsu = dgains;
+    int64_t nnz = 0;
+    TSNE_HIP(hipMemcpyAsync(&nnz, d_row_ptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    s->nnz = nnz;
     Workspace &ws = ctx->ws;
+    for (int b = 0; b < 2; ++b) {
+        const std::string k = std::to_string(b);
+        s->rp[b] = ws.get<int64_t>("opt.rp" + k, n + 1);
+        s->col[b] = ws.get<int32_t>("opt.col" + k, nnz + 1);
+        s->val[b] = ws.get<double>("opt.val" + k, nnz + 1);
+        s->Y[b] = ws.get<double>("opt.Y" + k, 2 * s->npad);
+        s->upd[b] = ws.get<double>("opt.upd" + k, 2 * s->npad);
+        s->gains[b] = ws.get<double>("opt.gains" + k, 2 * s->npad);
+        s->orig[b] = ws.get<int32_t>("opt.orig" + k, n);
+    }
+    s->cur = 0;
+    TSNE_HIP(hipMemcpyAsync(s->rp[0], d_row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->col[0], d_col, sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->val[0], d_P, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemsetAsync(s->Y[0], 0, sizeof(double) * 2 * s->npad, st));
+    TSNE_HIP(hipMemcpyAsync(s->Y[0], dY, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->upd[0], dupd, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->gains[0], dgains, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(iota_i32, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->orig[0], n);
+    s->rowlen = ws.get<int64_t>("opt.rowlen", n + 1);
+    size_t tb = 0;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->rowlen, s->rp[1], (int)(n + 1), st));
+    s->scan_tmp_bytes = tb;
+    s->scan_tmp = ws.get<uint8_t>("opt.scan_tmp", tb);
     s->Ynew = ws.get<double>("opt.Ynew", 2 * s->npad);
     s->F = ws.get<double2>("opt.F", s->npad);
     s->z = ws.get<double>("opt.z", s->npad);
@@ -305,11 +428,37 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
     s->visits = ws.get<unsigned long long>("opt.visits", 1);
-    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, ctx->stream));
-    TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, ctx->stream));
-    TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, ctx->stream));
+    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, st));
+    TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
+    TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
     bh_alloc(ctx, s->tree, n);
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
+    TSNE_LAUNCH_CHECK();
+}
+
+// make every rank's copy of upd / gains current (each rank updates only its labels)
+static void gather_working_set(tsne_ctx *ctx, OptState *s) {
+    if (ctx->world == 1) return;
+    const int c = s->cur;
+    comm_allgather_bytes(ctx, s->upd[c] + 2 * s->r0, s->upd[c], sizeof(double) * 2 * s->chunk);
+    comm_allgather_bytes(ctx, s->gains[c] + 2 * s->r0, s->gains[c], sizeof(double) * 2 * s->chunk);
+}
+
+// renumber labels into the Morton order of this iteration's tree
+static void relabel(tsne_ctx *ctx, OptState *s) {
+    hipStream_t st = ctx->stream;
+    const int64_t n = s->n;
+    const int a = s->cur, b = 1 - a;
+    gather_working_set(ctx, s);
+    hipLaunchKernelGGL(relabel_state, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, s->tree.idx_sorted, n,
+                       s->Y[a], s->upd[a], s->gains[a], s->orig[a], s->rp[a], s->Y[b], s->upd[b], s->gains[b],
+                       s->orig[b], s->rowlen);
+    size_t tb = s->scan_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, s->rowlen, s->rp[b], (int)(n + 1), st));
+    hipLaunchKernelGGL(relabel_rows, dim3(ceil_div(n, 4)), dim3(256), 0, st, s->tree.idx_sorted, s->tree.inv, n,
+                       s->rp[a], s->col[a], s->val[a], s->rp[b], s->col[b], s->val[b]);
+    TSNE_LAUNCH_CHECK();
+    s->cur = b;
 }
 
 void opt_step(tsne_ctx *ctx, int32_t t) {
@@ -325,12 +474,14 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const double mom = (t <= n1) ? p.initial_momentum : p.final_momentum;
     const int want_loss = (t % 10 == 0);
     const int64_t n = s->n;
+    const int c = s->cur;
+    double *Y = s->Y[c];
     if (s->profile) {
         TSNE_HIP(hipMemsetAsync(s->visits, 0, sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 1. tree
-    bh_build(ctx, s->tree, s->Y);
+    bh_build(ctx, s->tree, Y);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's slice of sorted points
     bh_repulsion(ctx, s->tree, p.theta, s->r0, s->r1, s->F, s->z, s->profile ? s->visits : nullptr);
@@ -346,9 +497,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // 4. attraction + update for owned rows
     const int64_t rows = s->r1 - s->r0;
     const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * 16, 256));
-    hipLaunchKernelGGL(attract_kernel<1>, dim3(blocks), dim3(256), 0, st, s->row_ptr, s->col, s->val,
-                       s->r0, s->r1, s->Y, s->tree.inv, s->F, s->scal, p.metric, ex, want_loss,
-                       nullptr, s->Ynew, s->upd, s->gains, p.min_gain, mom, p.learning_rate, s->part);
+    hipLaunchKernelGGL(attract_kernel<1>, dim3(blocks), dim3(256), 0, st, s->rp[c], s->col[c], s->val[c],
+                       s->r0, s->r1, Y, s->tree.inv, s->F, s->scal, p.metric, ex, want_loss,
+                       nullptr, s->Ynew, s->upd[c], s->gains[c], p.min_gain, mom, p.learning_rate, s->part);
     TSNE_LAUNCH_CHECK();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     if (want_loss) {
@@ -366,8 +517,11 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 2, k, s->part);
         hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
     }
-    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 2, 256)), dim3(256), 0, st, s->Ynew, n, 2, s->scal + 2, s->Y);
+    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 2, 256)), dim3(256), 0, st, s->Ynew, n, 2, s->scal + 2, Y);
+    // the caller's Y, original order
+    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, Y, s->orig[c], n, s->Yu);
     TSNE_LAUNCH_CHECK();
+    if (t % RELABEL_EVERY == 0) relabel(ctx, s);
     if (s->profile) {
         TSNE_HIP(hipEventRecord(s->ev[5], st));
         TSNE_HIP(hipEventSynchronize(s->ev[5]));
@@ -380,6 +534,21 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipMemcpy(&v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
         s->last_visits = (int64_t)v;
     }
+}
+
+// Write upd / gains (and Y) back to the caller's buffers in the original order.
+void opt_sync(tsne_ctx *ctx) {
+    OptState *s = ctx->opt;
+    TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    hipStream_t st = ctx->stream;
+    gather_working_set(ctx, s);
+    const int c = s->cur;
+    const int64_t n = s->n;
+    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Y[c], s->orig[c], n, s->Yu);
+    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->upd[c], s->orig[c], n, s->updu);
+    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->gains[c], s->orig[c], n,
+                       s->gainsu);
+    TSNE_LAUNCH_CHECK();
 }
 
 int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap) {

@@ -56,6 +56,7 @@ SIGNATURES = {
     "tsne_dev_joint_distribution": (C.c_int, [P, P, P, P, I64, I64, P, P, P, PI64]),
     "tsne_dev_opt_setup": (C.c_int, [P, C.POINTER(Params), P, P, P, I64, P, P, P]),
     "tsne_dev_opt_step": (C.c_int, [P, I32]),
+    "tsne_dev_opt_sync": (C.c_int, [P]),
     "tsne_dev_opt_losses": (C.c_int, [P, P, P, I32, PI32]),
     "tsne_dev_opt_profile": (C.c_int, [P, I32, P, PI64]),
 }

@@ -181,6 +181,9 @@ class Context:
     def dev_opt_step(self, t):
         check(lib().tsne_dev_opt_step(self._h, t))
 
+    def dev_opt_sync(self):
+        check(lib().tsne_dev_opt_sync(self._h))
+
     def dev_opt_losses(self, cap=1024):
         keys = np.zeros(cap, dtype=np.int32)
         vals = np.zeros(cap)
