@@ -121,14 +121,12 @@ __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const doubl
 }
 
 __global__ void gather_sorted(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted,
-                              int64_t n, double2 *__restrict__ pos, float2 *__restrict__ pos32,
-                              int32_t *__restrict__ inv) {
+                              int64_t n, double2 *__restrict__ pos, int32_t *__restrict__ inv) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     int32_t i = idx_sorted[s];
     const double x = Y[2 * i], y = Y[2 * i + 1];
     pos[s] = make_double2(x, y);
-    pos32[s] = make_float2((float)x, (float)y);
     inv[i] = (int32_t)s;
 }
 
@@ -195,8 +193,17 @@ __device__ __forceinline__ double ld_sys(const double *p) {
     return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+constexpr int AGG = 10;   // sx, sy, x0, x1, y0, y1, hmin, cnt, rball, (pad)
+
+// rball: radius of a disc around the node's centre of mass inside which a
+// query opens EVERY real cell of the subtree (so the subtree is all leaves
+// for it).  A cell u is opened by q iff h_u / D(q, c_u) >= theta, i.e. q lies
+// in the disc |q - c_u| <= sqrt(h_u / theta); ball(c_v, R_v) is inside
+// ball(c_c, R_c) when R_v + |c_v - c_c| <= R_c, hence
+// R_v = min(sqrt(h_v/theta) [real v], R_c - |c_v - c_c| over children c),
+// shrunk by a relative 1e-9 per level for rounding.  Leaves impose nothing.
 __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
-                          const double *__restrict__ Wp, BHNode *nodes, double *agg,
+                          const double *__restrict__ Wp, double inv_theta, BHNode *nodes, double *agg,
                           const int32_t *__restrict__ parent_leaf,
                           const int32_t *__restrict__ parent_node, int32_t *arrive) {
     const int m = meta[0];
@@ -210,7 +217,7 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
             return;                                      // first arriver stops
         const int32_t l = nodes[p].left, r = nodes[p].right, dl = nodes[p].delta;
         double a[2][7];                                  // sx, sy, x0, x1, y0, y1, hmin
-        double c[2];
+        double c[2], rb[2];
         const int32_t ch[2] = {l, r};
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -219,11 +226,13 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
                 a[k][0] = q.x; a[k][1] = q.y; a[k][2] = q.x; a[k][3] = q.x; a[k][4] = q.y; a[k][5] = q.y;
                 a[k][6] = __builtin_inf();
                 c[k] = 1.0;
+                rb[k] = __builtin_inf();
             } else {
-                const double *g = agg + 8 * (int64_t)ch[k];
+                const double *g = agg + AGG * (int64_t)ch[k];
 #pragma unroll
                 for (int f = 0; f < 7; ++f) a[k][f] = ld_sys(g + f);
                 c[k] = ld_sys(g + 7);
+                rb[k] = ld_sys(g + 8);
             }
         }
         const double cnt = c[0] + c[1];
@@ -238,16 +247,28 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
         else real = (nodes[par].delta >> 1) < dlev;      // first node of its quad level
         const double h = real ? ldexp(W, -dlev) : -1.0;  // -1 = transparent
         const double hmin = fmin(real ? h : __builtin_inf(), fmin(a[0][6], a[1][6]));
-        double *g = agg + 8 * (int64_t)p;
+        const double cx = sx / cnt, cy = sy / cnt;       // centerOfMass = sum / cumSize
+        double rball = real ? sqrt(h * inv_theta) : __builtin_inf();
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (ch[k] >= 0) {
+                const double ccx = a[k][0] / c[k], ccy = a[k][1] / c[k];
+                const double dd = sqrt((cx - ccx) * (cx - ccx) + (cy - ccy) * (cy - ccy));
+                rball = fmin(rball, rb[k] - dd);
+            }
+        }
+        rball = rball > 0.0 ? rball * (1.0 - 1e-9) : 0.0;
+        double *g = agg + AGG * (int64_t)p;
         st_sys(g + 0, sx); st_sys(g + 1, sy);
         st_sys(g + 2, x0); st_sys(g + 3, x1); st_sys(g + 4, y0); st_sys(g + 5, y1);
-        st_sys(g + 6, hmin); st_sys(g + 7, cnt);
+        st_sys(g + 6, hmin); st_sys(g + 7, cnt); st_sys(g + 8, rball);
         BHNode &nd = nodes[p];                           // read by the traversal (next launch)
-        nd.cx = sx / cnt;                                // centerOfMass = sum / cumSize
-        nd.cy = sy / cnt;
+        nd.cx = cx;
+        nd.cy = cy;
         nd.cnt = (int32_t)cnt;
         nd.h = h;
         nd.hmin = hmin;
+        nd.rball = rball;
         nd.bx0 = x0; nd.bx1 = x1; nd.by0 = y0; nd.by1 = y1;
         p = par;
     }
@@ -276,34 +297,21 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
     zs += r;
 }
 
-// The same pair term in fp32 for dense leaf tiles (pair terms only; the
-// per-chunk sums are accumulated in fp64 by the caller).  A pair whose fp32
-// squared distance is 0 (the query itself, exact duplicates, and points equal
-// to it within fp32 rounding) contributes nothing.
-__device__ __forceinline__ void leaf_force32(float qx, float qy, float px, float py, float &fx,
-                                             float &fy, float &zs) {
-    const float dx = qx - px, dy = qy - py;
-    const float D = __fmaf_rn(dx, dx, dy * dy);
-    float r = __builtin_amdgcn_rcpf(1.0f + D);
-    r = (D == 0.0f) ? 0.0f : r;
-    const float sc = r * r;
-    fx = __fmaf_rn(sc, dx, fx);
-    fy = __fmaf_rn(sc, dy, fy);
-    zs += r;
-}
-
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
 // (node, lane mask).  Every lane takes exactly its own reference decision;
 // the wave visits the union of the lanes' opened nodes.  Fast path: if for a
-// lane EVERY real cell of a subtree would be opened (the largest squared
-// distance from the query to the subtree's bounding box is below
-// hmin/theta, with a rounding margin), the reference would reach every leaf
-// of that subtree, so the lane sums the subtree's leaves directly -- a dense
-// N-body tile over a contiguous range of sorted points, with no criterion
-// evaluations and no stack traffic.  That is the near-exact regime of a
-// small embedding.
+// lane EVERY real cell of a subtree would be opened, the reference would
+// reach every leaf of that subtree, so the lane sums the subtree's leaves
+// directly -- a dense N-body tile over a contiguous range of sorted points,
+// with no criterion evaluations and no stack traffic.  That is the
+// near-exact regime of a small embedding.
+// Two conservative all-open tests, either suffices (rounding margins kept):
+//  * ball: |q - com|^2 <= rball^2, where ball(com, rball) lies inside every
+//    descendant cell's "opened" disc |q - c_u|^2 <= h_u / theta (bottom_up);
+//  * box: max squared distance from q to the subtree's bounding box
+//    <= hmin / theta (hmin = smallest real cell half-width inside).
 __global__ __launch_bounds__(256) void bh_traverse(
-    const double2 *__restrict__ pos, const float2 *__restrict__ pos32, const BHNode *__restrict__ nodes,
+    const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
     const int32_t *__restrict__ meta, double theta, int64_t s0, int64_t s1,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
@@ -317,7 +325,6 @@ __global__ __launch_bounds__(256) void bh_traverse(
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
-    const float qxf = (float)qx, qyf = (float)qy;
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0;
     int sp = 0;
@@ -340,40 +347,35 @@ __global__ __launch_bounds__(256) void bh_traverse(
             continue;
         }
         const BHNode nd = nodes[ref];
-        // all-open test (per lane) -> direct tile over the subtree's leaves
+        // all-open tests (per lane) -> direct tile over the subtree's leaves
         bool tile = false;
         if (act) {
-            const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-            const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
-            const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-            const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-            tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12);
+            const double cdx = qx - nd.cx, cdy = qy - nd.cy;
+            const double dc = cdx * cdx + cdy * cdy;
+            tile = dc <= nd.rball * nd.rball * (1.0 - 1e-9);
+            if (!tile) {
+                const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+                const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
+                tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12);
+            }
         }
         const uint64_t tm = __ballot(tile);
         if (tm) {
-            // fp32 pair terms over 64-point chunks, chunk sums accumulated in fp64
             const int a = nd.first, b = nd.last;
             if (tile) nvis += (unsigned long long)(b - a + 1);
-            for (int c0 = a; c0 <= b; c0 += 64) {
-                const int c1 = min(b + 1, c0 + 64);
-                float ax = 0.f, ay = 0.f, az = 0.f;
-                int p = c0;
-                for (; p + 8 <= c1; p += 8) {
+            int p = a;
+            for (; p + 8 <= b + 1; p += 8) {
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        const float2 pp = pos32[p + u];
-                        leaf_force32(qxf, qyf, pp.x, pp.y, ax, ay, az);
-                    }
+                for (int u = 0; u < 8; ++u) {
+                    const double2 pp = pos[p + u];
+                    if (tile) leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
                 }
-                for (; p < c1; ++p) {
-                    const float2 pp = pos32[p];
-                    leaf_force32(qxf, qyf, pp.x, pp.y, ax, ay, az);
-                }
-                if (tile) {
-                    fx += (double)ax;
-                    fy += (double)ay;
-                    zs += (double)az;
-                }
+            }
+            for (; p <= b; ++p) {
+                const double2 pp = pos[p];
+                if (tile) leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
             }
             act = act && !tile;
         }
@@ -426,9 +428,8 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.idx_sorted = ws.get<int32_t>("bh.idx_sorted", n);
     t.inv = ws.get<int32_t>("bh.inv", n);
     t.pos = ws.get<double2>("bh.pos", n);
-    t.pos32 = ws.get<float2>("bh.pos32", n + 64);
     t.nodes = ws.get<BHNode>("bh.nodes", n);
-    t.agg = ws.get<double>("bh.agg", 8 * (size_t)n);
+    t.agg = ws.get<double>("bh.agg", AGG * (size_t)n);
     t.parent_leaf = ws.get<int32_t>("bh.parent_leaf", n);
     t.parent_node = ws.get<int32_t>("bh.parent_node", n);
     t.arrive = ws.get<int32_t>("bh.arrive", n);
@@ -443,7 +444,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.sort_tmp = ws.get<uint8_t>("bh.sort_tmp", tb);
 }
 
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY) {
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
     hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
@@ -453,10 +454,11 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY) {
     size_t tb = t.sort_tmp_bytes;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
                                                (int)n, 0, 64, st));
-    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.pos32, t.inv);
+    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
                        t.nodes, t.parent_leaf, t.parent_node, t.arrive);
-    hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, t.nodes,
+    const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
+    hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
     TSNE_LAUNCH_CHECK();
@@ -466,7 +468,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                   double2 *dF, double *dz, unsigned long long *visits) {
     if (s1 <= s0) return;
     const int64_t waves = ceil_div(s1 - s0, 64);
-    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.pos32, t.nodes,
+    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes,
                        t.meta, theta, s0, s1, dF, dz, visits);
     TSNE_LAUNCH_CHECK();
 }

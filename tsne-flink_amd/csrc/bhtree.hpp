@@ -18,7 +18,7 @@ struct __attribute__((aligned(16))) BHNode {
     int32_t right;
     int32_t delta;    // common-prefix length in bits (62+ = key tie)
     int32_t first, last;  // leaf range [first, last] in sorted order
-    int32_t pad0, pad1;
+    double rball;     // all-open ball radius around (cx, cy), see bottom_up
 };
 
 struct BHTree {
@@ -28,9 +28,8 @@ struct BHTree {
     int32_t *idx = nullptr, *idx_sorted = nullptr;  // sorted position -> original row
     int32_t *inv = nullptr;                         // original row -> sorted position
     double2 *pos = nullptr;                         // sorted positions (leaves + queries)
-    float2 *pos32 = nullptr;                        // the same rounded to fp32 (dense tiles)
     BHNode *nodes = nullptr;
-    double *agg = nullptr;      // per-node bottom-up aggregates (8 doubles)
+    double *agg = nullptr;      // per-node bottom-up aggregates (AGG doubles)
     int32_t *parent_leaf = nullptr, *parent_node = nullptr;
     int32_t *arrive = nullptr;
     int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref
@@ -43,7 +42,7 @@ struct BHTree {
 // Allocate (from ctx->ws) for n points.
 void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
 // Build the tree of all n points of Y (n x 2, device).
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY);
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta);
 // Repulsion for sorted positions [s0, s1): F (double2) and z (sum of Q)
 // written at the sorted position; visits (nullable) += node evaluations.
 void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,

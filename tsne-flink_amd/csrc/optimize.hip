@@ -337,7 +337,7 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     hipStream_t st = ctx->stream;
     BHTree t;
     bh_alloc(ctx, t, n);
-    bh_build(ctx, t, dY);
+    bh_build(ctx, t, dY, theta);
     double2 *F = ctx->ws.get<double2>("grad.F", n);
     double *z = ctx->ws.get<double>("grad.z", n);
     double *part = ctx->ws.get<double>("grad.part", NPART);
@@ -481,7 +481,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 1. tree
-    bh_build(ctx, s->tree, Y);
+    bh_build(ctx, s->tree, Y, p.theta);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's slice of sorted points
     bh_repulsion(ctx, s->tree, p.theta, s->r0, s->r1, s->F, s->z, s->profile ? s->visits : nullptr);
