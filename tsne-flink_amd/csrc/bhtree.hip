@@ -297,6 +297,41 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
     zs += r;
 }
 
+// Pair term for dense tiles, without the equality test (see the caller):
+// r = 1/(1 + dx^2 + dy^2) with the 1 folded into the FMA chain.
+__device__ __forceinline__ void pair_force(double qx, double qy, double px, double py, double &fx,
+                                           double &fy, double &zs) {
+    const double dx = qx - px, dy = qy - py;
+    const double x = __fma_rn(dx, dx, __fma_rn(dy, dy, 1.0));
+    double r = __builtin_amdgcn_rcp(x);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    const double sc = r * r;
+    fx = __fma_rn(sc, dx, fx);
+    fy = __fma_rn(sc, dy, fy);
+    zs += r;
+}
+
+// Number of points whose coordinates equal pos[s] exactly (itself included);
+// they sit in the same equal-key run of the sorted order.
+__global__ void dup_count(const double2 *__restrict__ pos, const uint64_t *__restrict__ keys, int64_t n,
+                          int32_t *__restrict__ dupc) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const double2 q = pos[s];
+    const uint64_t k = keys[s];
+    int32_t c = 1;
+    for (int64_t t = s - 1; t >= 0 && keys[t] == k; --t) {
+        const double2 p = pos[t];
+        c += (p.x == q.x && p.y == q.y);
+    }
+    for (int64_t t = s + 1; t < n && keys[t] == k; ++t) {
+        const double2 p = pos[t];
+        c += (p.x == q.x && p.y == q.y);
+    }
+    dupc[s] = c;
+}
+
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
 // (node, lane mask).  Every lane takes exactly its own reference decision;
 // the wave visits the union of the lanes' opened nodes.  Fast path: if for a
@@ -311,11 +346,12 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
 //  * box: max squared distance from q to the subtree's bounding box
 //    <= hmin / theta (hmin = smallest real cell half-width inside).
 __global__ __launch_bounds__(256) void bh_traverse(
-    const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+    const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const int32_t *__restrict__ meta, double theta, int64_t s0, int64_t s1,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
+    __shared__ double2 tbuf[4][64];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t s = s0 + ((int64_t)blockIdx.x * 4 + w) * 64 + lane;
     const bool valid = s < s1;
@@ -365,17 +401,50 @@ __global__ __launch_bounds__(256) void bh_traverse(
         if (tm) {
             const int a = nd.first, b = nd.last;
             if (tile) nvis += (unsigned long long)(b - a + 1);
-            int p = a;
-            for (; p + 8 <= b + 1; p += 8) {
+            if (nd.delta < 62) {
+                // The range holds whole equal-key runs, so either all of the query's
+                // exact duplicates (itself included) are in it or none is.  They add
+                // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
+                // unmasked and the duplicate count is taken off z once.
+                // Points are staged through LDS 64 at a time (one coalesced
+                // dwordx4 load per lane, the next chunk prefetched into registers)
+                // and read back as wave-uniform broadcasts.
+                double tx = 0.0, ty = 0.0, tz = 0.0;
+                double2 *buf = tbuf[w];
+                double2 nxt = make_double2(0.0, 0.0);
+                if (a + lane <= b) nxt = pos[a + lane];
+                for (int c0 = a; c0 <= b; c0 += 64) {
+                    const int cnt = min(64, b - c0 + 1);
+                    __builtin_amdgcn_wave_barrier();
+                    buf[lane] = nxt;
+                    if (c0 + 64 + lane <= b) nxt = pos[c0 + 64 + lane];
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+                    __builtin_amdgcn_wave_barrier();
+                    int j = 0;
+                    for (; j + 8 <= cnt; j += 8) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const double2 pp = pos[p + u];
+                        for (int u = 0; u < 8; ++u) {
+                            const double2 pp = buf[j + u];
+                            pair_force(qx, qy, pp.x, pp.y, tx, ty, tz);
+                        }
+                    }
+                    for (; j < cnt; ++j) {
+                        const double2 pp = buf[j];
+                        pair_force(qx, qy, pp.x, pp.y, tx, ty, tz);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (tile) {
+                    fx += tx;
+                    fy += ty;
+                    zs += tz - ((s >= a && s <= b) ? (double)dupc[s] : 0.0);
+                }
+            } else {
+                for (int p = a; p <= b; ++p) {
+                    const double2 pp = pos[p];
                     if (tile) leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
                 }
-            }
-            for (; p <= b; ++p) {
-                const double2 pp = pos[p];
-                if (tile) leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
             }
             act = act && !tile;
         }
@@ -427,6 +496,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.idx = ws.get<int32_t>("bh.idx", n);
     t.idx_sorted = ws.get<int32_t>("bh.idx_sorted", n);
     t.inv = ws.get<int32_t>("bh.inv", n);
+    t.dupc = ws.get<int32_t>("bh.dupc", n);
     t.pos = ws.get<double2>("bh.pos", n);
     t.nodes = ws.get<BHNode>("bh.nodes", n);
     t.agg = ws.get<double>("bh.agg", AGG * (size_t)n);
@@ -455,6 +525,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
                                                (int)n, 0, 64, st));
     hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
+    hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc);
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
                        t.nodes, t.parent_leaf, t.parent_node, t.arrive);
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
@@ -468,7 +539,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                   double2 *dF, double *dz, unsigned long long *visits) {
     if (s1 <= s0) return;
     const int64_t waves = ceil_div(s1 - s0, 64);
-    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes,
+    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
                        t.meta, theta, s0, s1, dF, dz, visits);
     TSNE_LAUNCH_CHECK();
 }

@@ -27,6 +27,7 @@ struct BHTree {
     uint64_t *keys = nullptr, *keys_sorted = nullptr;
     int32_t *idx = nullptr, *idx_sorted = nullptr;  // sorted position -> original row
     int32_t *inv = nullptr;                         // original row -> sorted position
+    int32_t *dupc = nullptr;                        // exact duplicates of each sorted point (incl. itself)
     double2 *pos = nullptr;                         // sorted positions (leaves + queries)
     BHNode *nodes = nullptr;
     double *agg = nullptr;      // per-node bottom-up aggregates (AGG doubles)
