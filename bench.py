@@ -160,6 +160,7 @@ def main():
     snaps = {}
     sync_barrier(world)
     t0 = time.perf_counter()
+    t_progress = t0
     for t in range(1, steps + 1):
         traced = a.trace and (t % a.trace == 0 or t == 1)
         if traced:
@@ -173,6 +174,9 @@ def main():
                              "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
         if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
             snaps[t] = Y[:n].cpu().numpy().copy()
+        if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
+            t_progress = time.perf_counter()
+            print(f"[bench] t={t}/{steps} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)
     sync_barrier(world)
     t_loop = max_over_ranks(time.perf_counter() - t0, world)
     losses = ctx.dev_opt_losses()
@@ -240,6 +244,7 @@ def cpu_baseline(snaps, a, n, steps):
     sel = np.random.default_rng(0).choice(n, q, replace=False)
     per_t = {}
     for t, Ys in sorted(snaps.items()):
+        print(f"[bench] cpu baseline sample at t={t}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         O.repulsion_queries(Ys, a.theta, Ys[sel], threads=threads)
         t_sample = time.perf_counter() - t0
