@@ -181,6 +181,21 @@ def test_gradient_matches_oracle(ctx, scale, theta, metric):
     assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
+@pytest.mark.parametrize("n,scale", [(20000, 1e-3), (20000, 0.03), (12000, 0.3)])
+def test_gradient_large_near_exact(ctx, n, scale):
+    """Near-exact regime of a small embedding at a size where the all-open
+    subtrees carry moments (moment path) and, at the larger scales, partly
+    fail the truncation bound (dense leaf tiles)."""
+    rp, col, val = random_problem(n, 10, seed=int(scale * 1000) + 3)
+    Y = np.random.default_rng(3).normal(size=(n, 2)) * scale
+    g, Z, loss = ctx.gradient(rp, col, val, Y, 0.5, exaggeration=12.0, want_loss=True)
+    r = O.gradient(rp, col, val, Y, 0.5, exaggeration=12.0, want_loss=True)
+    assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
+    assert np.abs(g - r["grad"]).max() <= 1e-9 * np.abs(r["grad"]).max()   # fp64-level in practice
+    assert abs(Z - r["Z"]) <= 1e-9 * r["Z"]
+    assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
+
+
 def test_gradient_points_outside_root_and_duplicates(ctx):
     # n = 2 on one side: W = range < |x| drops points from the reference tree
     n = 400

@@ -34,6 +34,33 @@ constexpr int LEVELS = 31;                 // 62 key bits
 constexpr uint64_t OUT_KEY = 1ull << 63;   // outside the root cell: sorts last
 constexpr int STACK = 128;                 // >= max tree depth (62 + 32) + 1
 
+// ---- Subtree moments (the all-open fast path, see bh_traverse)
+// For a subtree every cell of which a query would open, the reference sums
+// 1/(1+D) and (q-y)/(1+D)^2 over all of the subtree's points (A15 at every
+// leaf).  With u = y - c about the subtree's bounding-box centre c, v = q - c,
+// A = |v|^2, E = D - A = |u|^2 - 2 v.u and B = 1/(1+A):
+//   1/(1+D)   = B   sum_k (-B E)^k,        1/(1+D)^2 = B^2 sum_k (k+1) (-B E)^k,
+// a series in rho = B max|E| <= B (R^2 + 2 |v| R) (R = the box half-diagonal).
+// Truncated at k = MOM_ORDER, every term is a polynomial of degree <= 2k+1 in
+// u, so the subtree sums follow from its moments sum u_x^a u_y^b
+// (a + b <= MOM_DEG), shifted to the query.  The path is taken only when the
+// truncation bound (MOM_ORDER+2) rho^(MOM_ORDER+1) / (1-rho)^2 <= MOM_TOL,
+// i.e. the result equals the reference's exact leaf sum to ~1e-14 relative
+// (fp64 rounding level); otherwise the dense leaf tile runs.  This turns the
+// near-exact O(N^2) phase of a small embedding into
+// O(N) moment evaluations.
+constexpr int MOM_ORDER = 4;
+constexpr int MOM_DEG = 2 * MOM_ORDER + 1;
+constexpr int MOM_K = (MOM_DEG + 1) * (MOM_DEG + 2) / 2;
+constexpr int MOM_MIN_POINTS = 64;
+constexpr int MOM_CHUNK = 2048;
+constexpr double MOM_TOL = 1e-14;
+constexpr int MOM_TASKS = 16;   // moment tasks recorded per query; more -> dense tiles
+// moment (a, b), a + b <= MOM_DEG: rows of decreasing length
+__host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }
+__host__ __device__ constexpr double fact(int k) { return k <= 1 ? 1.0 : k * fact(k - 1); }
+__host__ __device__ constexpr double binom(int k, int i) { return fact(k) / (fact(i) * fact(k - i)); }
+
 __global__ void bbox_partial(const double *__restrict__ Y, int64_t n, double *__restrict__ part) {
     __shared__ double sm[4][4];
     double mnx = __builtin_inf(), mxx = -__builtin_inf(), mny = __builtin_inf(), mxy = -__builtin_inf();
@@ -77,6 +104,7 @@ __global__ void bbox_final(const double *__restrict__ part, int nb, double *__re
         const double a = sm[0][1] - sm[0][0], c = sm[0][3] - sm[0][2];
         *W = a > c ? a : c;  // scala.math.max(maxX - minX, maxY - minY)
         meta[0] = 0;
+        meta[2] = 0;
     }
 }
 
@@ -332,6 +360,220 @@ __global__ void dup_count(const double2 *__restrict__ pos, const uint64_t *__res
     dupc[s] = c;
 }
 
+
+// ---- subtree moments: chunk counts, item map, per-item partial sums, reduce
+__device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double &cy, double &R) {
+    cx = 0.5 * (nd.bx0 + nd.bx1);
+    cy = 0.5 * (nd.by0 + nd.by1);
+    const double ex = 0.5 * (nd.bx1 - nd.bx0), ey = 0.5 * (nd.by1 - nd.by0);
+    R = sqrt(ex * ex + ey * ey) * (1.0 + 1e-12);
+}
+
+__global__ void moment_count(const BHNode *__restrict__ nodes, int64_t n, const int32_t *__restrict__ meta,
+                             int32_t *__restrict__ cnt, int32_t *__restrict__ list, int32_t *__restrict__ meta_w) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const int m = meta[0];
+    int32_t c = 0;
+    if (i < m - 1) {
+        const BHNode &nd = nodes[i];
+        if (nd.cnt >= MOM_MIN_POINTS && nd.delta < 62) {
+            c = (nd.cnt + MOM_CHUNK - 1) / MOM_CHUNK;
+            list[atomicAdd(&meta_w[2], 1)] = (int32_t)i;
+        }
+    }
+    cnt[i] = c;
+}
+
+__global__ void moment_fill(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
+                            const int32_t *__restrict__ cnt, const int32_t *__restrict__ off,
+                            int32_t *__restrict__ item) {
+    const int nl = meta[2];
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nl; e += gridDim.x * blockDim.x) {
+        const int node = list[e];
+        for (int c = 0; c < cnt[node]; ++c) item[off[node] + c] = node;
+    }
+}
+
+// One wave per item (<= MOM_CHUNK points of one node): lanes accumulate the
+// scaled moments u_x^a u_y^b / (a! b!) in registers, then a fixed shuffle tree.
+__global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ pos,
+                                                    const BHNode *__restrict__ nodes,
+                                                    const int32_t *__restrict__ off, int64_t n,
+                                                    const int32_t *__restrict__ item,
+                                                    double *__restrict__ part) {
+    const int total = off[n];
+    const int lane = lane_id();
+    const int nw = gridDim.x * (blockDim.x >> 6);
+    for (int it = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < total; it += nw) {
+        const int node = __builtin_amdgcn_readfirstlane(item[it]);
+        const int c = it - off[node];
+        const BHNode &nd = nodes[node];
+        double cx, cy, R;
+        box_centre(nd, cx, cy, R);
+        const int p0 = nd.first + c * MOM_CHUNK;
+        const int p1 = min(nd.last + 1, p0 + MOM_CHUNK);
+        double acc[MOM_K];
+#pragma unroll
+        for (int k = 0; k < MOM_K; ++k) acc[k] = 0.0;
+        for (int p = p0 + lane; p < p1; p += 64) {
+            const double2 q = pos[p];
+            const double ux = q.x - cx, uy = q.y - cy;
+            double X[MOM_DEG + 1], Yv[MOM_DEG + 1];
+            X[0] = 1.0; Yv[0] = 1.0;
+#pragma unroll
+            for (int e = 1; e <= MOM_DEG; ++e) {
+                X[e] = X[e - 1] * ux * (1.0 / e);
+                Yv[e] = Yv[e - 1] * uy * (1.0 / e);
+            }
+#pragma unroll
+            for (int a = 0; a <= MOM_DEG; ++a)
+#pragma unroll
+                for (int b = 0; b <= MOM_DEG; ++b)
+                    if (a + b <= MOM_DEG) acc[midx(a, b)] = __fma_rn(X[a], Yv[b], acc[midx(a, b)]);
+        }
+#pragma unroll
+        for (int k = 0; k < MOM_K; ++k) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) part[(int64_t)it * MOM_K + k] = v;
+        }
+    }
+}
+
+// One wave per moment-carrying node: lanes over moments, chunks summed in order.
+__global__ void moment_reduce(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
+                              const int32_t *__restrict__ cnt, const int32_t *__restrict__ off,
+                              const double *__restrict__ part, double *__restrict__ mom) {
+    const int nl = meta[2];
+    const int lane = lane_id();
+    const int nw = gridDim.x * (blockDim.x >> 6);
+    for (int e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < nl; e += nw) {
+        const int node = list[e];
+        const int o = off[node], c = cnt[node];
+        for (int k = lane; k < MOM_K; k += 64) {
+            double s = 0.0;
+            for (int j = 0; j < c; ++j) s += part[(int64_t)(o + j) * MOM_K + k];
+            mom[(int64_t)node * MOM_K + k] = s;
+        }
+    }
+}
+
+// Subtree sums for one lane's query from the node's moments (see the header).
+// Returns z += sum 1/(1+D), (fx, fy) += sum (q - y)/(1+D)^2 over the subtree's
+// points, the query itself and its exact duplicates included (D = 0: they add
+// 1 to z and 0 to F; the traversal subtracts them).
+__device__ __forceinline__ void moment_eval(const double *mu, double vx, double vy, double &fx, double &fy,
+                                            double &zs) {
+    const double A = vx * vx + vy * vy;
+    const double B = 1.0 / (1.0 + A);
+    // omega_i (z) and phi_i (F) weights of S_i = sum D^i, Sx_i = sum D^i w
+    double om[MOM_ORDER + 1], ph[MOM_ORDER + 1];
+    {
+        double Ap[MOM_ORDER + 1], Bp[MOM_ORDER + 3];
+        Ap[0] = 1.0; Bp[0] = 1.0;
+#pragma unroll
+        for (int k = 1; k <= MOM_ORDER; ++k) Ap[k] = Ap[k - 1] * A;
+#pragma unroll
+        for (int k = 1; k <= MOM_ORDER + 2; ++k) Bp[k] = Bp[k - 1] * B;
+#pragma unroll
+        for (int i = 0; i <= MOM_ORDER; ++i) {
+            double so = 0.0, sp = 0.0;
+#pragma unroll
+            for (int k = 0; k <= MOM_ORDER; ++k) {
+                if (k < i) continue;
+                so += binom(k, i) * Ap[k - i] * Bp[k + 1];
+                sp += (k + 1) * binom(k, i) * Ap[k - i] * Bp[k + 2];
+            }
+            om[i] = (i & 1) ? -so : so;
+            ph[i] = (i & 1) ? sp : -sp;
+        }
+    }
+    // shift to the query: w = u - v; X[e] = (-v_x)^e / e!
+    double X[MOM_DEG + 1], Yv[MOM_DEG + 1];
+    X[0] = 1.0; Yv[0] = 1.0;
+#pragma unroll
+    for (int e = 1; e <= MOM_DEG; ++e) {
+        X[e] = X[e - 1] * (-vx) * (1.0 / e);
+        Yv[e] = Yv[e - 1] * (-vy) * (1.0 / e);
+    }
+    double z = 0.0, gx = 0.0, gy = 0.0;
+#pragma unroll
+    for (int a = 0; a <= MOM_DEG; ++a) {
+        double lam[MOM_DEG + 1];         // lam[b'] = sum_a' mu(a', b') X[a - a']
+#pragma unroll
+        for (int b1 = 0; b1 <= MOM_DEG; ++b1) {
+            if (a + b1 > MOM_DEG) continue;
+            double t = 0.0;
+#pragma unroll
+            for (int a1 = 0; a1 <= MOM_DEG; ++a1)
+                if (a1 <= a) t = __fma_rn(mu[midx(a1, b1)], X[a - a1], t);
+            lam[b1] = t;
+        }
+#pragma unroll
+        for (int b = 0; b <= MOM_DEG; ++b) {
+            if (a + b > MOM_DEG) continue;
+            if ((a & 1) && (b & 1)) continue;
+            if (!(a & 1) && !(b & 1) && a + b > 2 * MOM_ORDER) continue;
+            double nu = 0.0;   // nu(a, b) / (a! b!) = sum_j w_x^a w_y^b / (a! b!)
+#pragma unroll
+            for (int b1 = 0; b1 <= MOM_DEG; ++b1)
+                if (b1 <= b) nu = __fma_rn(lam[b1], Yv[b - b1], nu);
+            if (!(a & 1) && !(b & 1)) {
+                const int i = (a + b) / 2;
+                z = __fma_rn(om[i] * (binom(i, a / 2) * fact(a) * fact(b)), nu, z);
+            } else if (a & 1) {
+                const int i = (a + b - 1) / 2;
+                gx = __fma_rn(ph[i] * (binom(i, (a - 1) / 2) * fact(a) * fact(b)), nu, gx);
+            } else {
+                const int i = (a + b - 1) / 2;
+                gy = __fma_rn(ph[i] * (binom(i, a / 2) * fact(a) * fact(b)), nu, gy);
+            }
+        }
+    }
+    zs += z;
+    fx += gx;
+    fy += gy;
+}
+
+// Truncation test of the moment path for query q and node nd.
+__device__ __forceinline__ bool moment_ok(const BHNode &nd, double qx, double qy) {
+    double cx, cy, R;
+    box_centre(nd, cx, cy, R);
+    const double vx = qx - cx, vy = qy - cy;
+    const double A = vx * vx + vy * vy;
+    const double rho = (R * R + 2.0 * sqrt(A) * R) / (1.0 + A) * (1.0 + 1e-12);
+    if (!(rho < 0.25)) return false;
+    double rp = rho;
+#pragma unroll
+    for (int k = 0; k < MOM_ORDER; ++k) rp *= rho;
+    return (MOM_ORDER + 2) * rp <= MOM_TOL * (1.0 - rho) * (1.0 - rho);
+}
+
+// Moment tasks of each query (sorted positions [s0, s1)), in traversal order,
+// added to the traversal's F and z.
+__global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ pos,
+                                                    const BHNode *__restrict__ nodes,
+                                                    const double *__restrict__ mom,
+                                                    const int32_t *__restrict__ mtask,
+                                                    const int32_t *__restrict__ mtask_n, int64_t s0,
+                                                    int64_t s1, double2 *__restrict__ F, double *__restrict__ Z) {
+    const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= s1) return;
+    const int nt = mtask_n[s - s0];
+    if (nt == 0) return;
+    const double2 q = pos[s];
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    for (int k = 0; k < nt; ++k) {
+        const int node = mtask[(s - s0) * MOM_TASKS + k];
+        double cx, cy, R;
+        box_centre(nodes[node], cx, cy, R);
+        moment_eval(mom + (int64_t)node * MOM_K, q.x - cx, q.y - cy, fx, fy, zs);
+    }
+    const double2 f = F[s];
+    F[s] = make_double2(f.x + fx, f.y + fy);
+    Z[s] = Z[s] + zs;
+}
+
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
 // (node, lane mask).  Every lane takes exactly its own reference decision;
 // the wave visits the union of the lanes' opened nodes.  Fast path: if for a
@@ -347,7 +589,8 @@ __global__ void dup_count(const double2 *__restrict__ pos, const uint64_t *__res
 //    <= hmin / theta (hmin = smallest real cell half-width inside).
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
-    const int32_t *__restrict__ meta, double theta, int64_t s0, int64_t s1,
+    int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n, const int32_t *__restrict__ meta, double theta,
+    int64_t s0, int64_t s1,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
@@ -364,6 +607,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0;
     int sp = 0;
+    int ntask = 0;
     const uint64_t vmask = __ballot(valid);
     if (root != INT32_MIN) {
         if (lane == 0) { sref[w][0] = root; smask[w][0] = vmask; }
@@ -406,13 +650,24 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 // exact duplicates (itself included) are in it or none is.  They add
                 // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
                 // unmasked and the duplicate count is taken off z once.
-                // Points are staged through LDS 64 at a time (one coalesced
-                // dwordx4 load per lane, the next chunk prefetched into registers)
-                // and read back as wave-uniform broadcasts.
+                // Moment path first (lanes whose truncation bound holds), then the
+                // dense tile for the rest: points staged through LDS 64 at a time
+                // (one coalesced dwordx4 load per lane, the next chunk prefetched
+                // into registers) and read back as wave-uniform broadcasts.
+                // Lanes whose truncation bound holds record a moment task (evaluated
+                // by moment_apply after the traversal, in recording order).
+                bool usem = false;
+                if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
+                    usem = moment_ok(nd, qx, qy);
+                    if (usem) mtask[(s - s0) * MOM_TASKS + ntask++] = ref;
+                }
                 double tx = 0.0, ty = 0.0, tz = 0.0;
+                const bool dense = tile && !usem;
+                if (__ballot(dense)) {
                 double2 *buf = tbuf[w];
                 double2 nxt = make_double2(0.0, 0.0);
                 if (a + lane <= b) nxt = pos[a + lane];
+                double ux = 0.0, uy = 0.0, uz = 0.0;
                 for (int c0 = a; c0 <= b; c0 += 64) {
                     const int cnt = min(64, b - c0 + 1);
                     __builtin_amdgcn_wave_barrier();
@@ -426,15 +681,17 @@ __global__ __launch_bounds__(256) void bh_traverse(
 #pragma unroll
                         for (int u = 0; u < 8; ++u) {
                             const double2 pp = buf[j + u];
-                            pair_force(qx, qy, pp.x, pp.y, tx, ty, tz);
+                            pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
                         }
                     }
                     for (; j < cnt; ++j) {
                         const double2 pp = buf[j];
-                        pair_force(qx, qy, pp.x, pp.y, tx, ty, tz);
+                        pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
+                if (dense) { tx = ux; ty = uy; tz = uz; }
+                }
                 if (tile) {
                     fx += tx;
                     fy += ty;
@@ -479,6 +736,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (valid) {
         F[s] = make_double2(fx, fy);
         Z[s] = zs;
+        mtask_n[s - s0] = ntask;
     }
     if (visits) {
         unsigned long long tot = wave_sum(nvis);
@@ -504,6 +762,21 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.parent_node = ws.get<int32_t>("bh.parent_node", n);
     t.arrive = ws.get<int32_t>("bh.arrive", n);
     t.meta = ws.get<int32_t>("bh.meta", 4);
+    t.mom = ws.get<double>("bh.mom", (size_t)n * MOM_K);
+    t.mom_cnt = ws.get<int32_t>("bh.mom_cnt", n + 1);
+    t.mom_off = ws.get<int32_t>("bh.mom_off", n + 1);
+    t.mom_list = ws.get<int32_t>("bh.mom_list", n);
+    // items <= sum over moment nodes of (cnt / MOM_CHUNK + 1); every point lies in
+    // at most 94 nested nodes (62 key bits + 32 tie-break bits)
+    t.mom_items_cap = n + ceil_div(n * 94, MOM_CHUNK);
+    t.mom_item = ws.get<int32_t>("bh.mom_item", t.mom_items_cap);
+    t.mom_part = ws.get<double>("bh.mom_part", (size_t)t.mom_items_cap * MOM_K);
+    t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
+    t.mtask_n = ws.get<int32_t>("bh.mtask_n", n);
+    size_t sb = 0;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, t.mom_cnt, t.mom_off, (int)(n + 1), ctx->stream));
+    t.scan_tmp_bytes = sb;
+    t.scan_tmp = ws.get<uint8_t>("bh.scan_tmp", sb);
     t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
     t.bbox_part = ws.get<double>("bh.bbox_part", 4 * (size_t)t.bbox_blocks);
     t.W = ws.get<double>("bh.W", 1);
@@ -532,6 +805,18 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
+    // subtree moments for the all-open fast path
+    hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_cnt,
+                       t.mom_list, t.meta);
+    size_t sb = t.scan_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.scan_tmp, sb, t.mom_cnt, t.mom_off, (int)(n + 1), st));
+    const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
+    hipLaunchKernelGGL(moment_fill, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
+                       t.mom_item);
+    hipLaunchKernelGGL(moment_items, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n, t.mom_item,
+                       t.mom_part);
+    hipLaunchKernelGGL(moment_reduce, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
+                       t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
 }
 
@@ -540,7 +825,9 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     if (s1 <= s0) return;
     const int64_t waves = ceil_div(s1 - s0, 64);
     hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.meta, theta, s0, s1, dF, dz, visits);
+                       t.mtask, t.mtask_n, t.meta, theta, s0, s1, dF, dz, visits);
+    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
+                       t.mtask, t.mtask_n, s0, s1, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

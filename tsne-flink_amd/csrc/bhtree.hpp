@@ -33,7 +33,19 @@ struct BHTree {
     double *agg = nullptr;      // per-node bottom-up aggregates (AGG doubles)
     int32_t *parent_leaf = nullptr, *parent_node = nullptr;
     int32_t *arrive = nullptr;
-    int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref
+    int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref, [2] = moment nodes
+    // subtree moments (see bhtree.hip "Subtree moments"): per internal node
+    // MOM_K scaled moments about its bounding-box centre, for nodes of
+    // >= MOM_MIN_POINTS points; built in chunks of MOM_CHUNK points.
+    double *mom = nullptr;       // n x MOM_K
+    double *mom_part = nullptr;  // item x MOM_K partial sums
+    int32_t *mom_cnt = nullptr, *mom_off = nullptr;  // chunks per node, exclusive scan (n + 1)
+    int32_t *mom_list = nullptr;                     // nodes that carry moments
+    int32_t *mom_item = nullptr;                     // item -> node
+    int32_t *mtask = nullptr, *mtask_n = nullptr;    // per query: moment tasks (node ids), count
+    int64_t mom_items_cap = 0;
+    void *scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
     double *bbox_part = nullptr, *W = nullptr;
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
