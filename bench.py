@@ -170,7 +170,9 @@ def main():
             ms_t, vis_t = ctx.dev_opt_profile(0)
             timeline.append({"t": t, "tree_ms": ms_t[0], "bh_ms": ms_t[1], "exchange_ms": ms_t[2],
                              "attract_ms": ms_t[3], "centre_ms": ms_t[4],
-                             "visits_per_point": vis_t / max(1, r1 - r0),
+                             "visits_per_point": vis_t[0] / max(1, r1 - r0),
+                             "moment_evals_per_point": vis_t[1] / max(1, r1 - r0),
+                             "dense_pairs_per_point": vis_t[2] / max(1, r1 - r0),
                              "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
         if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
             snaps[t] = Y[:n].cpu().numpy().copy()

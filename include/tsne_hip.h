@@ -177,9 +177,11 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
 /* Per-stage timing of the last step (HIP events on the ctx stream), in ms:
  * [0] tree build, [1] BH repulsion kernel, [2] (F, z) exchange + Z reduce,
  * [3] attraction + update kernel, [4] loss, embedding exchange, centring.
- * Also the number of BH node evaluations (lane visits) of the last step.
+ * Also BH work counters of the last step (visits_out3, may be NULL):
+ * [0] reference-equivalent node evaluations (lane visits; a leaf tile of m
+ * points counts m), [1] subtree-moment evaluations, [2] dense pair terms.
  * enable: 1 on, 0 off, -1 leave unchanged. */
-int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *visits_out);
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *visits_out3);
 
 #ifdef __cplusplus
 }

@@ -181,7 +181,7 @@ def test_gradient_matches_oracle(ctx, scale, theta, metric):
     assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
-@pytest.mark.parametrize("n,scale", [(20000, 1e-3), (20000, 0.03), (12000, 0.3)])
+@pytest.mark.parametrize("n,scale", [(20000, 1e-4), (20000, 1e-3), (20000, 0.03), (12000, 0.3)])
 def test_gradient_large_near_exact(ctx, n, scale):
     """Near-exact regime of a small embedding at a size where the all-open
     subtrees carry moments (moment path) and, at the larger scales, partly
@@ -320,3 +320,30 @@ def test_device_optimizer_matches_host_path(ctx):
     assert np.array_equal(dY.cpu().numpy(), Yh)
     assert np.array_equal(du.cpu().numpy(), uh) and np.array_equal(dg.cpu().numpy(), gh)
     assert ctx.dev_opt_losses() == lh
+
+
+def test_moment_path_engaged(ctx):
+    """Tiny embedding (the first iterations): every query's whole tree is one
+    near-exact subtree, evaluated from the root's moments (one moment task per
+    point, no dense pair terms), and the step still matches the host path."""
+    import torch
+    n = 20000
+    rp, col, val = random_problem(n, 10, seed=51)
+    Y0 = np.random.default_rng(9).normal(size=(n, 2)) * 1e-4
+    p = default_params(iterations=3, theta=0.5)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    dY, du, dg = t(Y0, torch.float64), torch.zeros((n, 2), dtype=torch.float64, device=dev), \
+        torch.ones((n, 2), dtype=torch.float64, device=dev)
+    ctx.dev_opt_setup(p, t(rp, torch.int64), t(col, torch.int32), t(val, torch.float64), n, dY, du, dg)
+    ctx.dev_opt_profile(1)
+    ctx.dev_opt_step(1)
+    _, cnt = ctx.dev_opt_profile(0)
+    assert cnt[1] == n and cnt[2] == 0, cnt
+    ctx.dev_opt_sync()
+    ctx.synchronize()
+    g = O.gradient(rp, col, val, Y0, 0.5, exaggeration=p.early_exaggeration)["grad"]
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    O.update(g, Yo, uo, go, p.min_gain, p.initial_momentum, p.learning_rate)
+    O.center(Yo)
+    assert np.abs(dY.cpu().numpy() - Yo).max() <= 1e-9 * np.abs(Yo).max()

@@ -55,7 +55,8 @@ constexpr int MOM_K = (MOM_DEG + 1) * (MOM_DEG + 2) / 2;
 constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-14;
-constexpr int MOM_TASKS = 16;   // moment tasks recorded per query; more -> dense tiles
+constexpr int MOM_TASKS = 32;   // moment tasks recorded per query; more -> dense tiles
+constexpr double BH_NEAR_TOL = 1e-10;   // near-exact subtree test (bh_traverse)
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
 __host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }
 __host__ __device__ constexpr double fact(int k) { return k <= 1 ? 1.0 : k * fact(k - 1); }
@@ -587,10 +588,19 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
 //    descendant cell's "opened" disc |q - c_u|^2 <= h_u / theta (bottom_up);
 //  * box: max squared distance from q to the subtree's bounding box
 //    <= hmin / theta (hmin = smallest real cell half-width inside).
+// A third test admits subtrees whose reference sum provably equals the exact
+// leaf sum to BH_NEAR_TOL relative: a cell c is summarised only when
+// h_c < theta D, and replacing its n_c points by their centre of mass changes
+// sum 1/(1+D) by at most (8 + 32 D) h_c^2 n_c (second-order Taylor; the first
+// order vanishes at the centre of mass) and sum (q-y)/(1+D)^2 by at most
+// ~24 sqrt(D) h_c^2 n_c.  With every point of the subtree within
+// D <= near_dmax of q (box corners), the relative deviation is below
+// ~48 theta^2 near_dmax^2 <= BH_NEAR_TOL (bh_near_dmax).  In the tiny-embedding
+// phase (extent ~1e-3) the root passes for every query: one moment task each.
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n, const int32_t *__restrict__ meta, double theta,
-    int64_t s0, int64_t s1,
+    double near_dmax, int64_t s0, int64_t s1,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
@@ -605,7 +615,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
     double fx = 0.0, fy = 0.0, zs = 0.0;
-    unsigned long long nvis = 0;
+    unsigned long long nvis = 0, ndense = 0;
     int sp = 0;
     int ntask = 0;
     const uint64_t vmask = __ballot(valid);
@@ -638,7 +648,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
                 const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
                 const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-                tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12);
+                tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
             }
         }
         const uint64_t tm = __ballot(tile);
@@ -690,7 +700,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
-                if (dense) { tx = ux; ty = uy; tz = uz; }
+                if (dense) { tx = ux; ty = uy; tz = uz; ndense += (unsigned long long)(b - a + 1); }
                 }
                 if (tile) {
                     fx += tx;
@@ -738,9 +748,14 @@ __global__ __launch_bounds__(256) void bh_traverse(
         Z[s] = zs;
         mtask_n[s - s0] = ntask;
     }
-    if (visits) {
-        unsigned long long tot = wave_sum(nvis);
-        if (lane == 0) atomicAdd(visits, tot);
+    if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms
+        const unsigned long long tv = wave_sum(nvis), tt = wave_sum((unsigned long long)ntask),
+                                 td = wave_sum(ndense);
+        if (lane == 0) {
+            atomicAdd(visits, tv);
+            atomicAdd(visits + 1, tt);
+            atomicAdd(visits + 2, td);
+        }
     }
 }
 
@@ -820,12 +835,21 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     TSNE_LAUNCH_CHECK();
 }
 
+// Largest D for which 48 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL (see bh_traverse).
+double bh_near_dmax(double theta) {
+    if (!(theta > 0.0)) return __builtin_inf();   // theta = 0: the reference opens every cell
+    double d = std::sqrt(BH_NEAR_TOL / (48.0 * theta * theta));
+    while (48.0 * theta * theta * d * d * (1.0 + 8.0 * d) > BH_NEAR_TOL) d *= 0.99;
+    return d;
+}
+
 void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits) {
     if (s1 <= s0) return;
+    const double near_dmax = bh_near_dmax(theta);
     const int64_t waves = ceil_div(s1 - s0, 64);
     hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.mtask, t.mtask_n, t.meta, theta, s0, s1, dF, dz, visits);
+                       t.mtask, t.mtask_n, t.meta, theta, near_dmax, s0, s1, dF, dz, visits);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, dF, dz);
     TSNE_LAUNCH_CHECK();

@@ -56,7 +56,7 @@ struct OptState {
     bool profile = false;
     hipEvent_t ev[6] = {};
     double last_ms[5] = {0, 0, 0, 0, 0};
-    int64_t last_visits = 0;
+    int64_t last_visits[3] = {0, 0, 0};
 };
 
 namespace {
@@ -120,58 +120,59 @@ __global__ void reduce_final(const double *__restrict__ part, int np, double *__
 }
 
 // MODE 0: grad only.  MODE 1: grad + updateEmbedding -> Ynew.
-// 16 lanes per CSR row (row_ptr indexed by the global row), 4 rows per wave;
-// each lane keeps 4 (col, val, Y_j) gathers in flight.
-template <int MODE>
+// LPR lanes per CSR row (row_ptr indexed by the global row), 64/LPR rows per
+// wave; each lane issues U (col, val) loads and then U dependent Y_j gathers
+// before any arithmetic, so a row of <= LPR*U entries costs two memory round
+// trips.  Tail slots gather Y_i with P = 0 (exact no-ops in the sums).  The
+// loss term (every 10th iteration) lives in its own instantiation so the
+// common path carries no log().
+template <int MODE, int LPR, int U, bool LOSS>
 __global__ __launch_bounds__(256) void attract_kernel(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
     const double *__restrict__ val, int64_t r0, int64_t r1, const double *__restrict__ Y,
     const int32_t *__restrict__ inv, const double2 *__restrict__ F, const double *__restrict__ scal,
-    int metric, double ex, int want_loss, double *__restrict__ grad, double *__restrict__ Ynew,
+    int metric, double ex, double *__restrict__ grad, double *__restrict__ Ynew,
     double *__restrict__ upd, double *__restrict__ gains, double min_gain, double mom, double lr,
     double *__restrict__ lpart) {
     __shared__ double sl[4];
-    const int sub = threadIdx.x & 15;
-    const int64_t i = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+    const int sub = threadIdx.x & (LPR - 1);
+    const int64_t i = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR);
     const double Z = scal[0];
     double lsum = 0.0;
     if (i < r1) {
         const double yx = Y[2 * i], yy = Y[2 * i + 1];
         double fx = 0.0, fy = 0.0;
         const int64_t e1 = row_ptr[i + 1];
-        int64_t e = row_ptr[i] + sub;
-        for (; e + 48 < e1; e += 64) {
-            int32_t j[4];
-            double pv[4];
+        for (int64_t e = row_ptr[i] + sub; e < e1; e += LPR * U) {
+            int32_t j[U];
+            double pv[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) { j[u] = col[e + 16 * u]; pv[u] = val[e + 16 * u]; }
-            double jx[4], jy[4];
+            for (int u = 0; u < U; ++u) {
+                const int64_t o = e + LPR * u;
+                const bool in = o < e1;
+                j[u] = in ? col[o] : (int32_t)i;
+                pv[u] = in ? val[o] : 0.0;
+            }
+            double jx[U], jy[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) { jx[u] = Y[2 * (int64_t)j[u]]; jy[u] = Y[2 * (int64_t)j[u] + 1]; }
+            for (int u = 0; u < U; ++u) {
+                const double2 yj = *reinterpret_cast<const double2 *>(Y + 2 * (int64_t)j[u]);
+                jx[u] = yj.x; jy[u] = yj.y;
+            }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const double pij = __dmul_rn(pv[u], ex);
                 const double q = qterm(yx, yy, jx[u], jy[u], metric);
-                const double s = __dmul_rn(pij, q);
-                fx = __dadd_rn(fx, __dmul_rn(s, __dsub_rn(yx, jx[u])));
-                fy = __dadd_rn(fy, __dmul_rn(s, __dsub_rn(yy, jy[u])));
-                if (want_loss) lsum += pij * log(pij / (q / Z));
+                const double sc = __dmul_rn(pij, q);
+                fx = __dadd_rn(fx, __dmul_rn(sc, __dsub_rn(yx, jx[u])));
+                fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yy, jy[u])));
+                if (LOSS && e + LPR * u < e1) lsum += pij * log(pij / (q / Z));
             }
         }
-        for (; e < e1; e += 16) {
-            const int32_t j = col[e];
-            const double pij = __dmul_rn(val[e], ex);
-            const double jx = Y[2 * (int64_t)j], jy = Y[2 * (int64_t)j + 1];
-            const double q = qterm(yx, yy, jx, jy, metric);
-            const double s = __dmul_rn(pij, q);
-            fx = __dadd_rn(fx, __dmul_rn(s, __dsub_rn(yx, jx)));
-            fy = __dadd_rn(fy, __dmul_rn(s, __dsub_rn(yy, jy)));
-            if (want_loss) lsum += pij * log(pij / (q / Z));
-        }
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            fx += __shfl_xor(fx, o, 16);
-            fy += __shfl_xor(fy, o, 16);
+        for (int o = LPR / 2; o > 0; o >>= 1) {
+            fx += __shfl_xor(fx, o, LPR);
+            fy += __shfl_xor(fy, o, LPR);
         }
         if (sub == 0) {
             const double2 f = F[inv[i]];
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(256) void attract_kernel(
             }
         }
     }
-    if (want_loss) {
+    if (LOSS) {
         lsum = wave_sum(lsum);
         if (lane_id() == 0) sl[threadIdx.x >> 6] = lsum;
         __syncthreads();
@@ -293,6 +294,53 @@ __global__ void relabel_rows(const int32_t *__restrict__ order, const int32_t *_
     }
 }
 
+
+// Attraction launch: variant (lanes per row x unroll) from TSNE_ATTRACT
+// ("16x4", "32x4", "64x4", "16x8", "32x8"); returns the block count (loss partials).
+struct AttractArgs {
+    const int64_t *rp; const int32_t *col; const double *val; int64_t r0, r1; const double *Y;
+    const int32_t *inv; const double2 *F; const double *scal; int metric; double ex;
+    double *grad, *Ynew, *upd, *gains; double min_gain, mom, lr; double *lpart;
+};
+
+template <int MODE, int LPR, int U>
+static int64_t attract_launch_v(hipStream_t st, const AttractArgs &a, bool loss) {
+    const int64_t rows = a.r1 - a.r0;
+    const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * LPR, 256));
+    if (loss)
+        hipLaunchKernelGGL((attract_kernel<MODE, LPR, U, true>), dim3(blocks), dim3(256), 0, st, a.rp, a.col, a.val,
+                           a.r0, a.r1, a.Y, a.inv, a.F, a.scal, a.metric, a.ex, a.grad, a.Ynew, a.upd, a.gains,
+                           a.min_gain, a.mom, a.lr, a.lpart);
+    else
+        hipLaunchKernelGGL((attract_kernel<MODE, LPR, U, false>), dim3(blocks), dim3(256), 0, st, a.rp, a.col,
+                           a.val, a.r0, a.r1, a.Y, a.inv, a.F, a.scal, a.metric, a.ex, a.grad, a.Ynew, a.upd,
+                           a.gains, a.min_gain, a.mom, a.lr, a.lpart);
+    return blocks;
+}
+
+static int attract_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("TSNE_ATTRACT");
+        const std::string s = e ? e : "";
+        v = s == "16x4" ? 0 : s == "32x4" ? 1 : s == "64x4" ? 2 : s == "16x8" ? 3 : s == "32x8" ? 4 : 1;
+    }
+    return v;
+}
+
+template <int MODE>
+static int64_t attract_launch(hipStream_t st, const AttractArgs &a, bool loss) {
+    switch (attract_variant()) {
+        case 0: return attract_launch_v<MODE, 16, 4>(st, a, loss);
+        case 2: return attract_launch_v<MODE, 64, 4>(st, a, loss);
+        case 3: return attract_launch_v<MODE, 16, 8>(st, a, loss);
+        case 4: return attract_launch_v<MODE, 32, 8>(st, a, loss);
+        default: return attract_launch_v<MODE, 32, 4>(st, a, loss);
+    }
+}
+
+// Upper bound of attract_launch's block count for rows rows.
+static int64_t attract_max_blocks(int64_t rows) { return std::max<int64_t>(1, ceil_div(rows * 64, 256)); }
 }  // namespace
 
 // ------------------------------------------------------------ single ops
@@ -345,12 +393,11 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     bh_repulsion(ctx, t, theta, 0, n, F, z, nullptr);
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, z, n, 1, 0, part);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, part, NPART, scal, 0.0);
-    const int64_t blocks = ceil_div(n * 16, 256);
-    double *lpart = ctx->ws.get<double>("grad.lpart", blocks);
-    const int want_loss = h_loss != nullptr;
-    hipLaunchKernelGGL(attract_kernel<0>, dim3(blocks), dim3(256), 0, st, d_row_ptr, d_col, d_P,
-                       (int64_t)0, n, dY, t.inv, F, scal, metric, exaggeration, want_loss, d_grad,
-                       nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, lpart);
+    double *lpart = ctx->ws.get<double>("grad.lpart", attract_max_blocks(n));
+    const bool want_loss = h_loss != nullptr;
+    AttractArgs aa{d_row_ptr, d_col, d_P, 0, n, dY, t.inv, F, scal, metric, exaggeration,
+                   d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, lpart};
+    const int64_t blocks = attract_launch<0>(st, aa, want_loss);
     TSNE_LAUNCH_CHECK();
     if (want_loss) hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, lpart, (int)blocks, scal + 1, 0.0);
     double hs[2] = {0, 0};
@@ -423,11 +470,11 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->F = ws.get<double2>("opt.F", s->npad);
     s->z = ws.get<double>("opt.z", s->npad);
     s->scal = ws.get<double>("opt.scal", 8);
-    s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, ceil_div(s->chunk * 16, 256)));
+    s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(s->chunk)));
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 1);
+    s->visits = ws.get<unsigned long long>("opt.visits", 3);
     TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
@@ -477,7 +524,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int c = s->cur;
     double *Y = s->Y[c];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 3 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 1. tree
@@ -495,11 +542,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 4. attraction + update for owned rows
-    const int64_t rows = s->r1 - s->r0;
-    const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * 16, 256));
-    hipLaunchKernelGGL(attract_kernel<1>, dim3(blocks), dim3(256), 0, st, s->rp[c], s->col[c], s->val[c],
-                       s->r0, s->r1, Y, s->tree.inv, s->F, s->scal, p.metric, ex, want_loss,
-                       nullptr, s->Ynew, s->upd[c], s->gains[c], p.min_gain, mom, p.learning_rate, s->part);
+    AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->tree.inv, s->F, s->scal, p.metric, ex,
+                   nullptr, s->Ynew, s->upd[c], s->gains[c], p.min_gain, mom, p.learning_rate, s->part};
+    const int64_t blocks = attract_launch<1>(st, aa, want_loss != 0);
     TSNE_LAUNCH_CHECK();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     if (want_loss) {
@@ -530,9 +575,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
             TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
-        unsigned long long v = 0;
-        TSNE_HIP(hipMemcpy(&v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
-        s->last_visits = (int64_t)v;
+        unsigned long long v[3] = {0, 0, 0};
+        TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 3; ++k) s->last_visits[k] = (int64_t)v[k];
     }
 }
 
@@ -575,7 +620,8 @@ void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits) {
     if (enable >= 0) s->profile = enable != 0;
     if (ms5)
         for (int k = 0; k < 5; ++k) ms5[k] = s->last_ms[k];
-    if (visits) *visits = s->last_visits;
+    if (visits)
+        for (int k = 0; k < 3; ++k) visits[k] = s->last_visits[k];
 }
 
 }  // namespace tsne

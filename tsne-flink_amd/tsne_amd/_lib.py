@@ -58,7 +58,7 @@ SIGNATURES = {
     "tsne_dev_opt_step": (C.c_int, [P, I32]),
     "tsne_dev_opt_sync": (C.c_int, [P]),
     "tsne_dev_opt_losses": (C.c_int, [P, P, P, I32, PI32]),
-    "tsne_dev_opt_profile": (C.c_int, [P, I32, P, PI64]),
+    "tsne_dev_opt_profile": (C.c_int, [P, I32, P, P]),
 }
 
 _lib = None

@@ -193,7 +193,8 @@ class Context:
         return dict(zip(keys[:k].tolist(), vals[:k].tolist()))
 
     def dev_opt_profile(self, enable=-1):
+        """-> (stage ms[5], BH counters [visits, moment evaluations, dense pair terms])"""
         ms = np.zeros(5)
-        visits = C.c_int64()
-        check(lib().tsne_dev_opt_profile(self._h, enable, _ptr(ms), C.byref(visits)))
-        return ms, visits.value
+        cnt = np.zeros(3, dtype=np.int64)
+        check(lib().tsne_dev_opt_profile(self._h, enable, _ptr(ms), _ptr(cnt)))
+        return ms, cnt.tolist()
