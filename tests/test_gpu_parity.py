@@ -193,7 +193,10 @@ def test_gradient_large_near_exact(ctx, n, scale):
     assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
     assert np.abs(g - r["grad"]).max() <= 1e-9 * np.abs(r["grad"]).max()   # fp64-level in practice
     assert abs(Z - r["Z"]) <= 1e-9 * r["Z"]
-    assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
+    if np.isnan(r["loss"]):   # some P_ij underflowed to 0: 0 * ln 0 (TsneHelpers.scala:300)
+        assert np.isnan(loss)
+    else:
+        assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
 def test_gradient_points_outside_root_and_duplicates(ctx):
