@@ -363,11 +363,15 @@ __global__ void dup_count(const double2 *__restrict__ pos, const uint64_t *__res
 
 
 // ---- subtree moments: chunk counts, item map, per-item partial sums, reduce
-__device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double &cy, double &R) {
-    cx = 0.5 * (nd.bx0 + nd.bx1);
-    cy = 0.5 * (nd.by0 + nd.by1);
-    const double ex = 0.5 * (nd.bx1 - nd.bx0), ey = 0.5 * (nd.by1 - nd.by0);
+__device__ __forceinline__ void box_centre(double bx0, double bx1, double by0, double by1, double &cx, double &cy,
+                                           double &R) {
+    cx = 0.5 * (bx0 + bx1);
+    cy = 0.5 * (by0 + by1);
+    const double ex = 0.5 * (bx1 - bx0), ey = 0.5 * (by1 - by0);
     R = sqrt(ex * ex + ey * ey) * (1.0 + 1e-12);
+}
+__device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double &cy, double &R) {
+    box_centre(nd.bx0, nd.bx1, nd.by0, nd.by1, cx, cy, R);
 }
 
 __global__ void moment_count(const BHNode *__restrict__ nodes, int64_t n, const int32_t *__restrict__ meta,
@@ -536,10 +540,10 @@ __device__ __forceinline__ void moment_eval(const double *mu, double vx, double 
     fy += gy;
 }
 
-// Truncation test of the moment path for query q and node nd.
-__device__ __forceinline__ bool moment_ok(const BHNode &nd, double qx, double qy) {
+// Truncation test of the moment path for query q and a subtree's bounding box.
+__device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, double by1, double qx, double qy) {
     double cx, cy, R;
-    box_centre(nd, cx, cy, R);
+    box_centre(bx0, bx1, by0, by1, cx, cy, R);
     const double vx = qx - cx, vy = qy - cy;
     const double A = vx * vx + vy * vy;
     const double rho = (R * R + 2.0 * sqrt(A) * R) / (1.0 + A) * (1.0 + 1e-12);
@@ -575,13 +579,88 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
     Z[s] = Z[s] + zs;
 }
 
+// fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
+// an IEEE division -- decided from a Newton-refined reciprocal, with the exact
+// division only within ~1e-14 (relative) of theta.
+__device__ __forceinline__ bool summarise(double h, double D, double theta) {
+    if (!(D > 1e-290)) return h / D < theta;   // 0, denormal or NaN: exact path
+    double r = __builtin_amdgcn_rcp(D);
+    r = __fma_rn(r, __fma_rn(-D, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-D, r, 1.0), r);
+    double qv = h * r;
+    qv = __fma_rn(__fma_rn(-D, qv, h), r, qv);
+    if (qv < theta * (1.0 - 1e-14)) return true;
+    if (qv > theta * (1.0 + 1e-14)) return false;
+    return h / D < theta;
+}
+
+// One summarised cell (QuadTree.scala:134-142): Q = 1/(1+D), m = n Q.
+__device__ __forceinline__ void cell_force(double dx, double dy, double D, int32_t n, double &fx, double &fy,
+                                           double &zs) {
+    const double x = 1.0 + D;
+    double Q = __builtin_amdgcn_rcp(x);
+    Q = __fma_rn(Q, __fma_rn(-x, Q, 1.0), Q);
+    Q = __fma_rn(Q, __fma_rn(-x, Q, 1.0), Q);
+    const double mult = __dmul_rn((double)n, Q);
+    const double sc = __dmul_rn(mult, Q);
+    fx = __dadd_rn(fx, __dmul_rn(sc, dx));
+    fy = __dadd_rn(fy, __dmul_rn(sc, dy));
+    zs = __dadd_rn(zs, mult);
+}
+
+// Quad records: one per real node, children found through transparent nodes.
+__global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos,
+                           const int32_t *__restrict__ meta, QRec *__restrict__ qrec) {
+    const int m = meta[0];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m - 1) return;
+    const BHNode &nd = nodes[i];
+    if (nd.h < 0.0) return;                 // transparent or key tie: no record
+    QRec &r = qrec[i];
+    r.cx = nd.cx; r.cy = nd.cy; r.rball = nd.rball; r.hmin = nd.hmin;
+    r.bx0 = nd.bx0; r.bx1 = nd.bx1; r.by0 = nd.by0; r.by1 = nd.by1;
+    r.first = nd.first; r.last = nd.last; r.cnt = nd.cnt;
+    // <= 3 transparent nodes per quad level: a 2-deep descent covers them
+    int32_t cand[4] = {nd.left, nd.right, 0, 0};
+    int ncand = 2;
+    int nc = 0;
+    auto put = [&](int32_t c) {
+        if (c < 0) {
+            const double2 p = pos[~c];
+            r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ch[nc] = QCH_LEAF; r.cref[nc] = c; r.ccnt[nc] = 1;
+        } else {
+            const BHNode &cn = nodes[c];
+            r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; r.ch[nc] = cn.delta >= 62 ? QCH_TIE : cn.h;
+            r.cref[nc] = c; r.ccnt[nc] = cn.cnt;
+        }
+        ++nc;
+    };
+    auto transparent = [&](int32_t c) { return c >= 0 && nodes[c].delta < 62 && nodes[c].h < 0.0; };
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int32_t c = cand[k];
+        if (transparent(c)) {
+            const int32_t l = nodes[c].left, rr = nodes[c].right;
+            if (transparent(l)) { put(nodes[l].left); put(nodes[l].right); } else put(l);
+            if (transparent(rr)) { put(nodes[rr].left); put(nodes[rr].right); } else put(rr);
+        } else {
+            put(c);
+        }
+    }
+    (void)ncand;
+    for (int k = nc; k < 4; ++k) { r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ch[k] = QCH_LEAF; r.cref[k] = 0; r.ccnt[k] = 0; }
+    r.nch = nc;
+}
+
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
-// (node, lane mask).  Every lane takes exactly its own reference decision;
-// the wave visits the union of the lanes' opened nodes.  Fast path: if for a
-// lane EVERY real cell of a subtree would be opened, the reference would
-// reach every leaf of that subtree, so the lane sums the subtree's leaves
-// directly -- a dense N-body tile over a contiguous range of sorted points,
-// with no criterion evaluations and no stack traffic.  That is the
+// (cell, lane mask) entries, one per cell that some lane OPENS.  Popping a
+// cell loads its quad record once; every lane that opened it then takes its
+// own reference decision for each quad child from the record (a leaf
+// interacts; a cell is summarised when max(hW,hH)/D < theta, else pushed with
+// the mask of the lanes that open it).  Fast path on pop: if for a lane EVERY
+// real cell of the subtree would be opened, the reference would reach every
+// leaf of it, so the lane sums the subtree's leaves directly (moment task or
+// dense tile over the contiguous range of sorted points).  That is the
 // near-exact regime of a small embedding.
 // Two conservative all-open tests, either suffices (rounding margins kept):
 //  * ball: |q - com|^2 <= rball^2, where ball(com, rball) lies inside every
@@ -599,8 +678,8 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
 // phase (extent ~1e-3) the root passes for every query: one moment task each.
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
-    int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n, const int32_t *__restrict__ meta, double theta,
-    double near_dmax, int64_t s0, int64_t s1,
+    const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
+    const int32_t *__restrict__ meta, double theta, double near_dmax, int64_t s0, int64_t s1,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
@@ -618,25 +697,38 @@ __global__ __launch_bounds__(256) void bh_traverse(
     unsigned long long nvis = 0, ndense = 0;
     int sp = 0;
     int ntask = 0;
-    const uint64_t vmask = __ballot(valid);
-    if (root != INT32_MIN) {
-        if (lane == 0) { sref[w][0] = root; smask[w][0] = vmask; }
-        sp = 1;
+    // ---- the root: a single point, a key-tie group, or a cell tested like any child
+    if (root == ~0) {
+        if (valid) { ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
+    } else if (root >= 0) {
+        const BHNode &rt = nodes[root];
+        if (rt.delta >= 62) {
+            for (int p = rt.first; p <= rt.last; ++p) {
+                const double2 pp = pos[p];
+                if (valid) { ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+            }
+        } else {
+            bool open = false;
+            if (valid) {
+                ++nvis;
+                const double dx = __dsub_rn(qx, rt.cx), dy = __dsub_rn(qy, rt.cy);
+                const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+                if (summarise(rt.h, D, theta)) cell_force(dx, dy, D, rt.cnt, fx, fy, zs);
+                else open = true;
+            }
+            const uint64_t om = __ballot(open);
+            if (om) {
+                if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
+                sp = 1;
+            }
+        }
     }
     while (sp > 0) {
         --sp;
         const int ref = __builtin_amdgcn_readfirstlane(sref[w][sp]);
         const uint64_t msk = smask[w][sp];
         bool act = (msk >> lane) & 1ull;
-        if (ref < 0) {
-            const double2 p = pos[~ref];
-            if (act) {
-                ++nvis;
-                leaf_force(qx, qy, p.x, p.y, fx, fy, zs);
-            }
-            continue;
-        }
-        const BHNode nd = nodes[ref];
+        const QRec &nd = qrec[ref];
         // all-open tests (per lane) -> direct tile over the subtree's leaves
         bool tile = false;
         if (act) {
@@ -651,29 +743,26 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
             }
         }
-        const uint64_t tm = __ballot(tile);
-        if (tm) {
+        if (__ballot(tile)) {
             const int a = nd.first, b = nd.last;
             if (tile) nvis += (unsigned long long)(b - a + 1);
-            if (nd.delta < 62) {
-                // The range holds whole equal-key runs, so either all of the query's
-                // exact duplicates (itself included) are in it or none is.  They add
-                // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
-                // unmasked and the duplicate count is taken off z once.
-                // Moment path first (lanes whose truncation bound holds), then the
-                // dense tile for the rest: points staged through LDS 64 at a time
-                // (one coalesced dwordx4 load per lane, the next chunk prefetched
-                // into registers) and read back as wave-uniform broadcasts.
-                // Lanes whose truncation bound holds record a moment task (evaluated
-                // by moment_apply after the traversal, in recording order).
-                bool usem = false;
-                if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
-                    usem = moment_ok(nd, qx, qy);
-                    if (usem) mtask[(s - s0) * MOM_TASKS + ntask++] = ref;
-                }
-                double tx = 0.0, ty = 0.0, tz = 0.0;
-                const bool dense = tile && !usem;
-                if (__ballot(dense)) {
+            // The range holds whole equal-key runs, so either all of the query's
+            // exact duplicates (itself included) are in it or none is.  They add
+            // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
+            // unmasked and the duplicate count is taken off z once.
+            // Lanes whose truncation bound holds record a moment task (evaluated
+            // by moment_apply after the traversal, in recording order); the rest
+            // run the dense tile: points staged through LDS 64 at a time (one
+            // coalesced dwordx4 load per lane, the next chunk prefetched into
+            // registers) and read back as wave-uniform broadcasts.
+            bool usem = false;
+            if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
+                usem = moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy);
+                if (usem) mtask[(s - s0) * MOM_TASKS + ntask++] = ref;
+            }
+            double tx = 0.0, ty = 0.0, tz = 0.0;
+            const bool dense = tile && !usem;
+            if (__ballot(dense)) {
                 double2 *buf = tbuf[w];
                 double2 nxt = make_double2(0.0, 0.0);
                 if (a + lane <= b) nxt = pos[a + lane];
@@ -701,46 +790,44 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (dense) { tx = ux; ty = uy; tz = uz; ndense += (unsigned long long)(b - a + 1); }
-                }
-                if (tile) {
-                    fx += tx;
-                    fy += ty;
-                    zs += tz - ((s >= a && s <= b) ? (double)dupc[s] : 0.0);
-                }
-            } else {
-                for (int p = a; p <= b; ++p) {
-                    const double2 pp = pos[p];
-                    if (tile) leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
-                }
+            }
+            if (tile) {
+                fx += tx;
+                fy += ty;
+                zs += tz - ((s >= a && s <= b) ? (double)dupc[s] : 0.0);
             }
             act = act && !tile;
         }
         if (__ballot(act) == 0) continue;
-        bool open = false;
-        if (nd.h < 0.0) {
-            open = act;                       // transparent: split inside a quad level
-        } else if (act) {
-            ++nvis;
-            const double dx = __dsub_rn(qx, nd.cx), dy = __dsub_rn(qy, nd.cy);
-            const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-            if (nd.h / D < theta) {           // max(hHeigth, hWidth) / D < theta
-                const double Q = 1.0 / (1.0 + D);
-                const double mult = __dmul_rn((double)nd.cnt, Q);
-                const double sc = __dmul_rn(mult, Q);
-                fx = __dadd_rn(fx, __dmul_rn(sc, dx));
-                fy = __dadd_rn(fy, __dmul_rn(sc, dy));
-                zs = __dadd_rn(zs, mult);
+        // the opened cell's quad children, from its record
+        const int nch = nd.nch;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c >= nch) break;
+            const double chh = nd.ch[c];
+            if (chh == QCH_LEAF) {
+                if (act) { ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
+            } else if (chh == QCH_TIE) {
+                const BHNode &tn = nodes[nd.cref[c]];
+                for (int p = tn.first; p <= tn.last; ++p) {
+                    const double2 pp = pos[p];
+                    if (act) { ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                }
             } else {
-                open = true;
+                bool open = false;
+                if (act) {
+                    ++nvis;
+                    const double dx = __dsub_rn(qx, nd.ccx[c]), dy = __dsub_rn(qy, nd.ccy[c]);
+                    const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+                    if (summarise(chh, D, theta)) cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                    else open = true;
+                }
+                const uint64_t om = __ballot(open);
+                if (om) {
+                    if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
+                    ++sp;
+                }
             }
-        }
-        const uint64_t om = __ballot(open);
-        if (om) {
-            if (lane == 0) {
-                sref[w][sp] = nd.right; smask[w][sp] = om;
-                sref[w][sp + 1] = nd.left; smask[w][sp + 1] = om;
-            }
-            sp += 2;
         }
     }
     if (valid) {
@@ -772,6 +859,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.dupc = ws.get<int32_t>("bh.dupc", n);
     t.pos = ws.get<double2>("bh.pos", n);
     t.nodes = ws.get<BHNode>("bh.nodes", n);
+    t.qrec = ws.get<QRec>("bh.qrec", n);
     t.agg = ws.get<double>("bh.agg", AGG * (size_t)n);
     t.parent_leaf = ws.get<int32_t>("bh.parent_leaf", n);
     t.parent_node = ws.get<int32_t>("bh.parent_node", n);
@@ -820,6 +908,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
+    hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, t.qrec);
     // subtree moments for the all-open fast path
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_cnt,
                        t.mom_list, t.meta);
@@ -849,7 +938,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     const double near_dmax = bh_near_dmax(theta);
     const int64_t waves = ceil_div(s1 - s0, 64);
     hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.mtask, t.mtask_n, t.meta, theta, near_dmax, s0, s1, dF, dz, visits);
+                       t.qrec, t.mtask, t.mtask_n, t.meta, theta, near_dmax, s0, s1, dF, dz, visits);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, dF, dz);
     TSNE_LAUNCH_CHECK();

@@ -21,6 +21,26 @@ struct __attribute__((aligned(16))) BHNode {
     double rball;     // all-open ball radius around (cx, cy), see bottom_up
 };
 
+// Quad-collapsed record of a real node (a reference quadtree cell): its own
+// tile-test data plus the summaries of its <= 4 quad children (found by
+// descending through transparent binary nodes), so that the traversal
+// evaluates all children of an opened cell from one record load and pushes
+// only children that some lane opens.  Child kinds (ch): >= 0 real cell of
+// half width ch (cref = node id); QCH_LEAF one point (cref = ~sorted index,
+// com = the point); QCH_TIE a key-tie group (cref = node id, all points
+// interact directly).
+constexpr double QCH_LEAF = -1.0;
+constexpr double QCH_TIE = -2.0;
+struct __attribute__((aligned(16))) QRec {
+    double cx, cy;              // centre of mass
+    double rball, hmin;         // all-open tests (see bottom_up)
+    double bx0, bx1, by0, by1;  // bounding box of the subtree's points
+    int32_t first, last;        // leaf range in sorted order
+    int32_t cnt, nch;           // cumSize, number of quad children
+    double ccx[4], ccy[4], ch[4];
+    int32_t cref[4], ccnt[4];
+};
+
 struct BHTree {
     int64_t n = 0;           // points (queries)
     // device arrays (ctx workspace)
@@ -30,6 +50,7 @@ struct BHTree {
     int32_t *dupc = nullptr;                        // exact duplicates of each sorted point (incl. itself)
     double2 *pos = nullptr;                         // sorted positions (leaves + queries)
     BHNode *nodes = nullptr;
+    QRec *qrec = nullptr;       // per binary node id, valid for real nodes
     double *agg = nullptr;      // per-node bottom-up aggregates (AGG doubles)
     int32_t *parent_leaf = nullptr, *parent_node = nullptr;
     int32_t *arrive = nullptr;
