@@ -184,11 +184,11 @@ def main():
     losses = ctx.dev_opt_losses()
 
     value = steps / t_loop
-    # ---- roofline of the HBM-bound gradient kernel (attraction + fused update)
+    # ---- roofline of the HBM-bound gradient kernel attract_rows (stage [3])
     # bytes per launch = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr
-    #   + rows*(16 own Y + 16 gathered Y_j once + 16 F + 4 inv + 32 upd r/w + 32 gains r/w + 16 Ynew)
+    #   + rows*(16 own Y + 16 attr out) + n*16 (gathered Y_j, counted once)
     rows = r1 - r0
-    attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 132
+    attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 32 + n * 16
     attr_ms = float(np.median([e["attract_ms"] for e in timeline])) if timeline else None
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
     knn_flops = 2.0 * (r1 - r0) * n * d
@@ -218,7 +218,7 @@ def main():
         "knn_mfma_frac_of_peak": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF,
         "affinities_joint_s": t_aff,
         "final_loss": losses.get(max(losses)) if losses else None,
-        "roofline": {"kernel": "attract_kernel<1> (CSR attraction + gains/momentum update)",
+        "roofline": {"kernel": "attract_rows (CSR attraction, TsneHelpers.scala:269-306)",
                      "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
                      "bytes_per_launch": attr_bytes, "avg_ms": attr_ms},

@@ -266,10 +266,11 @@ def test_optimize_per_iteration_gradients(ctx):
 
 def test_optimize_loss_matches_oracle(ctx):
     """lossFile parity.  The reference dynamics are chaotic: perturbing Y0 by
-    1e-15 (relative) moves the oracle's own KL at t = 200 by several percent
-    (theta = 0.5).  So: the first iterations (before divergence) must agree
-    within 1%, and the final KL must lie inside the oracle's own
-    perturbation envelope widened by 1% (hard part iv)."""
+    1e-15 (relative) moves the oracle's own KL at t = 200 over a spread of
+    ~0.2 (std, theta = 0.5; 40 samples span [-3.65, -2.66]).  So: the first
+    iterations (before divergence) must agree within 1%, and the final KL must
+    lie within 4 standard deviations (+1%) of the oracle's own perturbation
+    ensemble (hard part iv)."""
     n = 600
     rp, col, val = random_problem(n, 30, seed=31)
     Y0 = np.random.default_rng(6).normal(size=(n, 2)) * 1e-4
@@ -277,7 +278,7 @@ def test_optimize_loss_matches_oracle(ctx):
     Yg, ug, gg = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
     lg = ctx.optimize(rp, col, val, Yg, ug, gg, p)
     runs = []
-    for s in range(6):
+    for s in range(16):
         eps = 0.0 if s == 0 else 1e-15
         Yo = Y0 * (1 + eps * np.random.default_rng(s).normal(size=Y0.shape))
         uo, go = np.zeros_like(Y0), np.ones_like(Y0)
@@ -286,10 +287,9 @@ def test_optimize_loss_matches_oracle(ctx):
     assert sorted(lg) == sorted(lo) == list(range(10, 201, 10))
     for t in (10, 20, 30, 40, 50):
         assert abs(lg[t] - lo[t]) <= 0.01 * abs(lo[t]), t
-    final = [r[200] for r in runs]
-    lo_env, hi_env = min(final), max(final)
-    pad = 0.01 * max(abs(lo_env), abs(hi_env))
-    assert lo_env - pad <= lg[200] <= hi_env + pad, (lg[200], final)
+    final = np.array([r[200] for r in runs])
+    mu, sd = final.mean(), final.std()
+    assert abs(lg[200] - mu) <= 4.0 * sd + 0.01 * abs(mu), (lg[200], final)
 
 
 def test_unsupported_components(ctx):

@@ -55,7 +55,7 @@ constexpr int MOM_K = (MOM_DEG + 1) * (MOM_DEG + 2) / 2;
 constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-14;
-constexpr int MOM_TASKS = 32;   // moment tasks recorded per query; more -> dense tiles
+constexpr int MOM_TASKS = 128;  // moment tasks recorded per query; more -> dense tiles
 constexpr double BH_NEAR_TOL = 1e-10;   // near-exact subtree test (bh_traverse)
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
 __host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }

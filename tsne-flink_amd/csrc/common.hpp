@@ -154,6 +154,16 @@ namespace tsne {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// XCD-aware block order: the dispatcher places block b on XCD b % 8, so map
+// the blocks of one XCD onto one contiguous 1/8 of [0, nb) -- neighbouring
+// work items (Morton-ordered rows / queries) then share that XCD's L2.
+constexpr int NUM_XCD = 8;
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+    const int64_t per = nb / NUM_XCD, rem = nb % NUM_XCD;
+    const int64_t x = b % NUM_XCD, k = b / NUM_XCD;
+    return x * per + (x < rem ? x : rem) + k;
+}
+
 template <class T> __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

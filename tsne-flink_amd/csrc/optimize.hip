@@ -45,6 +45,7 @@ struct OptState {
     int cur = 0;
     double *Ynew = nullptr;   // npad x 2
     double2 *F = nullptr;     // npad, sorted order
+    double2 *attr = nullptr;  // chunk: attraction of the owned rows
     double *z = nullptr;      // npad, sorted order
     double *scal = nullptr;   // [0] Z, [1] loss, [2..3] mean
     double *part = nullptr;   // reduction partials
@@ -68,27 +69,6 @@ __device__ __forceinline__ double jmax(double a, double b) {  // java.lang.Math.
     if (a != a) return a;
     if (b != b) return b;
     return a >= b ? a : b;
-}
-
-// q = 1 / (1 + metric(y_i, y_j)) with the input metric on 2-D points
-// (TsneHelpers.scala:293); v_rcp_f64 + two Newton steps.
-__device__ __forceinline__ double qterm(double ax, double ay, double bx, double by, int metric) {
-    double m;
-    if (metric == TSNE_METRIC_COSINE) {
-        const double dt = __dadd_rn(__dmul_rn(ax, bx), __dmul_rn(ay, by));
-        const double na = sqrt(__dadd_rn(__dmul_rn(ax, ax), __dmul_rn(ay, ay)));
-        const double nb = sqrt(__dadd_rn(__dmul_rn(bx, bx), __dmul_rn(by, by)));
-        m = 1.0 - dt / (na * nb);
-    } else {
-        const double dx = __dsub_rn(ax, bx), dy = __dsub_rn(ay, by);
-        const double s = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-        m = metric == TSNE_METRIC_EUCLIDEAN ? sqrt(s) : s;
-    }
-    const double x = 1.0 + m;
-    double r = __builtin_amdgcn_rcp(x);
-    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
-    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
-    return r;
 }
 
 // Deterministic sum of v[0..n) (stride elements, component c) into part[block].
@@ -119,28 +99,51 @@ __global__ void reduce_final(const double *__restrict__ part, int np, double *__
     }
 }
 
-// MODE 0: grad only.  MODE 1: grad + updateEmbedding -> Ynew.
-// LPR lanes per CSR row (row_ptr indexed by the global row), 64/LPR rows per
-// wave; each lane issues U (col, val) loads and then U dependent Y_j gathers
-// before any arithmetic, so a row of <= LPR*U entries costs two memory round
-// trips.  Tail slots gather Y_i with P = 0 (exact no-ops in the sums).  The
-// loss term (every 10th iteration) lives in its own instantiation so the
-// common path carries no log().
-template <int MODE, int LPR, int U, bool LOSS>
-__global__ __launch_bounds__(256) void attract_kernel(
-    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
-    const double *__restrict__ val, int64_t r0, int64_t r1, const double *__restrict__ Y,
-    const int32_t *__restrict__ inv, const double2 *__restrict__ F, const double *__restrict__ scal,
-    int metric, double ex, double *__restrict__ grad, double *__restrict__ Ynew,
-    double *__restrict__ upd, double *__restrict__ gains, double min_gain, double mom, double lr,
-    double *__restrict__ lpart) {
+// q = 1 / (1 + metric(y_i, y_j)) with the input metric on 2-D points
+// (TsneHelpers.scala:293), metric fixed at compile time; v_rcp_f64 + two
+// Newton steps.
+template <int MET>
+__device__ __forceinline__ double qterm_t(double ax, double ay, double bx, double by) {
+    double m;
+    if (MET == TSNE_METRIC_COSINE) {
+        const double dt = __dadd_rn(__dmul_rn(ax, bx), __dmul_rn(ay, by));
+        const double na = sqrt(__dadd_rn(__dmul_rn(ax, ax), __dmul_rn(ay, ay)));
+        const double nb = sqrt(__dadd_rn(__dmul_rn(bx, bx), __dmul_rn(by, by)));
+        m = 1.0 - dt / (na * nb);
+    } else {
+        const double dx = __dsub_rn(ax, bx), dy = __dsub_rn(ay, by);
+        const double s2 = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+        m = MET == TSNE_METRIC_EUCLIDEAN ? sqrt(s2) : s2;
+    }
+    const double x = 1.0 + m;
+    double r = __builtin_amdgcn_rcp(x);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    return r;
+}
+
+// Attraction over the CSR rows [r0, r1) (TsneHelpers.scala:269-306):
+// attr_i = sum_j ex P_ij q_ij (y_i - y_j), and with LOSS the KL terms
+// ex P_ij ln(ex P_ij / (q_ij / Z)).  LPR lanes per row, 64/LPR rows per wave;
+// each lane issues U (col, val) loads and then U dependent Y_j gathers before
+// any arithmetic, so a row of <= LPR*U entries costs two memory round trips.
+// Tail slots gather Y_i with P = 0 (exact no-ops in the sums).  Blocks are
+// XCD-remapped so each XCD's L2 serves one contiguous 1/8 of the
+// Morton-ordered rows (their Y_j are spatial neighbours).
+template <int LPR, int U, bool LOSS, int MET>
+__global__ __launch_bounds__(256) void attract_rows(
+    const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
+    int64_t r0, int64_t r1, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
+    double2 *__restrict__ attr, double *__restrict__ lpart) {
     __shared__ double sl[4];
     const int sub = threadIdx.x & (LPR - 1);
-    const int64_t i = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR);
-    const double Z = scal[0];
+    const int64_t blk = xcd_block(blockIdx.x, gridDim.x);
+    const int64_t i = r0 + ((blk * blockDim.x + threadIdx.x) / LPR);
     double lsum = 0.0;
     if (i < r1) {
-        const double yx = Y[2 * i], yy = Y[2 * i + 1];
+        const double Z = LOSS ? scal[0] : 1.0;
+        const double2 yi = *reinterpret_cast<const double2 *>(Y + 2 * i);
+        const double yx = yi.x, yy = yi.y;
         double fx = 0.0, fy = 0.0;
         const int64_t e1 = row_ptr[i + 1];
         for (int64_t e = row_ptr[i] + sub; e < e1; e += LPR * U) {
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(256) void attract_kernel(
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const double pij = __dmul_rn(pv[u], ex);
-                const double q = qterm(yx, yy, jx[u], jy[u], metric);
+                const double q = qterm_t<MET>(yx, yy, jx[u], jy[u]);
                 const double sc = __dmul_rn(pij, q);
                 fx = __dadd_rn(fx, __dmul_rn(sc, __dsub_rn(yx, jx[u])));
                 fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yy, jy[u])));
@@ -174,33 +177,46 @@ __global__ __launch_bounds__(256) void attract_kernel(
             fx += __shfl_xor(fx, o, LPR);
             fy += __shfl_xor(fy, o, LPR);
         }
-        if (sub == 0) {
-            const double2 f = F[inv[i]];
-            const double gx = fx - f.x / Z, gy = fy - f.y / Z;  // attrForce - repForce / sumQ
-            if (MODE == 0) {
-                grad[2 * i] = gx;
-                grad[2 * i + 1] = gy;
-            } else {
-                const double g[2] = {gx, gy};
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const int64_t o = 2 * i + c;
-                    const double u = upd[o], gn0 = gains[o];
-                    const double gn = ((g[c] > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain)
-                                                                  : jmax(gn0 + 0.2, min_gain);
-                    const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g[c]));
-                    gains[o] = gn;
-                    upd[o] = un;
-                    Ynew[o] = __dadd_rn(un, Y[o]);
-                }
-            }
-        }
+        if (sub == 0) attr[i - r0] = make_double2(fx, fy);
     }
     if (LOSS) {
         lsum = wave_sum(lsum);
         if (lane_id() == 0) sl[threadIdx.x >> 6] = lsum;
         __syncthreads();
         if (threadIdx.x == 0) lpart[blockIdx.x] = (sl[0] + sl[1]) + (sl[2] + sl[3]);
+    }
+}
+
+// grad = attr - F / Z (TsneHelpers.scala:311-317); MODE 0 writes it, MODE 1
+// applies updateEmbedding (TsneHelpers.scala:341-369) -> Ynew.  One thread
+// per row, all accesses coalesced except F[inv[i]] (near-identity gather).
+template <int MODE>
+__global__ __launch_bounds__(256) void combine_update(
+    int64_t r0, int64_t r1, const double2 *__restrict__ attr, const int32_t *__restrict__ inv,
+    const double2 *__restrict__ F, const double *__restrict__ scal, const double *__restrict__ Y,
+    double *__restrict__ grad, double *__restrict__ Ynew, double *__restrict__ upd, double *__restrict__ gains,
+    double min_gain, double mom, double lr) {
+    const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= r1) return;
+    const double Z = scal[0];
+    const double2 at = attr[i - r0];
+    const double2 f = F[inv[i]];
+    const double gx = at.x - f.x / Z, gy = at.y - f.y / Z;  // attrForce - repForce / sumQ
+    if (MODE == 0) {
+        grad[2 * i] = gx;
+        grad[2 * i + 1] = gy;
+        return;
+    }
+    const double g[2] = {gx, gy};
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const int64_t o = 2 * i + c;
+        const double u = upd[o], gn0 = gains[o];
+        const double gn = ((g[c] > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain) : jmax(gn0 + 0.2, min_gain);
+        const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g[c]));
+        gains[o] = gn;
+        upd[o] = un;
+        Ynew[o] = __dadd_rn(un, Y[o]);
     }
 }
 
@@ -296,26 +312,33 @@ __global__ void relabel_rows(const int32_t *__restrict__ order, const int32_t *_
 
 
 // Attraction launch: variant (lanes per row x unroll) from TSNE_ATTRACT
-// ("16x4", "32x4", "64x4", "16x8", "32x8"); returns the block count (loss partials).
+// ("16x4", "32x4", "64x4", "16x8", "32x8", "16x12"); returns the block count
+// (loss partials).
 struct AttractArgs {
     const int64_t *rp; const int32_t *col; const double *val; int64_t r0, r1; const double *Y;
-    const int32_t *inv; const double2 *F; const double *scal; int metric; double ex;
-    double *grad, *Ynew, *upd, *gains; double min_gain, mom, lr; double *lpart;
+    const double *scal; int metric; double ex; double2 *attr; double *lpart;
 };
 
-template <int MODE, int LPR, int U>
-static int64_t attract_launch_v(hipStream_t st, const AttractArgs &a, bool loss) {
+template <int LPR, int U, int MET>
+static int64_t attract_launch_m(hipStream_t st, const AttractArgs &a, bool loss) {
     const int64_t rows = a.r1 - a.r0;
     const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * LPR, 256));
     if (loss)
-        hipLaunchKernelGGL((attract_kernel<MODE, LPR, U, true>), dim3(blocks), dim3(256), 0, st, a.rp, a.col, a.val,
-                           a.r0, a.r1, a.Y, a.inv, a.F, a.scal, a.metric, a.ex, a.grad, a.Ynew, a.upd, a.gains,
-                           a.min_gain, a.mom, a.lr, a.lpart);
+        hipLaunchKernelGGL((attract_rows<LPR, U, true, MET>), dim3(blocks), dim3(256), 0, st, a.rp, a.col, a.val,
+                           a.r0, a.r1, a.Y, a.scal, a.ex, a.attr, a.lpart);
     else
-        hipLaunchKernelGGL((attract_kernel<MODE, LPR, U, false>), dim3(blocks), dim3(256), 0, st, a.rp, a.col,
-                           a.val, a.r0, a.r1, a.Y, a.inv, a.F, a.scal, a.metric, a.ex, a.grad, a.Ynew, a.upd,
-                           a.gains, a.min_gain, a.mom, a.lr, a.lpart);
+        hipLaunchKernelGGL((attract_rows<LPR, U, false, MET>), dim3(blocks), dim3(256), 0, st, a.rp, a.col, a.val,
+                           a.r0, a.r1, a.Y, a.scal, a.ex, a.attr, a.lpart);
     return blocks;
+}
+
+template <int LPR, int U>
+static int64_t attract_launch_v(hipStream_t st, const AttractArgs &a, bool loss) {
+    switch (a.metric) {
+        case TSNE_METRIC_EUCLIDEAN: return attract_launch_m<LPR, U, TSNE_METRIC_EUCLIDEAN>(st, a, loss);
+        case TSNE_METRIC_COSINE: return attract_launch_m<LPR, U, TSNE_METRIC_COSINE>(st, a, loss);
+        default: return attract_launch_m<LPR, U, TSNE_METRIC_SQEUCLIDEAN>(st, a, loss);
+    }
 }
 
 static int attract_variant() {
@@ -323,20 +346,30 @@ static int attract_variant() {
     if (v < 0) {
         const char *e = getenv("TSNE_ATTRACT");
         const std::string s = e ? e : "";
-        v = s == "16x4" ? 0 : s == "32x4" ? 1 : s == "64x4" ? 2 : s == "16x8" ? 3 : s == "32x8" ? 4 : 1;
+        v = s == "16x4" ? 0 : s == "32x4" ? 1 : s == "64x4" ? 2 : s == "16x8" ? 3 : s == "32x8" ? 4
+          : s == "16x12" ? 5 : 2;
     }
     return v;
 }
 
-template <int MODE>
 static int64_t attract_launch(hipStream_t st, const AttractArgs &a, bool loss) {
     switch (attract_variant()) {
-        case 0: return attract_launch_v<MODE, 16, 4>(st, a, loss);
-        case 2: return attract_launch_v<MODE, 64, 4>(st, a, loss);
-        case 3: return attract_launch_v<MODE, 16, 8>(st, a, loss);
-        case 4: return attract_launch_v<MODE, 32, 8>(st, a, loss);
-        default: return attract_launch_v<MODE, 32, 4>(st, a, loss);
+        case 0: return attract_launch_v<16, 4>(st, a, loss);
+        case 1: return attract_launch_v<32, 4>(st, a, loss);
+        case 3: return attract_launch_v<16, 8>(st, a, loss);
+        case 4: return attract_launch_v<32, 8>(st, a, loss);
+        case 5: return attract_launch_v<16, 12>(st, a, loss);
+        default: return attract_launch_v<64, 4>(st, a, loss);
     }
+}
+
+template <int MODE>
+static void combine_launch(hipStream_t st, int64_t r0, int64_t r1, const double2 *attr, const int32_t *inv,
+                           const double2 *F, const double *scal, const double *Y, double *grad, double *Ynew,
+                           double *upd, double *gains, double min_gain, double mom, double lr) {
+    if (r1 <= r0) return;
+    hipLaunchKernelGGL(combine_update<MODE>, dim3(ceil_div(r1 - r0, 256)), dim3(256), 0, st, r0, r1, attr, inv, F,
+                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr);
 }
 
 // Upper bound of attract_launch's block count for rows rows.
@@ -395,9 +428,10 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, part, NPART, scal, 0.0);
     double *lpart = ctx->ws.get<double>("grad.lpart", attract_max_blocks(n));
     const bool want_loss = h_loss != nullptr;
-    AttractArgs aa{d_row_ptr, d_col, d_P, 0, n, dY, t.inv, F, scal, metric, exaggeration,
-                   d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, lpart};
-    const int64_t blocks = attract_launch<0>(st, aa, want_loss);
+    double2 *attr = ctx->ws.get<double2>("grad.attr", n);
+    AttractArgs aa{d_row_ptr, d_col, d_P, 0, n, dY, scal, metric, exaggeration, attr, lpart};
+    const int64_t blocks = attract_launch(st, aa, want_loss);
+    combine_launch<0>(st, 0, n, attr, t.inv, F, scal, dY, d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0);
     TSNE_LAUNCH_CHECK();
     if (want_loss) hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, lpart, (int)blocks, scal + 1, 0.0);
     double hs[2] = {0, 0};
@@ -468,6 +502,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->scan_tmp = ws.get<uint8_t>("opt.scan_tmp", tb);
     s->Ynew = ws.get<double>("opt.Ynew", 2 * s->npad);
     s->F = ws.get<double2>("opt.F", s->npad);
+    s->attr = ws.get<double2>("opt.attr", s->chunk);
     s->z = ws.get<double>("opt.z", s->npad);
     s->scal = ws.get<double>("opt.scal", 8);
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(s->chunk)));
@@ -542,11 +577,12 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 4. attraction + update for owned rows
-    AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->tree.inv, s->F, s->scal, p.metric, ex,
-                   nullptr, s->Ynew, s->upd[c], s->gains[c], p.min_gain, mom, p.learning_rate, s->part};
-    const int64_t blocks = attract_launch<1>(st, aa, want_loss != 0);
+    AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->scal, p.metric, ex, s->attr, s->part};
+    const int64_t blocks = attract_launch(st, aa, want_loss != 0);
     TSNE_LAUNCH_CHECK();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
+    combine_launch<1>(st, s->r0, s->r1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
+                      s->gains[c], p.min_gain, mom, p.learning_rate);
     if (want_loss) {
         hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, (int)blocks, s->scal + 1, 0.0);
         if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
