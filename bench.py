@@ -173,6 +173,8 @@ def main():
                              "visits_per_point": vis_t[0] / max(1, r1 - r0),
                              "moment_evals_per_point": vis_t[1] / max(1, r1 - r0),
                              "dense_pairs_per_point": vis_t[2] / max(1, r1 - r0),
+                             "pops_per_wave": vis_t[3] / max(1, (r1 - r0) / 64),
+                             "dense_points_per_wave": vis_t[4] / max(1, (r1 - r0) / 64),
                              "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
         if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
             snaps[t] = Y[:n].cpu().numpy().copy()

@@ -178,11 +178,12 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
  * [0] tree build, [1] BH repulsion kernel, [2] (F, z) exchange + Z reduce,
  * [3] attraction kernel (attract_rows), [4] combine + update, loss, embedding
  * exchange, centring.
- * Also BH work counters of the last step (visits_out3, may be NULL):
+ * Also BH work counters of the last step (counters_out5, may be NULL):
  * [0] reference-equivalent node evaluations (lane visits; a leaf tile of m
- * points counts m), [1] subtree-moment evaluations, [2] dense pair terms.
+ * points counts m), [1] subtree-moment evaluations, [2] dense pair terms,
+ * [3] wave-level cell pops, [4] wave-level dense tile points.
  * enable: 1 on, 0 off, -1 leave unchanged. */
-int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *visits_out3);
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out5);
 
 #ifdef __cplusplus
 }

@@ -56,7 +56,8 @@ constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-14;
 constexpr int MOM_TASKS = 128;  // moment tasks recorded per query; more -> dense tiles
-constexpr double BH_NEAR_TOL = 1e-10;   // near-exact subtree test (bh_traverse)
+constexpr double BH_NEAR_TOL = 1e-7;    // near-exact subtree test (bh_traverse): 1000x below
+                                        // the north-star 1e-4 gradient tolerance
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
 __host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }
 __host__ __device__ constexpr double fact(int k) { return k <= 1 ? 1.0 : k * fact(k - 1); }
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
     double fx = 0.0, fy = 0.0, zs = 0.0;
-    unsigned long long nvis = 0, ndense = 0;
+    unsigned long long nvis = 0, ndense = 0, wpops = 0, wdense = 0;   // w*: wave-level work
     int sp = 0;
     int ntask = 0;
     // ---- the root: a single point, a key-tie group, or a cell tested like any child
@@ -725,6 +726,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     }
     while (sp > 0) {
         --sp;
+        ++wpops;
         const int ref = __builtin_amdgcn_readfirstlane(sref[w][sp]);
         const uint64_t msk = smask[w][sp];
         bool act = (msk >> lane) & 1ull;
@@ -763,6 +765,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
             double tx = 0.0, ty = 0.0, tz = 0.0;
             const bool dense = tile && !usem;
             if (__ballot(dense)) {
+                wdense += (unsigned long long)(b - a + 1);
                 double2 *buf = tbuf[w];
                 double2 nxt = make_double2(0.0, 0.0);
                 if (a + lane <= b) nxt = pos[a + lane];
@@ -835,13 +838,16 @@ __global__ __launch_bounds__(256) void bh_traverse(
         Z[s] = zs;
         mtask_n[s - s0] = ntask;
     }
-    if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms
+    if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms,
+                    // [3] wave-level pops, [4] wave-level dense tile points
         const unsigned long long tv = wave_sum(nvis), tt = wave_sum((unsigned long long)ntask),
                                  td = wave_sum(ndense);
         if (lane == 0) {
             atomicAdd(visits, tv);
             atomicAdd(visits + 1, tt);
             atomicAdd(visits + 2, td);
+            atomicAdd(visits + 3, wpops);
+            atomicAdd(visits + 4, wdense);
         }
     }
 }

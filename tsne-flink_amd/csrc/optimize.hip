@@ -49,6 +49,7 @@ struct OptState {
     double *z = nullptr;      // npad, sorted order
     double *scal = nullptr;   // [0] Z, [1] loss, [2..3] mean
     double *part = nullptr;   // reduction partials
+    double *part2 = nullptr;  // second-level partials (NPART)
     double *loss = nullptr;   // per loss slot
     int32_t loss_slots = 0;
     std::vector<int32_t> loss_written;
@@ -57,7 +58,7 @@ struct OptState {
     bool profile = false;
     hipEvent_t ev[6] = {};
     double last_ms[5] = {0, 0, 0, 0, 0};
-    int64_t last_visits[3] = {0, 0, 0};
+    int64_t last_visits[5] = {0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -433,7 +434,10 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     const int64_t blocks = attract_launch(st, aa, want_loss);
     combine_launch<0>(st, 0, n, attr, t.inv, F, scal, dY, d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0);
     TSNE_LAUNCH_CHECK();
-    if (want_loss) hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, lpart, (int)blocks, scal + 1, 0.0);
+    if (want_loss) {   // two-level: block partials -> NPART -> 1
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, lpart, blocks, 1, 0, part);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, part, NPART, scal + 1, 0.0);
+    }
     double hs[2] = {0, 0};
     TSNE_HIP(hipMemcpyAsync(hs, scal, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     TSNE_HIP(hipStreamSynchronize(st));
@@ -506,10 +510,11 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->z = ws.get<double>("opt.z", s->npad);
     s->scal = ws.get<double>("opt.scal", 8);
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(s->chunk)));
+    s->part2 = ws.get<double>("opt.part2", NPART);
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 3);
+    s->visits = ws.get<unsigned long long>("opt.visits", 5);
     TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
@@ -559,7 +564,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int c = s->cur;
     double *Y = s->Y[c];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 3 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 5 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 1. tree
@@ -584,7 +589,8 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     combine_launch<1>(st, s->r0, s->r1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
                       s->gains[c], p.min_gain, mom, p.learning_rate);
     if (want_loss) {
-        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, (int)blocks, s->scal + 1, 0.0);
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
         if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
         const int slot = t / 10 - 1;
         if (slot >= 0 && slot < s->loss_slots) {
@@ -611,9 +617,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
             TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
-        unsigned long long v[3] = {0, 0, 0};
+        unsigned long long v[5] = {0, 0, 0, 0, 0};
         TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
-        for (int k = 0; k < 3; ++k) s->last_visits[k] = (int64_t)v[k];
+        for (int k = 0; k < 5; ++k) s->last_visits[k] = (int64_t)v[k];
     }
 }
 
@@ -657,7 +663,7 @@ void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits) {
     if (ms5)
         for (int k = 0; k < 5; ++k) ms5[k] = s->last_ms[k];
     if (visits)
-        for (int k = 0; k < 3; ++k) visits[k] = s->last_visits[k];
+        for (int k = 0; k < 5; ++k) visits[k] = s->last_visits[k];
 }
 
 }  // namespace tsne
