@@ -32,7 +32,10 @@ namespace {
 
 constexpr int LEVELS = 31;                 // 62 key bits
 constexpr uint64_t OUT_KEY = 1ull << 63;   // outside the root cell: sorts last
-constexpr int STACK = 128;                 // >= max tree depth (62 + 32) + 1
+constexpr int STACK = 256;                 // batch pops while <= STACK/2 entries, then depth-first
+                                           // (+3 per level, <= 35 levels): never overflows
+constexpr int KPOP = 4;                    // cells popped (records fetched) per round
+constexpr int QREC_V4 = sizeof(QRec) / 16; // 16-byte pieces of a record
 
 // ---- Subtree moments (the all-open fast path, see bh_traverse)
 // For a subtree every cell of which a query would open, the reference sums
@@ -685,6 +688,9 @@ __global__ __launch_bounds__(256) void bh_traverse(
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
     __shared__ double2 tbuf[4][64];
+    __shared__ QRec srec[4][KPOP];
+    __shared__ int32_t bref[4][KPOP];
+    __shared__ uint64_t bmask[4][KPOP];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t s = s0 + ((int64_t)blockIdx.x * 4 + w) * 64 + lane;
     const bool valid = s < s1;
@@ -724,13 +730,27 @@ __global__ __launch_bounds__(256) void bh_traverse(
             }
         }
     }
+    // Pop up to KPOP cells at a time: their records are fetched with one
+    // round of coalesced 16-byte vector loads into LDS (the pops' memory
+    // latencies overlap), then processed one by one from LDS broadcasts.
     while (sp > 0) {
-        --sp;
+        const int k = sp > STACK / 2 ? 1 : (sp < KPOP ? sp : KPOP);
+        sp -= k;
+        if (lane < k) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
+        if (lane < QREC_V4 * k) {
+            const int rr = lane / QREC_V4, part = lane - rr * QREC_V4;
+            const int rf = sref[w][sp + rr];
+            reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
+        __builtin_amdgcn_wave_barrier();
+        for (int r = 0; r < k; ++r) {
         ++wpops;
-        const int ref = __builtin_amdgcn_readfirstlane(sref[w][sp]);
-        const uint64_t msk = smask[w][sp];
+        const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
+        const uint64_t msk = bmask[w][r];
         bool act = (msk >> lane) & 1ull;
-        const QRec &nd = qrec[ref];
+        const QRec &nd = srec[w][r];
         // all-open tests (per lane) -> direct tile over the subtree's leaves
         bool tile = false;
         if (act) {
@@ -831,6 +851,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     ++sp;
                 }
             }
+        }
         }
     }
     if (valid) {
