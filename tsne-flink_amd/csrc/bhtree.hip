@@ -584,17 +584,14 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
 }
 
 // fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
-// an IEEE division -- decided from a Newton-refined reciprocal, with the exact
-// division only within ~1e-14 (relative) of theta.
+// an IEEE division -- decided by comparing h with theta * D outside a 1e-14
+// relative band (where the rounded quotient cannot cross theta), and by the
+// exact division inside it.  D = 0 or denormal gives h > theta D: opened, as
+// h / 0 = inf is not < theta.
 __device__ __forceinline__ bool summarise(double h, double D, double theta) {
-    if (!(D > 1e-290)) return h / D < theta;   // 0, denormal or NaN: exact path
-    double r = __builtin_amdgcn_rcp(D);
-    r = __fma_rn(r, __fma_rn(-D, r, 1.0), r);
-    r = __fma_rn(r, __fma_rn(-D, r, 1.0), r);
-    double qv = h * r;
-    qv = __fma_rn(__fma_rn(-D, qv, h), r, qv);
-    if (qv < theta * (1.0 - 1e-14)) return true;
-    if (qv > theta * (1.0 + 1e-14)) return false;
+    const double t = theta * D;
+    if (h < t * (1.0 - 1e-14)) return true;
+    if (h > t * (1.0 + 1e-14)) return false;
     return h / D < theta;
 }
 
