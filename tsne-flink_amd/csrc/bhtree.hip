@@ -32,9 +32,9 @@ namespace {
 
 constexpr int LEVELS = 31;                 // 62 key bits
 constexpr uint64_t OUT_KEY = 1ull << 63;   // outside the root cell: sorts last
-constexpr int STACK = 256;                 // batch pops while <= STACK/2 entries, then depth-first
+constexpr int STACK = 320;                 // batch pops while <= STACK/2 entries, then depth-first
                                            // (+3 per level, <= 35 levels): never overflows
-constexpr int KPOP = 4;                    // cells popped (records fetched) per round
+constexpr int KPOP = 8;                    // cells popped (records fetched) per round
 constexpr int QREC_V4 = sizeof(QRec) / 16; // 16-byte pieces of a record
 
 // ---- Subtree moments (the all-open fast path, see bh_traverse)
@@ -689,7 +689,9 @@ __global__ __launch_bounds__(256) void bh_traverse(
     __shared__ int32_t bref[4][KPOP];
     __shared__ uint64_t bmask[4][KPOP];
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int64_t s = s0 + ((int64_t)blockIdx.x * 4 + w) * 64 + lane;
+    // XCD-aware: each XCD walks one contiguous 1/8 of the Morton-ordered
+    // queries, so the cells its waves touch stay in its own L2
+    const int64_t s = s0 + (xcd_block(blockIdx.x, gridDim.x) * 4 + w) * 64 + lane;
     const bool valid = s < s1;
     if (__ballot(valid) == 0) return;
     const int root = meta[1];
@@ -734,8 +736,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
         const int k = sp > STACK / 2 ? 1 : (sp < KPOP ? sp : KPOP);
         sp -= k;
         if (lane < k) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
-        if (lane < QREC_V4 * k) {
-            const int rr = lane / QREC_V4, part = lane - rr * QREC_V4;
+        for (int e = lane; e < QREC_V4 * k; e += 64) {
+            const int rr = e / QREC_V4, part = e - rr * QREC_V4;
             const int rf = sref[w][sp + rr];
             reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
         }
