@@ -32,9 +32,8 @@ namespace {
 
 constexpr int LEVELS = 31;                 // 62 key bits
 constexpr uint64_t OUT_KEY = 1ull << 63;   // outside the root cell: sorts last
-constexpr int STACK = 320;                 // batch pops while <= STACK/2 entries, then depth-first
-                                           // (+3 per level, <= 35 levels): never overflows
-constexpr int KPOP = 8;                    // cells popped (records fetched) per round
+constexpr int STACK = 320;                 // batch pops (<= 8 cells) while <= STACK/2 entries, then
+                                           // depth-first (+3 per level, <= 35 levels): never overflows
 constexpr int QREC_V4 = sizeof(QRec) / 16; // 16-byte pieces of a record
 
 // ---- Subtree moments (the all-open fast path, see bh_traverse)
@@ -117,12 +116,13 @@ __global__ void bbox_final(const double *__restrict__ part, int nb, double *__re
 __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const double *__restrict__ Wp,
                             uint64_t *__restrict__ keys, int32_t *__restrict__ idx,
                             int32_t *__restrict__ meta) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i0 < n;
+    const int64_t i = live ? i0 : n - 1;
     const double W = *Wp;
     const double px = Y[2 * i], py = Y[2 * i + 1];
     double x = 0.0, y = 0.0, hw = W, hh = W;
-    bool in = (__dsub_rn(x, hw) <= px) && (__dadd_rn(x, hw) >= px) && (__dsub_rn(y, hh) <= py) &&
+    bool in = live && (__dsub_rn(x, hw) <= px) && (__dadd_rn(x, hw) >= px) && (__dsub_rn(y, hh) <= py) &&
               (__dadd_rn(y, hh) >= py);
     uint64_t key = 0;
     if (in) {
@@ -145,12 +145,16 @@ __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const doubl
             hh = nh;
             key = (key << 2) | (uint64_t)q;
         }
-        atomicAdd(&meta[0], 1);
     } else {
         key = OUT_KEY;
     }
-    keys[i] = key;
-    idx[i] = (int32_t)i;
+    if (live) {
+        keys[i] = key;
+        idx[i] = (int32_t)i;
+    }
+    // in-root count m: one atomic per wave
+    const uint64_t b = __ballot(in);
+    if (lane_id() == 0 && b) atomicAdd(&meta[0], (int)__popcll(b));
 }
 
 __global__ void gather_sorted(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted,
@@ -677,6 +681,7 @@ __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__re
 // D <= near_dmax of q (box corners), the relative deviation is below
 // ~48 theta^2 near_dmax^2 <= BH_NEAR_TOL (bh_near_dmax).  In the tiny-embedding
 // phase (extent ~1e-3) the root passes for every query: one moment task each.
+template <int KPOP, bool XCD>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
@@ -691,7 +696,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const int lane = lane_id(), w = threadIdx.x >> 6;
     // XCD-aware: each XCD walks one contiguous 1/8 of the Morton-ordered
     // queries, so the cells its waves touch stay in its own L2
-    const int64_t s = s0 + (xcd_block(blockIdx.x, gridDim.x) * 4 + w) * 64 + lane;
+    const int64_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t s = s0 + (blk * 4 + w) * 64 + lane;
     const bool valid = s < s1;
     if (__ballot(valid) == 0) return;
     const int root = meta[1];
@@ -963,7 +969,13 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     if (s1 <= s0) return;
     const double near_dmax = bh_near_dmax(theta);
     const int64_t waves = ceil_div(s1 - s0, 64);
-    hipLaunchKernelGGL(bh_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
+    // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD-aware block order (TSNE_BH_XCD)
+    static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
+    static const bool xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) != 0 : false; }();
+    auto kern = kp >= 8 ? (xcd ? bh_traverse<8, true> : bh_traverse<8, false>)
+              : kp >= 4 ? (xcd ? bh_traverse<4, true> : bh_traverse<4, false>)
+                        : (xcd ? bh_traverse<1, true> : bh_traverse<1, false>);
+    hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
                        t.qrec, t.mtask, t.mtask_n, t.meta, theta, near_dmax, s0, s1, dF, dz, visits);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, dF, dz);
