@@ -382,13 +382,23 @@ __device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double 
     box_centre(nd.bx0, nd.bx1, nd.by0, nd.by1, cx, cy, R);
 }
 
+// Moments are built only when the previous traversal had tiles that could use
+// them (mom_flag[1] > 0); mom_flag[0] tells this build's traversal whether
+// they exist.  Eligible tiles are counted even when they are off, so the next
+// iteration turns them back on.
+__global__ void moment_gate(int32_t *mom_flag) {
+    mom_flag[0] = mom_flag[1] > 0;
+    mom_flag[1] = 0;
+}
+
 __global__ void moment_count(const BHNode *__restrict__ nodes, int64_t n, const int32_t *__restrict__ meta,
-                             int32_t *__restrict__ cnt, int32_t *__restrict__ list, int32_t *__restrict__ meta_w) {
+                             const int32_t *__restrict__ mom_flag, int32_t *__restrict__ cnt,
+                             int32_t *__restrict__ list, int32_t *__restrict__ meta_w) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     const int m = meta[0];
     int32_t c = 0;
-    if (i < m - 1) {
+    if (i < m - 1 && mom_flag[0]) {
         const BHNode &nd = nodes[i];
         if (nd.cnt >= MOM_MIN_POINTS && nd.delta < 62) {
             c = (nd.cnt + MOM_CHUNK - 1) / MOM_CHUNK;
@@ -685,8 +695,8 @@ template <int KPOP, bool XCD>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
-    const int32_t *__restrict__ meta, double theta, double near_dmax, int64_t s0, int64_t s1,
-    double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
+    const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t s0,
+    int64_t s1, double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
     __shared__ double2 tbuf[4][64];
@@ -708,7 +718,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0, ndense = 0, wpops = 0, wdense = 0;   // w*: wave-level work
     int sp = 0;
-    int ntask = 0;
+    int ntask = 0, nwant = 0;
+    const bool mom_on = mom_flag[0] != 0;
     // ---- the root: a single point, a key-tie group, or a cell tested like any child
     if (root == ~0) {
         if (valid) { ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
@@ -785,7 +796,11 @@ __global__ __launch_bounds__(256) void bh_traverse(
             bool usem = false;
             if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
                 usem = moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy);
-                if (usem) mtask[(s - s0) * MOM_TASKS + ntask++] = ref;
+                if (usem) {
+                    ++nwant;
+                    if (mom_on) mtask[(s - s0) * MOM_TASKS + ntask++] = ref;
+                    else usem = false;
+                }
             }
             double tx = 0.0, ty = 0.0, tz = 0.0;
             const bool dense = tile && !usem;
@@ -864,6 +879,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
         Z[s] = zs;
         mtask_n[s - s0] = ntask;
     }
+    const int wwant = wave_sum(nwant);
+    if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
     if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms,
                     // [3] wave-level pops, [4] wave-level dense tile points
         const unsigned long long tv = wave_sum(nvis), tt = wave_sum((unsigned long long)ntask),
@@ -906,6 +923,10 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.mom_items_cap = n + ceil_div(n * 94, MOM_CHUNK);
     t.mom_item = ws.get<int32_t>("bh.mom_item", t.mom_items_cap);
     t.mom_part = ws.get<double>("bh.mom_part", (size_t)t.mom_items_cap * MOM_K);
+    t.mom_flag = ws.get<int32_t>("bh.mom_flag", 2);
+    const int32_t flag_init[2] = {1, 1};   // first build: moments on
+    TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
     t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
     t.mtask_n = ws.get<int32_t>("bh.mtask_n", n);
     size_t sb = 0;
@@ -942,8 +963,9 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
     hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, t.qrec);
     // subtree moments for the all-open fast path
-    hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_cnt,
-                       t.mom_list, t.meta);
+    hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag);
+    hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_flag,
+                       t.mom_cnt, t.mom_list, t.meta);
     size_t sb = t.scan_tmp_bytes;
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.scan_tmp, sb, t.mom_cnt, t.mom_off, (int)(n + 1), st));
     const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
@@ -976,7 +998,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
               : kp >= 4 ? (xcd ? bh_traverse<4, true> : bh_traverse<4, false>)
                         : (xcd ? bh_traverse<1, true> : bh_traverse<1, false>);
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.mtask, t.mtask_n, t.meta, theta, near_dmax, s0, s1, dF, dz, visits);
+                       t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dF, dz, visits);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, dF, dz);
     TSNE_LAUNCH_CHECK();

@@ -64,6 +64,7 @@ struct BHTree {
     int32_t *mom_list = nullptr;                     // nodes that carry moments
     int32_t *mom_item = nullptr;                     // item -> node
     int32_t *mtask = nullptr, *mtask_n = nullptr;    // per query: moment tasks (node ids), count
+    int32_t *mom_flag = nullptr;                     // [0] moments built, [1] eligible tiles seen
     int64_t mom_items_cap = 0;
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
