@@ -691,12 +691,13 @@ __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__re
 // D <= near_dmax of q (box corners), the relative deviation is below
 // ~48 theta^2 near_dmax^2 <= BH_NEAR_TOL (bh_near_dmax).  In the tiny-embedding
 // phase (extent ~1e-3) the root passes for every query: one moment task each.
-template <int KPOP, bool XCD>
+template <int KPOP>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t s0,
-    int64_t s1, double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits) {
+    int64_t s1, int xcd_chunk, double2 *__restrict__ F, double *__restrict__ Z,
+    unsigned long long *__restrict__ visits) {
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
     __shared__ double2 tbuf[4][64];
@@ -706,7 +707,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const int lane = lane_id(), w = threadIdx.x >> 6;
     // XCD-aware: each XCD walks one contiguous 1/8 of the Morton-ordered
     // queries, so the cells its waves touch stay in its own L2
-    const int64_t blk = XCD ? xcd_block(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t s = s0 + (blk * 4 + w) * 64 + lane;
     const bool valid = s < s1;
     if (__ballot(valid) == 0) return;
@@ -991,14 +992,14 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     if (s1 <= s0) return;
     const double near_dmax = bh_near_dmax(theta);
     const int64_t waves = ceil_div(s1 - s0, 64);
-    // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD-aware block order (TSNE_BH_XCD)
+    // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD block order (TSNE_BH_XCD = run
+    // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
-    static const bool xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) != 0 : false; }();
-    auto kern = kp >= 8 ? (xcd ? bh_traverse<8, true> : bh_traverse<8, false>)
-              : kp >= 4 ? (xcd ? bh_traverse<4, true> : bh_traverse<4, false>)
-                        : (xcd ? bh_traverse<1, true> : bh_traverse<1, false>);
+    static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
+    auto kern = kp >= 8 ? bh_traverse<8> : kp >= 4 ? bh_traverse<4> : bh_traverse<1>;
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dF, dz, visits);
+                       t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, xcd, dF, dz,
+                       visits);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, dF, dz);
     TSNE_LAUNCH_CHECK();

@@ -163,6 +163,15 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
     const int64_t x = b % NUM_XCD, k = b / NUM_XCD;
     return x * per + (x < rem ? x : rem) + k;
 }
+// Chunked variant: runs of C consecutive logical blocks go to one XCD and the
+// runs rotate over the XCDs (locality within a run, balance across XCDs);
+// bijective on [0, nb), identity on the tail that does not fill 8 runs.
+__device__ __forceinline__ int64_t xcd_block_chunked(int64_t b, int64_t nb, int64_t C) {
+    const int64_t G = (int64_t)NUM_XCD * C, full = (nb / G) * G;
+    if (b >= full) return b;
+    const int64_t x = b % NUM_XCD, k = b / NUM_XCD;
+    return (k / C) * G + x * C + (k % C);
+}
 
 template <class T> __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -125,52 +125,65 @@ __device__ __forceinline__ double qterm_t(double ax, double ay, double bx, doubl
 
 // Attraction over the CSR rows [r0, r1) (TsneHelpers.scala:269-306):
 // attr_i = sum_j ex P_ij q_ij (y_i - y_j), and with LOSS the KL terms
-// ex P_ij ln(ex P_ij / (q_ij / Z)).  LPR lanes per row, 64/LPR rows per wave;
-// each lane issues U (col, val) loads and then U dependent Y_j gathers before
-// any arithmetic, so a row of <= LPR*U entries costs two memory round trips.
-// Tail slots gather Y_i with P = 0 (exact no-ops in the sums).  Blocks are
-// XCD-remapped so each XCD's L2 serves one contiguous 1/8 of the
-// Morton-ordered rows (their Y_j are spatial neighbours).
+// ex P_ij ln(ex P_ij / (q_ij / Z)).  LPR lanes per row, 64/LPR rows per wave
+// step; each lane issues U (col, val) loads and then U dependent Y_j gathers
+// before any arithmetic, so a row of <= LPR*U entries costs two memory round
+// trips.  Tail slots gather Y_i with P = 0 (exact no-ops in the sums).
+// Persistent, XCD-partitioned grid (gridDim.x a multiple of 8): the blocks
+// the dispatcher places on XCD x (blockIdx % 8 == x) stride over the x-th
+// contiguous eighth of the Morton-ordered rows, so that XCD's L2 holds the
+// spatially local Y_j of its rows, and waves stay resident across rows (PMC:
+// one-row-per-wave launches kept only ~3.7 waves per SIMD in flight).
 template <int LPR, int U, bool LOSS, int MET>
 __global__ __launch_bounds__(256) void attract_rows(
     const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col, const double *__restrict__ val,
     int64_t r0, int64_t r1, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
     double2 *__restrict__ attr, double *__restrict__ lpart) {
     __shared__ double sl[4];
+    constexpr int RPW = 64 / LPR;   // rows per wave step
     const int sub = threadIdx.x & (LPR - 1);
-    const int64_t blk = xcd_block(blockIdx.x, gridDim.x);
-    const int64_t i = r0 + ((blk * blockDim.x + threadIdx.x) / LPR);
+    const int x = blockIdx.x % NUM_XCD;
+    const int64_t bpx = gridDim.x / NUM_XCD;                   // blocks per XCD
+    const int64_t nrows = r1 - r0;
+    const int64_t q0 = r0 + nrows * x / NUM_XCD, q1 = r0 + nrows * (x + 1) / NUM_XCD;
+    const int64_t wv = (int64_t)(blockIdx.x / NUM_XCD) * 4 + (threadIdx.x >> 6);
+    const int64_t nwv = bpx * 4;
+    const int rsub = (threadIdx.x & 63) / LPR;
+    const double Z = LOSS ? scal[0] : 1.0;
     double lsum = 0.0;
-    if (i < r1) {
-        const double Z = LOSS ? scal[0] : 1.0;
-        const double2 yi = *reinterpret_cast<const double2 *>(Y + 2 * i);
-        const double yx = yi.x, yy = yi.y;
+    for (int64_t i = q0 + wv * RPW + rsub; i - rsub < q1; i += nwv * RPW) {
+        const bool live = i < q1;
         double fx = 0.0, fy = 0.0;
-        const int64_t e1 = row_ptr[i + 1];
-        for (int64_t e = row_ptr[i] + sub; e < e1; e += LPR * U) {
-            int32_t j[U];
-            double pv[U];
+        double yx = 0.0, yy = 0.0;
+        if (live) {
+            const double2 yi = *reinterpret_cast<const double2 *>(Y + 2 * i);
+            yx = yi.x; yy = yi.y;
+            const int64_t e1 = row_ptr[i + 1];
+            for (int64_t e = row_ptr[i] + sub; e < e1; e += LPR * U) {
+                int32_t j[U];
+                double pv[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t o = e + LPR * u;
-                const bool in = o < e1;
-                j[u] = in ? col[o] : (int32_t)i;
-                pv[u] = in ? val[o] : 0.0;
-            }
-            double jx[U], jy[U];
+                for (int u = 0; u < U; ++u) {
+                    const int64_t o = e + LPR * u;
+                    const bool in = o < e1;
+                    j[u] = in ? col[o] : (int32_t)i;
+                    pv[u] = in ? val[o] : 0.0;
+                }
+                double jx[U], jy[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const double2 yj = *reinterpret_cast<const double2 *>(Y + 2 * (int64_t)j[u]);
-                jx[u] = yj.x; jy[u] = yj.y;
-            }
+                for (int u = 0; u < U; ++u) {
+                    const double2 yj = *reinterpret_cast<const double2 *>(Y + 2 * (int64_t)j[u]);
+                    jx[u] = yj.x; jy[u] = yj.y;
+                }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const double pij = __dmul_rn(pv[u], ex);
-                const double q = qterm_t<MET>(yx, yy, jx[u], jy[u]);
-                const double sc = __dmul_rn(pij, q);
-                fx = __dadd_rn(fx, __dmul_rn(sc, __dsub_rn(yx, jx[u])));
-                fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yy, jy[u])));
-                if (LOSS && e + LPR * u < e1) lsum += pij * log(pij / (q / Z));
+                for (int u = 0; u < U; ++u) {
+                    const double pij = __dmul_rn(pv[u], ex);
+                    const double q = qterm_t<MET>(yx, yy, jx[u], jy[u]);
+                    const double sc = __dmul_rn(pij, q);
+                    fx = __dadd_rn(fx, __dmul_rn(sc, __dsub_rn(yx, jx[u])));
+                    fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yy, jy[u])));
+                    if (LOSS && e + LPR * u < e1) lsum += pij * log(pij / (q / Z));
+                }
             }
         }
 #pragma unroll
@@ -178,7 +191,7 @@ __global__ __launch_bounds__(256) void attract_rows(
             fx += __shfl_xor(fx, o, LPR);
             fy += __shfl_xor(fy, o, LPR);
         }
-        if (sub == 0) attr[i - r0] = make_double2(fx, fy);
+        if (live && sub == 0) attr[i - r0] = make_double2(fx, fy);
     }
     if (LOSS) {
         lsum = wave_sum(lsum);
@@ -320,10 +333,22 @@ struct AttractArgs {
     const double *scal; int metric; double ex; double2 *attr; double *lpart;
 };
 
+// persistent grid: 8 resident waves per SIMD, a multiple of the XCD count
+static int64_t attract_grid(int64_t rows, int lpr) {
+    static const int cus = [] {
+        int dev = 0, c = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return c;
+    }();
+    const int64_t full = round_up(cus * 8, NUM_XCD);
+    const int64_t need = round_up(std::max<int64_t>(1, ceil_div(rows * lpr, 256)), NUM_XCD);
+    return std::min(full, need);
+}
+
 template <int LPR, int U, int MET>
 static int64_t attract_launch_m(hipStream_t st, const AttractArgs &a, bool loss) {
     const int64_t rows = a.r1 - a.r0;
-    const int64_t blocks = std::max<int64_t>(1, ceil_div(rows * LPR, 256));
+    const int64_t blocks = attract_grid(rows, LPR);
     if (loss)
         hipLaunchKernelGGL((attract_rows<LPR, U, true, MET>), dim3(blocks), dim3(256), 0, st, a.rp, a.col, a.val,
                            a.r0, a.r1, a.Y, a.scal, a.ex, a.attr, a.lpart);
