@@ -717,7 +717,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
     double fx = 0.0, fy = 0.0, zs = 0.0;
-    unsigned long long nvis = 0, ndense = 0, wpops = 0, wdense = 0;   // w*: wave-level work
+    unsigned long long nvis = 0, ndense = 0, nevals = 0, wpops = 0, wdense = 0, wslots = 0;   // w*: wave-level
     int sp = 0;
     int ntask = 0, nwant = 0;
     const bool mom_on = mom_flag[0] != 0;
@@ -845,6 +845,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
         if (__ballot(act) == 0) continue;
         // the opened cell's quad children, from its record
         const int nch = nd.nch;
+        wslots += (unsigned long long)nch;
+        if (act) nevals += (unsigned long long)nch;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (c >= nch) break;
@@ -883,7 +885,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const int wwant = wave_sum(nwant);
     if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
     if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms,
-                    // [3] wave-level pops, [4] wave-level dense tile points
+                    // [3] wave-level pops, [4] wave-level dense tile points, [5] lane child
+                    // evaluations, [6] wave child slots (lane utilisation = [5] / (64 [6]))
         const unsigned long long tv = wave_sum(nvis), tt = wave_sum((unsigned long long)ntask),
                                  td = wave_sum(ndense);
         if (lane == 0) {
@@ -892,6 +895,11 @@ __global__ __launch_bounds__(256) void bh_traverse(
             atomicAdd(visits + 2, td);
             atomicAdd(visits + 3, wpops);
             atomicAdd(visits + 4, wdense);
+            atomicAdd(visits + 6, wslots);
+        }
+        const unsigned long long te = wave_sum(nevals);
+        if (lane == 0) {
+            atomicAdd(visits + 5, te);
         }
     }
 }
