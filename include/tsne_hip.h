@@ -182,9 +182,10 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
  * [0] reference-equivalent node evaluations (lane visits; a leaf tile of m
  * points counts m), [1] subtree-moment evaluations, [2] dense pair terms,
  * [3] wave-level cell pops, [4] wave-level dense tile points, [5] lane child
- * evaluations, [6] wave child slots (lane utilisation = [5] / (64 * [6])).
+ * evaluations, [6] wave child slots (lane utilisation = [5] / (64 * [6])),
+ * [7] heaviest wave (its pops + dense tile points / 16).
  * enable: 1 on, 0 off, -1 leave unchanged. */
-int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out7);
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out8);
 
 #ifdef __cplusplus
 }

@@ -600,12 +600,14 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
 // fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
 // an IEEE division -- decided by comparing h with theta * D outside a 1e-14
 // relative band (where the rounded quotient cannot cross theta), and by the
-// exact division inside it.  D = 0 or denormal gives h > theta D: opened, as
-// h / 0 = inf is not < theta.
-__device__ __forceinline__ bool summarise(double h, double D, double theta) {
-    const double t = theta * D;
-    if (h < t * (1.0 - 1e-14)) return true;
-    if (h > t * (1.0 + 1e-14)) return false;
+// exact division inside it.  Df may be the FMA-evaluated D (within 1 ulp of
+// the reference's dx*dx + dy*dy); the exact path recomputes the latter.
+// D = 0 or denormal gives h > theta D: opened, as h / 0 = inf is not < theta.
+__device__ __forceinline__ bool summarise(double h, double Df, double dx, double dy, double th_lo, double th_hi,
+                                          double theta) {
+    if (h < th_lo * Df) return true;
+    if (h > th_hi * Df) return false;
+    const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
     return h / D < theta;
 }
 
@@ -616,11 +618,11 @@ __device__ __forceinline__ void cell_force(double dx, double dy, double D, int32
     double Q = __builtin_amdgcn_rcp(x);
     Q = __fma_rn(Q, __fma_rn(-x, Q, 1.0), Q);
     Q = __fma_rn(Q, __fma_rn(-x, Q, 1.0), Q);
-    const double mult = __dmul_rn((double)n, Q);
-    const double sc = __dmul_rn(mult, Q);
-    fx = __dadd_rn(fx, __dmul_rn(sc, dx));
-    fy = __dadd_rn(fy, __dmul_rn(sc, dy));
-    zs = __dadd_rn(zs, mult);
+    const double mult = (double)n * Q;
+    const double sc = mult * Q;
+    fx = __fma_rn(sc, dx, fx);
+    fy = __fma_rn(sc, dy, fy);
+    zs += mult;
 }
 
 // Quad records: one per real node, children found through transparent nodes.
@@ -713,6 +715,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (__ballot(valid) == 0) return;
     const int root = meta[1];
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
+    const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
@@ -735,9 +738,9 @@ __global__ __launch_bounds__(256) void bh_traverse(
             bool open = false;
             if (valid) {
                 ++nvis;
-                const double dx = __dsub_rn(qx, rt.cx), dy = __dsub_rn(qy, rt.cy);
-                const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-                if (summarise(rt.h, D, theta)) cell_force(dx, dy, D, rt.cnt, fx, fy, zs);
+                const double dx = qx - rt.cx, dy = qy - rt.cy;
+                const double D = __fma_rn(dx, dx, dy * dy);
+                if (summarise(rt.h, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rt.cnt, fx, fy, zs);
                 else open = true;
             }
             const uint64_t om = __ballot(open);
@@ -863,9 +866,9 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 bool open = false;
                 if (act) {
                     ++nvis;
-                    const double dx = __dsub_rn(qx, nd.ccx[c]), dy = __dsub_rn(qy, nd.ccy[c]);
-                    const double D = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
-                    if (summarise(chh, D, theta)) cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                    const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                    const double D = __fma_rn(dx, dx, dy * dy);
+                    if (summarise(chh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
                     else open = true;
                 }
                 const uint64_t om = __ballot(open);
@@ -896,6 +899,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
             atomicAdd(visits + 3, wpops);
             atomicAdd(visits + 4, wdense);
             atomicAdd(visits + 6, wslots);
+            atomicMax(visits + 7, wpops + wdense / 16);   // heaviest wave (pops + dense/16)
         }
         const unsigned long long te = wave_sum(nevals);
         if (lane == 0) {
