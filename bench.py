@@ -177,6 +177,7 @@ def main():
                              "dense_points_per_wave": vis_t[4] / max(1, (r1 - r0) / 64),
                              "lane_utilisation": vis_t[5] / max(1, 64 * vis_t[6]),
                              "heaviest_wave_vs_mean": vis_t[7] / max(1e-9, (vis_t[3] + vis_t[4] / 16) / max(1, (r1 - r0) / 64)),
+                             "max_wave_pops": vis_t[8], "max_wave_dense_points": vis_t[9],
                              "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
         if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
             snaps[t] = Y[:n].cpu().numpy().copy()

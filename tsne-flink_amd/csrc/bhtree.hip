@@ -900,6 +900,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
             atomicAdd(visits + 4, wdense);
             atomicAdd(visits + 6, wslots);
             atomicMax(visits + 7, wpops + wdense / 16);   // heaviest wave (pops + dense/16)
+            atomicMax(visits + 8, wpops);
+            atomicMax(visits + 9, wdense);
         }
         const unsigned long long te = wave_sum(nevals);
         if (lane == 0) {

@@ -245,11 +245,11 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
     });
 }
 
-int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out8) {
+int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out10) {
     return guard([&] {
         check_ctx(ctx);
         DeviceGuard g(ctx->device);
-        opt_profile(ctx, enable, ms_out5, counters_out8);
+        opt_profile(ctx, enable, ms_out5, counters_out10);
     });
 }
 

@@ -58,7 +58,7 @@ struct OptState {
     bool profile = false;
     hipEvent_t ev[6] = {};
     double last_ms[5] = {0, 0, 0, 0, 0};
-    int64_t last_visits[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t last_visits[10] = {};
 };
 
 namespace {
@@ -539,7 +539,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 8);
+    s->visits = ws.get<unsigned long long>("opt.visits", 10);
     TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
@@ -589,7 +589,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int c = s->cur;
     double *Y = s->Y[c];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 8 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 10 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 1. tree
@@ -642,9 +642,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
             TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
-        unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long v[10] = {};
         TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
-        for (int k = 0; k < 8; ++k) s->last_visits[k] = (int64_t)v[k];
+        for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
     }
 }
 
@@ -688,7 +688,7 @@ void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits) {
     if (ms5)
         for (int k = 0; k < 5; ++k) ms5[k] = s->last_ms[k];
     if (visits)
-        for (int k = 0; k < 8; ++k) visits[k] = s->last_visits[k];
+        for (int k = 0; k < 10; ++k) visits[k] = s->last_visits[k];
 }
 
 }  // namespace tsne

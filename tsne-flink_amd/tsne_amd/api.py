@@ -194,8 +194,9 @@ class Context:
 
     def dev_opt_profile(self, enable=-1):
         """-> (stage ms[5], BH counters [visits, moment evaluations, dense pair terms,
-        wave-level pops, wave-level dense tile points, lane child evaluations, wave child slots, heaviest wave])"""
+        wave-level pops, wave-level dense tile points, lane child evaluations, wave child slots, heaviest wave, max wave pops,
+        max wave dense points])"""
         ms = np.zeros(5)
-        cnt = np.zeros(8, dtype=np.int64)
+        cnt = np.zeros(10, dtype=np.int64)
         check(lib().tsne_dev_opt_profile(self._h, enable, _ptr(ms), _ptr(cnt)))
         return ms, cnt.tolist()
