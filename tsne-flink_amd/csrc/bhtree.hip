@@ -693,13 +693,40 @@ __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__re
 // D <= near_dmax of q (box corners), the relative deviation is below
 // ~48 theta^2 near_dmax^2 <= BH_NEAR_TOL (bh_near_dmax).  In the tiny-embedding
 // phase (extent ~1e-3) the root passes for every query: one moment task each.
-template <int KPOP>
+// Bits L*i of b (i = 0 .. 64/L - 1) gathered into bits i.
+template <int L> __device__ __forceinline__ uint64_t compress_stride(uint64_t b) {
+    if (L == 1) return b;
+    if (L == 2) {
+        b &= 0x5555555555555555ull;
+        b = (b | (b >> 1)) & 0x3333333333333333ull;
+        b = (b | (b >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        b = (b | (b >> 4)) & 0x00FF00FF00FF00FFull;
+        b = (b | (b >> 8)) & 0x0000FFFF0000FFFFull;
+        return (b | (b >> 16)) & 0xFFFFFFFFull;
+    }
+    b &= 0x1111111111111111ull;   // L == 4
+    b = (b | (b >> 3)) & 0x0303030303030303ull;
+    b = (b | (b >> 6)) & 0x000F000F000F000Full;
+    b = (b | (b >> 12)) & 0x000000FF000000FFull;
+    return (b | (b >> 24)) & 0xFFFFull;
+}
+
+// Traversal kernel (see the comment above).  L lanes per query: a wave holds
+// 64/L Morton-consecutive queries, lane l serves query l / L and the quad
+// children c = l % L, l % L + L, ...; a dense tile's points are split over
+// the L lanes of a query.  L > 1 shortens the sequential pop chain of the
+// heaviest waves (late iterations are bound by one wave in a dense cluster
+// core: up to 30x the mean pops) and halves/quarters the union of opened
+// cells per wave.  Per-query sums are reduced over its L lanes in a fixed
+// order at the end.
+template <int KPOP, int L>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t s0,
     int64_t s1, int xcd_chunk, double2 *__restrict__ F, double *__restrict__ Z,
     unsigned long long *__restrict__ visits) {
+    constexpr int QG = 64 / L;   // queries per wave
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
     __shared__ double2 tbuf[4][64];
@@ -707,12 +734,12 @@ __global__ __launch_bounds__(256) void bh_traverse(
     __shared__ int32_t bref[4][KPOP];
     __shared__ uint64_t bmask[4][KPOP];
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    // XCD-aware: each XCD walks one contiguous 1/8 of the Morton-ordered
-    // queries, so the cells its waves touch stay in its own L2
+    const int qi = lane / L, cs = lane % L;
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
-    const int64_t s = s0 + (blk * 4 + w) * 64 + lane;
+    const int64_t s = s0 + (blk * 4 + w) * QG + qi;
     const bool valid = s < s1;
     if (__ballot(valid) == 0) return;
+    const bool lead = cs == 0;   // the lane that writes per-query results
     const int root = meta[1];
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
@@ -726,24 +753,24 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const bool mom_on = mom_flag[0] != 0;
     // ---- the root: a single point, a key-tie group, or a cell tested like any child
     if (root == ~0) {
-        if (valid) { ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
+        if (valid && lead) { ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
     } else if (root >= 0) {
         const BHNode &rt = nodes[root];
         if (rt.delta >= 62) {
-            for (int p = rt.first; p <= rt.last; ++p) {
+            for (int p = rt.first + cs; p <= rt.last; p += L) {
                 const double2 pp = pos[p];
                 if (valid) { ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
             }
         } else {
             bool open = false;
-            if (valid) {
+            if (valid && lead) {
                 ++nvis;
                 const double dx = qx - rt.cx, dy = qy - rt.cy;
                 const double D = __fma_rn(dx, dx, dy * dy);
                 if (summarise(rt.h, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rt.cnt, fx, fy, zs);
                 else open = true;
             }
-            const uint64_t om = __ballot(open);
+            const uint64_t om = compress_stride<L>(__ballot(open));
             if (om) {
                 if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
                 sp = 1;
@@ -766,121 +793,147 @@ __global__ __launch_bounds__(256) void bh_traverse(
         __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
         __builtin_amdgcn_wave_barrier();
         for (int r = 0; r < k; ++r) {
-        ++wpops;
-        const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
-        const uint64_t msk = bmask[w][r];
-        bool act = (msk >> lane) & 1ull;
-        const QRec &nd = srec[w][r];
-        // all-open tests (per lane) -> direct tile over the subtree's leaves
-        bool tile = false;
-        if (act) {
-            const double cdx = qx - nd.cx, cdy = qy - nd.cy;
-            const double dc = cdx * cdx + cdy * cdy;
-            tile = dc <= nd.rball * nd.rball * (1.0 - 1e-9);
-            if (!tile) {
-                const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-                const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
-                const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-                const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-                tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
-            }
-        }
-        if (__ballot(tile)) {
-            const int a = nd.first, b = nd.last;
-            if (tile) nvis += (unsigned long long)(b - a + 1);
-            // The range holds whole equal-key runs, so either all of the query's
-            // exact duplicates (itself included) are in it or none is.  They add
-            // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
-            // unmasked and the duplicate count is taken off z once.
-            // Lanes whose truncation bound holds record a moment task (evaluated
-            // by moment_apply after the traversal, in recording order); the rest
-            // run the dense tile: points staged through LDS 64 at a time (one
-            // coalesced dwordx4 load per lane, the next chunk prefetched into
-            // registers) and read back as wave-uniform broadcasts.
-            bool usem = false;
-            if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
-                usem = moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy);
-                if (usem) {
-                    ++nwant;
-                    if (mom_on) mtask[(s - s0) * MOM_TASKS + ntask++] = ref;
-                    else usem = false;
+            ++wpops;
+            const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
+            const uint64_t msk = bmask[w][r];
+            bool act = (msk >> qi) & 1ull;
+            const QRec &nd = srec[w][r];
+            // all-open tests (per query, computed alike by its L lanes) -> direct tile
+            bool tile = false;
+            if (act) {
+                const double cdx = qx - nd.cx, cdy = qy - nd.cy;
+                const double dc = cdx * cdx + cdy * cdy;
+                tile = dc <= nd.rball * nd.rball * (1.0 - 1e-9);
+                if (!tile) {
+                    const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+                    const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                    const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                    const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
+                    tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
                 }
             }
-            double tx = 0.0, ty = 0.0, tz = 0.0;
-            const bool dense = tile && !usem;
-            if (__ballot(dense)) {
-                wdense += (unsigned long long)(b - a + 1);
-                double2 *buf = tbuf[w];
-                double2 nxt = make_double2(0.0, 0.0);
-                if (a + lane <= b) nxt = pos[a + lane];
-                double ux = 0.0, uy = 0.0, uz = 0.0;
-                for (int c0 = a; c0 <= b; c0 += 64) {
-                    const int cnt = min(64, b - c0 + 1);
-                    __builtin_amdgcn_wave_barrier();
-                    buf[lane] = nxt;
-                    if (c0 + 64 + lane <= b) nxt = pos[c0 + 64 + lane];
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
-                    __builtin_amdgcn_wave_barrier();
-                    int j = 0;
-                    for (; j + 8 <= cnt; j += 8) {
+            if (__ballot(tile)) {
+                const int a = nd.first, b = nd.last;
+                if (tile && lead) nvis += (unsigned long long)(b - a + 1);
+                // The range holds whole equal-key runs, so either all of the query's
+                // exact duplicates (itself included) are in it or none is.  They add
+                // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
+                // unmasked and the duplicate count is taken off z once.
+                // Queries whose truncation bound holds record a moment task
+                // (evaluated by moment_apply after the traversal, in recording
+                // order); the rest run the dense tile: points staged through LDS
+                // 64 at a time (one coalesced dwordx4 load per lane, the next
+                // chunk prefetched into registers), each of a query's L lanes
+                // summing every L-th point.
+                bool usem = false;
+                if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
+                    usem = moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy);
+                    if (usem) {
+                        if (lead) ++nwant;
+                        if (mom_on) {
+                            if (lead) mtask[(s - s0) * MOM_TASKS + ntask] = ref;
+                            ++ntask;
+                        } else {
+                            usem = false;
+                        }
+                    }
+                }
+                double tx = 0.0, ty = 0.0, tz = 0.0;
+                const bool dense = tile && !usem;
+                if (__ballot(dense)) {
+                    wdense += (unsigned long long)(b - a + 1);
+                    double2 *buf = tbuf[w];
+                    double2 nxt = make_double2(0.0, 0.0);
+                    if (a + lane <= b) nxt = pos[a + lane];
+                    double ux = 0.0, uy = 0.0, uz = 0.0;
+                    for (int c0 = a; c0 <= b; c0 += 64) {
+                        const int cnt = min(64, b - c0 + 1);
+                        __builtin_amdgcn_wave_barrier();
+                        buf[lane] = nxt;
+                        if (c0 + 64 + lane <= b) nxt = pos[c0 + 64 + lane];
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+                        __builtin_amdgcn_wave_barrier();
+                        int j = cs;
+                        for (; j + 7 * L < cnt; j += 8 * L) {
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) {
-                            const double2 pp = buf[j + u];
+                            for (int u = 0; u < 8; ++u) {
+                                const double2 pp = buf[j + u * L];
+                                pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                            }
+                        }
+                        for (; j < cnt; j += L) {
+                            const double2 pp = buf[j];
                             pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
                         }
                     }
-                    for (; j < cnt; ++j) {
-                        const double2 pp = buf[j];
-                        pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                    __builtin_amdgcn_wave_barrier();
+                    if (dense) {
+                        tx = ux; ty = uy; tz = uz;
+                        if (lead) ndense += (unsigned long long)(b - a + 1);
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                if (dense) { tx = ux; ty = uy; tz = uz; ndense += (unsigned long long)(b - a + 1); }
+                if (tile) {
+                    fx += tx;
+                    fy += ty;
+                    zs += tz - ((lead && s >= a && s <= b) ? (double)dupc[s] : 0.0);
+                }
+                act = act && !tile;
             }
-            if (tile) {
-                fx += tx;
-                fy += ty;
-                zs += tz - ((s >= a && s <= b) ? (double)dupc[s] : 0.0);
-            }
-            act = act && !tile;
-        }
-        if (__ballot(act) == 0) continue;
-        // the opened cell's quad children, from its record
-        const int nch = nd.nch;
-        wslots += (unsigned long long)nch;
-        if (act) nevals += (unsigned long long)nch;
+            if (__ballot(act) == 0) continue;
+            // the opened cell's quad children, from its record; lane serves c = cs + L*kk
+            const int nch = nd.nch;
+            wslots += (unsigned long long)nch;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (c >= nch) break;
-            const double chh = nd.ch[c];
-            if (chh == QCH_LEAF) {
-                if (act) { ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
-            } else if (chh == QCH_TIE) {
-                const BHNode &tn = nodes[nd.cref[c]];
-                for (int p = tn.first; p <= tn.last; ++p) {
-                    const double2 pp = pos[p];
-                    if (act) { ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
-                }
-            } else {
+            for (int kk = 0; kk < 4 / L; ++kk) {
+                const int c = cs + L * kk;
                 bool open = false;
-                if (act) {
-                    ++nvis;
-                    const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                    const double D = __fma_rn(dx, dx, dy * dy);
-                    if (summarise(chh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
-                    else open = true;
+                if (c < nch) {
+                    const double chh = nd.ch[c];
+                    if (act) ++nevals;
+                    if (chh == QCH_LEAF) {
+                        if (act) { ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
+                    } else if (chh == QCH_TIE) {
+                        if (act) {
+                            const BHNode &tn = nodes[nd.cref[c]];
+                            for (int p = tn.first; p <= tn.last; ++p) {
+                                const double2 pp = pos[p];
+                                ++nvis;
+                                leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
+                            }
+                        }
+                    } else if (act) {
+                        ++nvis;
+                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                        const double D = __fma_rn(dx, dx, dy * dy);
+                        if (summarise(chh, D, dx, dy, th_lo, th_hi, theta))
+                            cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                        else
+                            open = true;
+                    }
                 }
-                const uint64_t om = __ballot(open);
-                if (om) {
-                    if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
-                    ++sp;
+                const uint64_t ob = __ballot(open);
+                if (ob) {
+#pragma unroll
+                    for (int c2 = 0; c2 < L; ++c2) {
+                        const uint64_t om = compress_stride<L>(ob >> c2);
+                        if (om) {
+                            if (lane == 0) { sref[w][sp] = nd.cref[L * kk + c2]; smask[w][sp] = om; }
+                            ++sp;
+                        }
+                    }
                 }
             }
-        }
         }
     }
-    if (valid) {
+    // per-query sums over its L lanes, fixed order
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) {
+        fx += __shfl_xor(fx, o, 64);
+        fy += __shfl_xor(fy, o, 64);
+        zs += __shfl_xor(zs, o, 64);
+    }
+    if (valid && lead) {
         F[s] = make_double2(fx, fy);
         Z[s] = zs;
         mtask_n[s - s0] = ntask;
@@ -889,23 +942,20 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
     if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms,
                     // [3] wave-level pops, [4] wave-level dense tile points, [5] lane child
-                    // evaluations, [6] wave child slots (lane utilisation = [5] / (64 [6]))
-        const unsigned long long tv = wave_sum(nvis), tt = wave_sum((unsigned long long)ntask),
-                                 td = wave_sum(ndense);
+                    // evaluations, [6] wave child slots x L (utilisation = [5] / (64 [6]))
+        const unsigned long long tv = wave_sum(nvis), tt = wave_sum(lead ? (unsigned long long)ntask : 0ull),
+                                 td = wave_sum(ndense), te = wave_sum(nevals);
         if (lane == 0) {
             atomicAdd(visits, tv);
             atomicAdd(visits + 1, tt);
             atomicAdd(visits + 2, td);
             atomicAdd(visits + 3, wpops);
             atomicAdd(visits + 4, wdense);
-            atomicAdd(visits + 6, wslots);
+            atomicAdd(visits + 5, te);
+            atomicAdd(visits + 6, wslots * L);
             atomicMax(visits + 7, wpops + wdense / 16);   // heaviest wave (pops + dense/16)
             atomicMax(visits + 8, wpops);
             atomicMax(visits + 9, wdense);
-        }
-        const unsigned long long te = wave_sum(nevals);
-        if (lane == 0) {
-            atomicAdd(visits + 5, te);
         }
     }
 }
@@ -1005,12 +1055,16 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                   double2 *dF, double *dz, unsigned long long *visits) {
     if (s1 <= s0) return;
     const double near_dmax = bh_near_dmax(theta);
-    const int64_t waves = ceil_div(s1 - s0, 64);
     // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD block order (TSNE_BH_XCD = run
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
     static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
-    auto kern = kp >= 8 ? bh_traverse<8> : kp >= 4 ? bh_traverse<4> : bh_traverse<1>;
+    static const int lq = [] { const char *e = getenv("TSNE_BH_LANES"); return e ? atoi(e) : 4; }();
+    auto kern = lq >= 4 ? (kp >= 8 ? bh_traverse<8, 4> : bh_traverse<4, 4>)
+              : lq >= 2 ? (kp >= 8 ? bh_traverse<8, 2> : bh_traverse<4, 2>)
+                        : (kp >= 8 ? bh_traverse<8, 1> : bh_traverse<4, 1>);
+    const int L = lq >= 4 ? 4 : lq >= 2 ? 2 : 1;
+    const int64_t waves = ceil_div((s1 - s0) * L, 64);
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
                        t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, xcd, dF, dz,
                        visits);
