@@ -1059,7 +1059,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
     static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
-    static const int lq = [] { const char *e = getenv("TSNE_BH_LANES"); return e ? atoi(e) : 4; }();
+    static const int lq = [] { const char *e = getenv("TSNE_BH_LANES"); return e ? atoi(e) : 1; }();
     auto kern = lq >= 4 ? (kp >= 8 ? bh_traverse<8, 4> : bh_traverse<4, 4>)
               : lq >= 2 ? (kp >= 8 ? bh_traverse<8, 2> : bh_traverse<4, 2>)
                         : (kp >= 8 ? bh_traverse<8, 1> : bh_traverse<4, 1>);
