@@ -627,7 +627,8 @@ __device__ __forceinline__ void cell_force(double dx, double dy, double D, int32
 
 // Quad records: one per real node, children found through transparent nodes.
 __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos,
-                           const int32_t *__restrict__ meta, QRec *__restrict__ qrec) {
+                           const int32_t *__restrict__ meta, double inv_theta, double near_dmax,
+                           QRec *__restrict__ qrec) {
     const int m = meta[0];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m - 1) return;
@@ -666,7 +667,12 @@ __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__re
     }
     (void)ncand;
     for (int k = nc; k < 4; ++k) { r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ch[k] = QCH_LEAF; r.cref[k] = 0; r.ccnt[k] = 0; }
-    r.nch = nc;
+    // QNCH_TILE: some query could pass an all-open test here.  The box test's
+    // max corner distance is at least the squared half-diagonal, so if that
+    // exceeds both hmin / theta and near_dmax (and rball = 0) no query can.
+    const double hx = 0.5 * (nd.bx1 - nd.bx0), hy = 0.5 * (nd.by1 - nd.by0);
+    const bool tile_possible = nd.rball > 0.0 || (hx * hx + hy * hy) * (1.0 - 1e-9) <= fmax(nd.hmin * inv_theta, near_dmax);
+    r.nch = nc | (tile_possible ? QNCH_TILE : 0);
 }
 
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
@@ -800,7 +806,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
             const QRec &nd = srec[w][r];
             // all-open tests (per query, computed alike by its L lanes) -> direct tile
             bool tile = false;
-            if (act) {
+            const int nflags = nd.nch;
+            if (act && (nflags & QNCH_TILE)) {
                 const double cdx = qx - nd.cx, cdy = qy - nd.cy;
                 const double dc = cdx * cdx + cdy * cdy;
                 tile = dc <= nd.rball * nd.rball * (1.0 - 1e-9);
@@ -882,7 +889,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
             }
             if (__ballot(act) == 0) continue;
             // the opened cell's quad children, from its record; lane serves c = cs + L*kk
-            const int nch = nd.nch;
+            const int nch = nflags & 0xff;
             wslots += (unsigned long long)nch;
 #pragma unroll
             for (int kk = 0; kk < 4 / L; ++kk) {
@@ -1008,6 +1015,14 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.sort_tmp = ws.get<uint8_t>("bh.sort_tmp", tb);
 }
 
+// Largest D for which 48 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL (see bh_traverse).
+double bh_near_dmax(double theta) {
+    if (!(theta > 0.0)) return __builtin_inf();   // theta = 0: the reference opens every cell
+    double d = std::sqrt(BH_NEAR_TOL / (48.0 * theta * theta));
+    while (48.0 * theta * theta * d * d * (1.0 + 8.0 * d) > BH_NEAR_TOL) d *= 0.99;
+    return d;
+}
+
 void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
@@ -1026,7 +1041,8 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
-    hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, t.qrec);
+    hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, inv_theta,
+                       bh_near_dmax(theta), t.qrec);
     // subtree moments for the all-open fast path
     hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag);
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_flag,
@@ -1041,14 +1057,6 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(moment_reduce, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
                        t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
-}
-
-// Largest D for which 48 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL (see bh_traverse).
-double bh_near_dmax(double theta) {
-    if (!(theta > 0.0)) return __builtin_inf();   // theta = 0: the reference opens every cell
-    double d = std::sqrt(BH_NEAR_TOL / (48.0 * theta * theta));
-    while (48.0 * theta * theta * d * d * (1.0 + 8.0 * d) > BH_NEAR_TOL) d *= 0.99;
-    return d;
 }
 
 void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,

@@ -31,12 +31,13 @@ struct __attribute__((aligned(16))) BHNode {
 // interact directly).
 constexpr double QCH_LEAF = -1.0;
 constexpr double QCH_TIE = -2.0;
+constexpr int32_t QNCH_TILE = 0x100;   // nch flag: an all-open tile test can pass here
 struct __attribute__((aligned(16))) QRec {
     double cx, cy;              // centre of mass
     double rball, hmin;         // all-open tests (see bottom_up)
     double bx0, bx1, by0, by1;  // bounding box of the subtree's points
     int32_t first, last;        // leaf range in sorted order
-    int32_t cnt, nch;           // cumSize, number of quad children
+    int32_t cnt, nch;           // cumSize, number of quad children | QNCH_TILE
     double ccx[4], ccy[4], ch[4];
     int32_t cref[4], ccnt[4];
 };
