@@ -72,6 +72,17 @@ void tsne_params_default(tsne_params *p);
 int tsne_metric_from_name(const char *name, int32_t *metric_out);
 /* Row shard [r0, r1) of rank `rank` out of `world` (contiguous, balanced). */
 int tsne_shard_rows(int64_t n, int32_t world, int32_t rank, int64_t *r0, int64_t *r1);
+/* Cost-balanced cuts of the Morton-sorted BH queries (the rule the multi-GPU
+ * optimizer applies on the device every iteration): bcost[b] = cost of the
+ * queries [b*bucket, (b+1)*bucket); bounds[0..world] with bounds[0] = 0,
+ * bounds[world] = n and bounds[r] = min(n, (b+1)*bucket) for the first bucket
+ * b whose inclusive cost prefix reaches total*r/world (a zero target cuts at
+ * 0; all-zero costs cut equal counts). */
+int tsne_balance_cuts(const uint64_t *bcost, int64_t nb, int64_t n, int32_t world, int32_t bucket,
+                      int64_t *bounds);
+/* The same cuts computed by the device kernel (bucket 256) from device
+ * buffers; for testing the kernel against tsne_balance_cuts. */
+int tsne_dev_balance_cuts(tsne_ctx *ctx, const uint64_t *d_bcost, int64_t n, int32_t world, int64_t *d_bounds);
 
 /* ---------------------------------------------------------------- context */
 int tsne_ctx_create(int32_t device, tsne_ctx **out);

@@ -351,3 +351,21 @@ def test_moment_path_engaged(ctx):
     O.update(g, Yo, uo, go, p.min_gain, p.initial_momentum, p.learning_rate)
     O.center(Yo)
     assert np.abs(dY.cpu().numpy() - Yo).max() <= 1e-9 * np.abs(Yo).max()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_device_balance_cuts_match_host_rule(ctx, world):
+    """The multi-GPU optimizer's per-iteration cost-balanced BH slices (device
+    kernel balance_slices) equal the host rule tsne_balance_cuts."""
+    import torch
+    rng = np.random.default_rng(world)
+    for n, zero_frac in ((1_000_000, 0.0), (300_000, 0.9), (5_000, 1.0)):
+        nb = -(-n // 256)
+        c = rng.integers(1, 5000, nb).astype(np.uint64)
+        c[rng.random(nb) < zero_frac] = 0
+        want = T.balance_cuts(c, n, world)
+        dc = torch.from_numpy(c.astype(np.int64)).cuda()
+        db = torch.zeros(world + 1, dtype=torch.int64, device="cuda")
+        ctx.dev_balance_cuts(dc, n, world, db)
+        ctx.synchronize()
+        assert db.cpu().numpy().tolist() == want.tolist(), (n, zero_frac)

@@ -1,14 +1,17 @@
 """The N>1 decomposition on CPU: world_size 2 over gloo.
 
 libtsne_hip's multi-GPU iteration (optimize.hip) is: every rank builds the
-same tree from the full Y; rank r computes BH repulsion for its contiguous
-slice of the Morton-sorted points; the (F, z) slices are all-gathered; Z is
-summed locally; rank r runs attraction + update for its rows of P
-(tsne_shard_rows); the updated Y slices are all-gathered; every rank centres.
-This test replays exactly that decomposition with the oracle as the compute
-and torch.distributed (gloo) as the exchange, and checks it reproduces the
-single-process reference iteration.  The slicing comes from the library's
-own host logic (tsne_shard_rows), which needs no GPU.
+same tree from the full Y; rank r computes BH repulsion for its slice of the
+Morton-sorted points, the slices cut by the previous iteration's measured
+per-bucket cost (tsne_balance_cuts: identical cuts on every rank after an
+all-reduce of the bucket costs); the zero-filled (F, z) buffers are
+all-reduced; Z is summed locally; rank r runs attraction + update for its
+rows of P (tsne_shard_rows); the updated Y slices are all-gathered; every
+rank centres.  This test replays exactly that decomposition with the oracle
+as the compute (a per-query force-magnitude cost) and torch.distributed
+(gloo) as the exchange, and checks it reproduces the single-process reference
+iteration.  The slicing comes from the library's own host logic, which needs
+no GPU.
 """
 import os
 import socket
@@ -55,19 +58,34 @@ def _worker(rank, world, port, T, out_path):
     chunk = -(-n // world)
     upd, gains = np.zeros_like(Y), np.ones_like(Y)
     losses = {}
+    BUCKET = 16
+    cut_log = []
+    nb = -(-n // BUCKET)
+    bounds = np.array([min(n, chunk * r) for r in range(world + 1)], dtype=np.int64)
     for t in range(1, T + 1):
         ex = 4.0 if t <= 101 else 1.0
         mom = 0.5 if t <= 20 else 0.8
-        # BH for this rank's slice of the sorted order
+        # BH for this rank's cost-balanced slice of the sorted order
         order = _sorted_order(Y)
-        sl = order[r0:r1]
-        rep_s, z_s = Ow.repulsion_queries(Y, 0.5, Y[sl])
-        buf = np.zeros((chunk, 3))
-        buf[: r1 - r0, :2] = rep_s
-        buf[: r1 - r0, 2] = z_s
-        gathered = [torch.zeros(chunk, 3, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(gathered, torch.from_numpy(buf))
-        full = torch.cat(gathered).numpy()[:n]
+        b0, b1 = int(bounds[rank]), int(bounds[rank + 1])
+        sl = order[b0:b1]
+        full = np.zeros((n, 3))
+        cost = np.zeros(nb, dtype=np.uint64)
+        if b1 > b0:
+            rep_s, z_s = Ow.repulsion_queries(Y, 0.5, Y[sl])
+            full[b0:b1, :2] = rep_s
+            full[b0:b1, 2] = z_s
+            # any per-query cost measured on the slice will do; the library uses its wave pops
+            vis = (1 + 100.0 * np.abs(rep_s).sum(1) / max(1e-300, np.abs(rep_s).sum(1).max())).astype(np.uint64)
+            np.add.at(cost, np.arange(b0, b1) // BUCKET, vis)
+        ft = torch.from_numpy(full)
+        dist.all_reduce(ft)                                    # zero-filled slices: exact sum
+        full = ft.numpy()
+        ct = torch.from_numpy(cost.astype(np.int64))
+        dist.all_reduce(ct)
+        bounds = TA.balance_cuts(ct.numpy().astype(np.uint64), n, world, bucket=BUCKET)
+        if rank == 0:
+            cut_log.append(bounds.tolist())
         rep = np.zeros((n, 2))
         z = np.zeros(n)
         rep[order] = full[:, :2]
@@ -89,7 +107,8 @@ def _worker(rank, world, port, T, out_path):
             dist.all_reduce(lt)
             losses[t] = float(lt.item())
     if rank == 0:
-        np.savez(out_path, Y=Y, keys=np.array(sorted(losses)), vals=np.array([losses[k] for k in sorted(losses)]))
+        np.savez(out_path, Y=Y, keys=np.array(sorted(losses)), vals=np.array([losses[k] for k in sorted(losses)]),
+                 cuts=np.array(cut_log))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -102,7 +121,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_sharded_iteration_matches_single_process(tmp_path, world):
     T = 30
     out = tmp_path / "sharded.npz"
@@ -116,3 +135,22 @@ def test_sharded_iteration_matches_single_process(tmp_path, world):
     for k, v in zip(res["keys"], res["vals"]):
         assert abs(v - ref[int(k)]) <= 1e-9 * abs(ref[int(k)])
     assert np.abs(res["Y"] - Y).max() <= 1e-9 * np.abs(Y).max()
+    cuts = res["cuts"]
+    assert (np.diff(cuts, axis=1) >= 0).all() and (cuts[:, 0] == 0).all() and (cuts[:, -1] == Y.shape[0]).all()
+    assert len({tuple(c) for c in cuts}) > 1        # the cuts follow the measured costs
+
+
+def test_balance_cuts_rule():
+    """tsne_balance_cuts (host mirror of the device rule in bhtree.hip)."""
+    import tsne_amd as TA
+    assert TA.balance_cuts([0, 0, 0, 0], 1000, 4).tolist() == [0, 250, 500, 750, 1000]
+    assert TA.balance_cuts([1, 1, 1, 1], 1000, 2).tolist() == [0, 512, 1000]
+    assert TA.balance_cuts([100, 1, 1, 1], 1000, 2).tolist() == [0, 256, 1000]
+    assert TA.balance_cuts([1], 10, 8).tolist() == [0, 0, 0, 0, 0, 0, 0, 0, 10]
+    rng = np.random.default_rng(0)
+    c = rng.integers(0, 1000, 500)
+    b = TA.balance_cuts(c, 500 * 256 - 7, 8)
+    pre = np.concatenate([[0], np.cumsum(c)])
+    for r in range(1, 8):
+        k = b[r] // 256
+        assert pre[k] >= c.sum() * r // 8 > pre[k - 1]

@@ -578,16 +578,18 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
                                                     const BHNode *__restrict__ nodes,
                                                     const double *__restrict__ mom,
                                                     const int32_t *__restrict__ mtask,
-                                                    const int32_t *__restrict__ mtask_n, int64_t s0,
-                                                    int64_t s1, double2 *__restrict__ F, double *__restrict__ Z) {
-    const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= s1) return;
-    const int nt = mtask_n[s - s0];
+                                                    const int32_t *__restrict__ mtask_n, int64_t g0,
+                                                    int64_t g1, const int64_t *__restrict__ dbounds,
+                                                    double2 *__restrict__ F, double *__restrict__ Z) {
+    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
+    const int64_t s = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < s0 || s >= s1) return;
+    const int nt = mtask_n[s];
     if (nt == 0) return;
     const double2 q = pos[s];
     double fx = 0.0, fy = 0.0, zs = 0.0;
     for (int k = 0; k < nt; ++k) {
-        const int node = mtask[(s - s0) * MOM_TASKS + k];
+        const int node = mtask[s * MOM_TASKS + k];
         double cx, cy, R;
         box_centre(nodes[node], cx, cy, R);
         moment_eval(mom + (int64_t)node * MOM_K, q.x - cx, q.y - cy, fx, fy, zs);
@@ -729,9 +731,9 @@ template <int KPOP, int L>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
-    const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t s0,
-    int64_t s1, int xcd_chunk, double2 *__restrict__ F, double *__restrict__ Z,
-    unsigned long long *__restrict__ visits) {
+    const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
+    int64_t g1, const int64_t *__restrict__ dbounds, int xcd_chunk, double2 *__restrict__ F,
+    double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost) {
     constexpr int QG = 64 / L;   // queries per wave
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
@@ -742,8 +744,10 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int qi = lane / L, cs = lane % L;
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
-    const int64_t s = s0 + (blk * 4 + w) * QG + qi;
-    const bool valid = s < s1;
+    // queries [s0, s1): this rank's slice (device bounds when cost-balanced across ranks)
+    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
+    const int64_t s = g0 + (blk * 4 + w) * QG + qi;
+    const bool valid = s >= s0 && s < s1;
     if (__ballot(valid) == 0) return;
     const bool lead = cs == 0;   // the lane that writes per-query results
     const int root = meta[1];
@@ -838,7 +842,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     if (usem) {
                         if (lead) ++nwant;
                         if (mom_on) {
-                            if (lead) mtask[(s - s0) * MOM_TASKS + ntask] = ref;
+                            if (lead) mtask[s * MOM_TASKS + ntask] = ref;
                             ++ntask;
                         } else {
                             usem = false;
@@ -943,10 +947,14 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (valid && lead) {
         F[s] = make_double2(fx, fy);
         Z[s] = zs;
-        mtask_n[s - s0] = ntask;
+        mtask_n[s] = ntask;
     }
     const int wwant = wave_sum(nwant);
     if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
+    if (bcost) {   // cost of this wave (in cell-pop units) into its first query's 256-query bucket
+        const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
+        if (lane == 0) atomicAdd(&bcost[sf >> 8], wpops + wdense / 48 + 4);
+    }
     if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms,
                     // [3] wave-level pops, [4] wave-level dense tile points, [5] lane child
                     // evaluations, [6] wave child slots x L (utilisation = [5] / (64 [6]))
@@ -1015,6 +1023,53 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.sort_tmp = ws.get<uint8_t>("bh.sort_tmp", tb);
 }
 
+// Cost-balanced query slices for the next iteration: one 1024-thread block
+// scans the (all-reduced, so identical on every rank) 256-query bucket costs
+// and cuts the sorted order into world pieces of equal cost.
+__global__ __launch_bounds__(1024) void balance_slices(const unsigned long long *__restrict__ bcost, int64_t nb,
+                                                       int64_t n, int world, int64_t *__restrict__ bounds) {
+    __shared__ unsigned long long part[1024];
+    __shared__ unsigned long long total;
+    const int t = threadIdx.x;
+    const int64_t per = (nb + 1023) / 1024, b0 = t * per, b1 = min(nb, b0 + per);
+    unsigned long long acc = 0;
+    for (int64_t b = b0; b < b1; ++b) acc += bcost[b];
+    part[t] = acc;
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long run = 0;
+        for (int k = 0; k < 1024; ++k) { const unsigned long long v = part[k]; part[k] = run; run += v; }
+        total = run;
+        bounds[0] = 0;
+        bounds[world] = n;
+        for (int r = 1; r < world; ++r)   // a zero target cuts at 0; the scan sets the others
+            bounds[r] = (run / world * r + (run % world) * r / world) == 0 ? 0 : n;
+    }
+    __syncthreads();
+    // thread t owns buckets [b0, b1) with exclusive prefix part[t]
+    unsigned long long run = part[t];
+    for (int64_t b = b0; b < b1; ++b) {
+        const unsigned long long nxt = run + bcost[b];
+        for (int r = 1; r < world; ++r) {
+            const unsigned long long target = total / world * r + (total % world) * r / world;
+            if (run < target && nxt >= target) bounds[r] = min(n, (b + 1) << 8);
+        }
+        run = nxt;
+    }
+    __syncthreads();
+    if (t == 0) {   // all-zero costs: equal counts; keep the cuts monotone
+        for (int r = 1; r < world; ++r) {
+            if (total == 0) bounds[r] = n * r / world;
+            if (bounds[r] < bounds[r - 1]) bounds[r] = bounds[r - 1];
+        }
+    }
+}
+
+void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int world, int64_t *bounds) {
+    hipLaunchKernelGGL(balance_slices, dim3(1), dim3(1024), 0, ctx->stream, bcost, ceil_div(n, 256), n, world, bounds);
+    TSNE_LAUNCH_CHECK();
+}
+
 // Largest D for which 48 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL (see bh_traverse).
 double bh_near_dmax(double theta) {
     if (!(theta > 0.0)) return __builtin_inf();   // theta = 0: the reference opens every cell
@@ -1060,7 +1115,8 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
 }
 
 void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
-                  double2 *dF, double *dz, unsigned long long *visits) {
+                  double2 *dF, double *dz, unsigned long long *visits, const int64_t *dbounds,
+                  unsigned long long *bcost) {
     if (s1 <= s0) return;
     const double near_dmax = bh_near_dmax(theta);
     // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD block order (TSNE_BH_XCD = run
@@ -1074,10 +1130,10 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     const int L = lq >= 4 ? 4 : lq >= 2 ? 2 : 1;
     const int64_t waves = ceil_div((s1 - s0) * L, 64);
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, xcd, dF, dz,
-                       visits);
+                       t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dbounds, xcd,
+                       dF, dz, visits, bcost);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.mtask, t.mtask_n, s0, s1, dF, dz);
+                       t.mtask, t.mtask_n, s0, s1, dbounds, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <new>
 
+#include "bhtree.hpp"
 #include "common.hpp"
 
 namespace tsne {
@@ -91,6 +92,42 @@ int tsne_shard_rows(int64_t n, int32_t world, int32_t rank, int64_t *r0, int64_t
         const int64_t a = std::min<int64_t>(n, chunk * rank);
         if (r0) *r0 = a;
         if (r1) *r1 = std::min<int64_t>(n, a + chunk);
+    });
+}
+
+int tsne_balance_cuts(const uint64_t *bcost, int64_t nb, int64_t n, int32_t world, int32_t bucket,
+                      int64_t *bounds) {
+    return guard([&] {
+        TSNE_REQUIRE(bounds != nullptr && (bcost != nullptr || nb == 0) && nb >= 0 && n >= 0 && world >= 1 &&
+                         bucket >= 1,
+                     "bad balance arguments");
+        uint64_t total = 0;
+        for (int64_t b = 0; b < nb; ++b) total += bcost[b];
+        bounds[0] = 0;
+        bounds[world] = n;
+        for (int r = 1; r < world; ++r) {
+            const uint64_t target = total / world * r + (total % world) * r / world;
+            bounds[r] = target == 0 ? 0 : n;
+            uint64_t run = 0;
+            for (int64_t b = 0; b < nb; ++b) {
+                const uint64_t nxt = run + bcost[b];
+                if (run < target && nxt >= target) { bounds[r] = std::min<int64_t>(n, (b + 1) * bucket); break; }
+                run = nxt;
+            }
+        }
+        for (int r = 1; r < world; ++r) {
+            if (total == 0) bounds[r] = n * r / world;
+            if (bounds[r] < bounds[r - 1]) bounds[r] = bounds[r - 1];
+        }
+    });
+}
+
+int tsne_dev_balance_cuts(tsne_ctx *ctx, const uint64_t *d_bcost, int64_t n, int32_t world, int64_t *d_bounds) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(d_bcost != nullptr && d_bounds != nullptr && n >= 0 && world >= 1, "bad balance arguments");
+        bh_balance(ctx, reinterpret_cast<const unsigned long long *>(d_bcost), n, world, d_bounds);
     });
 }
 

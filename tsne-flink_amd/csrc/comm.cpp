@@ -1,8 +1,10 @@
 // comm.cpp -- RCCL (over xGMI) for the row-sharded multi-GPU path: one
 // process per GPU, the unique id shipped out of band by the caller.
-// Per optimizer iteration the only traffic is the all-gather of the (F, z)
-// slices, the all-gather of the updated embedding slices, and every 10th
-// iteration a one-double all-reduce of the loss.
+// Per optimizer iteration the traffic is an all-reduce of the zero-filled
+// (F, z) buffers holding each rank's cost-balanced BH slice, an all-reduce of
+// the 256-query bucket costs (n/256 integers), the all-gather of the updated
+// embedding slices, and every 10th iteration a one-double all-reduce of the
+// loss.
 #include <rccl/rccl.h>
 
 #include "common.hpp"
@@ -55,6 +57,12 @@ void comm_allgather_bytes(tsne_ctx *ctx, const void *send, void *recv, size_t by
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
     nccl_check(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, ctx->comm->comm, ctx->stream),
                "ncclAllGather");
+}
+
+void comm_allreduce_sum_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) {
+    TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
+    nccl_check(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, ctx->comm->comm, ctx->stream),
+               "ncclAllReduce");
 }
 
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count) {

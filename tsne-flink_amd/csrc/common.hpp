@@ -146,6 +146,7 @@ void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id);
 void comm_destroy(tsne_ctx *ctx);
 void comm_allgather_bytes(tsne_ctx *ctx, const void *send, void *recv, size_t bytes_per_rank);
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count);
+void comm_allreduce_sum_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count);
 
 }  // namespace tsne
 

@@ -49,6 +49,8 @@ struct OptState {
     double *Ynew = nullptr;   // npad x 2
     double2 *F = nullptr;     // npad, sorted order
     double2 *attr = nullptr;  // chunk: attraction of the owned rows
+    int64_t *bounds = nullptr;             // world + 1: BH query slices (device)
+    unsigned long long *bcost = nullptr;   // 256-query bucket costs of the last traversal
     double *z = nullptr;      // npad, sorted order
     double *scal = nullptr;   // [0] Z, [1] loss, [2..3] mean
     double *part = nullptr;   // reduction partials
@@ -552,6 +554,14 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->Ynew = ws.get<double>("opt.Ynew", 2 * s->npad);
     s->F = ws.get<double2>("opt.F", s->npad);
     s->attr = ws.get<double2>("opt.attr", s->chunk);
+    s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
+    s->bounds = ws.get<int64_t>("opt.bounds", ctx->world + 1);
+    {
+        std::vector<int64_t> b0(ctx->world + 1);
+        for (int r = 0; r <= ctx->world; ++r) b0[r] = std::min<int64_t>(n, s->chunk * r);
+        TSNE_HIP(hipMemcpyAsync(s->bounds, b0.data(), sizeof(int64_t) * b0.size(), hipMemcpyHostToDevice, st));
+        TSNE_HIP(hipStreamSynchronize(st));
+    }
     s->z = ws.get<double>("opt.z", s->npad);
     s->scal = ws.get<double>("opt.scal", 8);
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(s->chunk)));
@@ -626,13 +636,27 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // 1. tree
     bh_build(ctx, s->tree, Y, p.theta);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
-    // 2. repulsion for this rank's slice of sorted points
-    bh_repulsion(ctx, s->tree, p.theta, s->r0, s->r1, s->F, s->z, s->profile ? s->visits : nullptr);
+    // 2. repulsion for this rank's slice of the Morton-sorted points.  With
+    // several ranks the slices are cut by the previous iteration's measured
+    // cost (bucket costs all-reduced, identical cuts on every rank), and the
+    // (F, z) slices are combined by an all-reduce over zero-filled buffers.
+    const int64_t nb = ceil_div(n, 256);
+    if (ctx->world > 1) {
+        TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * n, st));
+        TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * n, st));
+        TSNE_HIP(hipMemsetAsync(s->bcost, 0, sizeof(unsigned long long) * nb, st));
+        bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr,
+                     s->bounds + ctx->rank, s->bcost);
+    } else {
+        bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
+    }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. exchange + Z
     if (ctx->world > 1) {
-        comm_allgather_bytes(ctx, s->F + s->r0, s->F, sizeof(double2) * s->chunk);
-        comm_allgather_bytes(ctx, s->z + s->r0, s->z, sizeof(double) * s->chunk);
+        comm_allreduce_sum_f64(ctx, reinterpret_cast<double *>(s->F), 2 * (size_t)n);
+        comm_allreduce_sum_f64(ctx, s->z, (size_t)n);
+        comm_allreduce_sum_u64(ctx, s->bcost, (size_t)nb);
+        bh_balance(ctx, s->bcost, n, ctx->world, s->bounds);
     }
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);

@@ -5,5 +5,6 @@ bench.py and __graft_entry__.  The library must be built in-tree
 (`make -C tsne-flink_amd`); there is no CPU fallback: every call fails loudly
 if the HIP library or a GPU is missing.
 """
-from ._lib import (METRICS, TsneError, lib, lib_path, metric_from_name, shard_rows)  # noqa: F401
+from ._lib import (METRICS, TsneError, balance_cuts, lib, lib_path, metric_from_name,  # noqa: F401
+                   shard_rows)
 from .api import Context, Params  # noqa: F401

@@ -35,6 +35,8 @@ SIGNATURES = {
     "tsne_params_default": (None, [C.POINTER(Params)]),
     "tsne_metric_from_name": (C.c_int, [C.c_char_p, PI32]),
     "tsne_shard_rows": (C.c_int, [I64, I32, I32, PI64, PI64]),
+    "tsne_balance_cuts": (C.c_int, [P, I64, I64, I32, I32, P]),
+    "tsne_dev_balance_cuts": (C.c_int, [P, P, I64, I32, P]),
     "tsne_ctx_create": (C.c_int, [I32, C.POINTER(P)]),
     "tsne_ctx_destroy": (C.c_int, [P]),
     "tsne_ctx_set_stream": (C.c_int, [P, P]),
@@ -101,3 +103,13 @@ def shard_rows(n, world, rank):
     a, b = C.c_int64(), C.c_int64()
     check(lib().tsne_shard_rows(n, world, rank, C.byref(a), C.byref(b)))
     return a.value, b.value
+
+
+def balance_cuts(bcost, n, world, bucket=256):
+    """tsne_balance_cuts: cost-balanced query cuts (host mirror of the device rule)."""
+    import numpy as np
+    b = np.ascontiguousarray(bcost, dtype=np.uint64)
+    out = np.zeros(world + 1, dtype=np.int64)
+    check(lib().tsne_balance_cuts(b.ctypes.data_as(C.c_void_p), b.size, n, world, bucket,
+                                  out.ctypes.data_as(C.c_void_p)))
+    return out

@@ -192,6 +192,10 @@ class Context:
         k = min(nl.value, cap)
         return dict(zip(keys[:k].tolist(), vals[:k].tolist()))
 
+    def dev_balance_cuts(self, bcost, n, world, bounds):
+        """tsne_dev_balance_cuts on device tensors (uint64/int64 bucket costs, int64 bounds[world+1])."""
+        check(lib().tsne_dev_balance_cuts(self._h, _ptr(bcost), n, world, _ptr(bounds)))
+
     def dev_opt_profile(self, enable=-1):
         """-> (stage ms[5], BH counters [visits, moment evaluations, dense pair terms,
         wave-level pops, wave-level dense tile points, lane child evaluations, wave child slots, heaviest wave, max wave pops,
