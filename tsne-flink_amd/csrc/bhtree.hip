@@ -382,12 +382,14 @@ __device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double 
     box_centre(nd.bx0, nd.bx1, nd.by0, nd.by1, cx, cy, R);
 }
 
-// Moments are built only when the previous traversal had tiles that could use
-// them (mom_flag[1] > 0); mom_flag[0] tells this build's traversal whether
-// they exist.  Eligible tiles are counted even when they are off, so the next
+// Moments are built only when the previous traversal had enough tiles that
+// could use them (mom_flag[1]); mom_flag[0] tells this build's traversal
+// whether they exist.  Eligible tiles are counted even when they are off, so the next
 // iteration turns them back on.
-__global__ void moment_gate(int32_t *mom_flag) {
-    mom_flag[0] = mom_flag[1] > 0;
+__global__ void moment_gate(int32_t *mom_flag, int64_t n) {
+    // worth building when the previous traversal had at least n / 64 eligible
+    // tiles (fewer go to dense tiles, cheaper than ~1 ms of moment building)
+    mom_flag[0] = (int64_t)mom_flag[1] >= (n >> 6) + 1;
     mom_flag[1] = 0;
 }
 
@@ -400,12 +402,17 @@ __global__ void moment_count(const BHNode *__restrict__ nodes, int64_t n, const 
     int32_t c = 0;
     if (i < m - 1 && mom_flag[0]) {
         const BHNode &nd = nodes[i];
-        if (nd.cnt >= MOM_MIN_POINTS && nd.delta < 62) {
-            c = (nd.cnt + MOM_CHUNK - 1) / MOM_CHUNK;
-            list[atomicAdd(&meta_w[2], 1)] = (int32_t)i;
-        }
+        if (nd.cnt >= MOM_MIN_POINTS && nd.delta < 62) c = (nd.cnt + MOM_CHUNK - 1) / MOM_CHUNK;
     }
     cnt[i] = c;
+    // append flagged nodes to the list: one atomic per wave
+    const uint64_t bal = __ballot(c > 0);
+    if (bal) {
+        int base = 0;
+        if (lane_id() == 0) base = atomicAdd(&meta_w[2], (int)__popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (c > 0) list[base + __popcll(bal & lanemask_lt())] = (int32_t)i;
+    }
 }
 
 __global__ void moment_fill(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
@@ -1004,7 +1011,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.mom_item = ws.get<int32_t>("bh.mom_item", t.mom_items_cap);
     t.mom_part = ws.get<double>("bh.mom_part", (size_t)t.mom_items_cap * MOM_K);
     t.mom_flag = ws.get<int32_t>("bh.mom_flag", 2);
-    const int32_t flag_init[2] = {1, 1};   // first build: moments on
+    const int32_t flag_init[2] = {1, INT32_MAX};   // first build: moments on
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
@@ -1099,7 +1106,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, inv_theta,
                        bh_near_dmax(theta), t.qrec);
     // subtree moments for the all-open fast path
-    hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag);
+    hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag, n);
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_flag,
                        t.mom_cnt, t.mom_list, t.meta);
     size_t sb = t.scan_tmp_bytes;
