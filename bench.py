@@ -174,7 +174,7 @@ def main():
                              "moment_evals_per_point": vis_t[1] / max(1, r1 - r0),
                              "dense_pairs_per_point": vis_t[2] / max(1, r1 - r0),
                              "pops_per_wave": vis_t[3] / max(1, (r1 - r0) / 64),
-                             "dense_points_per_wave": vis_t[4] / max(1, (r1 - r0) / 64),
+                             "tile_points_per_wave": vis_t[4] / max(1, (r1 - r0) / 64),
                              "lane_utilisation": vis_t[5] / max(1, 64 * vis_t[6]),
                              "heaviest_wave_vs_mean": vis_t[7] / max(1e-9, (vis_t[3] + vis_t[4] / 16) / max(1, (r1 - r0) / 64)),
                              "max_wave_pops": vis_t[8], "max_wave_dense_points": vis_t[9],

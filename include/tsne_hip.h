@@ -192,10 +192,10 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
  * Also BH work counters of the last step (counters_out5, may be NULL):
  * [0] reference-equivalent node evaluations (lane visits; a leaf tile of m
  * points counts m), [1] subtree-moment evaluations, [2] dense pair terms,
- * [3] wave-level cell pops, [4] wave-level dense tile points, [5] lane child
+ * [3] wave-level cell pops, [4] wave-level tile points, [5] lane child
  * evaluations, [6] wave child slots (lane utilisation = [5] / (64 * [6])),
- * [7] heaviest wave (its pops + dense tile points / 16), [8] most pops of a
- * wave, [9] most dense tile points of a wave.
+ * [7] heaviest wave (its pops + tile points / 16), [8] most pops of a
+ * wave, [9] most tile points of a wave.
  * enable: 1 on, 0 off, -1 leave unchanged. */
 int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out10);
 

@@ -57,7 +57,6 @@ constexpr int MOM_K = (MOM_DEG + 1) * (MOM_DEG + 2) / 2;
 constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-14;
-constexpr int MOM_TASKS = 128;  // moment tasks recorded per query; more -> dense tiles
 constexpr double BH_NEAR_TOL = 1e-7;    // near-exact subtree test (bh_traverse): 1000x below
                                         // the north-star 1e-4 gradient tolerance
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
@@ -579,33 +578,6 @@ __device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, do
     return (MOM_ORDER + 2) * rp <= MOM_TOL * (1.0 - rho) * (1.0 - rho);
 }
 
-// Moment tasks of each query (sorted positions [s0, s1)), in traversal order,
-// added to the traversal's F and z.
-__global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ pos,
-                                                    const BHNode *__restrict__ nodes,
-                                                    const double *__restrict__ mom,
-                                                    const int32_t *__restrict__ mtask,
-                                                    const int32_t *__restrict__ mtask_n, int64_t g0,
-                                                    int64_t g1, const int64_t *__restrict__ dbounds,
-                                                    double2 *__restrict__ F, double *__restrict__ Z) {
-    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
-    const int64_t s = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < s0 || s >= s1) return;
-    const int nt = mtask_n[s];
-    if (nt == 0) return;
-    const double2 q = pos[s];
-    double fx = 0.0, fy = 0.0, zs = 0.0;
-    for (int k = 0; k < nt; ++k) {
-        const int node = mtask[s * MOM_TASKS + k];
-        double cx, cy, R;
-        box_centre(nodes[node], cx, cy, R);
-        moment_eval(mom + (int64_t)node * MOM_K, q.x - cx, q.y - cy, fx, fy, zs);
-    }
-    const double2 f = F[s];
-    F[s] = make_double2(f.x + fx, f.y + fy);
-    Z[s] = Z[s] + zs;
-}
-
 // fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
 // an IEEE division -- decided by comparing h with theta * D outside a 1e-14
 // relative band (where the rounded quotient cannot cross theta), and by the
@@ -708,55 +680,36 @@ __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__re
 // D <= near_dmax of q (box corners), the relative deviation is below
 // ~48 theta^2 near_dmax^2 <= BH_NEAR_TOL (bh_near_dmax).  In the tiny-embedding
 // phase (extent ~1e-3) the root passes for every query: one moment task each.
-// Bits L*i of b (i = 0 .. 64/L - 1) gathered into bits i.
-template <int L> __device__ __forceinline__ uint64_t compress_stride(uint64_t b) {
-    if (L == 1) return b;
-    if (L == 2) {
-        b &= 0x5555555555555555ull;
-        b = (b | (b >> 1)) & 0x3333333333333333ull;
-        b = (b | (b >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-        b = (b | (b >> 4)) & 0x00FF00FF00FF00FFull;
-        b = (b | (b >> 8)) & 0x0000FFFF0000FFFFull;
-        return (b | (b >> 16)) & 0xFFFFFFFFull;
-    }
-    b &= 0x1111111111111111ull;   // L == 4
-    b = (b | (b >> 3)) & 0x0303030303030303ull;
-    b = (b | (b >> 6)) & 0x000F000F000F000Full;
-    b = (b | (b >> 12)) & 0x000000FF000000FFull;
-    return (b | (b >> 24)) & 0xFFFFull;
-}
+// Dense leaf tiles are not run inside the traversal: the wave appends (leaf
+// range, lane mask) to its own task list (DENSE_CAP entries; when full, the
+// lanes simply keep traversing the subtree -- the reference's own path) and
+// dense_apply sums the tiles afterwards.  This keeps the traversal at <= 64
+// VGPRs (8 waves per SIMD to hide the record fetches) instead of ~100.
 
-// Traversal kernel (see the comment above).  L lanes per query: a wave holds
-// 64/L Morton-consecutive queries, lane l serves query l / L and the quad
-// children c = l % L, l % L + L, ...; a dense tile's points are split over
-// the L lanes of a query.  L > 1 shortens the sequential pop chain of the
-// heaviest waves (late iterations are bound by one wave in a dense cluster
-// core: up to 30x the mean pops) and halves/quarters the union of opened
-// cells per wave.  Per-query sums are reduced over its L lanes in a fixed
-// order at the end.
-template <int KPOP, int L>
+// Traversal kernel (see the comment above).  STATS: per-wave work counters
+// (profiling, and the bucket costs of the multi-GPU balancing); the
+// production instantiation carries none.
+template <int KPOP, bool STATS>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
-    const QRec *__restrict__ qrec, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
+    const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
     int64_t g1, const int64_t *__restrict__ dbounds, int xcd_chunk, double2 *__restrict__ F,
     double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost) {
-    constexpr int QG = 64 / L;   // queries per wave
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
-    __shared__ double2 tbuf[4][64];
     __shared__ QRec srec[4][KPOP];
     __shared__ int32_t bref[4][KPOP];
     __shared__ uint64_t bmask[4][KPOP];
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int qi = lane / L, cs = lane % L;
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t wid = blk * 4 + w;   // wave slot: queries g0 + 64 wid .. + 63, tile list wid
     // queries [s0, s1): this rank's slice (device bounds when cost-balanced across ranks)
     const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
-    const int64_t s = g0 + (blk * 4 + w) * QG + qi;
+    const int64_t s = g0 + wid * 64 + lane;
     const bool valid = s >= s0 && s < s1;
+    if (lane == 0) ttask_n[wid] = 0;
     if (__ballot(valid) == 0) return;
-    const bool lead = cs == 0;   // the lane that writes per-query results
     const int root = meta[1];
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
@@ -764,30 +717,30 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
     double fx = 0.0, fy = 0.0, zs = 0.0;
-    unsigned long long nvis = 0, ndense = 0, nevals = 0, wpops = 0, wdense = 0, wslots = 0;   // w*: wave-level
+    unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
     int sp = 0;
-    int ntask = 0, nwant = 0;
-    const bool mom_on = mom_flag[0] != 0;
+    int ntt = 0;
+    TileTask *mytt = ttask + wid * TILE_CAP;
     // ---- the root: a single point, a key-tie group, or a cell tested like any child
     if (root == ~0) {
-        if (valid && lead) { ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
+        if (valid) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
     } else if (root >= 0) {
         const BHNode &rt = nodes[root];
         if (rt.delta >= 62) {
-            for (int p = rt.first + cs; p <= rt.last; p += L) {
+            for (int p = rt.first; p <= rt.last; ++p) {
                 const double2 pp = pos[p];
-                if (valid) { ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                if (valid) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
             }
         } else {
             bool open = false;
-            if (valid && lead) {
-                ++nvis;
+            if (valid) {
+                if (STATS) ++nvis;
                 const double dx = qx - rt.cx, dy = qy - rt.cy;
                 const double D = __fma_rn(dx, dx, dy * dy);
                 if (summarise(rt.h, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rt.cnt, fx, fy, zs);
                 else open = true;
             }
-            const uint64_t om = compress_stride<L>(__ballot(open));
+            const uint64_t om = __ballot(open);
             if (om) {
                 if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
                 sp = 1;
@@ -810,12 +763,12 @@ __global__ __launch_bounds__(256) void bh_traverse(
         __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
         __builtin_amdgcn_wave_barrier();
         for (int r = 0; r < k; ++r) {
-            ++wpops;
+            if (STATS) ++wpops;
             const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
             const uint64_t msk = bmask[w][r];
-            bool act = (msk >> qi) & 1ull;
+            bool act = (msk >> lane) & 1ull;
             const QRec &nd = srec[w][r];
-            // all-open tests (per query, computed alike by its L lanes) -> direct tile
+            // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
             bool tile = false;
             const int nflags = nd.nch;
             if (act && (nflags & QNCH_TILE)) {
@@ -830,98 +783,48 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
                 }
             }
-            if (__ballot(tile)) {
-                const int a = nd.first, b = nd.last;
-                if (tile && lead) nvis += (unsigned long long)(b - a + 1);
-                // The range holds whole equal-key runs, so either all of the query's
-                // exact duplicates (itself included) are in it or none is.  They add
-                // dx = dy = 0 to F and exactly r = 1 each to z: pair terms run
-                // unmasked and the duplicate count is taken off z once.
-                // Queries whose truncation bound holds record a moment task
-                // (evaluated by moment_apply after the traversal, in recording
-                // order); the rest run the dense tile: points staged through LDS
-                // 64 at a time (one coalesced dwordx4 load per lane, the next
-                // chunk prefetched into registers), each of a query's L lanes
-                // summing every L-th point.
-                bool usem = false;
-                if (tile && nd.cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
-                    usem = moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy);
-                    if (usem) {
-                        if (lead) ++nwant;
-                        if (mom_on) {
-                            if (lead) mtask[s * MOM_TASKS + ntask] = ref;
-                            ++ntask;
-                        } else {
-                            usem = false;
-                        }
+            const uint64_t tm = __ballot(tile);
+            if (tm) {
+                // The wave records (subtree, lanes) for tile_apply, or, when its
+                // list is full, the lanes keep traversing (the reference's path).
+                // The range holds whole equal-key runs, so either all of the
+                // query's exact duplicates (itself included) are in it or none
+                // is; they add exactly 1 each to z in the leaf sum: taken off here.
+                if (ntt < TILE_CAP) {
+                    const int a = nd.first, b = nd.last;
+                    if (lane == 0) {
+                        TileTask tt; tt.ref = ref; tt.first = a; tt.last = b; tt.pad = nd.cnt; tt.mask = tm;
+                        mytt[ntt] = tt;
                     }
-                }
-                double tx = 0.0, ty = 0.0, tz = 0.0;
-                const bool dense = tile && !usem;
-                if (__ballot(dense)) {
-                    wdense += (unsigned long long)(b - a + 1);
-                    double2 *buf = tbuf[w];
-                    double2 nxt = make_double2(0.0, 0.0);
-                    if (a + lane <= b) nxt = pos[a + lane];
-                    double ux = 0.0, uy = 0.0, uz = 0.0;
-                    for (int c0 = a; c0 <= b; c0 += 64) {
-                        const int cnt = min(64, b - c0 + 1);
-                        __builtin_amdgcn_wave_barrier();
-                        buf[lane] = nxt;
-                        if (c0 + 64 + lane <= b) nxt = pos[c0 + 64 + lane];
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
-                        __builtin_amdgcn_wave_barrier();
-                        int j = cs;
-                        for (; j + 7 * L < cnt; j += 8 * L) {
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                const double2 pp = buf[j + u * L];
-                                pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
-                            }
-                        }
-                        for (; j < cnt; j += L) {
-                            const double2 pp = buf[j];
-                            pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
-                        }
+                    ++ntt;
+                    if (STATS) wtile += (unsigned long long)(b - a + 1);
+                    if (tile) {
+                        if (STATS) nvis += (unsigned long long)(b - a + 1);
+                        if (s >= a && s <= b) zs -= (double)dupc[s];
                     }
-                    __builtin_amdgcn_wave_barrier();
-                    if (dense) {
-                        tx = ux; ty = uy; tz = uz;
-                        if (lead) ndense += (unsigned long long)(b - a + 1);
-                    }
+                    act = act && !tile;
                 }
-                if (tile) {
-                    fx += tx;
-                    fy += ty;
-                    zs += tz - ((lead && s >= a && s <= b) ? (double)dupc[s] : 0.0);
-                }
-                act = act && !tile;
             }
             if (__ballot(act) == 0) continue;
-            // the opened cell's quad children, from its record; lane serves c = cs + L*kk
+            // the opened cell's quad children, from its record
             const int nch = nflags & 0xff;
-            wslots += (unsigned long long)nch;
+            if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
 #pragma unroll
-            for (int kk = 0; kk < 4 / L; ++kk) {
-                const int c = cs + L * kk;
-                bool open = false;
-                if (c < nch) {
-                    const double chh = nd.ch[c];
-                    if (act) ++nevals;
-                    if (chh == QCH_LEAF) {
-                        if (act) { ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
-                    } else if (chh == QCH_TIE) {
-                        if (act) {
-                            const BHNode &tn = nodes[nd.cref[c]];
-                            for (int p = tn.first; p <= tn.last; ++p) {
-                                const double2 pp = pos[p];
-                                ++nvis;
-                                leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
-                            }
-                        }
-                    } else if (act) {
-                        ++nvis;
+            for (int c = 0; c < 4; ++c) {
+                if (c >= nch) break;
+                const double chh = nd.ch[c];
+                if (chh == QCH_LEAF) {
+                    if (act) { if (STATS) ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
+                } else if (chh == QCH_TIE) {
+                    const BHNode &tn = nodes[nd.cref[c]];
+                    for (int p = tn.first; p <= tn.last; ++p) {
+                        const double2 pp = pos[p];
+                        if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                    }
+                } else {
+                    bool open = false;
+                    if (act) {
+                        if (STATS) ++nvis;
                         const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
                         const double D = __fma_rn(dx, dx, dy * dy);
                         if (summarise(chh, D, dx, dy, th_lo, th_hi, theta))
@@ -929,55 +832,143 @@ __global__ __launch_bounds__(256) void bh_traverse(
                         else
                             open = true;
                     }
-                }
-                const uint64_t ob = __ballot(open);
-                if (ob) {
-#pragma unroll
-                    for (int c2 = 0; c2 < L; ++c2) {
-                        const uint64_t om = compress_stride<L>(ob >> c2);
-                        if (om) {
-                            if (lane == 0) { sref[w][sp] = nd.cref[L * kk + c2]; smask[w][sp] = om; }
-                            ++sp;
-                        }
+                    const uint64_t om = __ballot(open);
+                    if (om) {
+                        if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
+                        ++sp;
                     }
                 }
             }
         }
     }
-    // per-query sums over its L lanes, fixed order
-#pragma unroll
-    for (int o = 1; o < L; o <<= 1) {
-        fx += __shfl_xor(fx, o, 64);
-        fy += __shfl_xor(fy, o, 64);
-        zs += __shfl_xor(zs, o, 64);
-    }
-    if (valid && lead) {
+    if (valid) {
         F[s] = make_double2(fx, fy);
         Z[s] = zs;
-        mtask_n[s] = ntask;
+    }
+    if (lane == 0) ttask_n[wid] = ntt;
+    if (STATS && bcost) {   // cost of this wave (in cell-pop units) into its first query's 256-query bucket
+        const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
+        if (lane == 0) atomicAdd(&bcost[sf >> 8], wpops + wtile / 48 + 4);
+    }
+    if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
+                             // [4] wave-level tile points, [5] lane child evaluations, [6] wave
+                             // child slots, [7..9] heaviest wave ([1], [2]: tile_apply)
+        const unsigned long long tv = wave_sum(nvis), te = wave_sum(nevals);
+        if (lane == 0) {
+            atomicAdd(visits, tv);
+            atomicAdd(visits + 3, wpops);
+            atomicAdd(visits + 4, wtile);
+            atomicAdd(visits + 5, te);
+            atomicAdd(visits + 6, wslots);
+            atomicMax(visits + 7, wpops + wtile / 16);   // heaviest wave (pops + tile points/16)
+            atomicMax(visits + 8, wpops);
+            atomicMax(visits + 9, wtile);
+        }
+    }
+}
+
+// The traversal waves' tiles, in recording order: one wave per traversal
+// wave (same 64 queries).  For every (subtree, lanes) task each lane of the
+// mask takes the subtree's exact leaf sum either from its moments (when the
+// series' truncation bound holds and moments were built this iteration; the
+// node's 55 moments staged in LDS, read as broadcasts) or densely (the
+// points staged through LDS 64 at a time: one coalesced dwordx4 load per
+// lane, the next chunk prefetched into registers, wave-uniform broadcasts).
+// Lanes whose bound holds are counted for the next iteration's moment gate.
+__global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+                                                  const double *__restrict__ mom,
+                                                  const TileTask *__restrict__ ttask,
+                                                  const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1,
+                                                  int xcd_chunk, int32_t *__restrict__ mom_flag,
+                                                  double2 *__restrict__ F, double *__restrict__ Z,
+                                                  unsigned long long *__restrict__ visits) {
+    __shared__ double2 tbuf[4][64];
+    __shared__ double smom[4][MOM_K];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t wid = blk * 4 + w;
+    if (g0 + wid * 64 >= g1) return;
+    const int nt = ttask_n[wid];
+    if (nt == 0) return;
+    const int64_t s = g0 + wid * 64 + lane;
+    double qx = 0.0, qy = 0.0;
+    if (s < g1) { const double2 q = pos[s]; qx = q.x; qy = q.y; }
+    const bool mom_on = mom_flag[0] != 0;
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    int nwant = 0;
+    unsigned long long nmom = 0, ndense = 0;
+    double2 *buf = tbuf[w];
+    const TileTask *mytt = ttask + wid * TILE_CAP;
+    for (int t = 0; t < nt; ++t) {
+        const TileTask tt = mytt[t];
+        const int ref = __builtin_amdgcn_readfirstlane(tt.ref);
+        const int a = __builtin_amdgcn_readfirstlane(tt.first), b = __builtin_amdgcn_readfirstlane(tt.last);
+        const int cnt = __builtin_amdgcn_readfirstlane(tt.pad);
+        const bool mine = (tt.mask >> lane) & 1ull;
+        bool usem = false;
+        if (mine && cnt >= MOM_MIN_POINTS) {
+            const BHNode &nd = nodes[ref];
+            if (moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy)) {
+                ++nwant;
+                usem = mom_on;
+            }
+        }
+        if (__ballot(usem)) {
+            __builtin_amdgcn_wave_barrier();
+            for (int k = lane; k < MOM_K; k += 64) smom[w][k] = mom[(int64_t)ref * MOM_K + k];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            const BHNode &nd = nodes[ref];
+            double cx, cy, R;
+            box_centre(nd, cx, cy, R);
+            double mx = 0.0, my = 0.0, mz = 0.0;
+            moment_eval(smom[w], qx - cx, qy - cy, mx, my, mz);
+            if (usem) { fx += mx; fy += my; zs += mz; ++nmom; }
+            __builtin_amdgcn_wave_barrier();
+        }
+        const bool dense = mine && !usem;
+        if (__ballot(dense)) {
+            double2 nxt = make_double2(0.0, 0.0);
+            if (a + lane <= b) nxt = pos[a + lane];
+            double ux = 0.0, uy = 0.0, uz = 0.0;
+            for (int c0 = a; c0 <= b; c0 += 64) {
+                const int cn = min(64, b - c0 + 1);
+                __builtin_amdgcn_wave_barrier();
+                buf[lane] = nxt;
+                if (c0 + 64 + lane <= b) nxt = pos[c0 + 64 + lane];
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS writes landed
+                __builtin_amdgcn_wave_barrier();
+                int j = 0;
+                for (; j + 4 <= cn; j += 4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const double2 pp = buf[j + u];
+                        pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                    }
+                }
+                for (; j < cn; ++j) {
+                    const double2 pp = buf[j];
+                    pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (dense) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)(b - a + 1); }
+        }
+    }
+    if (s < g1 && (fx != 0.0 || fy != 0.0 || zs != 0.0)) {
+        const double2 f = F[s];
+        F[s] = make_double2(f.x + fx, f.y + fy);
+        Z[s] = Z[s] + zs;
     }
     const int wwant = wave_sum(nwant);
     if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
-    if (bcost) {   // cost of this wave (in cell-pop units) into its first query's 256-query bucket
-        const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
-        if (lane == 0) atomicAdd(&bcost[sf >> 8], wpops + wdense / 48 + 4);
-    }
-    if (visits) {   // [0] reference-equivalent node evaluations, [1] moment tasks, [2] dense pair terms,
-                    // [3] wave-level pops, [4] wave-level dense tile points, [5] lane child
-                    // evaluations, [6] wave child slots x L (utilisation = [5] / (64 [6]))
-        const unsigned long long tv = wave_sum(nvis), tt = wave_sum(lead ? (unsigned long long)ntask : 0ull),
-                                 td = wave_sum(ndense), te = wave_sum(nevals);
+    if (visits) {   // [1] moment evaluations, [2] dense pair terms
+        const unsigned long long tm = wave_sum(nmom), td = wave_sum(ndense);
         if (lane == 0) {
-            atomicAdd(visits, tv);
-            atomicAdd(visits + 1, tt);
+            atomicAdd(visits + 1, tm);
             atomicAdd(visits + 2, td);
-            atomicAdd(visits + 3, wpops);
-            atomicAdd(visits + 4, wdense);
-            atomicAdd(visits + 5, te);
-            atomicAdd(visits + 6, wslots * L);
-            atomicMax(visits + 7, wpops + wdense / 16);   // heaviest wave (pops + dense/16)
-            atomicMax(visits + 8, wpops);
-            atomicMax(visits + 9, wdense);
         }
     }
 }
@@ -1014,8 +1005,9 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     const int32_t flag_init[2] = {1, INT32_MAX};   // first build: moments on
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
-    t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
-    t.mtask_n = ws.get<int32_t>("bh.mtask_n", n);
+    t.tile_waves = ceil_div(n, 64) + 4;
+    t.ttask = ws.get<TileTask>("bh.ttask", (size_t)t.tile_waves * TILE_CAP);
+    t.ttask_n = ws.get<int32_t>("bh.ttask_n", t.tile_waves);
     size_t sb = 0;
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, t.mom_cnt, t.mom_off, (int)(n + 1), ctx->stream));
     t.scan_tmp_bytes = sb;
@@ -1130,17 +1122,16 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
     static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
-    static const int lq = [] { const char *e = getenv("TSNE_BH_LANES"); return e ? atoi(e) : 1; }();
-    auto kern = lq >= 4 ? (kp >= 8 ? bh_traverse<8, 4> : bh_traverse<4, 4>)
-              : lq >= 2 ? (kp >= 8 ? bh_traverse<8, 2> : bh_traverse<4, 2>)
-                        : (kp >= 8 ? bh_traverse<8, 1> : bh_traverse<4, 1>);
-    const int L = lq >= 4 ? 4 : lq >= 2 ? 2 : 1;
-    const int64_t waves = ceil_div((s1 - s0) * L, 64);
+    const bool stats = visits != nullptr || bcost != nullptr;
+    auto kern = kp >= 8 ? (stats ? bh_traverse<8, true> : bh_traverse<8, false>)
+                        : (stats ? bh_traverse<4, true> : bh_traverse<4, false>);
+    const int64_t waves = ceil_div(s1 - s0, 64);
+    TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.mtask, t.mtask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dbounds, xcd,
-                       dF, dz, visits, bcost);
-    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.mtask, t.mtask_n, s0, s1, dbounds, dF, dz);
+                       t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dbounds, xcd, dF,
+                       dz, visits, bcost);
+    hipLaunchKernelGGL(tile_apply, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
+                       t.ttask, t.ttask_n, s0, s1, xcd, t.mom_flag, dF, dz, visits);
     TSNE_LAUNCH_CHECK();
 }
 

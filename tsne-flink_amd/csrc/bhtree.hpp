@@ -4,6 +4,14 @@
 
 namespace tsne {
 
+// A leaf tile of one traversal wave: the subtree (node, leaf range) whose
+// exact leaf sum the lanes of `mask` take (by moments or densely, tile_apply).
+constexpr int TILE_CAP = 1024;   // tiles per wave; beyond, lanes keep traversing
+struct TileTask {
+    int32_t ref, first, last, pad;
+    uint64_t mask;
+};
+
 // Internal node of the binary radix tree over sorted Morton keys.  A node
 // whose common prefix ends inside a quad level is "transparent" (h == 0:
 // always opened); otherwise it IS the reference quadtree cell of half width
@@ -64,8 +72,10 @@ struct BHTree {
     int32_t *mom_cnt = nullptr, *mom_off = nullptr;  // chunks per node, exclusive scan (n + 1)
     int32_t *mom_list = nullptr;                     // nodes that carry moments
     int32_t *mom_item = nullptr;                     // item -> node
-    int32_t *mtask = nullptr, *mtask_n = nullptr;    // per query: moment tasks (node ids), count
     int32_t *mom_flag = nullptr;                     // [0] moments built, [1] eligible tiles seen
+    TileTask *ttask = nullptr;                       // per traversal wave: tile list
+    int32_t *ttask_n = nullptr;
+    int64_t tile_waves = 0;
     int64_t mom_items_cap = 0;
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
