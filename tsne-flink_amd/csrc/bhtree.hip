@@ -57,6 +57,7 @@ constexpr int MOM_K = (MOM_DEG + 1) * (MOM_DEG + 2) / 2;
 constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-14;
+constexpr int MOM_TASKS = 128;  // moment evaluations recorded per query; more -> dense tiles
 constexpr double BH_NEAR_TOL = 1e-7;    // near-exact subtree test (bh_traverse): 1000x below
                                         // the north-star 1e-4 gradient tolerance
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
@@ -578,6 +579,33 @@ __device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, do
     return (MOM_ORDER + 2) * rp <= MOM_TOL * (1.0 - rho) * (1.0 - rho);
 }
 
+// Moment tasks of each query (sorted positions [s0, s1)), in traversal order,
+// added to the traversal's F and z.
+__global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ pos,
+                                                    const BHNode *__restrict__ nodes,
+                                                    const double *__restrict__ mom,
+                                                    const int32_t *__restrict__ mtask,
+                                                    const int32_t *__restrict__ mtask_n, int64_t g0,
+                                                    int64_t g1, const int64_t *__restrict__ dbounds,
+                                                    double2 *__restrict__ F, double *__restrict__ Z) {
+    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
+    const int64_t s = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < s0 || s >= s1) return;
+    const int nt = mtask_n[s];
+    if (nt == 0) return;
+    const double2 q = pos[s];
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    for (int k = 0; k < nt; ++k) {
+        const int node = mtask[s * MOM_TASKS + k];
+        double cx, cy, R;
+        box_centre(nodes[node], cx, cy, R);
+        moment_eval(mom + (int64_t)node * MOM_K, q.x - cx, q.y - cy, fx, fy, zs);
+    }
+    const double2 f = F[s];
+    F[s] = make_double2(f.x + fx, f.y + fy);
+    Z[s] = Z[s] + zs;
+}
+
 // fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
 // an IEEE division -- decided by comparing h with theta * D outside a 1e-14
 // relative band (where the rounded quotient cannot cross theta), and by the
@@ -869,34 +897,38 @@ __global__ __launch_bounds__(256) void bh_traverse(
 
 // The traversal waves' tiles, in recording order: one wave per traversal
 // wave (same 64 queries).  For every (subtree, lanes) task each lane of the
-// mask takes the subtree's exact leaf sum either from its moments (when the
-// series' truncation bound holds and moments were built this iteration; the
-// node's 55 moments staged in LDS, read as broadcasts) or densely (the
-// points staged through LDS 64 at a time: one coalesced dwordx4 load per
-// lane, the next chunk prefetched into registers, wave-uniform broadcasts).
-// Lanes whose bound holds are counted for the next iteration's moment gate.
+// mask takes the subtree's exact leaf sum either from its moments -- when the
+// series' truncation bound holds and moments were built this iteration, the
+// lane appends the node to its own moment list, evaluated lane-parallel by
+// moment_apply -- or densely: the points staged through LDS 64 at a time (one
+// coalesced dwordx4 load per lane, the next chunk prefetched into registers)
+// and read back as wave-uniform broadcasts.  Lanes whose bound holds are
+// counted for the next iteration's moment gate.
 __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
                                                   const double *__restrict__ mom,
                                                   const TileTask *__restrict__ ttask,
                                                   const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1,
                                                   int xcd_chunk, int32_t *__restrict__ mom_flag,
+                                                  int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
                                                   double2 *__restrict__ F, double *__restrict__ Z,
                                                   unsigned long long *__restrict__ visits) {
     __shared__ double2 tbuf[4][64];
-    __shared__ double smom[4][MOM_K];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
     if (g0 + wid * 64 >= g1) return;
-    const int nt = ttask_n[wid];
-    if (nt == 0) return;
     const int64_t s = g0 + wid * 64 + lane;
+    const int nt = ttask_n[wid];
+    if (nt == 0) {
+        if (s < g1) mtask_n[s] = 0;
+        return;
+    }
     double qx = 0.0, qy = 0.0;
     if (s < g1) { const double2 q = pos[s]; qx = q.x; qy = q.y; }
     const bool mom_on = mom_flag[0] != 0;
     double fx = 0.0, fy = 0.0, zs = 0.0;
-    int nwant = 0;
-    unsigned long long nmom = 0, ndense = 0;
+    int nwant = 0, ntask = 0;
+    unsigned long long ndense = 0;
     double2 *buf = tbuf[w];
     const TileTask *mytt = ttask + wid * TILE_CAP;
     for (int t = 0; t < nt; ++t) {
@@ -906,26 +938,15 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
         const int cnt = __builtin_amdgcn_readfirstlane(tt.pad);
         const bool mine = (tt.mask >> lane) & 1ull;
         bool usem = false;
-        if (mine && cnt >= MOM_MIN_POINTS) {
+        if (mine && cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
             const BHNode &nd = nodes[ref];
             if (moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy)) {
                 ++nwant;
-                usem = mom_on;
+                if (mom_on) {
+                    usem = true;
+                    mtask[s * MOM_TASKS + ntask++] = ref;
+                }
             }
-        }
-        if (__ballot(usem)) {
-            __builtin_amdgcn_wave_barrier();
-            for (int k = lane; k < MOM_K; k += 64) smom[w][k] = mom[(int64_t)ref * MOM_K + k];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0);
-            __builtin_amdgcn_wave_barrier();
-            const BHNode &nd = nodes[ref];
-            double cx, cy, R;
-            box_centre(nd, cx, cy, R);
-            double mx = 0.0, my = 0.0, mz = 0.0;
-            moment_eval(smom[w], qx - cx, qy - cy, mx, my, mz);
-            if (usem) { fx += mx; fy += my; zs += mz; ++nmom; }
-            __builtin_amdgcn_wave_barrier();
         }
         const bool dense = mine && !usem;
         if (__ballot(dense)) {
@@ -957,15 +978,18 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
             if (dense) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)(b - a + 1); }
         }
     }
-    if (s < g1 && (fx != 0.0 || fy != 0.0 || zs != 0.0)) {
-        const double2 f = F[s];
-        F[s] = make_double2(f.x + fx, f.y + fy);
-        Z[s] = Z[s] + zs;
+    if (s < g1) {
+        mtask_n[s] = ntask;
+        if (fx != 0.0 || fy != 0.0 || zs != 0.0) {
+            const double2 f = F[s];
+            F[s] = make_double2(f.x + fx, f.y + fy);
+            Z[s] = Z[s] + zs;
+        }
     }
     const int wwant = wave_sum(nwant);
     if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
     if (visits) {   // [1] moment evaluations, [2] dense pair terms
-        const unsigned long long tm = wave_sum(nmom), td = wave_sum(ndense);
+        const unsigned long long tm = wave_sum((unsigned long long)ntask), td = wave_sum(ndense);
         if (lane == 0) {
             atomicAdd(visits + 1, tm);
             atomicAdd(visits + 2, td);
@@ -1005,6 +1029,8 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     const int32_t flag_init[2] = {1, INT32_MAX};   // first build: moments on
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
+    t.mtask_n = ws.get<int32_t>("bh.mtask_n", n);
     t.tile_waves = ceil_div(n, 64) + 4;
     t.ttask = ws.get<TileTask>("bh.ttask", (size_t)t.tile_waves * TILE_CAP);
     t.ttask_n = ws.get<int32_t>("bh.ttask_n", t.tile_waves);
@@ -1131,7 +1157,9 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                        t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dbounds, xcd, dF,
                        dz, visits, bcost);
     hipLaunchKernelGGL(tile_apply, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.ttask, t.ttask_n, s0, s1, xcd, t.mom_flag, dF, dz, visits);
+                       t.ttask, t.ttask_n, s0, s1, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits);
+    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
+                       t.mtask, t.mtask_n, s0, s1, dbounds, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

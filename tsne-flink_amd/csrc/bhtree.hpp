@@ -73,6 +73,7 @@ struct BHTree {
     int32_t *mom_list = nullptr;                     // nodes that carry moments
     int32_t *mom_item = nullptr;                     // item -> node
     int32_t *mom_flag = nullptr;                     // [0] moments built, [1] eligible tiles seen
+    int32_t *mtask = nullptr, *mtask_n = nullptr;    // per query: moment evaluations (node ids), count
     TileTask *ttask = nullptr;                       // per traversal wave: tile list
     int32_t *ttask_n = nullptr;
     int64_t tile_waves = 0;
