@@ -6,7 +6,7 @@ namespace tsne {
 
 // A leaf tile of one traversal wave: the subtree (node, leaf range) whose
 // exact leaf sum the lanes of `mask` take (by moments or densely, tile_apply).
-constexpr int TILE_CAP = 1024;   // tiles per wave; beyond, lanes keep traversing
+constexpr int TILE_CAP = 8192;   // tiles per wave; beyond, lanes keep traversing
 struct TileTask {
     int32_t ref, first, last, pad;
     uint64_t mask;
