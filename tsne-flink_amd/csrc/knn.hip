@@ -140,20 +140,38 @@ __global__ __launch_bounds__(256) void knn_filter(
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
+    // K chunks of 32 staged through LDS; the next chunk's global loads are
+    // issued into registers before the current chunk's MFMAs (software
+    // pipelining: the loads' latency hides behind the matrix work).
+    float4 pq[4], pc[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int idx = tid + it * 256;
+        const int r = idx >> 3, c4 = (idx & 7) * 4;
+        pq[it] = *reinterpret_cast<const float4 *>(X32 + (qb + r) * dpad + c4);
+        pc[it] = *reinterpret_cast<const float4 *>(X32 + (cb + r) * dpad + c4);
+    }
     for (int k0 = 0; k0 < dpad; k0 += KC) {
         // stage 128 x 32 of queries and of candidates: 1024 float4 each, 4 per thread
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
-            int idx = tid + it * 256;
-            int r = idx >> 3, c4 = (idx & 7) * 4;
-            float4 vq = *reinterpret_cast<const float4 *>(X32 + (qb + r) * dpad + k0 + c4);
-            float4 vc = *reinterpret_cast<const float4 *>(X32 + (cb + r) * dpad + k0 + c4);
+            const int idx = tid + it * 256;
+            const int r = idx >> 3, c4 = (idx & 7) * 4;
             float *dq = Qs + r * LDSW + c4;
             float *dc = Cs + r * LDSW + c4;
-            dq[0] = vq.x; dq[1] = vq.y; dq[2] = vq.z; dq[3] = vq.w;
-            dc[0] = vc.x; dc[1] = vc.y; dc[2] = vc.z; dc[3] = vc.w;
+            dq[0] = pq[it].x; dq[1] = pq[it].y; dq[2] = pq[it].z; dq[3] = pq[it].w;
+            dc[0] = pc[it].x; dc[1] = pc[it].y; dc[2] = pc[it].z; dc[3] = pc[it].w;
         }
         __syncthreads();
+        if (k0 + KC < dpad) {
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int idx = tid + it * 256;
+                const int r = idx >> 3, c4 = (idx & 7) * 4;
+                pq[it] = *reinterpret_cast<const float4 *>(X32 + (qb + r) * dpad + k0 + KC + c4);
+                pc[it] = *reinterpret_cast<const float4 *>(X32 + (cb + r) * dpad + k0 + KC + c4);
+            }
+        }
         const int lr = lane & 31, lk = lane >> 5;
 #pragma unroll
         for (int s = 0; s < KC / 2; ++s) {
