@@ -84,3 +84,95 @@ def test_cli_execution_plan(tmp_path):
     assert r.returncode == 0
     plan = (tmp_path / "tsne_executionPlan.json").read_text()
     assert "pairwiseAffinities" in plan and "optimize" in plan
+
+
+COO_HARNESS = r'''
+#include <cstdio>
+#include <cstdlib>
+#include "coo_reader.hpp"
+using namespace tsne_flink;
+int main(int argc, char **argv) {
+    const int threads = std::atoi(argv[2]), dim = std::atoi(argv[3]);
+    try {
+        CooTriples t = readCooFile(argv[1], threads);
+        auto rows = cooToVectors(t, dim);
+        std::printf("%zu %zu\n", t.i.size(), rows.size());
+        for (auto &r : rows) {
+            std::printf("%d", r.first);
+            for (double x : r.second) std::printf(" %.17g", x);
+            std::printf("\n");
+        }
+    } catch (const std::exception &e) {
+        std::printf("ERR %s\n", e.what());
+    }
+    return 0;
+}
+'''
+
+
+@pytest.fixture(scope="module")
+def coo_exe(tmp_path_factory):
+    d = tmp_path_factory.mktemp("coo")
+    src = d / "c.cpp"
+    src.write_text(COO_HARNESS)
+    exe = d / "c"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-pthread", f"-I{PKG / 'host'}", str(src),
+                           str(PKG / "host" / "coo_reader.cpp"), "-o", str(exe)])
+    return exe
+
+
+def _py_read(text, dim):
+    """Tsne.readInput restated: rows by first appearance, x_i[j] += v in file order."""
+    rows, order = {}, []
+    for line in text.splitlines():
+        line = line.rstrip("\r")
+        if not line:
+            continue
+        i, j, v = line.split(",")
+        i, j = int(i), int(j)
+        if i not in rows:
+            rows[i] = [0.0] * dim
+            order.append(i)
+        rows[i][j] += float(v)
+    return [(i, rows[i]) for i in order]
+
+
+def _run(coo_exe, path, threads, dim):
+    out = subprocess.check_output([str(coo_exe), str(path), str(threads), str(dim)], text=True).splitlines()
+    if out[0].startswith("ERR"):
+        return out[0]
+    return [(int(l.split()[0]), [float(x) for x in l.split()[1:]]) for l in out[1:]]
+
+
+def test_coo_reader_formats(coo_exe, tmp_path):
+    text = "3,0,1.5\r\n3,1,-2e-3\n\n-7,2,1E300\n3,0,0.25\n12,1,4.9e-324\n-7,0,-0.0\n12,2,0.1\n"
+    p = tmp_path / "a.csv"
+    p.write_text(text)
+    assert _run(coo_exe, p, 1, 3) == _py_read(text, 3)
+    bad = tmp_path / "b.csv"
+    bad.write_text("1,2,3\n1;2;3\n")
+    assert _run(coo_exe, bad, 1, 3).startswith("ERR bad line: 1;2;3")
+    oob = tmp_path / "c.csv"
+    oob.write_text("1,3,1.0\n")
+    assert "out of dimension" in _run(coo_exe, oob, 1, 3)
+
+
+def test_coo_reader_parallel_equals_sequential(coo_exe, tmp_path):
+    import numpy as np
+    rng = np.random.default_rng(0)
+    n, dim = 20000, 16
+    ids = rng.permutation(n * 3)[:n]
+    lines = []
+    for r in range(n):
+        for j in rng.choice(dim, 6, replace=False):
+            lines.append(f"{ids[r]},{j},{rng.normal() * 10.0 ** int(rng.integers(-5, 5))!r}")
+    rng.shuffle(lines)
+    lines += lines[:5000]                      # duplicates: summed in file order
+    text = "\n".join(lines) + "\n"
+    assert len(text) > (1 << 20)               # multi-threaded path
+    p = tmp_path / "big.csv"
+    p.write_text(text)
+    want = _py_read(text, dim)
+    assert _run(coo_exe, p, 1, dim) == want
+    assert _run(coo_exe, p, 7, dim) == want
+    assert _run(coo_exe, p, 16, dim) == want

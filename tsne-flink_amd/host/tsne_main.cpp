@@ -22,6 +22,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "coo_reader.hpp"
 #include "tsne_helpers.hpp"
 
 using namespace tsne_flink;
@@ -59,48 +60,17 @@ struct Params {
     long getLong(const std::string &k, long def) const { return has(k) ? (long)std::stod(getRequired(k)) : def; }
 };
 
-// Tsne.readInput (Tsne.scala:138-153): COO "i,j,v" lines -> dense vectors.
+// Tsne.readInput (Tsne.scala:138-153): COO "i,j,v" lines -> dense vectors
+// (parallel mmap reader, coo_reader.cpp).
 Vectors readInput(const std::string &path, int dimension) {
-    std::ifstream f(path);
-    if (!f) throw std::runtime_error("cannot open " + path);
-    std::unordered_map<int32_t, size_t> slot;
-    Vectors out;
-    std::string line;
-    while (std::getline(f, line)) {
-        if (line.empty()) continue;
-        const char *s = line.c_str();
-        char *e;
-        long i = std::strtol(s, &e, 10);
-        if (*e != ',') throw std::runtime_error("bad line: " + line);
-        long j = std::strtol(e + 1, &e, 10);
-        if (*e != ',') throw std::runtime_error("bad line: " + line);
-        double v = std::strtod(e + 1, &e);
-        if (j < 0 || j >= dimension) throw std::out_of_range("index " + std::to_string(j) + " out of dimension");
-        auto it = slot.find((int32_t)i);
-        if (it == slot.end()) {
-            it = slot.emplace((int32_t)i, out.size()).first;
-            out.push_back({(int32_t)i, std::vector<double>(dimension, 0.0)});
-        }
-        out[it->second].second[j] += v;  // VectorBuilder.add accumulates
-    }
-    return out;
+    return cooToVectors(readCooFile(path), dimension);
 }
 
 // Tsne.readDistanceMatrix (Tsne.scala:155-159): raw (i, j, d) triples.
 std::vector<Triple> readDistanceMatrix(const std::string &path) {
-    std::ifstream f(path);
-    if (!f) throw std::runtime_error("cannot open " + path);
-    std::vector<Triple> out;
-    std::string line;
-    while (std::getline(f, line)) {
-        if (line.empty()) continue;
-        const char *s = line.c_str();
-        char *e;
-        long i = std::strtol(s, &e, 10);
-        long j = std::strtol(e + 1, &e, 10);
-        double v = std::strtod(e + 1, &e);
-        out.push_back({(int32_t)i, (int32_t)j, v});
-    }
+    const CooTriples t = readCooFile(path);
+    std::vector<Triple> out(t.i.size());
+    for (size_t e = 0; e < out.size(); ++e) out[e] = {t.i[e], t.j[e], t.v[e]};
     return out;
 }
 
