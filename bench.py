@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--trace", type=int, default=50, help="profile every N-th timed iteration (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
+    ap.add_argument("--locality", action="store_true",
+                    help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
 
 
@@ -231,11 +233,33 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps)
+    if rank == 0 and a.locality:
+        locality_report(Y[:n], orp, oc, n)
     if rank == 0:
         print(json.dumps(out))
     ctx.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def locality_report(Y, rp, col, n):
+    """Diagnostic: how far apart (in Morton rank of the final embedding, i.e.
+    the optimizer's relabelled row order) the endpoints of P's edges lie --
+    the CSR attraction's Y_j gathers hit L2 only for near edges."""
+    q = ((Y - Y.min(0).values) / (Y.max(0).values - Y.min(0).values + 1e-300) * (2 ** 20 - 1)).long()
+    key = torch.zeros(n, dtype=torch.int64, device=Y.device)
+    for b in range(20):
+        key |= ((q[:, 0] >> b) & 1) << (2 * b) | ((q[:, 1] >> b) & 1) << (2 * b + 1)
+    rank = torch.empty_like(key)
+    rank[torch.argsort(key)] = torch.arange(n, device=Y.device)
+    rows = torch.repeat_interleave(torch.arange(n, device=Y.device), rp[1:n + 1] - rp[:n])
+    dist = (rank[rows] - rank[col[:rows.numel()].long()]).abs().double()
+    qs = torch.tensor([0.5, 0.75, 0.9, 0.99], dtype=torch.float64, device=Y.device)
+    sample = dist[torch.randint(0, dist.numel(), (1 << 22,), device=Y.device)]
+    for w in (64, 512, 2048, 16384, 131072):
+        frac = (dist <= w).double().mean().item()
+        print(f"[locality] |rank_i - rank_j| <= {w:6d}: {frac:.3f}", file=sys.stderr)
+    print(f"[locality] quantiles 50/75/90/99%: {torch.quantile(sample, qs).tolist()}", file=sys.stderr)
 
 
 def cpu_baseline(snaps, a, n, steps):
