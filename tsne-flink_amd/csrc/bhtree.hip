@@ -113,6 +113,26 @@ __global__ void bbox_final(const double *__restrict__ part, int nb, double *__re
 }
 
 // Morton key by replaying the reference cell arithmetic (no FMA contraction).
+// Fast path: away from cell boundaries the replay's digits are those of the
+// exact quantisation X = (p + W) / (2W) * 2^31 (every coarser boundary is
+// also a level-31 boundary, and the reference's rounded cell centres sit
+// within a few ulps of the exact ones), so a point whose fixed-point
+// coordinates are more than 1e-4 of a level-31 cell away from every boundary
+// takes the quantised digits; the rest (a fraction ~4e-4) and every
+// out-of-range case replay the reference arithmetic.
+__device__ __forceinline__ bool quant_digits(double p, double W, uint32_t &q) {
+    const double t = (p + W) / (2.0 * W) * 2147483648.0;   // in [0, 2^31] for in-root points
+    if (!(t >= 0.0 && t < 2147483648.0)) return false;
+    const double f = floor(t);
+    const double fr = t - f;
+    // t carries <= ~3 ulp(2^31) = 1.4e-6 of rounding, the reference's cell
+    // centres <= 31 roundings = 7.4e-6 (both in level-31 cell units): a band
+    // of 1e-4 is far outside both
+    if (fr < 1e-4 || fr > 1.0 - 1e-4) return false;          // near a boundary: replay
+    q = (uint32_t)f;
+    return true;
+}
+
 __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const double *__restrict__ Wp,
                             uint64_t *__restrict__ keys, int32_t *__restrict__ idx,
                             int32_t *__restrict__ meta) {
@@ -125,7 +145,17 @@ __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const doubl
     bool in = live && (__dsub_rn(x, hw) <= px) && (__dadd_rn(x, hw) >= px) && (__dsub_rn(y, hh) <= py) &&
               (__dadd_rn(y, hh) >= py);
     uint64_t key = 0;
-    if (in) {
+    uint32_t qx, qy;
+    if (in && W > 0.0 && quant_digits(px, W, qx) && quant_digits(py, W, qy)) {
+        // digit l: (west/east from x, north/south from y): q = 2 * south + east,
+        // south = y below the centre = high bit of qy clear
+        uint64_t k = 0;
+        for (int l = 30; l >= 0; --l) {
+            const uint32_t east = (qx >> l) & 1u, south = 1u - ((qy >> l) & 1u);
+            k = (k << 2) | (uint64_t)(2u * south + east);
+        }
+        key = k;
+    } else if (in) {
         for (int l = 0; l < LEVELS; ++l) {
             const double nw = __dmul_rn(0.5, hw), nh = __dmul_rn(0.5, hw);
             const double xw = __dsub_rn(x, nw), xe = __dadd_rn(x, nw);
