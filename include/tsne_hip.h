@@ -187,8 +187,9 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
                         int32_t *n_loss);
 /* Per-stage timing of the last step (HIP events on the ctx stream), in ms:
  * [0] tree build, [1] BH repulsion kernel, [2] (F, z) exchange + Z reduce,
- * [3] attraction kernel (attract_rows), [4] combine + update, loss, embedding
- * exchange, centring.
+ * [3] attraction kernel (attract_rows, timed on the stream it runs on: outside
+ * loss iterations a second stream concurrent with [0]-[2]), [4] wait for it,
+ * combine + update, loss, embedding exchange, centring.
  * Also BH work counters of the last step (counters_out5, may be NULL):
  * [0] reference-equivalent node evaluations (lane visits; a leaf tile of m
  * points counts m), [1] subtree-moment evaluations, [2] dense pair terms,

@@ -60,6 +60,11 @@ struct OptState {
     BHTree tree;
     bool profile = false;
     hipEvent_t ev[6] = {};
+    // The attraction sums need only Y and P (not F or Z), so outside loss
+    // iterations they run on a second stream concurrently with the tree
+    // build and the BH traversal (latency-bound kernels that leave CUs idle).
+    hipStream_t side = nullptr;
+    hipEvent_t ev_y = nullptr, ev_attr = nullptr, ev_a0 = nullptr, ev_a1 = nullptr;
     double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits[10] = {};
 };
@@ -477,8 +482,15 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
 
 void opt_destroy(tsne_ctx *ctx) {
     if (!ctx->opt) return;
-    for (auto &e : ctx->opt->ev)
+    OptState *s = ctx->opt;
+    for (auto &e : s->ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {s->ev_y, s->ev_attr, s->ev_a0, s->ev_a1})
+        if (e) (void)hipEventDestroy(e);
+    if (s->side) {
+        (void)hipStreamSynchronize(s->side);
+        (void)hipStreamDestroy(s->side);
+    }
     delete ctx->opt;
     ctx->opt = nullptr;
 }
@@ -557,6 +569,11 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
     bh_alloc(ctx, s->tree, n);
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
+    TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+    TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
+    TSNE_HIP(hipEventCreateWithFlags(&s->ev_attr, hipEventDisableTiming));
+    TSNE_HIP(hipEventCreate(&s->ev_a0));
+    TSNE_HIP(hipEventCreate(&s->ev_a1));
     TSNE_LAUNCH_CHECK();
 }
 
@@ -606,6 +623,19 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipMemsetAsync(s->visits, 0, 10 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
+    // 0. attraction sums on the side stream (not in loss iterations: the KL
+    // terms need Z), concurrent with 1-3
+    AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->scal, p.metric, ex, s->attr, s->part};
+    const bool overlap = !want_loss;
+    if (overlap) {
+        TSNE_HIP(hipEventRecord(s->ev_y, st));
+        TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
+        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a0, s->side));
+        attract_launch(s->side, aa, false);
+        TSNE_LAUNCH_CHECK();
+        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a1, s->side));
+        TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
+    }
     // 1. tree
     bh_build(ctx, s->tree, Y, p.theta);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
@@ -634,10 +664,16 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
-    // 4. attraction + update for owned rows
-    AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->scal, p.metric, ex, s->attr, s->part};
-    const int64_t blocks = attract_launch(st, aa, want_loss != 0);
-    TSNE_LAUNCH_CHECK();
+    // 4. attraction (loss iterations: here, after Z) + update for owned rows
+    int64_t blocks = 0;
+    if (overlap) {
+        TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
+    } else {
+        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a0, st));
+        blocks = attract_launch(st, aa, true);
+        TSNE_LAUNCH_CHECK();
+        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a1, st));
+    }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     combine_launch<1>(st, s->r0, s->r1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
                       s->gains[c], p.min_gain, mom, p.learning_rate);
@@ -665,9 +701,10 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (s->profile) {
         TSNE_HIP(hipEventRecord(s->ev[5], st));
         TSNE_HIP(hipEventSynchronize(s->ev[5]));
-        for (int k = 0; k < 5; ++k) {
+        for (int k = 0; k < 5; ++k) {   // [3]: the attraction kernel alone, on its own stream
             float ms = 0.f;
-            TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+            if (k == 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev_a0, s->ev_a1));
+            else TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
         unsigned long long v[10] = {};
