@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--trace", type=int, default=50, help="profile every N-th timed iteration (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
+    ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as gpurun_out/Y_t<t>.npy")
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
@@ -183,6 +184,9 @@ def main():
                              "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
         if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
             snaps[t] = Y[:n].cpu().numpy().copy()
+        if rank == 0 and a.dump_y and t in {int(v) for v in a.dump_y.split(",")}:
+            os.makedirs("gpurun_out", exist_ok=True)
+            np.save(f"gpurun_out/Y_t{t}.npy", Y[:n].cpu().numpy())
         if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
             t_progress = time.perf_counter()
             print(f"[bench] t={t}/{steps} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)
