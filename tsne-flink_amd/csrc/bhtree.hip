@@ -774,6 +774,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
+    const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
     int sp = 0;
@@ -858,7 +859,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     if (STATS) wtile += (unsigned long long)(b - a + 1);
                     if (tile) {
                         if (STATS) nvis += (unsigned long long)(b - a + 1);
-                        if (s >= a && s <= b) zs -= (double)dupc[s];
+                        if (s >= a && s <= b) zs -= (double)ndup;
                     }
                     act = act && !tile;
                 }
