@@ -36,7 +36,7 @@ typedef enum {
     TSNE_ERR_ARG = -1,          /* IllegalArgumentException in the reference */
     TSNE_ERR_HIP = -2,          /* HIP runtime / kernel launch failure */
     TSNE_ERR_NOMEM = -3,
-    TSNE_ERR_UNSUPPORTED = -4,  /* e.g. n_components != 2 (Cell.scala:32 require) */
+    TSNE_ERR_UNSUPPORTED = -4,  /* e.g. n_components not 2 or 3 (Cell.scala:32 requires 2) */
     TSNE_ERR_CAPACITY = -5,     /* caller buffer too small; required size reported */
     TSNE_ERR_COMM = -6,         /* RCCL failure */
     TSNE_ERR_NO_DEVICE = -7
@@ -51,7 +51,7 @@ typedef enum {
 
 /* Optimizer parameters; defaults = Tsne.scala:47-63 + TsneHelpers.scala:386. */
 typedef struct {
-    int32_t n_components;       /* --nComponents, 2 */
+    int32_t n_components;       /* --nComponents, 2 (3: octree extension) */
     int32_t metric;             /* --metric, sqeuclidean (used for the attractive q) */
     double learning_rate;       /* --learningRate, 1000 */
     int32_t iterations;         /* --iterations, 300 */
@@ -133,6 +133,14 @@ int tsne_gradient(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, con
                   int64_t n, const double *Y, int32_t metric, double theta, double exaggeration,
                   double *grad_out, double *sumq_out, double *loss_out);
 
+/* gradient for c = 2 (== tsne_gradient) or c = 3: the 3-D octree extension
+ * (the reference itself requires 2-D, Cell.scala:32): root
+ * Cell(0,0,0,W) with W = max(dX, dY, dZ), 8 children (upper/lower x NW, NE,
+ * SW, SE), the same max(h)/D < theta criterion on squared 3-D distances.
+ * Y, grad_out: n x c.  Other c -> TSNE_ERR_UNSUPPORTED. */
+int tsne_gradient_c(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *P, int64_t n,
+                    int32_t c, const double *Y, int32_t metric, double theta, double exaggeration,
+                    double *grad_out, double *sumq_out, double *loss_out);
 /* updateEmbedding (TsneHelpers.scala:341-369), in place on Y, upd, gains. */
 int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *grad, double *Y,
                           double *upd, double *gains, double min_gain, double momentum,
@@ -148,7 +156,7 @@ int tsne_init_working_set(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed, do
                           double *upd, double *gains);
 
 /* optimize (TsneHelpers.scala:396-430): all iterations on the device; Y,
- * upd and gains (n x 2) are read and written back.  loss_keys / loss_vals
+ * upd and gains (n x n_components, 2 or 3) are read and written back.  loss_keys / loss_vals
  * receive (t, KL) for every t % 10 == 0 (the "loss" accumulator,
  * TsneHelpers.scala:297-300), at most loss_cap entries. */
 int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_ptr,
@@ -171,13 +179,14 @@ int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const i
 
 /* Device-resident optimizer.  setup copies the FULL P (every rank holds it;
  * rank r computes rows [r*ceil(n/world), ...) of the optimizer's internal
- * point labels) and the working set (Y, upd, gains: n x 2, original point
+ * point labels) and the working set (Y, upd, gains: n x n_components, original point
  * order) into its own state and allocates the workspace; step runs global
  * iteration t (1-based) with the reference phase schedule and rewrites the
  * caller's Y (original order) at the end of every step; sync also writes
  * back upd and gains.  Losses for t % 10 == 0 stay on the device and are read
  * by tsne_dev_opt_losses.  Internally the points are relabelled into Morton
- * order every 25 iterations (cache locality of the CSR attraction). */
+ * order every 25 iterations (cache locality of the CSR attraction; 2-D only).
+ * n_components = 3 runs the octree extension (see tsne_gradient_c). */
 int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *d_row_ptr,
                        const int32_t *d_col, const double *d_P, int64_t n, double *d_Y,
                        double *d_upd, double *d_gains);

@@ -505,3 +505,193 @@ int oracle_attraction_rows(const int64_t *row_ptr, const int32_t *col, const dou
     if (loss) *loss = l;
     return 0;
 }
+
+/* ---------------------------------------------------- 3-D octree (extension)
+ * The reference supports only 2-D embeddings (Cell.scala:32 requires
+ * len == 2; nComponents = 3 crashes).  SURVEY.md section 8f defines the 3-D
+ * extension as the natural generalisation, restated here and documented in
+ * root Cell(0, 0, 0, W) with W = max(dX, dY, dZ); capacity 1;
+ * subDivide halves hWidth for all three extents; children tried and summed
+ * in the order upper (z >= cz) NW, NE, SW, SE, then lower NW, NE, SW, SE
+ * (closed intervals: west iff x <= cx, north iff y >= cy, upper iff z >= cz);
+ * criterion max(h) / D < theta with D the squared 3-D distance.
+ * No reference output exists for this path: parity unpinned (self-consistency
+ * of this restatement: theta = 0 equals the exact O(N^2) sums, tested). */
+typedef struct {
+    double x, y, z, hw;
+    double sumx, sumy, sumz, comx, comy, comz;
+    double px, py, pz;
+    int32_t cum, leaf, has_point;
+    int32_t child[8];
+} onode_t;
+
+typedef struct { onode_t *v; int64_t n, cap; } otree_t;
+
+static int32_t ot_new(otree_t *t, double x, double y, double z, double hw) {
+    if (t->n == t->cap) {
+        t->cap = t->cap ? 2 * t->cap : 1024;
+        t->v = (onode_t *)realloc(t->v, sizeof(onode_t) * (size_t)t->cap);
+    }
+    onode_t *q = &t->v[t->n];
+    memset(q, 0, sizeof(*q));
+    q->x = x; q->y = y; q->z = z; q->hw = hw; q->leaf = 1;
+    for (int c = 0; c < 8; ++c) q->child[c] = -1;
+    return (int32_t)t->n++;
+}
+
+static int ocell_contains(const onode_t *q, double px, double py, double pz) {
+    return (q->x - q->hw <= px) && (q->x + q->hw >= px) && (q->y - q->hw <= py) && (q->y + q->hw >= py) &&
+           (q->z - q->hw <= pz) && (q->z + q->hw >= pz);
+}
+
+static int ot_insert(otree_t *t, int32_t ni, double px, double py, double pz);
+
+static int ot_insert_sub(otree_t *t, int32_t ni, double px, double py, double pz) {
+    for (int c = 0; c < 8; ++c) {
+        int32_t ch = t->v[ni].child[c];
+        if (ch >= 0 && ocell_contains(&t->v[ch], px, py, pz)) {
+            if (ot_insert(t, ch, px, py, pz)) return 1;
+        }
+    }
+    return 0;
+}
+
+static void ot_subdivide(otree_t *t, int32_t ni) {
+    double x = t->v[ni].x, y = t->v[ni].y, z = t->v[ni].z, h = 0.5 * t->v[ni].hw;
+    int32_t ch[8];
+    for (int c = 0; c < 8; ++c) {
+        double cx = (c & 1) ? x + h : x - h;     /* east : west */
+        double cy = (c & 2) ? y - h : y + h;     /* south : north */
+        double cz = (c & 4) ? z - h : z + h;     /* lower : upper */
+        ch[c] = ot_new(t, cx, cy, cz, h);
+    }
+    for (int c = 0; c < 8; ++c) t->v[ni].child[c] = ch[c];
+}
+
+static int ot_insert(otree_t *t, int32_t ni, double px, double py, double pz) {
+    onode_t *q = &t->v[ni];
+    if (!ocell_contains(q, px, py, pz)) return 0;
+    q->sumx += px; q->sumy += py; q->sumz += pz;
+    q->cum += 1;
+    q->comx = q->sumx / (double)q->cum;
+    q->comy = q->sumy / (double)q->cum;
+    q->comz = q->sumz / (double)q->cum;
+    if (q->leaf) {
+        if (q->has_point) {
+            if (q->px == px && q->py == py && q->pz == pz) return 1;
+            double lx = q->px, ly = q->py, lz = q->pz;
+            ot_subdivide(t, ni);
+            t->v[ni].leaf = 0;
+            ot_insert_sub(t, ni, lx, ly, lz);
+            ot_insert_sub(t, ni, px, py, pz);
+            t->v[ni].has_point = 0;
+            return 1;
+        }
+        q->has_point = 1; q->px = px; q->py = py; q->pz = pz;
+        return 1;
+    }
+    return ot_insert_sub(t, ni, px, py, pz);
+}
+
+static void ot_repulsive(const otree_t *t, int32_t ni, double px, double py, double pz, double theta,
+                         double *f, double *sq) {
+    const onode_t *q = &t->v[ni];
+    if ((q->leaf && q->cum == 0) || (q->leaf && q->px == px && q->py == py && q->pz == pz)) {
+        f[0] = f[1] = f[2] = 0.0; *sq = 0.0;
+        return;
+    }
+    double dx = px - q->comx, dy = py - q->comy, dz = pz - q->comz;
+    double D = dx * dx + dy * dy + dz * dz;
+    if (q->leaf || (q->hw / D < theta)) {
+        double Q = 1.0 / (1.0 + D);
+        double mult = (double)q->cum * Q;
+        double s = mult * Q;
+        *sq = 0.0 + mult;
+        f[0] = s * dx; f[1] = s * dy; f[2] = s * dz;
+        return;
+    }
+    double a[3] = {0, 0, 0}, as = 0;
+    for (int c = 0; c < 8; ++c) {
+        double cf[3], cs;
+        ot_repulsive(t, q->child[c], px, py, pz, theta, cf, &cs);
+        if (c == 0) { a[0] = cf[0]; a[1] = cf[1]; a[2] = cf[2]; as = cs; }
+        else { a[0] = a[0] + cf[0]; a[1] = a[1] + cf[1]; a[2] = a[2] + cf[2]; as = as + cs; }
+    }
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; *sq = as;
+}
+
+static void build_otree(otree_t *t, const double *Y, int64_t n) {
+    double mn[3], mx[3];
+    for (int k = 0; k < 3; ++k) mn[k] = mx[k] = Y[k];
+    for (int64_t i = 1; i < n; ++i)
+        for (int k = 0; k < 3; ++k) { mn[k] = fmin(mn[k], Y[3 * i + k]); mx[k] = fmax(mx[k], Y[3 * i + k]); }
+    double W = fmax(fmax(mx[0] - mn[0], mx[1] - mn[1]), mx[2] - mn[2]);
+    t->v = NULL; t->n = t->cap = 0;
+    ot_new(t, 0.0, 0.0, 0.0, W);
+    for (int64_t i = 0; i < n; ++i) ot_insert(t, 0, Y[3 * i], Y[3 * i + 1], Y[3 * i + 2]);
+}
+
+int oracle_gradient3(const int64_t *row_ptr, const int32_t *col, const double *val,
+                     int64_t n, const double *Y, int metric, double theta,
+                     double exaggeration, double *grad, double *sumq_out, double *loss_out,
+                     double *rep_out, double *zi_out, int threads) {
+    if (!row_ptr || !Y || n < 1) return -1;
+    otree_t t;
+    build_otree(&t, Y, n);
+    double *rep = (double *)malloc(sizeof(double) * 3 * (size_t)n);
+    double *zi = (double *)malloc(sizeof(double) * (size_t)n);
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+#endif
+    for (int64_t i = 0; i < n; ++i)
+        ot_repulsive(&t, 0, Y[3 * i], Y[3 * i + 1], Y[3 * i + 2], theta, rep + 3 * i, zi + i);
+    free(t.v);
+    double Z = 0.0;
+    for (int64_t i = 0; i < n; ++i) Z = Z + zi[i];
+    double loss = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        double g[3] = {0, 0, 0};
+        const double *yi = Y + 3 * i;
+        for (int64_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+            const double *yj = Y + 3 * (int64_t)col[e];
+            double pij = val[e] * exaggeration;
+            double qij = 1.0 / (1.0 + oracle_metric(yi, yj, 3, metric));
+            double s = pij * qij;
+            for (int k = 0; k < 3; ++k) g[k] = g[k] + s * (yi[k] - yj[k]);
+            if (loss_out) loss += pij * log(pij / (qij / Z));
+        }
+        for (int k = 0; k < 3; ++k) grad[3 * i + k] = g[k] - rep[3 * i + k] / Z;
+    }
+    if (sumq_out) *sumq_out = Z;
+    if (loss_out) *loss_out = loss;
+    if (rep_out) memcpy(rep_out, rep, sizeof(double) * 3 * (size_t)n);
+    if (zi_out) memcpy(zi_out, zi, sizeof(double) * (size_t)n);
+    free(rep); free(zi);
+    return 0;
+}
+
+int oracle_optimize3(const int64_t *row_ptr, const int32_t *col, const double *val,
+                     int64_t n, double *Y, double *upd, double *gains, int metric,
+                     double learning_rate, int32_t iterations, double early_exaggeration,
+                     double initial_momentum, double final_momentum, double theta,
+                     int32_t *loss_keys, double *loss_vals, int32_t *n_loss, int threads) {
+    int32_t n1 = iterations < 20 ? iterations : 20;
+    int32_t n2 = (iterations - n1) < 81 ? (iterations - n1) : 81;
+    int32_t nl = 0;
+    double *grad = (double *)malloc(sizeof(double) * 3 * (size_t)n);
+    for (int32_t t = 1; t <= iterations; ++t) {
+        double ex = (t <= n1 + n2) ? early_exaggeration : 1.0;
+        double mom = (t <= n1) ? initial_momentum : final_momentum;
+        int want_loss = (t % 10 == 0);
+        double loss = 0.0, Z = 0.0;
+        oracle_gradient3(row_ptr, col, val, n, Y, metric, theta, ex, grad, &Z,
+                         want_loss ? &loss : NULL, NULL, NULL, threads);
+        if (want_loss && loss_keys) { loss_keys[nl] = t; loss_vals[nl] = loss; ++nl; }
+        oracle_update(n, 3, grad, Y, upd, gains, 0.01, mom, learning_rate);
+        oracle_center(n, 3, Y);
+    }
+    if (n_loss) *n_loss = nl;
+    free(grad);
+    return 0;
+}

@@ -100,6 +100,19 @@ int oracle_optimize(const int64_t *row_ptr, const int32_t *col, const double *va
                     double initial_momentum, double final_momentum, double theta,
                     int32_t *loss_keys, double *loss_vals, int32_t *n_loss, int threads);
 
+/* 3-D extension (octree): the natural generalisation of the
+ * quadtree path, defined in tsne_oracle.c; Y, grad, rep are n x 3.
+ * Parity unpinned (no reference output exists for nComponents = 3). */
+int oracle_gradient3(const int64_t *row_ptr, const int32_t *col, const double *val,
+                     int64_t n, const double *Y, int metric, double theta,
+                     double exaggeration, double *grad, double *sumq, double *loss,
+                     double *rep, double *zi, int threads);
+int oracle_optimize3(const int64_t *row_ptr, const int32_t *col, const double *val,
+                     int64_t n, double *Y, double *upd, double *gains, int metric,
+                     double learning_rate, int32_t iterations, double early_exaggeration,
+                     double initial_momentum, double final_momentum, double theta,
+                     int32_t *loss_keys, double *loss_vals, int32_t *n_loss, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -166,3 +166,41 @@ def attraction_rows(row_ptr, col, val, Y, rep, Z, r0, r1, metric="sqeuclidean", 
                                       C.byref(loss) if want_loss else None)
     assert rc == 0
     return grad, (loss.value if want_loss else None)
+
+
+def gradient3(row_ptr, col, val, Y, theta, metric="sqeuclidean", exaggeration=1.0,
+              want_loss=False, threads=1):
+    """3-D extension (octree restatement, parity unpinned: see tsne_oracle.h)."""
+    n = Y.shape[0]
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    grad = np.zeros((n, 3))
+    rep = np.zeros((n, 3))
+    zi = np.zeros(n)
+    z = D(0)
+    loss = D(0)
+    rc = lib().oracle_gradient3(_p(np.ascontiguousarray(row_ptr, np.int64), I64),
+                                _p(np.ascontiguousarray(col, np.int32), I32),
+                                _p(np.ascontiguousarray(val, np.float64), D), I64(n), _p(Y, D),
+                                C.c_int(METRICS[metric]), D(theta), D(exaggeration),
+                                _p(grad, D), C.byref(z), C.byref(loss) if want_loss else None,
+                                _p(rep, D), _p(zi, D), C.c_int(threads))
+    assert rc == 0
+    return dict(grad=grad, Z=z.value, loss=loss.value if want_loss else None, rep=rep, zi=zi)
+
+
+def optimize3(row_ptr, col, val, Y, upd, gains, metric="sqeuclidean", learning_rate=1000.0,
+              iterations=300, early_exaggeration=4.0, initial_momentum=0.5,
+              final_momentum=0.8, theta=0.25, threads=1):
+    n = Y.shape[0]
+    keys = np.zeros(iterations // 10 + 1, dtype=np.int32)
+    vals = np.zeros(iterations // 10 + 1)
+    nl = I32(0)
+    rc = lib().oracle_optimize3(_p(np.ascontiguousarray(row_ptr, np.int64), I64),
+                                _p(np.ascontiguousarray(col, np.int32), I32),
+                                _p(np.ascontiguousarray(val, np.float64), D), I64(n),
+                                _p(Y, D), _p(upd, D), _p(gains, D), C.c_int(METRICS[metric]),
+                                D(learning_rate), I32(iterations), D(early_exaggeration),
+                                D(initial_momentum), D(final_momentum), D(theta),
+                                _p(keys, I32), _p(vals, D), C.byref(nl), C.c_int(threads))
+    assert rc == 0
+    return dict(zip(keys[:nl.value].tolist(), vals[:nl.value].tolist()))

@@ -295,8 +295,8 @@ def test_optimize_loss_matches_oracle(ctx):
 
 def test_unsupported_components(ctx):
     rp, col, val = triples_to_csr(G["denseJointProbabilitiesResults"], 10)
-    Y = np.zeros((10, 3))
-    p = default_params(n_components=3)
+    Y = np.zeros((10, 4))
+    p = default_params(n_components=4)
     with pytest.raises(T.TsneError) as e:
         ctx.optimize(rp, col, val, Y, np.zeros_like(Y), np.ones_like(Y), p)
     assert e.value.status == -4
@@ -369,3 +369,62 @@ def test_device_balance_cuts_match_host_rule(ctx, world):
         ctx.dev_balance_cuts(dc, n, world, db)
         ctx.synchronize()
         assert db.cpu().numpy().tolist() == want.tolist(), (n, zero_frac)
+
+
+# ------------------------------------------- 3-D embeddings (octree extension)
+@pytest.mark.parametrize("n,scale,theta", [
+    (600, 1.0, 0.0), (3000, 1e-4, 0.5), (3000, 0.05, 0.5), (3000, 1.0, 0.5), (3000, 20.0, 0.25),
+    (20000, 3.0, 0.5)])
+def test_gradient3_matches_oracle(ctx, n, scale, theta):
+    """nComponents = 3: the GPU octree vs the octree
+    restatement (oracle/tsne_oracle.c oracle_gradient3; parity unpinned by
+    the reference, which requires 2-D)."""
+    rp, col, val = random_problem(n, 10, seed=n + int(scale * 100))
+    Y = np.random.default_rng(n).normal(size=(n, 3)) * scale
+    g, Z, loss = ctx.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
+    r = O.gradient3(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
+    tol = 1e-12 if theta == 0.0 else 1e-6
+    assert np.abs(g - r["grad"]).max() <= tol * np.abs(r["grad"]).max()
+    assert abs(Z - r["Z"]) <= 1e-7 * r["Z"]
+    assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
+
+
+def test_gradient3_outside_root_and_metrics(ctx):
+    n = 800
+    rp, col, val = random_problem(n, 10, seed=12)
+    Y = np.random.default_rng(3).normal(size=(n, 3)) + np.array([4.0, -2.0, 1.0])   # points outside the root
+    # (exact duplicates are a documented deviation: the reference restarts their
+    # multiplicity at every split of their leaf, QuadTree.scala:57-60)
+    for metric in ("sqeuclidean", "euclidean", "cosine"):
+        g, Z, _ = ctx.gradient(rp, col, val, Y, 0.5, metric=metric)
+        r = O.gradient3(rp, col, val, Y, 0.5, metric=metric)
+        assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max(), metric
+
+
+def test_optimize3_matches_oracle_and_device_path(ctx):
+    import torch
+    n = 500
+    rp, col, val = random_problem(n, 30, seed=33)
+    Y0 = np.random.default_rng(7).normal(size=(n, 3)) * 1e-4
+    p = default_params(n_components=3, iterations=60, theta=0.5)
+    Yh, uh, gh = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lh = ctx.optimize(rp, col, val, Yh, uh, gh, p)
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lo = O.optimize3(rp, col, val, Yo, uo, go, iterations=60, theta=0.5)
+    assert sorted(lh) == sorted(lo) == list(range(10, 61, 10))
+    for t in (10, 20, 30):
+        assert abs(lh[t] - lo[t]) <= 0.01 * abs(lo[t]), t
+    assert np.isfinite(Yh).all() and np.abs(Yh.mean(0)).max() <= 1e-9 * (1 + np.abs(Yh).max())
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    dY = t(Y0, torch.float64)
+    du = torch.zeros((n, 3), dtype=torch.float64, device=dev)
+    dg = torch.ones((n, 3), dtype=torch.float64, device=dev)
+    ctx.dev_opt_setup(p, t(rp, torch.int64), t(col, torch.int32), t(val, torch.float64), n, dY, du, dg)
+    for it in range(1, 61):
+        ctx.dev_opt_step(it)
+    ctx.dev_opt_sync()
+    ctx.synchronize()
+    assert np.array_equal(dY.cpu().numpy(), Yh)
+    assert np.array_equal(dg.cpu().numpy(), gh)
+    assert ctx.dev_opt_losses() == lh

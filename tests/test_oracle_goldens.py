@@ -160,3 +160,39 @@ def test_bh_reference_criterion_scale_dependence():
     ex = O.gradient(rp, *none, big, theta=0.0)
     bh = O.gradient(rp, *none, big, theta=0.5)
     assert bh["visits"].mean() < 0.2 * ex["visits"].mean()
+
+
+# ----------------------------------------------- 3-D extension (octree restatement)
+def _exact3(Y):
+    """O(N^2) repulsion sums sum_j (y_i - y_j)/(1+D)^2, sum_j 1/(1+D), j != i."""
+    d = Y[:, None, :] - Y[None, :, :]
+    D = (d ** 2).sum(-1)
+    q = 1.0 / (1.0 + D)
+    np.fill_diagonal(q, 0.0)
+    return (q[:, :, None] ** 2 * d).sum(1), q.sum(1)
+
+
+def test_octree_theta0_is_exact():
+    """theta = 0 opens every cell: the 3-D restatement equals the exact sums."""
+    rng = np.random.default_rng(4)
+    Y = rng.normal(size=(400, 3))
+    rp = np.zeros(401, dtype=np.int64)
+    none = (np.zeros(0, np.int32), np.zeros(0))
+    r = O.gradient3(rp, *none, Y, theta=0.0)
+    rep, zi = _exact3(Y)
+    assert np.abs(r["rep"] - rep).max() <= 1e-12 * np.abs(rep).max()
+    assert np.abs(r["zi"] - zi).max() <= 1e-12 * zi.max()
+
+
+def test_octree_bh_error_shrinks_with_theta():
+    rng = np.random.default_rng(5)
+    Y = rng.normal(size=(500, 3))
+    rp = np.zeros(501, dtype=np.int64)
+    none = (np.zeros(0, np.int32), np.zeros(0))
+    rep, zi = _exact3(Y)
+    err = []
+    for theta in (0.5, 0.1, 0.02):
+        r = O.gradient3(rp, *none, Y, theta=theta)
+        assert abs(r["Z"] - zi.sum()) <= 0.05 * zi.sum()
+        err.append(np.abs(r["rep"] - rep).max())
+    assert err[0] > err[1] > err[2] and err[2] <= 1e-2 * np.abs(rep).max()

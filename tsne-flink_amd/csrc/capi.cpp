@@ -383,6 +383,29 @@ int tsne_gradient(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, con
     });
 }
 
+int tsne_gradient_c(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *P, int64_t n,
+                    int32_t c, const double *Y, int32_t metric, double theta, double exaggeration,
+                    double *grad_out, double *sumq_out, double *loss_out) {
+    if (c == 2) return tsne_gradient(ctx, row_ptr, col, P, n, Y, metric, theta, exaggeration, grad_out, sumq_out,
+                                     loss_out);
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        if (c != 3) fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
+        TSNE_REQUIRE(row_ptr && Y && grad_out && n >= 1 && row_ptr[0] == 0, "bad arguments");
+        TSNE_REQUIRE(metric >= 0 && metric <= 2, "unknown metric");
+        const int64_t nnz = row_ptr[n];
+        int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)n + 1);
+        int32_t *dc = upload(ctx, "h.col", col, (size_t)nnz);
+        double *dp = upload(ctx, "h.p", P, (size_t)nnz);
+        double *dY = upload(ctx, "h.Y", Y, (size_t)n * 3);
+        double *dg = ctx->ws.get<double>("h.grad", (size_t)n * 3);
+        gradient3_device(ctx, drp, dc, dp, n, dY, metric, theta, exaggeration, dg, sumq_out, loss_out);
+        download(ctx, grad_out, dg, (size_t)n * 3);
+        sync(ctx);
+    });
+}
+
 int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *grad, double *Y, double *upd,
                           double *gains, double min_gain, double momentum, double learning_rate) {
     return guard([&] {
@@ -439,8 +462,9 @@ int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_p
         check_ctx(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(params && row_ptr && Y && upd && gains && n >= 1 && row_ptr[0] == 0, "bad arguments");
-        if (params->n_components != 2)
-            fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (Cell.contains requires 2-D points)");
+        if (params->n_components != 2 && params->n_components != 3)
+            fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
+        const size_t C = (size_t)params->n_components;
         const int64_t nnz = row_ptr[n];
         for (int64_t e = 0; e < nnz; ++e)
             if (col[e] < 0 || col[e] >= n) fail(TSNE_ERR_ARG, "column index out of range");
@@ -448,15 +472,15 @@ int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_p
         int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)n + 1);
         int32_t *dc = upload(ctx, "h.col", col, (size_t)nnz);
         double *dp = upload(ctx, "h.p", P, (size_t)nnz);
-        double *dY = upload(ctx, "h.Yopt", Y, (size_t)n * 2);
-        double *du = upload(ctx, "h.updopt", upd, (size_t)n * 2);
-        double *dn = upload(ctx, "h.gainsopt", gains, (size_t)n * 2);
+        double *dY = upload(ctx, "h.Yopt", Y, (size_t)n * C);
+        double *du = upload(ctx, "h.updopt", upd, (size_t)n * C);
+        double *dn = upload(ctx, "h.gainsopt", gains, (size_t)n * C);
         opt_setup(ctx, params, drp, dc, dp, n, dY, du, dn);
         for (int32_t t = 1; t <= params->iterations; ++t) opt_step(ctx, t);
         opt_sync(ctx);
-        download(ctx, Y, dY, (size_t)n * 2);
-        download(ctx, upd, du, (size_t)n * 2);
-        download(ctx, gains, dn, (size_t)n * 2);
+        download(ctx, Y, dY, (size_t)n * C);
+        download(ctx, upd, du, (size_t)n * C);
+        download(ctx, gains, dn, (size_t)n * C);
         sync(ctx);
         int32_t k = opt_losses(ctx, loss_keys, loss_vals, loss_cap);
         if (n_loss) *n_loss = k;

@@ -131,6 +131,10 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
                      double theta, double exaggeration, double *d_grad, double *h_sumq,
                      double *h_loss);
 
+void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col, const double *d_P, int64_t n,
+                      const double *dY, int32_t metric, double theta, double exaggeration, double *d_grad,
+                      double *h_sumq, double *h_loss);
+
 void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr,
                const int32_t *d_col, const double *d_P, int64_t n, double *dY, double *dupd,
                double *dgains);

@@ -1,0 +1,569 @@
+// octree.hip -- Barnes-Hut octree build + traversal for 3-D embeddings on
+// gfx950 (the SURVEY.md 8f extension of QuadTree.scala:38-152 /
+// Cell.scala:31-36 to nComponents = 3; restated in oracle/tsne_oracle.c).
+//
+// Same equivalence argument as bhtree.hip: Morton digits replay the cell
+// arithmetic (child centres c -/+ 0.5 h, closed containment tried in the
+// order upper NW, NE, SW, SE, lower NW, NE, SW, SE), so cells are the
+// restatement's; a cell whose points all sit in one child forms a chain
+// summarised at its deepest cell (the criterion is monotone along it);
+// leaves interact directly, a leaf equal to the query contributes nothing;
+// points outside the root cell are queries only.  Deviations:
+// exact duplicates count with full multiplicity, cells deeper than 21 levels
+// are not split (all their points interact directly), and subtrees entirely
+// within D <= near_dmax of a query are summed exactly (<= BH_NEAR_TOL3
+// relative from the restatement's cell sums).
+//
+// The traversal is the 2-D design without its quad-collapsed records and
+// moments: a wave of 64 Morton-consecutive queries shares an LDS stack of
+// (node, lane mask); per popped node each lane first tries the all-open /
+// near-exact tile test (exact leaf sum over the node's contiguous range,
+// points staged through LDS), then evaluates the node's two binary children.
+#include <hipcub/hipcub.hpp>
+
+#include "octree.hpp"
+
+namespace tsne {
+namespace {
+
+constexpr int LEVELS3 = 21;                 // 63 key bits
+constexpr uint64_t OUT_KEY3 = 1ull << 63;   // outside the root cell: sorts last
+constexpr int STACK3 = 256;                 // single pops, <= 2 pushes each: depth-bounded
+constexpr double BH_NEAR_TOL3 = 1e-7;
+constexpr int AGG3 = 12;                    // sx, sy, sz, x0, x1, y0, y1, z0, z1, hmin, cnt, rball
+
+__global__ void bbox3_partial(const double *__restrict__ Y, int64_t n, double *__restrict__ part) {
+    __shared__ double sm[4][6];
+    double mn[3], mx[3];
+    for (int k = 0; k < 3; ++k) { mn[k] = __builtin_inf(); mx[k] = -__builtin_inf(); }
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        for (int k = 0; k < 3; ++k) { mn[k] = fmin(mn[k], Y[3 * i + k]); mx[k] = fmax(mx[k], Y[3 * i + k]); }
+    const int w = threadIdx.x >> 6;
+    for (int k = 0; k < 3; ++k) {
+        mn[k] = wave_min(mn[k]);
+        mx[k] = wave_max(mx[k]);
+        if (lane_id() == 0) { sm[w][2 * k] = mn[k]; sm[w][2 * k + 1] = mx[k]; }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < 4; ++v)
+            for (int k = 0; k < 3; ++k) {
+                sm[0][2 * k] = fmin(sm[0][2 * k], sm[v][2 * k]);
+                sm[0][2 * k + 1] = fmax(sm[0][2 * k + 1], sm[v][2 * k + 1]);
+            }
+        for (int k = 0; k < 6; ++k) part[blockIdx.x * 6 + k] = sm[0][k];
+    }
+}
+
+__global__ void bbox3_final(const double *__restrict__ part, int nb, double *__restrict__ W,
+                            int32_t *__restrict__ meta) {
+    __shared__ double sm[4][6];
+    double mn[3], mx[3];
+    for (int k = 0; k < 3; ++k) { mn[k] = __builtin_inf(); mx[k] = -__builtin_inf(); }
+    for (int b = threadIdx.x; b < nb; b += blockDim.x)
+        for (int k = 0; k < 3; ++k) { mn[k] = fmin(mn[k], part[6 * b + 2 * k]); mx[k] = fmax(mx[k], part[6 * b + 2 * k + 1]); }
+    const int w = threadIdx.x >> 6;
+    for (int k = 0; k < 3; ++k) {
+        mn[k] = wave_min(mn[k]);
+        mx[k] = wave_max(mx[k]);
+        if (lane_id() == 0) { sm[w][2 * k] = mn[k]; sm[w][2 * k + 1] = mx[k]; }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int v = 1; v < 4; ++v)
+            for (int k = 0; k < 3; ++k) {
+                sm[0][2 * k] = fmin(sm[0][2 * k], sm[v][2 * k]);
+                sm[0][2 * k + 1] = fmax(sm[0][2 * k + 1], sm[v][2 * k + 1]);
+            }
+        const double a = sm[0][1] - sm[0][0], b = sm[0][3] - sm[0][2], c = sm[0][5] - sm[0][4];
+        const double ab = a > b ? a : b;
+        *W = ab > c ? ab : c;   // max(maxX - minX, maxY - minY, maxZ - minZ)
+        meta[0] = 0;
+    }
+}
+
+// fixed-point digits away from cell boundaries (see bhtree.hip quant_digits):
+// 21 levels, band 1e-4 of a level-21 cell
+__device__ __forceinline__ bool quant21(double p, double W, uint32_t &q) {
+    const double t = (p + W) / (2.0 * W) * 2097152.0;   // 2^21
+    if (!(t >= 0.0 && t < 2097152.0)) return false;
+    const double f = floor(t);
+    const double fr = t - f;
+    if (fr < 1e-4 || fr > 1.0 - 1e-4) return false;
+    q = (uint32_t)f;
+    return true;
+}
+
+// digit c = 4 lower + 2 south + east, tried in ascending c (the child order)
+__global__ void morton3_keys(const double *__restrict__ Y, int64_t n, const double *__restrict__ Wp,
+                             uint64_t *__restrict__ keys, int32_t *__restrict__ idx, int32_t *__restrict__ meta) {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i0 < n;
+    const int64_t i = live ? i0 : n - 1;
+    const double W = *Wp;
+    const double px = Y[3 * i], py = Y[3 * i + 1], pz = Y[3 * i + 2];
+    double x = 0.0, y = 0.0, z = 0.0, h = W;
+    bool in = live && (__dsub_rn(x, h) <= px) && (__dadd_rn(x, h) >= px) && (__dsub_rn(y, h) <= py) &&
+              (__dadd_rn(y, h) >= py) && (__dsub_rn(z, h) <= pz) && (__dadd_rn(z, h) >= pz);
+    uint64_t key = 0;
+    uint32_t qx, qy, qz;
+    if (in && W > 0.0 && quant21(px, W, qx) && quant21(py, W, qy) && quant21(pz, W, qz)) {
+        for (int l = LEVELS3 - 1; l >= 0; --l) {
+            const uint32_t east = (qx >> l) & 1u, south = 1u - ((qy >> l) & 1u), lower = 1u - ((qz >> l) & 1u);
+            key = (key << 3) | (uint64_t)(4u * lower + 2u * south + east);
+        }
+    } else if (in) {
+        for (int l = 0; l < LEVELS3; ++l) {
+            const double nh = __dmul_rn(0.5, h);
+            const double xw = __dsub_rn(x, nh), xe = __dadd_rn(x, nh);
+            const double yn = __dadd_rn(y, nh), ys = __dsub_rn(y, nh);
+            const double zu = __dadd_rn(z, nh), zl = __dsub_rn(z, nh);
+            const bool inW = (__dsub_rn(xw, nh) <= px) && (__dadd_rn(xw, nh) >= px);
+            const bool inE = (__dsub_rn(xe, nh) <= px) && (__dadd_rn(xe, nh) >= px);
+            const bool inN = (__dsub_rn(yn, nh) <= py) && (__dadd_rn(yn, nh) >= py);
+            const bool inS = (__dsub_rn(ys, nh) <= py) && (__dadd_rn(ys, nh) >= py);
+            const bool inU = (__dsub_rn(zu, nh) <= pz) && (__dadd_rn(zu, nh) >= pz);
+            const bool inL = (__dsub_rn(zl, nh) <= pz) && (__dadd_rn(zl, nh) >= pz);
+            int c = 7;   // lower SE, or a rounding gap (see bhtree.hip)
+            for (int t = 0; t < 8; ++t) {
+                const bool ok = ((t & 1) ? inE : inW) && ((t & 2) ? inS : inN) && ((t & 4) ? inL : inU);
+                if (ok) { c = t; break; }
+            }
+            x = (c & 1) ? xe : xw;
+            y = (c & 2) ? ys : yn;
+            z = (c & 4) ? zl : zu;
+            h = nh;
+            key = (key << 3) | (uint64_t)c;
+        }
+    } else {
+        key = OUT_KEY3;
+    }
+    if (live) {
+        keys[i] = key;
+        idx[i] = (int32_t)i;
+    }
+    const uint64_t b = __ballot(in);
+    if (lane_id() == 0 && b) atomicAdd(&meta[0], (int)__popcll(b));
+}
+
+__global__ void gather3(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted, int64_t n,
+                        double4 *__restrict__ pos, int32_t *__restrict__ inv) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int32_t i = idx_sorted[s];
+    pos[s] = make_double4(Y[3 * i], Y[3 * i + 1], Y[3 * i + 2], 0.0);
+    inv[i] = (int32_t)s;
+}
+
+__global__ void dup_count3(const double4 *__restrict__ pos, const uint64_t *__restrict__ keys, int64_t n,
+                           int32_t *__restrict__ dupc) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const double4 q = pos[s];
+    const uint64_t k = keys[s];
+    int32_t c = 1;
+    for (int64_t t = s - 1; t >= 0 && keys[t] == k; --t) {
+        const double4 p = pos[t];
+        c += (p.x == q.x && p.y == q.y && p.z == q.z);
+    }
+    for (int64_t t = s + 1; t < n && keys[t] == k; ++t) {
+        const double4 p = pos[t];
+        c += (p.x == q.x && p.y == q.y && p.z == q.z);
+    }
+    dupc[s] = c;
+}
+
+// common-prefix bits of sorted keys i and j within the 63-bit Morton field
+// (ties extend with the index bits); -1 out of range
+__device__ __forceinline__ int kdelta3(const uint64_t *__restrict__ k, int m, int i, int j) {
+    if (j < 0 || j >= m) return -1;
+    const uint64_t a = k[i], b = k[j];
+    if (a == b) return 63 + __clz((unsigned)(i ^ j));
+    return __clzll((long long)(a ^ b)) - 1;
+}
+
+__global__ void karras3(const uint64_t *__restrict__ k, const int32_t *__restrict__ meta, OctNode *__restrict__ nodes,
+                        int32_t *__restrict__ parent_leaf, int32_t *__restrict__ parent_node,
+                        int32_t *__restrict__ arrive) {
+    const int m = meta[0];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m - 1) return;
+    arrive[i] = 0;
+    const int dr = kdelta3(k, m, i, i + 1), dl = kdelta3(k, m, i, i - 1);
+    const int d = (dr > dl) ? 1 : -1;
+    const int dmin = d > 0 ? dl : dr;
+    int lmax = 2;
+    while (kdelta3(k, m, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (kdelta3(k, m, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = kdelta3(k, m, i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (kdelta3(k, m, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int lo = min(i, j), hi = max(i, j);
+    int left, right;
+    if (lo == gamma) { left = ~gamma; parent_leaf[gamma] = i; }
+    else { left = gamma; parent_node[gamma] = i; }
+    if (hi == gamma + 1) { right = ~(gamma + 1); parent_leaf[gamma + 1] = i; }
+    else { right = gamma + 1; parent_node[gamma + 1] = i; }
+    nodes[i].left = left;
+    nodes[i].right = right;
+    nodes[i].delta = dnode;
+    nodes[i].first = lo;
+    nodes[i].last = hi;
+    if (i == 0) parent_node[0] = -1;
+}
+
+__device__ __forceinline__ void st_sys3(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys3(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Bottom-up sums / boxes / hmin / rball (bhtree.hip bottom_up, one more axis).
+__global__ void bottom_up3(const double4 *__restrict__ pos, const int32_t *__restrict__ meta,
+                           const double *__restrict__ Wp, double inv_theta, OctNode *nodes, double *agg,
+                           const int32_t *__restrict__ parent_leaf, const int32_t *__restrict__ parent_node,
+                           int32_t *arrive) {
+    const int m = meta[0];
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= m || m < 2) return;
+    const double W = *Wp;
+    int p = parent_leaf[s];
+    while (p >= 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+        const int32_t ch[2] = {nodes[p].left, nodes[p].right};
+        const int32_t dl = nodes[p].delta;
+        double a[2][10];   // sx, sy, sz, x0, x1, y0, y1, z0, z1, hmin
+        double c[2], rb[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (ch[k] < 0) {
+                const double4 q = pos[~ch[k]];
+                a[k][0] = q.x; a[k][1] = q.y; a[k][2] = q.z;
+                a[k][3] = q.x; a[k][4] = q.x; a[k][5] = q.y; a[k][6] = q.y; a[k][7] = q.z; a[k][8] = q.z;
+                a[k][9] = __builtin_inf();
+                c[k] = 1.0;
+                rb[k] = __builtin_inf();
+            } else {
+                const double *g = agg + AGG3 * (int64_t)ch[k];
+#pragma unroll
+                for (int f = 0; f < 10; ++f) a[k][f] = ld_sys3(g + f);
+                c[k] = ld_sys3(g + 10);
+                rb[k] = ld_sys3(g + 11);
+            }
+        }
+        const double cnt = c[0] + c[1];
+        const double sx = a[0][0] + a[1][0], sy = a[0][1] + a[1][1], sz = a[0][2] + a[1][2];
+        const double x0 = fmin(a[0][3], a[1][3]), x1 = fmax(a[0][4], a[1][4]);
+        const double y0 = fmin(a[0][5], a[1][5]), y1 = fmax(a[0][6], a[1][6]);
+        const double z0 = fmin(a[0][7], a[1][7]), z1 = fmax(a[0][8], a[1][8]);
+        const int par = parent_node[p];
+        const int dlev = dl / 3;
+        bool real;
+        if (dl >= 63) real = false;                       // keys tie below 21 levels
+        else if (par < 0) real = true;                    // root cell chain
+        else real = (nodes[par].delta / 3) < dlev;        // first node of its level
+        const double h = real ? ldexp(W, -dlev) : -1.0;
+        const double hmin = fmin(real ? h : __builtin_inf(), fmin(a[0][9], a[1][9]));
+        const double cx = sx / cnt, cy = sy / cnt, cz = sz / cnt;
+        double rball = real ? sqrt(h * inv_theta) : __builtin_inf();
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (ch[k] >= 0) {
+                const double ex = cx - a[k][0] / c[k], ey = cy - a[k][1] / c[k], ez = cz - a[k][2] / c[k];
+                rball = fmin(rball, rb[k] - sqrt(ex * ex + ey * ey + ez * ez));
+            }
+        }
+        rball = rball > 0.0 ? rball * (1.0 - 1e-9) : 0.0;
+        double *g = agg + AGG3 * (int64_t)p;
+        st_sys3(g + 0, sx); st_sys3(g + 1, sy); st_sys3(g + 2, sz);
+        st_sys3(g + 3, x0); st_sys3(g + 4, x1); st_sys3(g + 5, y0); st_sys3(g + 6, y1);
+        st_sys3(g + 7, z0); st_sys3(g + 8, z1); st_sys3(g + 9, hmin);
+        st_sys3(g + 10, cnt); st_sys3(g + 11, rball);
+        OctNode &nd = nodes[p];
+        nd.cx = cx; nd.cy = cy; nd.cz = cz;
+        nd.cnt = (int32_t)cnt;
+        nd.h = h;
+        nd.hmin = hmin;
+        nd.rball = rball;
+        nd.bx0 = x0; nd.bx1 = x1; nd.by0 = y0; nd.by1 = y1; nd.bz0 = z0; nd.bz1 = z1;
+        p = par;
+    }
+}
+
+__global__ void set_root3(int32_t *meta) {
+    const int m = meta[0];
+    meta[1] = (m >= 2) ? 0 : (m == 1 ? ~0 : INT32_MIN);
+}
+
+// 1 / x: v_rcp_f64 + two Newton steps (the IEEE quotient, bhtree.hip)
+__device__ __forceinline__ double rcp2(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    return r;
+}
+
+// a leaf point (zero if equal to the query)
+__device__ __forceinline__ void leaf3(double qx, double qy, double qz, double px, double py, double pz, double &fx,
+                                      double &fy, double &fz, double &zs) {
+    if (px == qx && py == qy && pz == qz) return;
+    const double dx = qx - px, dy = qy - py, dz = qz - pz;
+    const double r = rcp2(1.0 + (dx * dx + dy * dy + dz * dz));
+    const double sc = r * r;
+    fx = __fma_rn(sc, dx, fx);
+    fy = __fma_rn(sc, dy, fy);
+    fz = __fma_rn(sc, dz, fz);
+    zs += r;
+}
+
+// a summarised cell: Q = 1/(1+D), m = n Q, F += m Q (q - com)
+__device__ __forceinline__ void cell3(double dx, double dy, double dz, double D, int32_t n, double &fx, double &fy,
+                                      double &fz, double &zs) {
+    const double Q = rcp2(1.0 + D);
+    const double mult = (double)n * Q;
+    const double sc = mult * Q;
+    fx = __fma_rn(sc, dx, fx);
+    fy = __fma_rn(sc, dy, fy);
+    fz = __fma_rn(sc, dz, fz);
+    zs += mult;
+}
+
+// fl(h / D) < theta (bhtree.hip summarise, 3-D D)
+__device__ __forceinline__ bool summarise3(double h, double dx, double dy, double dz, double th_lo, double th_hi,
+                                           double theta) {
+    const double D = __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz));
+    if (h < th_lo * D) return true;
+    if (h > th_hi * D) return false;
+    return h / D < theta;
+}
+
+__global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ pos, const int32_t *__restrict__ dupc,
+                                                    const OctNode *__restrict__ nodes,
+                                                    const int32_t *__restrict__ meta, double theta, double near_dmax,
+                                                    int64_t g0, int64_t g1, const int64_t *__restrict__ dbounds,
+                                                    double *__restrict__ F, double *__restrict__ Z) {
+    __shared__ int32_t sref[4][STACK3];
+    __shared__ uint64_t smask[4][STACK3];
+    __shared__ double4 tbuf[4][64];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + w;
+    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
+    const int64_t s = g0 + wid * 64 + lane;
+    const bool valid = s >= s0 && s < s1;
+    if (__ballot(valid) == 0) return;
+    const int root = meta[1];
+    const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
+    const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
+    double qx = 0.0, qy = 0.0, qz = 0.0;
+    if (valid) { const double4 q = pos[s]; qx = q.x; qy = q.y; qz = q.z; }
+    const double qmag = fabs(qx) + fabs(qy) + fabs(qz);
+    const int ndup = valid ? dupc[s] : 0;
+    double fx = 0.0, fy = 0.0, fz = 0.0, zs = 0.0;
+    double4 *buf = tbuf[w];
+    int sp = 0;
+    if (root == ~0) {
+        if (valid) { const double4 p = pos[0]; leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs); }
+    } else if (root >= 0) {
+        const OctNode &rt = nodes[root];
+        if (rt.delta >= 63) {
+            for (int p = rt.first; p <= rt.last; ++p) {
+                const double4 pp = pos[p];
+                if (valid) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+            }
+        } else {
+            bool open = false;
+            if (valid) {
+                const double dx = qx - rt.cx, dy = qy - rt.cy, dz = qz - rt.cz;
+                if (summarise3(rt.h, dx, dy, dz, th_lo, th_hi, theta))
+                    cell3(dx, dy, dz, dx * dx + dy * dy + dz * dz, rt.cnt, fx, fy, fz, zs);
+                else
+                    open = true;
+            }
+            const uint64_t om = __ballot(open);
+            if (om) {
+                if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
+                sp = 1;
+            }
+        }
+    }
+    while (sp > 0) {
+        --sp;
+        const int ref = __builtin_amdgcn_readfirstlane(sref[w][sp]);
+        const uint64_t msk = smask[w][sp];
+        bool act = (msk >> lane) & 1ull;
+        const OctNode &nd = nodes[ref];
+        // all-open (ball / box with hmin) or near-exact: the exact leaf sum
+        bool tile = false;
+        if (act) {
+            const double cdx = qx - nd.cx, cdy = qy - nd.cy, cdz = qz - nd.cz;
+            tile = cdx * cdx + cdy * cdy + cdz * cdz <= nd.rball * nd.rball * (1.0 - 1e-9);
+            if (!tile) {
+                const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1) +
+                                           fabs(nd.bz0) + fabs(nd.bz1));
+                const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                const double dzm = fmax(fabs(qz - nd.bz0), fabs(qz - nd.bz1)) + ex;
+                const double dmax = (dxm * dxm + dym * dym + dzm * dzm) * (1.0 + 1e-12);
+                tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
+            }
+        }
+        if (__ballot(tile)) {
+            // points staged through LDS 64 at a time, read back as broadcasts; the
+            // query's exact duplicates (itself included) add 1 each to z: taken off
+            const int a = nd.first, b = nd.last;
+            double ux = 0.0, uy = 0.0, uz = 0.0, uq = 0.0;
+            for (int c0 = a; c0 <= b; c0 += 64) {
+                const int cn = min(64, b - c0 + 1);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < cn) buf[lane] = pos[c0 + lane];
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+                if (tile) {
+                    for (int j = 0; j < cn; ++j) {
+                        const double4 pp = buf[j];
+                        const double dx = qx - pp.x, dy = qy - pp.y, dz = qz - pp.z;
+                        const double r = rcp2(__fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0))));
+                        const double sc = r * r;
+                        ux = __fma_rn(sc, dx, ux);
+                        uy = __fma_rn(sc, dy, uy);
+                        uz = __fma_rn(sc, dz, uz);
+                        uq += r;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (tile) {
+                fx += ux; fy += uy; fz += uz;
+                zs += uq - ((s >= a && s <= b) ? (double)ndup : 0.0);
+                act = false;
+            }
+        }
+        if (__ballot(act) == 0) continue;
+        const int32_t chs[2] = {nd.left, nd.right};
+        // push order: right first, so the left (lower keys: earlier children) pops first
+        int32_t push_ref[2];
+        uint64_t push_mask[2] = {0ull, 0ull};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int32_t ch = chs[k];
+            push_ref[k] = ch;
+            if (ch < 0) {
+                const double4 p = pos[~ch];
+                if (act) leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs);
+                continue;
+            }
+            const OctNode &cn = nodes[ch];
+            if (cn.delta >= 63) {                       // key-tie group: all points interact
+                for (int p = cn.first; p <= cn.last; ++p) {
+                    const double4 pp = pos[p];
+                    if (act) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+                }
+            } else if (cn.h < 0.0) {                    // transparent: opened with its parent
+                push_mask[k] = __ballot(act);
+            } else {
+                bool open = false;
+                if (act) {
+                    const double dx = qx - cn.cx, dy = qy - cn.cy, dz = qz - cn.cz;
+                    if (summarise3(cn.h, dx, dy, dz, th_lo, th_hi, theta))
+                        cell3(dx, dy, dz, __fma_rn(dx, dx, __fma_rn(dy, dy, dz * dz)), cn.cnt, fx, fy, fz, zs);
+                    else
+                        open = true;
+                }
+                push_mask[k] = __ballot(open);
+            }
+        }
+#pragma unroll
+        for (int k = 1; k >= 0; --k) {
+            if (push_mask[k]) {
+                if (lane == 0) { sref[w][sp] = push_ref[k]; smask[w][sp] = push_mask[k]; }
+                ++sp;
+            }
+        }
+    }
+    if (valid) {
+        F[3 * s] = fx;
+        F[3 * s + 1] = fy;
+        F[3 * s + 2] = fz;
+        Z[s] = zs;
+    }
+}
+
+}  // namespace
+
+void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
+    Workspace &ws = ctx->ws;
+    t.n = n;
+    t.keys = ws.get<uint64_t>("oct.keys", n);
+    t.keys_sorted = ws.get<uint64_t>("oct.keys_sorted", n);
+    t.idx = ws.get<int32_t>("oct.idx", n);
+    t.idx_sorted = ws.get<int32_t>("oct.idx_sorted", n);
+    t.inv = ws.get<int32_t>("oct.inv", n);
+    t.dupc = ws.get<int32_t>("oct.dupc", n);
+    t.pos = ws.get<double4>("oct.pos", n);
+    t.nodes = ws.get<OctNode>("oct.nodes", n);
+    t.agg = ws.get<double>("oct.agg", AGG3 * (size_t)n);
+    t.parent_leaf = ws.get<int32_t>("oct.parent_leaf", n);
+    t.parent_node = ws.get<int32_t>("oct.parent_node", n);
+    t.arrive = ws.get<int32_t>("oct.arrive", n);
+    t.meta = ws.get<int32_t>("oct.meta", 4);
+    t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
+    t.bbox_part = ws.get<double>("oct.bbox_part", 6 * (size_t)t.bbox_blocks);
+    t.W = ws.get<double>("oct.W", 1);
+    size_t tb = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n, 0,
+                                               64, ctx->stream));
+    t.sort_tmp_bytes = tb;
+    t.sort_tmp = ws.get<uint8_t>("oct.sort_tmp", tb);
+}
+
+void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
+    hipStream_t st = ctx->stream;
+    const int64_t n = t.n;
+    hipLaunchKernelGGL(bbox3_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
+    hipLaunchKernelGGL(bbox3_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
+    hipLaunchKernelGGL(morton3_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
+    TSNE_LAUNCH_CHECK();
+    size_t tb = t.sort_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n,
+                                               0, 64, st));
+    hipLaunchKernelGGL(gather3, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
+    hipLaunchKernelGGL(dup_count3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc);
+    hipLaunchKernelGGL(karras3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, t.meta, t.nodes,
+                       t.parent_leaf, t.parent_node, t.arrive);
+    const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
+    hipLaunchKernelGGL(bottom_up3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
+                       t.agg, t.parent_leaf, t.parent_node, t.arrive);
+    hipLaunchKernelGGL(set_root3, dim3(1), dim3(1), 0, st, t.meta);
+    TSNE_LAUNCH_CHECK();
+}
+
+// Largest D with 72 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL3: the 2-D bound
+// (bhtree.hip bh_near_dmax) scaled by 12/8 for the larger 3-D cell diagonal
+// (second-order remainder (2 + 8D) r^2 / 2 with r^2 <= 12 h^2 instead of 8 h^2).
+static double oct_near_dmax(double theta) {
+    if (!(theta > 0.0)) return __builtin_inf();
+    double d = std::sqrt(BH_NEAR_TOL3 / (72.0 * theta * theta));
+    while (72.0 * theta * theta * d * d * (1.0 + 8.0 * d) > BH_NEAR_TOL3) d *= 0.99;
+    return d;
+}
+
+void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF, double *dz,
+                   const int64_t *dbounds) {
+    if (s1 <= s0) return;
+    const int64_t waves = ceil_div(s1 - s0, 64);
+    hipLaunchKernelGGL(oct_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
+                       t.meta, theta, oct_near_dmax(theta), s0, s1, dbounds, dF, dz);
+    TSNE_LAUNCH_CHECK();
+}
+
+}  // namespace tsne

@@ -1,0 +1,53 @@
+// octree.hpp -- GPU Barnes-Hut octree for 3-D embeddings (nComponents = 3).
+//
+// The reference supports only 2-D embeddings (Cell.scala:32 requires
+// len == 2).  SURVEY.md section 8f asks for the natural generalisation, which
+// oracle/tsne_oracle.c restates (root Cell(0, 0, 0, W), W = max(dX, dY, dZ),
+// capacity 1, children upper/lower x NW, NE, SW, SE, criterion h / D < theta
+// with D the squared 3-D distance).  The GPU build follows bhtree.hpp's
+// design: Morton keys replaying the cell arithmetic (21 levels x 3 bits), a
+// Karras binary radix tree whose nodes at a level boundary are the octree
+// cells (the rest transparent), and a wave-shared traversal stack.
+#pragma once
+#include "common.hpp"
+
+namespace tsne {
+
+struct __attribute__((aligned(16))) OctNode {
+    double cx, cy, cz;            // centre of mass
+    double h;                     // half width of the cell, < 0 = transparent
+    double hmin;                  // min h over the real cells of the subtree (+inf if none)
+    double rball;                 // all-open ball radius around the centre of mass
+    double bx0, bx1, by0, by1, bz0, bz1;   // bounding box of the subtree's points
+    int32_t cnt;                  // cumSize
+    int32_t left, right;          // >= 0 internal node, < 0 leaf ~sorted index
+    int32_t delta;                // common-prefix bits (63+ = key tie)
+    int32_t first, last;          // leaf range in sorted order
+};
+
+struct OctTree {
+    int64_t n = 0;
+    uint64_t *keys = nullptr, *keys_sorted = nullptr;
+    int32_t *idx = nullptr, *idx_sorted = nullptr;   // sorted position -> original row
+    int32_t *inv = nullptr;                          // original row -> sorted position
+    int32_t *dupc = nullptr;                         // exact duplicates of each sorted point
+    double4 *pos = nullptr;                          // sorted positions (x, y, z, 0)
+    OctNode *nodes = nullptr;
+    double *agg = nullptr;
+    int32_t *parent_leaf = nullptr, *parent_node = nullptr, *arrive = nullptr;
+    int32_t *meta = nullptr;                         // [0] in-root points m, [1] root ref
+    double *bbox_part = nullptr, *W = nullptr;
+    void *sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    int bbox_blocks = 0;
+};
+
+void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n);
+// Octree of all n points of Y (n x 3, device).
+void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta);
+// Repulsion for the sorted queries [s0, s1) (dbounds: device {begin, end}
+// overriding them, nullable): F (n x 3, sorted order) and z written there.
+void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF,
+                   double *dz, const int64_t *dbounds = nullptr);
+
+}  // namespace tsne

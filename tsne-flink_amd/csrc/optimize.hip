@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "bhtree.hpp"
+#include "octree.hpp"
 
 namespace tsne {
 
@@ -58,6 +59,12 @@ struct OptState {
     std::vector<int32_t> loss_written;
     unsigned long long *visits = nullptr;
     BHTree tree;
+    // 3-D embeddings (nComponents = 3, the SURVEY.md 8f octree extension):
+    // C = 3 uses the octree, F3 (npad x 3, sorted order) and attr3 (chunk x 3);
+    // no relabelling, no side stream, equal-count BH slices across ranks.
+    int C = 2;
+    OctTree otree;
+    double *F3 = nullptr, *attr3 = nullptr;
     bool profile = false;
     hipEvent_t ev[6] = {};
     // The attraction sums need only Y and P (not F or Z), so outside loss
@@ -333,6 +340,123 @@ __global__ void relabel_rows(const int32_t *__restrict__ order, const int32_t *_
 }
 
 
+// ---- 3-D (nComponents = 3) optimizer kernels
+// q = 1 / (1 + metric(y_i, y_j)) on 3-D points (TsneHelpers.scala:293)
+template <int MET>
+__device__ __forceinline__ double qterm3(const double *a, const double *b) {
+    double m;
+    if (MET == TSNE_METRIC_COSINE) {
+        double dt = 0.0, na = 0.0, nb = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            dt = __dadd_rn(dt, __dmul_rn(a[k], b[k]));
+            na = __dadd_rn(na, __dmul_rn(a[k], a[k]));
+            nb = __dadd_rn(nb, __dmul_rn(b[k], b[k]));
+        }
+        m = 1.0 - dt / (sqrt(na) * sqrt(nb));
+    } else {
+        double s2 = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            const double d = __dsub_rn(a[k], b[k]);
+            s2 = __dadd_rn(s2, __dmul_rn(d, d));
+        }
+        m = MET == TSNE_METRIC_EUCLIDEAN ? sqrt(s2) : s2;
+    }
+    const double x = 1.0 + m;
+    double r = __builtin_amdgcn_rcp(x);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    return r;
+}
+
+// One wave per row (grid-stride), lanes over the row's entries, then a
+// wave reduction: attr_i = sum_j ex P_ij q_ij (y_i - y_j); LOSS adds the KL
+// terms into one partial per block (TsneHelpers.scala:269-306).
+template <bool LOSS, int MET>
+__global__ __launch_bounds__(256) void attract3(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
+                                                const double *__restrict__ val, int64_t r0, int64_t r1,
+                                                const double *__restrict__ Y, const double *__restrict__ scal,
+                                                double ex, double *__restrict__ attr, double *__restrict__ lpart) {
+    __shared__ double sl[4];
+    const int lane = lane_id();
+    const double Z = LOSS ? scal[0] : 1.0;
+    double lsum = 0.0;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t i = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < r1; i += nw) {
+        const double yi[3] = {Y[3 * i], Y[3 * i + 1], Y[3 * i + 2]};
+        double f[3] = {0.0, 0.0, 0.0};
+        for (int64_t e = row_ptr[i] + lane; e < row_ptr[i + 1]; e += 64) {
+            const int64_t j = col[e];
+            const double yj[3] = {Y[3 * j], Y[3 * j + 1], Y[3 * j + 2]};
+            const double pij = __dmul_rn(val[e], ex);
+            const double q = qterm3<MET>(yi, yj);
+            const double sc = __dmul_rn(pij, q);
+            for (int k = 0; k < 3; ++k) f[k] = __dadd_rn(f[k], __dmul_rn(sc, __dsub_rn(yi[k], yj[k])));
+            if (LOSS) lsum += pij * log(pij / (q / Z));
+        }
+        for (int k = 0; k < 3; ++k) {
+            const double v = wave_sum(f[k]);
+            if (lane == 0) attr[3 * (i - r0) + k] = v;
+        }
+    }
+    if (LOSS) {
+        lsum = wave_sum(lsum);
+        if (lane == 0) sl[threadIdx.x >> 6] = lsum;
+        __syncthreads();
+        if (threadIdx.x == 0) lpart[blockIdx.x] = (sl[0] + sl[1]) + (sl[2] + sl[3]);
+    }
+}
+
+// grad = attr - F / Z, then (MODE 1) updateEmbedding -> Ynew (3 components)
+template <int MODE>
+__global__ __launch_bounds__(256) void combine_update3(int64_t r0, int64_t r1, const double *__restrict__ attr,
+                                                       const int32_t *__restrict__ inv, const double *__restrict__ F,
+                                                       const double *__restrict__ scal, const double *__restrict__ Y,
+                                                       double *__restrict__ grad, double *__restrict__ Ynew,
+                                                       double *__restrict__ upd, double *__restrict__ gains,
+                                                       double min_gain, double mom, double lr) {
+    const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= r1) return;
+    const double Z = scal[0];
+    const int64_t si = inv[i];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const double g = attr[3 * (i - r0) + c] - F[3 * si + c] / Z;
+        const int64_t o = 3 * i + c;
+        if (MODE == 0) { grad[o] = g; continue; }
+        const double u = upd[o], gn0 = gains[o];
+        const double gn = ((g > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain) : jmax(gn0 + 0.2, min_gain);
+        const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g));
+        gains[o] = gn;
+        upd[o] = un;
+        Ynew[o] = __dadd_rn(un, Y[o]);
+    }
+}
+
+// dst[orig[i]] = src[i], c components
+__global__ void scatter_to_user_c(const double *__restrict__ src, const int32_t *__restrict__ orig, int64_t n,
+                                  int32_t c, double *__restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = orig[i];
+    for (int k = 0; k < c; ++k) dst[c * o + k] = src[c * i + k];
+}
+
+static int64_t attract3_blocks(int64_t rows) { return std::max<int64_t>(1, std::min<int64_t>(8192, ceil_div(rows, 4))); }
+
+static int64_t attract3_launch(hipStream_t st, const int64_t *rp, const int32_t *col, const double *val, int64_t r0,
+                               int64_t r1, const double *Y, const double *scal, int metric, double ex, double *attr,
+                               double *lpart, bool loss) {
+    const int64_t blocks = attract3_blocks(r1 - r0);
+    if (r1 <= r0) return 0;
+#define TSNE_A3(L, M) \
+    hipLaunchKernelGGL((attract3<L, M>), dim3(blocks), dim3(256), 0, st, rp, col, val, r0, r1, Y, scal, ex, attr, lpart)
+    if (metric == TSNE_METRIC_EUCLIDEAN) { if (loss) TSNE_A3(true, TSNE_METRIC_EUCLIDEAN); else TSNE_A3(false, TSNE_METRIC_EUCLIDEAN); }
+    else if (metric == TSNE_METRIC_COSINE) { if (loss) TSNE_A3(true, TSNE_METRIC_COSINE); else TSNE_A3(false, TSNE_METRIC_COSINE); }
+    else { if (loss) TSNE_A3(true, TSNE_METRIC_SQEUCLIDEAN); else TSNE_A3(false, TSNE_METRIC_SQEUCLIDEAN); }
+#undef TSNE_A3
+    return blocks;
+}
+
 // Attraction launch: variant (lanes per row x unroll) from TSNE_ATTRACT
 // ("16x4", "32x4", "64x4", "16x8", "32x8", "16x12"); returns the block count
 // (loss partials).
@@ -478,6 +602,41 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     if (h_loss) *h_loss = hs[1];
 }
 
+// 3-D gradient (octree): same contract as gradient_device, Y / grad n x 3.
+void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col, const double *d_P, int64_t n,
+                      const double *dY, int32_t metric, double theta, double exaggeration, double *d_grad,
+                      double *h_sumq, double *h_loss) {
+    TSNE_REQUIRE(n >= 1, "empty embedding");
+    hipStream_t st = ctx->stream;
+    OctTree t;
+    oct_alloc(ctx, t, n);
+    oct_build(ctx, t, dY, theta);
+    double *F = ctx->ws.get<double>("grad3.F", 3 * (size_t)n);
+    double *z = ctx->ws.get<double>("grad.z", n);
+    double *part = ctx->ws.get<double>("grad.part", NPART);
+    double *scal = ctx->ws.get<double>("grad.scal", 4);
+    oct_repulsion(ctx, t, theta, 0, n, F, z);
+    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, z, n, 1, 0, part);
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, part, NPART, scal, 0.0);
+    const bool want_loss = h_loss != nullptr;
+    double *lpart = ctx->ws.get<double>("grad3.lpart", attract3_blocks(n));
+    double *attr = ctx->ws.get<double>("grad3.attr", 3 * (size_t)n);
+    const int64_t blocks = attract3_launch(st, d_row_ptr, d_col, d_P, 0, n, dY, scal, metric, exaggeration, attr,
+                                           lpart, want_loss);
+    hipLaunchKernelGGL(combine_update3<0>, dim3(ceil_div(n, 256)), dim3(256), 0, st, 0, n, attr, t.inv, F, scal, dY,
+                       d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0);
+    TSNE_LAUNCH_CHECK();
+    if (want_loss) {
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, lpart, blocks, 1, 0, part);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, part, NPART, scal + 1, 0.0);
+    }
+    double hs[2] = {0, 0};
+    TSNE_HIP(hipMemcpyAsync(hs, scal, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    if (h_sumq) *h_sumq = hs[0];
+    if (h_loss) *h_loss = hs[1];
+}
+
 // ------------------------------------------------------------ optimizer
 
 void opt_destroy(tsne_ctx *ctx) {
@@ -498,8 +657,8 @@ void opt_destroy(tsne_ctx *ctx) {
 void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, const int32_t *d_col,
                const double *d_P, int64_t n, double *dY, double *dupd, double *dgains) {
     TSNE_REQUIRE(p != nullptr, "params is NULL");
-    if (p->n_components != 2)
-        fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (Cell.contains requires 2-D points)");
+    if (p->n_components != 2 && p->n_components != 3)
+        fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
     TSNE_REQUIRE(n >= 1, "empty embedding");
     TSNE_REQUIRE(p->metric >= 0 && p->metric <= 2, "unknown metric");
     hipStream_t st = ctx->stream;
@@ -507,6 +666,8 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     OptState *s = new OptState();
     ctx->opt = s;
     s->p = *p;
+    s->C = p->n_components;
+    const int C = s->C;
     s->n = n;
     s->chunk = ceil_div(n, ctx->world);
     s->npad = s->chunk * ctx->world;
@@ -525,19 +686,19 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         s->rp[b] = ws.get<int64_t>("opt.rp" + k, n + 1);
         s->col[b] = ws.get<int32_t>("opt.col" + k, nnz + 1);
         s->val[b] = ws.get<double>("opt.val" + k, nnz + 1);
-        s->Y[b] = ws.get<double>("opt.Y" + k, 2 * s->npad);
-        s->upd[b] = ws.get<double>("opt.upd" + k, 2 * s->npad);
-        s->gains[b] = ws.get<double>("opt.gains" + k, 2 * s->npad);
+        s->Y[b] = ws.get<double>("opt.Y" + k, C * s->npad);
+        s->upd[b] = ws.get<double>("opt.upd" + k, C * s->npad);
+        s->gains[b] = ws.get<double>("opt.gains" + k, C * s->npad);
         s->orig[b] = ws.get<int32_t>("opt.orig" + k, n);
     }
     s->cur = 0;
     TSNE_HIP(hipMemcpyAsync(s->rp[0], d_row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
     TSNE_HIP(hipMemcpyAsync(s->col[0], d_col, sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, st));
     TSNE_HIP(hipMemcpyAsync(s->val[0], d_P, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
-    TSNE_HIP(hipMemsetAsync(s->Y[0], 0, sizeof(double) * 2 * s->npad, st));
-    TSNE_HIP(hipMemcpyAsync(s->Y[0], dY, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, st));
-    TSNE_HIP(hipMemcpyAsync(s->upd[0], dupd, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, st));
-    TSNE_HIP(hipMemcpyAsync(s->gains[0], dgains, sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemsetAsync(s->Y[0], 0, sizeof(double) * C * s->npad, st));
+    TSNE_HIP(hipMemcpyAsync(s->Y[0], dY, sizeof(double) * C * n, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->upd[0], dupd, sizeof(double) * C * n, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->gains[0], dgains, sizeof(double) * C * n, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(iota_i32, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->orig[0], n);
     s->rowlen = ws.get<int64_t>("opt.rowlen", n + 1);
     size_t tb = 0;
@@ -545,7 +706,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->scan_tmp_bytes = tb;
     s->scan_tmp = ws.get<uint8_t>("opt.scan_tmp", tb);
 
-    s->Ynew = ws.get<double>("opt.Ynew", 2 * s->npad);
+    s->Ynew = ws.get<double>("opt.Ynew", C * s->npad);
     s->F = ws.get<double2>("opt.F", s->npad);
     s->attr = ws.get<double2>("opt.attr", s->chunk);
     s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
@@ -564,10 +725,18 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
     s->visits = ws.get<unsigned long long>("opt.visits", 10);
-    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * 2 * s->npad, st));
+    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * C * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
-    bh_alloc(ctx, s->tree, n);
+    if (C == 3) {
+        oct_alloc(ctx, s->otree, n);
+        s->F3 = ws.get<double>("opt.F3", 3 * (size_t)s->npad);
+        s->attr3 = ws.get<double>("opt.attr3", 3 * (size_t)s->chunk);
+        s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract3_blocks(s->chunk)));
+        TSNE_HIP(hipMemsetAsync(s->F3, 0, sizeof(double) * 3 * s->npad, st));
+    } else {
+        bh_alloc(ctx, s->tree, n);
+    }
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
     TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
@@ -581,8 +750,9 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
 static void gather_working_set(tsne_ctx *ctx, OptState *s) {
     if (ctx->world == 1) return;
     const int c = s->cur;
-    comm_allgather_bytes(ctx, s->upd[c] + 2 * s->r0, s->upd[c], sizeof(double) * 2 * s->chunk);
-    comm_allgather_bytes(ctx, s->gains[c] + 2 * s->r0, s->gains[c], sizeof(double) * 2 * s->chunk);
+    const int C = s->C;
+    comm_allgather_bytes(ctx, s->upd[c] + C * s->r0, s->upd[c], sizeof(double) * C * s->chunk);
+    comm_allgather_bytes(ctx, s->gains[c] + C * s->r0, s->gains[c], sizeof(double) * C * s->chunk);
 }
 
 // renumber labels into the Morton order of this iteration's tree
@@ -604,10 +774,90 @@ static void relabel(tsne_ctx *ctx, OptState *s) {
     s->cur = b;
 }
 
+// One iteration of the 3-D (octree) optimizer: the opt_step sequence without
+// relabelling or the side stream; BH slices are the equal-count cuts of setup.
+static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
+    hipStream_t st = ctx->stream;
+    const tsne_params &p = s->p;
+    const int32_t T = p.iterations;
+    const int32_t n1 = std::min(T, 20);
+    const int32_t n2 = std::min(T - n1, 81);
+    const double ex = (t <= n1 + n2) ? p.early_exaggeration : 1.0;
+    const double mom = (t <= n1) ? p.initial_momentum : p.final_momentum;
+    const bool want_loss = (t % 10 == 0);
+    const int64_t n = s->n;
+    double *Y = s->Y[0];
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[0], st));
+    oct_build(ctx, s->otree, Y, p.theta);
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
+    if (ctx->world > 1) {
+        TSNE_HIP(hipMemsetAsync(s->F3, 0, sizeof(double) * 3 * n, st));
+        TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * n, st));
+        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z, s->bounds + ctx->rank);
+    } else {
+        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z);
+    }
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
+    if (ctx->world > 1) {
+        comm_allreduce_sum_f64(ctx, s->F3, 3 * (size_t)n);
+        comm_allreduce_sum_f64(ctx, s->z, (size_t)n);
+    }
+    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
+    if (s->profile) {
+        TSNE_HIP(hipEventRecord(s->ev[3], st));
+        TSNE_HIP(hipEventRecord(s->ev_a0, st));
+    }
+    const int64_t blocks = attract3_launch(st, s->rp[0], s->col[0], s->val[0], s->r0, s->r1, Y, s->scal, p.metric,
+                                           ex, s->attr3, s->part, want_loss);
+    if (s->profile) {
+        TSNE_HIP(hipEventRecord(s->ev_a1, st));
+        TSNE_HIP(hipEventRecord(s->ev[4], st));
+    }
+    if (s->r1 > s->r0)
+        hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->r1 - s->r0, 256)), dim3(256), 0, st, s->r0, s->r1,
+                           s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[0], s->gains[0],
+                           p.min_gain, mom, p.learning_rate);
+    TSNE_LAUNCH_CHECK();
+    if (want_loss) {
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
+        if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
+        const int slot = t / 10 - 1;
+        if (slot >= 0 && slot < s->loss_slots) {
+            TSNE_HIP(hipMemcpyAsync(s->loss + slot, s->scal + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
+            s->loss_written[slot] = t;
+        }
+    }
+    if (ctx->world > 1) comm_allgather_bytes(ctx, s->Ynew + 3 * s->r0, s->Ynew, sizeof(double) * 3 * s->chunk);
+    for (int k = 0; k < 3; ++k) {
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 3, k, s->part);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
+    }
+    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, 3, s->scal + 2, Y);
+    TSNE_HIP(hipMemcpyAsync(s->Yu, Y, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st));
+    TSNE_LAUNCH_CHECK();
+    if (s->profile) {
+        TSNE_HIP(hipEventRecord(s->ev[5], st));
+        TSNE_HIP(hipEventSynchronize(s->ev[5]));
+        for (int k = 0; k < 5; ++k) {
+            float ms = 0.f;
+            if (k == 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev_a0, s->ev_a1));
+            else TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+            s->last_ms[k] = ms;
+        }
+        for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
+    }
+}
+
 void opt_step(tsne_ctx *ctx, int32_t t) {
     OptState *s = ctx->opt;
     TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
     TSNE_REQUIRE(t >= 1, "iteration numbers start at 1");
+    if (s->C == 3) {
+        opt_step3(ctx, s, t);
+        return;
+    }
     hipStream_t st = ctx->stream;
     const tsne_params &p = s->p;
     const int32_t T = p.iterations;
@@ -721,9 +971,11 @@ void opt_sync(tsne_ctx *ctx) {
     gather_working_set(ctx, s);
     const int c = s->cur;
     const int64_t n = s->n;
-    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Y[c], s->orig[c], n, s->Yu);
-    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->upd[c], s->orig[c], n, s->updu);
-    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->gains[c], s->orig[c], n,
+    const int C = s->C;
+    hipLaunchKernelGGL(scatter_to_user_c, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Y[c], s->orig[c], n, C, s->Yu);
+    hipLaunchKernelGGL(scatter_to_user_c, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->upd[c], s->orig[c], n, C,
+                       s->updu);
+    hipLaunchKernelGGL(scatter_to_user_c, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->gains[c], s->orig[c], n, C,
                        s->gainsu);
     TSNE_LAUNCH_CHECK();
 }

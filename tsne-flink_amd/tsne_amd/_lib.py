@@ -49,6 +49,7 @@ SIGNATURES = {
     "tsne_pairwise_affinities": (C.c_int, [P, P, P, I64, D, P]),
     "tsne_joint_distribution": (C.c_int, [P, P, P, P, I64, I64, P, P, P, PI64]),
     "tsne_gradient": (C.c_int, [P, P, P, P, I64, P, I32, D, D, P, PD, PD]),
+    "tsne_gradient_c": (C.c_int, [P, P, P, P, I64, I32, P, I32, D, D, P, PD, PD]),
     "tsne_update_embedding": (C.c_int, [P, I64, I32, P, P, P, P, D, D, D]),
     "tsne_center_embedding": (C.c_int, [P, I64, I32, P]),
     "tsne_init_working_set": (C.c_int, [P, I64, I32, U64, P, P, P]),

@@ -113,16 +113,17 @@ class Context:
 
     def gradient(self, row_ptr, col, P, Y, theta, metric="sqeuclidean", exaggeration=1.0,
                  want_loss=False):
-        """TsneHelpers.scala:221-318 -> (grad[n,2], Z, loss or None)."""
+        """TsneHelpers.scala:221-318 -> (grad[n,c], Z, loss or None); c = Y.shape[1]
+        is 2 (quadtree) or 3 (the octree extension, tsne_gradient_c)."""
         Y = _f64(Y)
-        n = Y.shape[0]
-        grad = np.zeros((n, 2))
+        n, c = Y.shape
+        grad = np.zeros((n, c))
         z = C.c_double()
         loss = C.c_double()
-        check(lib().tsne_gradient(self._h, _ptr(np.ascontiguousarray(row_ptr, np.int64)),
-                                  _ptr(np.ascontiguousarray(col, np.int32)), _ptr(_f64(P)), n,
-                                  _ptr(Y), METRICS[metric], theta, exaggeration, _ptr(grad),
-                                  C.byref(z), C.byref(loss) if want_loss else None))
+        check(lib().tsne_gradient_c(self._h, _ptr(np.ascontiguousarray(row_ptr, np.int64)),
+                                    _ptr(np.ascontiguousarray(col, np.int32)), _ptr(_f64(P)), n, c,
+                                    _ptr(Y), METRICS[metric], theta, exaggeration, _ptr(grad),
+                                    C.byref(z), C.byref(loss) if want_loss else None))
         return grad, z.value, (loss.value if want_loss else None)
 
     def updateEmbedding(self, grad, Y, upd, gains, min_gain, momentum, learning_rate):
@@ -151,6 +152,8 @@ class Context:
     def optimize(self, row_ptr, col, P, Y, upd, gains, params):
         """TsneHelpers.scala:396-430, in place; returns {iteration: loss}."""
         n = Y.shape[0]
+        if Y.shape[1] != params.n_components:
+            raise ValueError("Y has %d columns, params.n_components is %d" % (Y.shape[1], params.n_components))
         cap = params.iterations // 10 + 1
         keys = np.zeros(cap, dtype=np.int32)
         vals = np.zeros(cap)
