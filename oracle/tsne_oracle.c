@@ -695,3 +695,41 @@ int oracle_optimize3(const int64_t *row_ptr, const int32_t *col, const double *v
     free(grad);
     return 0;
 }
+
+/* 3-D sharded-path helpers (the 2-D ones above, one more component). */
+int oracle_repulsion3_queries(const double *Y, int64_t n, double theta, const double *Q, int64_t nq,
+                              double *rep, double *zi, int threads) {
+    if (!Y || n < 1 || nq < 0) return -1;
+    otree_t t;
+    build_otree(&t, Y, n);
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 64)
+#endif
+    for (int64_t i = 0; i < nq; ++i)
+        ot_repulsive(&t, 0, Q[3 * i], Q[3 * i + 1], Q[3 * i + 2], theta, rep + 3 * i, zi + i);
+    free(t.v);
+    return 0;
+}
+
+int oracle_attraction3_rows(const int64_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                            const double *Y, int metric, double exaggeration, const double *rep,
+                            double Z, int64_t r0, int64_t r1, double *grad, double *loss) {
+    if (!row_ptr || !Y || r0 < 0 || r1 > n || r0 > r1) return -1;
+    double l = 0.0;
+    for (int64_t i = r0; i < r1; ++i) {
+        double g[3] = {0, 0, 0};
+        const double *yi = Y + 3 * i;
+        for (int64_t e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+            const double *yj = Y + 3 * (int64_t)col[e];
+            double pij = val[e] * exaggeration;
+            double qij = 1.0 / (1.0 + oracle_metric(yi, yj, 3, metric));
+            double s = pij * qij;
+            for (int k = 0; k < 3; ++k) g[k] = g[k] + s * (yi[k] - yj[k]);
+            if (loss) l += pij * log(pij / (qij / Z));
+        }
+        for (int k = 0; k < 3; ++k) grad[3 * (i - r0) + k] = g[k] - rep[3 * i + k] / Z;
+    }
+    if (loss) *loss = l;
+    return 0;
+}

@@ -107,6 +107,11 @@ int oracle_gradient3(const int64_t *row_ptr, const int32_t *col, const double *v
                      int64_t n, const double *Y, int metric, double theta,
                      double exaggeration, double *grad, double *sumq, double *loss,
                      double *rep, double *zi, int threads);
+int oracle_repulsion3_queries(const double *Y, int64_t n, double theta, const double *Q, int64_t nq,
+                              double *rep, double *zi, int threads);
+int oracle_attraction3_rows(const int64_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                            const double *Y, int metric, double exaggeration, const double *rep,
+                            double Z, int64_t r0, int64_t r1, double *grad, double *loss);
 int oracle_optimize3(const int64_t *row_ptr, const int32_t *col, const double *val,
                      int64_t n, double *Y, double *upd, double *gains, int metric,
                      double learning_rate, int32_t iterations, double early_exaggeration,

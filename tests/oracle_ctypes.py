@@ -204,3 +204,30 @@ def optimize3(row_ptr, col, val, Y, upd, gains, metric="sqeuclidean", learning_r
                                 _p(keys, I32), _p(vals, D), C.byref(nl), C.c_int(threads))
     assert rc == 0
     return dict(zip(keys[:nl.value].tolist(), vals[:nl.value].tolist()))
+
+
+def repulsion3_queries(Y, theta, Q, threads=1):
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    Q = np.ascontiguousarray(Q, dtype=np.float64)
+    rep = np.zeros((Q.shape[0], 3))
+    zi = np.zeros(Q.shape[0])
+    rc = lib().oracle_repulsion3_queries(_p(Y, D), I64(Y.shape[0]), D(theta), _p(Q, D), I64(Q.shape[0]),
+                                         _p(rep, D), _p(zi, D), C.c_int(threads))
+    assert rc == 0
+    return rep, zi
+
+
+def attraction3_rows(row_ptr, col, val, Y, rep, Z, r0, r1, metric="sqeuclidean", exaggeration=1.0,
+                     want_loss=False):
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    rep = np.ascontiguousarray(rep, dtype=np.float64)
+    grad = np.zeros((r1 - r0, 3))
+    loss = D(0)
+    rc = lib().oracle_attraction3_rows(_p(np.ascontiguousarray(row_ptr, np.int64), I64),
+                                       _p(np.ascontiguousarray(col, np.int32), I32),
+                                       _p(np.ascontiguousarray(val, np.float64), D), I64(Y.shape[0]),
+                                       _p(Y, D), C.c_int(METRICS[metric]), D(exaggeration), _p(rep, D),
+                                       D(Z), I64(r0), I64(r1), _p(grad, D),
+                                       C.byref(loss) if want_loss else None)
+    assert rc == 0
+    return grad, (loss.value if want_loss else None)

@@ -154,3 +154,78 @@ def test_balance_cuts_rule():
     for r in range(1, 8):
         k = b[r] // 256
         assert pre[k] >= c.sum() * r // 8 > pre[k - 1]
+
+
+def _worker3(rank, world, port, T, out_path):
+    """The 3-D (octree) decomposition of optimize.hip opt_step3: equal-count
+    slices of the sorted order for BH, all-reduced (F, z), rows of P by
+    tsne_shard_rows, all-gathered Y slices, local centring."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root / "tsne-flink_amd"))
+    sys.path.insert(0, str(root / "tests"))
+    import oracle_ctypes as Ow
+    import tsne_amd as TA
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    (rp, col, val), _ = _problem()
+    Y = np.random.default_rng(8).normal(size=(rp.shape[0] - 1, 3)) * 1e-2
+    n = Y.shape[0]
+    r0, r1 = TA.shard_rows(n, world, rank)
+    chunk = -(-n // world)
+    upd, gains = np.zeros_like(Y), np.ones_like(Y)
+    losses = {}
+    for t in range(1, T + 1):
+        ex = 4.0 if t <= 101 else 1.0
+        mom = 0.5 if t <= 20 else 0.8
+        order = np.lexsort((Y[:, 2], Y[:, 1], Y[:, 0]))
+        b0, b1 = min(n, chunk * rank), min(n, chunk * (rank + 1))
+        full = np.zeros((n, 4))
+        if b1 > b0:
+            rep_s, z_s = Ow.repulsion3_queries(Y, 0.5, Y[order[b0:b1]])
+            full[b0:b1, :3] = rep_s
+            full[b0:b1, 3] = z_s
+        ft = torch.from_numpy(full)
+        dist.all_reduce(ft)
+        full = ft.numpy()
+        rep = np.zeros((n, 3))
+        z = np.zeros(n)
+        rep[order] = full[:, :3]
+        z[order] = full[:, 3]
+        Z = z.sum()
+        g, lpart = Ow.attraction3_rows(rp, col, val, Y, rep, Z, r0, r1, exaggeration=ex, want_loss=(t % 10 == 0))
+        Yr, ur, gr = Y[r0:r1].copy(), upd[r0:r1].copy(), gains[r0:r1].copy()
+        Ow.update(np.ascontiguousarray(g), Yr, ur, gr, 0.01, mom, 200.0)
+        upd[r0:r1], gains[r0:r1] = ur, gr
+        ybuf = np.zeros((chunk, 3))
+        ybuf[: r1 - r0] = Yr
+        gy = [torch.zeros(chunk, 3, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(gy, torch.from_numpy(ybuf))
+        Y = np.ascontiguousarray(torch.cat(gy).numpy()[:n])
+        Ow.center(Y)
+        if t % 10 == 0:
+            lt = torch.tensor([lpart], dtype=torch.float64)
+            dist.all_reduce(lt)
+            losses[t] = float(lt.item())
+    if rank == 0:
+        np.savez(out_path, Y=Y, keys=np.array(sorted(losses)), vals=np.array([losses[k] for k in sorted(losses)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_octree_iteration_matches_single_process(tmp_path):
+    T, world = 20, 2
+    out = tmp_path / "sharded3.npz"
+    mp.start_processes(_worker3, args=(world, _free_port(), T, str(out)), nprocs=world,
+                       start_method="spawn", join=True)
+    res = np.load(out)
+    (rp, col, val), _ = _problem()
+    Y = np.random.default_rng(8).normal(size=(rp.shape[0] - 1, 3)) * 1e-2
+    upd, gains = np.zeros_like(Y), np.ones_like(Y)
+    ref = O.optimize3(rp, col, val, Y, upd, gains, learning_rate=200.0, iterations=T, theta=0.5)
+    assert list(res["keys"]) == sorted(ref)
+    for k, v in zip(res["keys"], res["vals"]):
+        assert abs(v - ref[int(k)]) <= 1e-9 * abs(ref[int(k)])
+    assert np.abs(res["Y"] - Y).max() <= 1e-9 * np.abs(Y).max()

@@ -137,14 +137,14 @@ WorkingSet TsneHelpers::initWorkingSet(const std::vector<int32_t> &ids, int32_t 
 std::vector<std::pair<int32_t, std::vector<double>>> TsneHelpers::gradient(const std::vector<Triple> &P,
                                                                          const WorkingSet &ws, int32_t metric,
                                                                          double theta, double exaggeration) {
-    if (ws.n_components != 2) check(TSNE_ERR_UNSUPPORTED);
     Csr c = toCsr(P, &ws.ids);
     const int64_t n = (int64_t)ws.ids.size();
-    std::vector<double> g((size_t)n * 2);
-    check(tsne_gradient(ctx_, c.row_ptr.data(), c.col.data(), c.val.data(), n, ws.y.data(), metric, theta,
-                        exaggeration, g.data(), nullptr, nullptr));
+    const int32_t nc = ws.n_components;   // 2, or 3 for the octree extension
+    std::vector<double> g((size_t)n * (size_t)std::max(nc, 1));
+    check(tsne_gradient_c(ctx_, c.row_ptr.data(), c.col.data(), c.val.data(), n, nc, ws.y.data(), metric, theta,
+                          exaggeration, g.data(), nullptr, nullptr));
     std::vector<std::pair<int32_t, std::vector<double>>> out;
-    for (int64_t i = 0; i < n; ++i) out.push_back({ws.ids[i], {g[2 * i], g[2 * i + 1]}});
+    for (int64_t i = 0; i < n; ++i) out.push_back({ws.ids[i], std::vector<double>(g.begin() + nc * i, g.begin() + nc * (i + 1))});
     return out;
 }
 

@@ -148,12 +148,17 @@ int main(int argc, char **argv) {
                    finalMomentum, theta, &loss);
         std::fprintf(stderr, "[tsne_hip] %ld iterations in %.3f s\n", iterations, now() - t3);
 
-        {   // result.map(x => (x._1, x._2(0), x._2(1))).writeAsCsv (Tsne.scala:86)
+        {   // result.map(x => (x._1, x._2(0), x._2(1))).writeAsCsv (Tsne.scala:86);
+            // the 3-D extension appends the third component
             FILE *f = std::fopen(outputPath.c_str(), "w");
             if (!f) throw std::runtime_error("cannot write " + outputPath);
-            for (size_t r = 0; r < ws.ids.size(); ++r)
-                std::fprintf(f, "%d,%s,%s\n", ws.ids[r], javaDouble(ws.y[2 * r]).c_str(),
-                             javaDouble(ws.y[2 * r + 1]).c_str());
+            const size_t nc = (size_t)ws.n_components;
+            for (size_t r = 0; r < ws.ids.size(); ++r) {
+                std::fprintf(f, "%d", ws.ids[r]);
+                for (size_t k = 0; k < std::min<size_t>(nc, 3); ++k)
+                    std::fprintf(f, ",%s", javaDouble(ws.y[nc * r + k]).c_str());
+                std::fprintf(f, "\n");
+            }
             std::fclose(f);
         }
         std::ofstream lf(lossFile);  // Tsne.scala:99-101
