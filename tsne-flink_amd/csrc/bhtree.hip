@@ -747,13 +747,14 @@ __global__ void build_qrec(const BHNode *__restrict__ nodes, const double2 *__re
 // Traversal kernel (see the comment above).  STATS: per-wave work counters
 // (profiling, and the bucket costs of the multi-GPU balancing); the
 // production instantiation carries none.
-template <int KPOP, bool STATS>
+template <int KPOP, int MODE>   // MODE 0 plain, 1 wave times for bcost only, 2 all counters
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
     int64_t g1, const int64_t *__restrict__ dbounds, int xcd_chunk, double2 *__restrict__ F,
     double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost) {
+    constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
     __shared__ QRec srec[4][KPOP];
@@ -768,6 +769,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const bool valid = s >= s0 && s < s1;
     if (lane == 0) ttask_n[wid] = 0;
     if (__ballot(valid) == 0) return;
+    const long long t_start = COST ? clock64() : 0;
     const int root = meta[1];
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
@@ -905,9 +907,14 @@ __global__ __launch_bounds__(256) void bh_traverse(
         Z[s] = zs;
     }
     if (lane == 0) ttask_n[wid] = ntt;
-    if (STATS && bcost) {   // cost of this wave (in cell-pop units) into its first query's 256-query bucket
+    if (COST && bcost) {   // cost of this wave into its first query's 256-query bucket
+        // MODE 1: the wave's own run time (shader clock / 64; the slices only
+        // move work between ranks, every query's sums are unchanged);
+        // MODE 2: cell pops + tile points / 48
+        const unsigned long long c =
+            MODE == 1 ? ((unsigned long long)(clock64() - t_start) >> 6) + 1 : wpops + wtile / 48 + 4;
         const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
-        if (lane == 0) atomicAdd(&bcost[sf >> 8], wpops + wtile / 48 + 4);
+        if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
     }
     if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
                              // [4] wave-level tile points, [5] lane child evaluations, [6] wave
@@ -1179,9 +1186,11 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
     static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
-    const bool stats = visits != nullptr || bcost != nullptr;
-    auto kern = kp >= 8 ? (stats ? bh_traverse<8, true> : bh_traverse<8, false>)
-                        : (stats ? bh_traverse<4, true> : bh_traverse<4, false>);
+    // counters only when asked for: visits need every counter, the multi-GPU
+    // cost buckets only the wave's pops and tile points
+    const int mode = visits ? 2 : (bcost ? 1 : 0);
+    auto kern = kp >= 8 ? (mode == 2 ? bh_traverse<8, 2> : mode == 1 ? bh_traverse<8, 1> : bh_traverse<8, 0>)
+                        : (mode == 2 ? bh_traverse<4, 2> : mode == 1 ? bh_traverse<4, 1> : bh_traverse<4, 0>);
     const int64_t waves = ceil_div(s1 - s0, 64);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
