@@ -182,9 +182,29 @@ __global__ void morton_keys(const double *__restrict__ Y, int64_t n, const doubl
         keys[i] = key;
         idx[i] = (int32_t)i;
     }
-    // in-root count m: one atomic per wave
-    const uint64_t b = __ballot(in);
-    if (lane_id() == 0 && b) atomicAdd(&meta[0], (int)__popcll(b));
+    (void)meta;   // the in-root count m is read off the sorted keys (count_in_root)
+}
+
+// m = number of in-root points = index of the first OUT_KEY in the sorted
+// keys: a 64-ary search by one wave (4 rounds of one load per lane at 1M),
+// instead of an atomic per wave on one counter (serialised in the L2).
+__global__ void count_in_root(const uint64_t *__restrict__ ks, int64_t n, int32_t *__restrict__ meta) {
+    const int lane = lane_id();
+    int64_t lo = 0, hi = n;   // answer in [lo, hi]
+    while (hi > lo) {
+        const int64_t step = (hi - lo + 63) / 64;
+        const int64_t p = lo + (int64_t)lane * step;   // probe: is ks[p] an out-of-root key?
+        const bool out = p < hi && ks[p] >= OUT_KEY;
+        const uint64_t b = __ballot(out || p >= hi);
+        const int f = b ? __ffsll((long long)b) - 1 : 64;   // first lane whose probe is out (or past hi)
+        // first out-of-root index lies in (lo + (f-1) step, lo + f step]
+        const int64_t nlo = f == 0 ? lo : lo + (int64_t)(f - 1) * step + 1;
+        const int64_t nhi = min(hi, lo + (int64_t)f * step);
+        if (f == 0) { hi = lo; break; }
+        lo = nlo;
+        hi = nhi;
+    }
+    if (lane == 0) meta[0] = (int32_t)lo;
 }
 
 __global__ void gather_sorted(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted,
@@ -423,26 +443,32 @@ __global__ void moment_gate(int32_t *mom_flag, int64_t n) {
     mom_flag[1] = 0;
 }
 
-__global__ void moment_count(const BHNode *__restrict__ nodes, int64_t n, const int32_t *__restrict__ meta,
+__global__ __launch_bounds__(1024) void moment_count(const BHNode *__restrict__ nodes, int64_t n, const int32_t *__restrict__ meta,
                              const int32_t *__restrict__ mom_flag, int32_t *__restrict__ cnt,
                              int32_t *__restrict__ list, int32_t *__restrict__ meta_w) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i > n) return;
     const int m = meta[0];
     int32_t c = 0;
     if (i < m - 1 && mom_flag[0]) {
         const BHNode &nd = nodes[i];
         if (nd.cnt >= MOM_MIN_POINTS && nd.delta < 62) c = (nd.cnt + MOM_CHUNK - 1) / MOM_CHUNK;
     }
-    cnt[i] = c;
-    // append flagged nodes to the list: one atomic per wave
+    if (i <= n) cnt[i] = c;
+    // append flagged nodes to the list: one atomic per 1024-thread block
+    // (list order is immaterial: every node's moments are its own)
+    __shared__ int wcnt[16], wbase[16];
+    const int w = threadIdx.x >> 6;
     const uint64_t bal = __ballot(c > 0);
-    if (bal) {
-        int base = 0;
-        if (lane_id() == 0) base = atomicAdd(&meta_w[2], (int)__popcll(bal));
-        base = __shfl(base, 0, 64);
-        if (c > 0) list[base + __popcll(bal & lanemask_lt())] = (int32_t)i;
+    if (lane_id() == 0) wcnt[w] = (int)__popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { wbase[k] = tot; tot += wcnt[k]; }
+        const int base = tot ? atomicAdd(&meta_w[2], tot) : 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) wbase[k] += base;
     }
+    __syncthreads();
+    if (c > 0) list[wbase[w] + __popcll(bal & lanemask_lt())] = (int32_t)i;
 }
 
 __global__ void moment_fill(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
@@ -1151,6 +1177,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     size_t tb = t.sort_tmp_bytes;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
                                                (int)n, 0, 64, st));
+    hipLaunchKernelGGL(count_in_root, dim3(1), dim3(64), 0, st, t.keys_sorted, n, t.meta);
     hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
     hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc);
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
@@ -1163,7 +1190,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
                        bh_near_dmax(theta), t.qrec);
     // subtree moments for the all-open fast path
     hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag, n);
-    hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_flag,
+    hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 1024)), dim3(1024), 0, st, t.nodes, n, t.meta, t.mom_flag,
                        t.mom_cnt, t.mom_list, t.meta);
     size_t sb = t.scan_tmp_bytes;
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.scan_tmp, sb, t.mom_cnt, t.mom_off, (int)(n + 1), st));

@@ -142,8 +142,26 @@ __global__ void morton3_keys(const double *__restrict__ Y, int64_t n, const doub
         keys[i] = key;
         idx[i] = (int32_t)i;
     }
-    const uint64_t b = __ballot(in);
-    if (lane_id() == 0 && b) atomicAdd(&meta[0], (int)__popcll(b));
+    (void)meta;   // in-root count: count_in_root3 on the sorted keys
+}
+
+// m = index of the first OUT_KEY3 in the sorted keys (64-ary search by one
+// wave; see bhtree.hip count_in_root)
+__global__ void count_in_root3(const uint64_t *__restrict__ ks, int64_t n, int32_t *__restrict__ meta) {
+    const int lane = lane_id();
+    int64_t lo = 0, hi = n;
+    while (hi > lo) {
+        const int64_t step = (hi - lo + 63) / 64;
+        const int64_t p = lo + (int64_t)lane * step;
+        const bool out = p >= hi || ks[p] >= OUT_KEY3;
+        const uint64_t b = __ballot(out);
+        const int f = b ? __ffsll((long long)b) - 1 : 64;
+        if (f == 0) break;
+        const int64_t nlo = lo + (int64_t)(f - 1) * step + 1;
+        hi = min(hi, lo + (int64_t)f * step);
+        lo = nlo;
+    }
+    if (lane == 0) meta[0] = (int32_t)lo;
 }
 
 __global__ void gather3(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted, int64_t n,
@@ -536,6 +554,7 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
     size_t tb = t.sort_tmp_bytes;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n,
                                                0, 64, st));
+    hipLaunchKernelGGL(count_in_root3, dim3(1), dim3(64), 0, st, t.keys_sorted, n, t.meta);
     hipLaunchKernelGGL(gather3, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
     hipLaunchKernelGGL(dup_count3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc);
     hipLaunchKernelGGL(karras3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, t.meta, t.nodes,
