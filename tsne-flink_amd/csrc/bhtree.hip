@@ -975,8 +975,10 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
                                                   int xcd_chunk, int32_t *__restrict__ mom_flag,
                                                   int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
                                                   double2 *__restrict__ F, double *__restrict__ Z,
-                                                  unsigned long long *__restrict__ visits) {
+                                                  unsigned long long *__restrict__ visits, int qmajor, int pack) {
     __shared__ double2 tbuf[4][64];
+    __shared__ uint64_t sbm[4][64];
+    __shared__ int smark[4][64];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
@@ -993,10 +995,71 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
     double fx = 0.0, fy = 0.0, zs = 0.0;
     int nwant = 0, ntask = 0;
     unsigned long long ndense = 0;
+    unsigned long long wt_tasks = 0, wt_dense_pts = 0, wt_momchk = 0;   // wave-level diagnostics
     double2 *buf = tbuf[w];
     const TileTask *mytt = ttask + wid * TILE_CAP;
-    for (int t = 0; t < nt; ++t) {
+    for (int t = 0; t < nt;) {
         const TileTask tt = mytt[t];
+        if (pack && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
+            // Packed round: the run of consecutive small tiles (no moments below
+            // MOM_MIN_POINTS) whose points fit 64 slots is staged as one batch of
+            // (point, tile lane mask) and swept once, each lane taking the points
+            // of its own tiles -- one staging round per <= 64 points instead of
+            // one per tile (tiles average ~9 points in the mid phase).
+            const int ti = t + lane;
+            int c_i = 1 << 20, a_i = 0;
+            uint64_t m_i = 0;
+            if (ti < nt) {
+                const TileTask h = mytt[ti];
+                const int c = h.last - h.first + 1;
+                if (c < MOM_MIN_POINTS) { c_i = c; a_i = h.first; m_i = h.mask; }
+            }
+            int S = c_i;   // inclusive prefix of the counts
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(S, o, 64);
+                if (lane >= o) S += v;
+            }
+            const int mtake = __popcll(__ballot(S <= 64));   // >= 1: tile t itself fits
+            const int total = __shfl(S, mtake - 1, 64);
+            __builtin_amdgcn_wave_barrier();
+            smark[w][lane] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < mtake) smark[w][S - c_i] = lane;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            int own = smark[w][lane];   // slot -> tile: running max of the start markers
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(own, o, 64);
+                if (lane >= o) own = max(own, v);
+            }
+            const int st = __shfl(S - c_i, own, 64), fa = __shfl(a_i, own, 64);
+            const uint64_t mk = __shfl(m_i, own, 64);
+            __builtin_amdgcn_wave_barrier();
+            buf[lane] = lane < total ? pos[fa + lane - st] : make_double2(0.0, 0.0);
+            sbm[w][lane] = lane < total ? mk : 0ull;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            double ux = 0.0, uy = 0.0, uz = 0.0;
+            int nmine = 0;
+            for (int j = 0; j < total; ++j) {
+                const double2 pp = buf[j];
+                if ((sbm[w][j] >> lane) & 1ull) {
+                    pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                    ++nmine;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            fx += ux; fy += uy; zs += uz;
+            ndense += (unsigned long long)nmine;
+            if (visits) { wt_tasks += (unsigned long long)mtake; wt_dense_pts += (unsigned long long)total; }
+            t += mtake;
+            continue;
+        }
+        ++t;
         const int ref = __builtin_amdgcn_readfirstlane(tt.ref);
         const int a = __builtin_amdgcn_readfirstlane(tt.first), b = __builtin_amdgcn_readfirstlane(tt.last);
         const int cnt = __builtin_amdgcn_readfirstlane(tt.pad);
@@ -1013,7 +1076,38 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
             }
         }
         const bool dense = mine && !usem;
-        if (__ballot(dense)) {
+        const uint64_t dm = __ballot(dense);
+        const int kq = __popcll(dm), cnt_t = b - a + 1;
+        if (visits) {
+            ++wt_tasks;
+            if (dm) wt_dense_pts += (unsigned long long)cnt_t;
+            if (cnt >= MOM_MIN_POINTS && (tt.mask != 0)) ++wt_momchk;
+        }
+        if (dm && qmajor && kq * ((cnt_t + 63) / 64 + 6) < cnt_t) {
+            // Few lanes, many points: query-major.  For each dense lane j in
+            // turn, all 64 lanes split the tile's points and a butterfly sum
+            // (fixed order: deterministic) hands lane j its total -- kq passes
+            // of cnt/64 pairs instead of cnt pairs with most lanes masked off.
+            uint64_t rem = dm;
+            while (rem) {
+                const int j = __ffsll((long long)rem) - 1;
+                rem &= rem - 1;
+                const double qjx = __shfl(qx, j, 64), qjy = __shfl(qy, j, 64);
+                double ux = 0.0, uy = 0.0, uz = 0.0;
+                int p = a + lane;
+                for (; p + 64 <= b; p += 128) {
+                    const double2 p0 = pos[p], p1 = pos[p + 64];
+                    pair_force(qjx, qjy, p0.x, p0.y, ux, uy, uz);
+                    pair_force(qjx, qjy, p1.x, p1.y, ux, uy, uz);
+                }
+                if (p <= b) {
+                    const double2 p0 = pos[p];
+                    pair_force(qjx, qjy, p0.x, p0.y, ux, uy, uz);
+                }
+                ux = wave_sum(ux); uy = wave_sum(uy); uz = wave_sum(uz);
+                if (lane == j) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)cnt_t; }
+            }
+        } else if (dm) {
             double2 nxt = make_double2(0.0, 0.0);
             if (a + lane <= b) nxt = pos[a + lane];
             double ux = 0.0, uy = 0.0, uz = 0.0;
@@ -1052,9 +1146,13 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
     }
     const int wwant = wave_sum(nwant);
     if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
-    if (visits) {   // [1] moment evaluations, [2] dense pair terms
+    if (visits) {   // [1] moment evaluations, [2] dense pair terms; [10..12] diagnostics:
+                    // tile tasks, wave-level dense points, tasks with a moment check
         const unsigned long long tm = wave_sum((unsigned long long)ntask), td = wave_sum(ndense);
         if (lane == 0) {
+            atomicAdd(visits + 10, wt_tasks);
+            atomicAdd(visits + 11, wt_dense_pts);
+            atomicAdd(visits + 12, wt_momchk);
             atomicAdd(visits + 1, tm);
             atomicAdd(visits + 2, td);
         }
@@ -1213,6 +1311,10 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
     static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
+    // dense tiles: query-major passes for sparse lane masks (TSNE_TILE_QMAJOR=0: lane-major only)
+    static const int qmajor = [] { const char *e = getenv("TSNE_TILE_QMAJOR"); return e ? atoi(e) : 1; }();
+    // small tiles: packed 64-slot rounds (TSNE_TILE_PACK=0: one round per tile)
+    static const int pack = [] { const char *e = getenv("TSNE_TILE_PACK"); return e ? atoi(e) : 1; }();
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the wave's pops and tile points
     const int mode = visits ? 2 : (bcost ? 1 : 0);
@@ -1224,7 +1326,7 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                        t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dbounds, xcd, dF,
                        dz, visits, bcost);
     hipLaunchKernelGGL(tile_apply, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.ttask, t.ttask_n, s0, s1, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits);
+                       t.ttask, t.ttask_n, s0, s1, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor, pack);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, dbounds, dF, dz);
     TSNE_LAUNCH_CHECK();

@@ -724,7 +724,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 10);
+    s->visits = ws.get<unsigned long long>("opt.visits", 16);
     TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * C * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
     TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
@@ -870,7 +870,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int c = s->cur;
     double *Y = s->Y[c];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 10 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 16 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 0. attraction sums on the side stream (not in loss iterations: the KL
@@ -957,9 +957,13 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
             else TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
-        unsigned long long v[10] = {};
+        unsigned long long v[16] = {};
         TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
         for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
+        static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
+        if (dbg)
+            fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu\n", t,
+                    v[10], v[11], v[12], v[1], v[2]);
     }
 }
 
