@@ -158,6 +158,9 @@ def test_gradient_golden(ctx):
     assert abs(Z - G["denseSumQ"]) <= 1e-9
 
 
+NEAR_TOL = 1e-6   # BH_NEAR_TOL (bhtree.hip): per-cell relative bound of the near-exact tiles
+
+
 def random_problem(n, k, seed):
     X = gmm(n, 10, seed=seed)
     oi, od = O.knn(X, k)
@@ -177,7 +180,7 @@ def test_gradient_matches_oracle(ctx, scale, theta, metric):
     r = O.gradient(rp, col, val, Y, theta, metric, exaggeration=4.0, want_loss=True)
     scale_g = np.abs(r["grad"]).max()
     assert np.abs(g - r["grad"]).max() <= 1e-4 * scale_g
-    assert abs(Z - r["Z"]) <= 1e-7 * r["Z"]   # BH_NEAR_TOL (bhtree.hip)
+    assert abs(Z - r["Z"]) <= NEAR_TOL * r["Z"]
     assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
@@ -191,9 +194,9 @@ def test_gradient_large_near_exact(ctx, n, scale):
     g, Z, loss = ctx.gradient(rp, col, val, Y, 0.5, exaggeration=12.0, want_loss=True)
     r = O.gradient(rp, col, val, Y, 0.5, exaggeration=12.0, want_loss=True)
     assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
-    # near-exact subtrees deviate from the reference by <= BH_NEAR_TOL = 1e-7 (bhtree.hip)
-    assert np.abs(g - r["grad"]).max() <= 1e-6 * np.abs(r["grad"]).max()
-    assert abs(Z - r["Z"]) <= 1e-7 * r["Z"]
+    # near-exact subtrees: each summarised cell within BH_NEAR_TOL of its exact leaf sum
+    assert np.abs(g - r["grad"]).max() <= 10 * NEAR_TOL * np.abs(r["grad"]).max()
+    assert abs(Z - r["Z"]) <= NEAR_TOL * r["Z"]
     if np.isnan(r["loss"]):   # some P_ij underflowed to 0: 0 * ln 0 (TsneHelpers.scala:300)
         assert np.isnan(loss)
     else:
@@ -208,7 +211,7 @@ def test_gradient_points_outside_root_and_duplicates(ctx):
     g, Z, _ = ctx.gradient(rp, col, val, Y, 0.5)
     r = O.gradient(rp, col, val, Y, 0.5)
     assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
-    assert abs(Z - r["Z"]) <= 1e-7 * r["Z"]   # BH_NEAR_TOL (bhtree.hip)
+    assert abs(Z - r["Z"]) <= NEAR_TOL * r["Z"]
 
 
 # ---------------------------------------------------------- update / centre

@@ -58,7 +58,7 @@ constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-14;
 constexpr int MOM_TASKS = 128;  // moment evaluations recorded per query; more -> dense tiles
-constexpr double BH_NEAR_TOL = 1e-7;    // near-exact subtree test (bh_traverse): 1000x below
+constexpr double BH_NEAR_TOL = 1e-6;    // near-exact subtree test (bh_traverse): 100x below
                                         // the north-star 1e-4 gradient tolerance
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
 __host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }
@@ -1260,8 +1260,11 @@ void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int w
 // Largest D for which 48 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL (see bh_traverse).
 double bh_near_dmax(double theta) {
     if (!(theta > 0.0)) return __builtin_inf();   // theta = 0: the reference opens every cell
-    double d = std::sqrt(BH_NEAR_TOL / (48.0 * theta * theta));
-    while (48.0 * theta * theta * d * d * (1.0 + 8.0 * d) > BH_NEAR_TOL) d *= 0.99;
+    // TSNE_BH_NEAR_TOL: experiment override of the tolerance (0 disables the test)
+    static const double tol = [] { const char *e = getenv("TSNE_BH_NEAR_TOL"); return e ? atof(e) : BH_NEAR_TOL; }();
+    if (!(tol > 0.0)) return -1.0;
+    double d = std::sqrt(tol / (48.0 * theta * theta));
+    while (48.0 * theta * theta * d * d * (1.0 + 8.0 * d) > tol) d *= 0.99;
     return d;
 }
 
