@@ -235,6 +235,14 @@ def main():
                      "bytes_per_launch": attr_bytes, "avg_ms": attr_ms},
         "timeline": timeline,
     }
+    # HBM bytes per launch of attract_rows from the committed PMC passes
+    # (profiles/r01_attract_traffic.json, scripts/gpu_pmc_attract.sh), valid for this workload
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_attract_traffic.json")
+    if os.path.exists(tf) and n == 1_000_000 and d == 128 and world == 1:
+        with open(tf) as fh:
+            tj = json.load(fh)
+        out["roofline"]["traffic"] = tj["traffic_bytes"]
+        out["roofline"]["traffic_source"] = tj["source"] + "; " + tj["window"] + "; " + tj["note"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps)
     if rank == 0 and a.locality:

@@ -132,7 +132,8 @@ int main(int argc, char **argv) {
     std::vector<double> Y = load_npy(argv[1], n);
     int nq = argc > 2 ? atoi(argv[2]) : 2048;
     double theta = 0.5;
-    double near_dmax = std::sqrt(1e-7 / (48 * theta * theta));
+    double tol = argc > 3 ? atof(argv[3]) : 1e-6;
+    double near_dmax = std::sqrt(tol / (48 * theta * theta));
     double x0 = 1e300, x1 = -1e300, y0 = 1e300, y1 = -1e300;
     for (long i = 0; i < n; ++i) {
         x0 = std::min(x0, Y[2 * i]); x1 = std::max(x1, Y[2 * i]);
