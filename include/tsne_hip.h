@@ -112,6 +112,16 @@ int tsne_ctx_rank(tsne_ctx *ctx, int32_t *rank, int32_t *world);
 int tsne_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metric,
              int32_t k, int64_t q0, int64_t q1, int32_t *idx_out, double *dist_out);
 
+/* projectKnn (TsneHelpers.scala:93-160, ZOrder.scala:25-42; --knnMethod
+ * project): candidates = the k Z-order neighbours on either side of each
+ * point in the input and in `iterations - 1` shifted copies x + r_s (shifts:
+ * (iterations-1) x d, uniform [0,1) vectors supplied by the caller -- the
+ * reference draws them unseeded), ranked by the exact fp64 metric; idx_out /
+ * dist_out: n x min(k, n-1), ascending by (distance, j).  The Z-order
+ * comparator is the reference's (signed XOR of the raw bit patterns) and is a
+ * total order for nonnegative inputs.  2*k*iterations <= 1024. */
+int tsne_project_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metric, int32_t k,
+                     int32_t iterations, const double *shifts, int32_t *idx_out, double *dist_out);
 /* pairwiseAffinities (TsneHelpers.scala:162-180 + 434-504): per CSR row the
  * beta binary search to entropy ln(perplexity); p_out has the layout of dist. */
 int tsne_pairwise_affinities(tsne_ctx *ctx, const int64_t *row_ptr, const double *dist,
@@ -169,6 +179,8 @@ int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_p
  * They do not synchronise unless a result size must reach the host. */
 int tsne_dev_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric,
                  int32_t k, int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist);
+int tsne_dev_project_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t k,
+                         int32_t iterations, const double *d_shifts, int32_t *d_idx, double *d_dist);
 int tsne_dev_pairwise_affinities(tsne_ctx *ctx, const int64_t *d_row_ptr, const double *d_dist,
                                  int64_t nrows, double perplexity, double *d_p);
 /* Fixed-k conditional rows (row i = entries [i*k, (i+1)*k)), symmetrised into

@@ -733,3 +733,83 @@ int oracle_attraction3_rows(const int64_t *row_ptr, const int32_t *col, const do
     if (loss) *loss = l;
     return 0;
 }
+
+/* ------------------------------------------------------------ projectKnn
+ * Approximate kNN of TsneHelpers.scala:93-160 with ZOrder.scala:25-42:
+ * for the input and for each shifted copy x + r_s (r_s = the caller's
+ * uniform [0,1)^d vectors, `iterations - 1` of them; the reference draws them
+ * unseeded), sort the points by the Z-order comparator and take the k
+ * points on either side of each point as candidates; the union of candidates
+ * is ranked by the exact metric on the ORIGINAL vectors and the k nearest
+ * kept, ordered by (distance, j).  compareByZorder XORs the raw IEEE bit
+ * patterns as SIGNED Java longs (less_msb); it is a total order for
+ * nonnegative inputs, the only case with a defined result (the parity tests
+ * use such data); exact duplicate vectors are ordered by index here. */
+static int z_greater(const double *a, const double *b, int32_t d) {
+    int32_t j = 0;
+    int64_t x = 0;
+    for (int32_t i = 0; i < d; ++i) {
+        int64_t ai, bi;
+        memcpy(&ai, a + i, 8);
+        memcpy(&bi, b + i, 8);
+        int64_t y = ai ^ bi;
+        if ((x < y) && (x < (x ^ y))) { j = i; x = y; }
+    }
+    return a[j] > b[j];
+}
+
+static const double *g_zx;
+static int32_t g_zd;
+static int z_cmp(const void *pa, const void *pb) {
+    int32_t i = *(const int32_t *)pa, j = *(const int32_t *)pb;
+    const double *a = g_zx + (int64_t)i * g_zd, *b = g_zx + (int64_t)j * g_zd;
+    if (z_greater(b, a, g_zd)) return -1;
+    if (z_greater(a, b, g_zd)) return 1;
+    return (i > j) - (i < j);
+}
+
+int oracle_project_knn(const double *X, int64_t n, int32_t d, int metric, int32_t k, int32_t iterations,
+                       const double *shifts, int32_t *idx, double *dist) {
+    if (!X || n < 2 || d < 1 || k < 1 || iterations < 1) return -1;
+    const int32_t kk = (int32_t)(k < n - 1 ? k : n - 1);
+    int32_t S = iterations;
+    int32_t **order = (int32_t **)malloc(sizeof(int32_t *) * S);
+    int32_t **rank = (int32_t **)malloc(sizeof(int32_t *) * S);
+    double *Xs = (double *)malloc(sizeof(double) * (size_t)(n * d));
+    for (int32_t s = 0; s < S; ++s) {
+        for (int64_t i = 0; i < n; ++i)
+            for (int32_t c = 0; c < d; ++c)
+                Xs[i * d + c] = s == 0 ? X[i * d + c] : X[i * d + c] + shifts[(int64_t)(s - 1) * d + c];
+        order[s] = (int32_t *)malloc(sizeof(int32_t) * n);
+        rank[s] = (int32_t *)malloc(sizeof(int32_t) * n);
+        for (int64_t i = 0; i < n; ++i) order[s][i] = (int32_t)i;
+        g_zx = Xs; g_zd = d;
+        qsort(order[s], (size_t)n, sizeof(int32_t), z_cmp);
+        for (int64_t p = 0; p < n; ++p) rank[s][order[s][p]] = (int32_t)p;
+    }
+    free(Xs);
+    int64_t cap = (int64_t)2 * k * S;
+    dj_t *c = (dj_t *)malloc(sizeof(dj_t) * (size_t)cap);
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t m = 0;
+        for (int32_t s = 0; s < S; ++s) {
+            int64_t p = rank[s][i];
+            for (int64_t q = p - k; q <= p + k; ++q) {
+                if (q < 0 || q >= n || q == p) continue;
+                int32_t j = order[s][q];
+                int dup = 0;
+                for (int64_t t = 0; t < m; ++t) if (c[t].j == j) { dup = 1; break; }
+                if (dup) continue;
+                c[m].j = j;
+                c[m].d = oracle_metric(X + i * d, X + (int64_t)j * d, d, metric);
+                ++m;
+            }
+        }
+        qsort(c, (size_t)m, sizeof(dj_t), cmp_dj);
+        for (int32_t t = 0; t < kk; ++t) { idx[i * kk + t] = c[t].j; dist[i * kk + t] = c[t].d; }
+    }
+    free(c);
+    for (int32_t s = 0; s < S; ++s) { free(order[s]); free(rank[s]); }
+    free(order); free(rank);
+    return 0;
+}

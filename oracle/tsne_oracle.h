@@ -107,6 +107,12 @@ int oracle_gradient3(const int64_t *row_ptr, const int32_t *col, const double *v
                      int64_t n, const double *Y, int metric, double theta,
                      double exaggeration, double *grad, double *sumq, double *loss,
                      double *rep, double *zi, int threads);
+/* projectKnn (TsneHelpers.scala:93-160, ZOrder.scala:25-42): Z-order
+ * neighbours of the input and of `iterations - 1` shifted copies (shifts:
+ * (iterations-1) x d, caller-supplied), ranked by the exact metric; idx/dist
+ * n x min(k, n-1), ascending by (d, j).  Defined for nonnegative inputs. */
+int oracle_project_knn(const double *X, int64_t n, int32_t d, int metric, int32_t k, int32_t iterations,
+                       const double *shifts, int32_t *idx, double *dist);
 int oracle_repulsion3_queries(const double *Y, int64_t n, double theta, const double *Q, int64_t nq,
                               double *rep, double *zi, int threads);
 int oracle_attraction3_rows(const int64_t *row_ptr, const int32_t *col, const double *val, int64_t n,

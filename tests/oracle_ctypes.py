@@ -231,3 +231,17 @@ def attraction3_rows(row_ptr, col, val, Y, rep, Z, r0, r1, metric="sqeuclidean",
                                        C.byref(loss) if want_loss else None)
     assert rc == 0
     return grad, (loss.value if want_loss else None)
+
+
+def project_knn(X, k, metric="sqeuclidean", iterations=3, shifts=None):
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    n, d = X.shape
+    kk = min(k, n - 1)
+    idx = np.zeros((n, kk), dtype=np.int32)
+    dist = np.zeros((n, kk))
+    sh = np.ascontiguousarray(np.asarray(shifts, dtype=np.float64).reshape(max(iterations - 1, 0), d)) \
+        if iterations > 1 else None
+    rc = lib().oracle_project_knn(_p(X, D), I64(n), I32(d), C.c_int(METRICS[metric]), I32(k), I32(iterations),
+                                  _p(sh, D), _p(idx, I32), _p(dist, D))
+    assert rc == 0, rc
+    return idx, dist

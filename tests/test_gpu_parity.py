@@ -431,3 +431,19 @@ def test_optimize3_matches_oracle_and_device_path(ctx):
     assert np.array_equal(dY.cpu().numpy(), Yh)
     assert np.array_equal(dg.cpu().numpy(), gh)
     assert ctx.dev_opt_losses() == lh
+
+
+# ------------------------------------------------ projectKnn (--knnMethod project)
+@pytest.mark.parametrize("n,d,k,it,metric", [
+    (3000, 16, 10, 3, "sqeuclidean"), (2000, 40, 30, 4, "euclidean"), (1500, 20, 12, 2, "cosine"),
+    (500, 1, 8, 1, "sqeuclidean"), (60, 5, 90, 3, "sqeuclidean")])
+def test_project_knn_matches_oracle(ctx, n, d, k, it, metric):
+    """GPU Z-order merge sorts + candidate ranking vs the restatement, on
+    nonnegative data (where the reference comparator is a total order)."""
+    rng = np.random.default_rng(n + d)
+    X = np.abs(rng.normal(size=(6, d)))[rng.integers(0, 6, n)] * 2 + rng.random((n, d))
+    sh = rng.random((it - 1, d))
+    gi, gd = ctx.projectKnn(X, k, metric, iterations=it, shifts=sh)
+    oi, od = O.project_knn(X, k, metric, iterations=it, shifts=sh)
+    assert np.array_equal(gi, oi)
+    assert np.array_equal(gd, od)

@@ -1,6 +1,7 @@
 """Host C++ layer (tsne-flink_amd/host): the Tsne.main-compatible CLI and the
-Java formatting used by the output / loss files.  CPU only: no GPU is touched
-(argument errors and --executionPlan return before any device work)."""
+Java formatting used by the output / loss files.  The CPU tests touch no GPU
+(argument errors and --executionPlan return before any device work); the
+gpu-marked test runs the CLI end to end."""
 import subprocess
 from pathlib import Path
 
@@ -176,3 +177,29 @@ def test_coo_reader_parallel_equals_sequential(coo_exe, tmp_path):
     assert _run(coo_exe, p, 1, dim) == want
     assert _run(coo_exe, p, 7, dim) == want
     assert _run(coo_exe, p, 16, dim) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,nc,extra", [("bruteforce", 2, []), ("project", 2, ["--knnIterations", "3"]),
+                                              ("partition", 3, [])])
+def test_cli_end_to_end_on_gpu(tmp_path, method, nc, extra):
+    """Tsne.main's path through the native CLI: COO input -> kNN (brute force,
+    Z-order projections, or the partition alias) -> affinities -> joint ->
+    optimize (2-D quadtree or the 3-D octree) -> `i,y0,y1[,y2]` CSV and the
+    Java HashMap loss file."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    n, d = 400, 8
+    X = np.abs(rng.normal(size=(4, d)))[rng.integers(0, 4, n)] * 3 + rng.random((n, d))
+    lines = [f"{i},{j},{float(X[i, j])!r}" for i in range(n) for j in range(d)]
+    (tmp_path / "in.csv").write_text("\n".join(lines) + "\n")
+    r = run("--input", "in.csv", "--output", "out.csv", "--dimension", str(d), "--knnMethod", method,
+            "--perplexity", "10", "--iterations", "50", "--nComponents", str(nc), "--theta", "0.5",
+            "--loss", "loss.txt", *extra, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    out = (tmp_path / "out.csv").read_text().splitlines()
+    assert len(out) == n and all(len(l.split(",")) == 1 + nc for l in out)
+    Y = np.array([[float(v) for v in l.split(",")[1:]] for l in out])
+    assert np.isfinite(Y).all()
+    loss = (tmp_path / "loss.txt").read_text()
+    assert loss.startswith("{") and "10=" in loss and "50=" in loss

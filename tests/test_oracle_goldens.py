@@ -196,3 +196,31 @@ def test_octree_bh_error_shrinks_with_theta():
         assert abs(r["Z"] - zi.sum()) <= 0.05 * zi.sum()
         err.append(np.abs(r["rep"] - rep).max())
     assert err[0] > err[1] > err[2] and err[2] <= 1e-2 * np.abs(rep).max()
+
+
+# ----------------------------------------------- projectKnn (Z-order candidates)
+def test_project_knn_exact_cases():
+    """Two cases where projectKnn provably equals the exact kNN: 1-D
+    nonnegative data (Z-order = numeric order, so the k nearest lie within k
+    sorted positions on either side) and k >= n-1 (every point a candidate)."""
+    rng = np.random.default_rng(2)
+    X1 = rng.random((300, 1)) * 10
+    pi, pd = O.project_knn(X1, 7, iterations=1)
+    ei, ed = O.knn(X1, 7)
+    assert np.array_equal(pd, ed) and np.array_equal(pi, ei)
+    X2 = rng.random((40, 6))
+    pi, pd = O.project_knn(X2, 45, iterations=2, shifts=rng.random((1, 6)))
+    ei, ed = O.knn(X2, 45)
+    assert np.array_equal(pi, ei) and np.array_equal(pd, ed)
+
+
+def test_project_knn_recall_improves_with_shifts():
+    rng = np.random.default_rng(3)
+    X = np.abs(rng.normal(size=(8, 12)))[rng.integers(0, 8, 1500)] * 3 + rng.random((1500, 12))
+    ei, _ = O.knn(X, 10)
+    rec = []
+    for it in (1, 4):
+        pi, pd = O.project_knn(X, 10, iterations=it, shifts=rng.random((it - 1, 12)))
+        assert (np.diff(pd, axis=1) >= 0).all()
+        rec.append(np.mean([len(set(a) & set(b)) / 10 for a, b in zip(pi, ei)]))
+    assert rec[1] > rec[0] > 0.2, rec

@@ -311,6 +311,34 @@ int tsne_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metri
     });
 }
 
+int tsne_project_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metric, int32_t k,
+                     int32_t iterations, const double *shifts, int32_t *idx_out, double *dist_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(X && idx_out && dist_out && n >= 2 && d >= 1 && iterations >= 1, "bad arguments");
+        TSNE_REQUIRE(iterations == 1 || shifts, "NULL shifts");
+        const int64_t kk = std::min<int64_t>(k, n - 1);
+        double *dX = upload(ctx, "h.X", X, (size_t)(n * d));
+        double *dr = iterations > 1 ? upload(ctx, "h.shifts", shifts, (size_t)(iterations - 1) * d) : nullptr;
+        int32_t *di = ctx->ws.get<int32_t>("h.pidx", (size_t)(n * kk));
+        double *dd = ctx->ws.get<double>("h.pdist", (size_t)(n * kk));
+        project_knn_device(ctx, dX, n, d, metric, k, iterations, dr, di, dd);
+        download(ctx, idx_out, di, (size_t)(n * kk));
+        download(ctx, dist_out, dd, (size_t)(n * kk));
+        sync(ctx);
+    });
+}
+
+int tsne_dev_project_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t k,
+                         int32_t iterations, const double *d_shifts, int32_t *d_idx, double *d_dist) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        project_knn_device(ctx, dX, n, d, metric, k, iterations, d_shifts, d_idx, d_dist);
+    });
+}
+
 int tsne_pairwise_affinities(tsne_ctx *ctx, const int64_t *row_ptr, const double *dist, int64_t nrows,
                              double perplexity, double *p_out) {
     return guard([&] {

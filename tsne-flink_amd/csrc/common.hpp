@@ -115,6 +115,8 @@ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 // ---- stage entry points (device pointers, enqueue on ctx->stream) ----
 void knn_device(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric,
                 int32_t k, int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist);
+void project_knn_device(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t k,
+                        int32_t iterations, const double *d_shifts, int32_t *d_idx, double *d_dist);
 void affinities_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const double *d_dist,
                        int64_t nrows, double perplexity, double *d_p);
 int64_t joint_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,

@@ -2,6 +2,7 @@
 #include "tsne_helpers.hpp"
 
 #include <algorithm>
+#include <random>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -77,6 +78,41 @@ std::vector<Triple> TsneHelpers::kNearestNeighbors(const Vectors &input, int32_t
     std::vector<int32_t> idx((size_t)(n * kk));
     std::vector<double> dist((size_t)(n * kk));
     check(tsne_knn(ctx_, X.data(), n, d, metric, k, 0, n, idx.data(), dist.data()));
+    std::vector<Triple> out;
+    out.reserve(idx.size());
+    for (int64_t r = 0; r < n; ++r)
+        for (int64_t t = 0; t < kk; ++t)
+            out.push_back({ids[r], ids[idx[(size_t)(r * kk + t)]], dist[(size_t)(r * kk + t)]});
+    return out;
+}
+
+// projectKnn (TsneHelpers.scala:93-160): the iterations-1 shift vectors are
+// uniform [0,1)^dimension draws (DenseVector.rand, unseeded in the reference)
+// from a 64-bit Mersenne twister seeded with randomState.
+std::vector<Triple> TsneHelpers::projectKnn(const Vectors &input, int32_t k, int32_t metric, int32_t iterations,
+                                            int64_t randomState) {
+    if (input.size() < 2) return {};
+    const int64_t n = (int64_t)input.size();
+    const int32_t d = (int32_t)input[0].second.size();
+    std::vector<size_t> order(input.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return input[a].first < input[b].first; });
+    std::vector<double> X((size_t)n * d);
+    std::vector<int32_t> ids(n);
+    for (int64_t r = 0; r < n; ++r) {
+        const auto &v = input[order[r]];
+        if ((int32_t)v.second.size() != d) throw std::invalid_argument("vectors of different lengths");
+        ids[r] = v.first;
+        std::memcpy(&X[(size_t)r * d], v.second.data(), sizeof(double) * d);
+    }
+    std::mt19937_64 rng((uint64_t)randomState);
+    std::vector<double> shifts((size_t)std::max(iterations - 1, 0) * d);
+    for (double &v : shifts) v = (double)(rng() >> 11) * 0x1.0p-53;
+    const int64_t kk = std::min<int64_t>(k, n - 1);
+    std::vector<int32_t> idx((size_t)(n * kk));
+    std::vector<double> dist((size_t)(n * kk));
+    check(tsne_project_knn(ctx_, X.data(), n, d, metric, k, iterations, shifts.empty() ? nullptr : shifts.data(),
+                           idx.data(), dist.data()));
     std::vector<Triple> out;
     out.reserve(idx.size());
     for (int64_t r = 0; r < n; ++r)

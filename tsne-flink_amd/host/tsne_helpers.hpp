@@ -49,6 +49,8 @@ class TsneHelpers {
     std::vector<Triple> kNearestNeighbors(const Vectors &input, int32_t k, int32_t metric);
     // TsneHelpers.scala:61-91: same exact result; `blocks` is only a tiling hint
     std::vector<Triple> partitionKnn(const Vectors &input, int32_t k, int32_t metric, int32_t blocks);
+    std::vector<Triple> projectKnn(const Vectors &input, int32_t k, int32_t metric, int32_t iterations,
+                                   int64_t randomState);
     // TsneHelpers.scala:162-180
     std::vector<Triple> pairwiseAffinities(const std::vector<Triple> &knn, double perplexity);
     // TsneHelpers.scala:182-196

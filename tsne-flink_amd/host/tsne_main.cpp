@@ -103,7 +103,7 @@ int main(int argc, char **argv) {
         const std::string lossFile = parameters.get("loss", parameters.get("lossFile", "loss.txt"));
         const std::string knnMethod = parameters.getRequired("knnMethod");
         const int device = (int)parameters.getLong("device", 0);
-        (void)parameters.getLong("knnIterations", 3);
+        const long knnIterations = parameters.getLong("knnIterations", 3);
         (void)parameters.getLong("knnBlocks", 1);
 
         if (getExecutionPlan) {  // Tsne.scala:89-95: write the plan instead of executing
@@ -129,7 +129,7 @@ int main(int argc, char **argv) {
             if (knnMethod == "bruteforce") knn = h.kNearestNeighbors(input, (int32_t)neighbors, metric);
             else if (knnMethod == "partition") knn = h.partitionKnn(input, (int32_t)neighbors, metric, 1);
             else if (knnMethod == "project")
-                throw std::invalid_argument("Knn method 'project' (approximate Z-order kNN) is not part of this build");
+                knn = h.projectKnn(input, (int32_t)neighbors, metric, (int32_t)knnIterations, randomState);
             else throw std::invalid_argument("Knn method '" + metricName + "' not defined");  // Tsne.scala:78
             std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", now() - t1);
         }

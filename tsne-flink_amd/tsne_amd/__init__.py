@@ -7,4 +7,4 @@ if the HIP library or a GPU is missing.
 """
 from ._lib import (METRICS, TsneError, balance_cuts, lib, lib_path, metric_from_name,  # noqa: F401
                    shard_rows)
-from .api import Context, Params  # noqa: F401
+from .api import Context, Params, project_shifts  # noqa: F401

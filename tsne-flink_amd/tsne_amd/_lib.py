@@ -47,6 +47,8 @@ SIGNATURES = {
     "tsne_ctx_rank": (C.c_int, [P, PI32, PI32]),
     "tsne_knn": (C.c_int, [P, P, I64, I32, I32, I32, I64, I64, P, P]),
     "tsne_pairwise_affinities": (C.c_int, [P, P, P, I64, D, P]),
+    "tsne_project_knn": (C.c_int, [P, P, I64, I32, I32, I32, I32, P, P, P]),
+    "tsne_dev_project_knn": (C.c_int, [P, P, I64, I32, I32, I32, I32, P, P, P]),
     "tsne_joint_distribution": (C.c_int, [P, P, P, P, I64, I64, P, P, P, PI64]),
     "tsne_gradient": (C.c_int, [P, P, P, P, I64, P, I32, D, D, P, PD, PD]),
     "tsne_gradient_c": (C.c_int, [P, P, P, P, I64, I32, P, I32, D, D, P, PD, PD]),

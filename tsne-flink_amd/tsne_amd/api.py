@@ -111,6 +111,21 @@ class Context:
                                             _ptr(orp), _ptr(oc), _ptr(ov), C.byref(nnz)))
         return orp, oc[:nnz.value].copy(), ov[:nnz.value].copy()
 
+    def projectKnn(self, X, k, metric="sqeuclidean", iterations=3, shifts=None, seed=0):
+        """TsneHelpers.scala:93-160 (--knnMethod project) -> (idx, dist), n x min(k, n-1).
+        shifts: (iterations-1) x d uniform [0,1) vectors (default: project_shifts(seed))."""
+        X = _f64(X)
+        n, d = X.shape
+        if shifts is None:
+            shifts = project_shifts(iterations, d, seed)
+        shifts = _f64(np.asarray(shifts).reshape(max(iterations - 1, 0), d))
+        kk = min(k, n - 1)
+        idx = np.zeros((n, kk), dtype=np.int32)
+        dist = np.zeros((n, kk))
+        check(lib().tsne_project_knn(self._h, _ptr(X), n, d, METRICS[metric], k, iterations,
+                                     _ptr(shifts) if iterations > 1 else None, _ptr(idx), _ptr(dist)))
+        return idx, dist
+
     def gradient(self, row_ptr, col, P, Y, theta, metric="sqeuclidean", exaggeration=1.0,
                  want_loss=False):
         """TsneHelpers.scala:221-318 -> (grad[n,c], Z, loss or None); c = Y.shape[1]
@@ -207,3 +222,9 @@ class Context:
         cnt = np.zeros(10, dtype=np.int64)
         check(lib().tsne_dev_opt_profile(self._h, enable, _ptr(ms), _ptr(cnt)))
         return ms, cnt.tolist()
+
+
+def project_shifts(iterations, d, seed=0):
+    """The projectKnn shift vectors: iterations-1 rows of uniform [0,1)^d
+    (DenseVector.rand, TsneHelpers.scala:97; seeded here, the reference is not)."""
+    return np.random.default_rng(seed).random((max(iterations - 1, 0), d))
