@@ -289,19 +289,38 @@ constexpr int AGG = 10;   // sx, sy, x0, x1, y0, y1, hmin, cnt, rball, (pad)
 // ball(c_c, R_c) when R_v + |c_v - c_c| <= R_c, hence
 // R_v = min(sqrt(h_v/theta) [real v], R_c - |c_v - c_c| over children c),
 // shrunk by a relative 1e-9 per level for rounding.  Leaves impose nothing.
-__global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
+// Nodes whose leaf range lies inside the workgroup's own BLK leaves (the
+// lowest ~log2(BLK) levels) hand off through LDS: workgroup-scope arrival
+// counters and aggregates, no cache-bypassing HBM round trip per level.  Only
+// a node whose parent spans several workgroups publishes its aggregates to
+// the system-scope array (its parent is combined as before).
+template <int BLK>
+__global__ __launch_bounds__(BLK) void bottom_up(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
                           const double *__restrict__ Wp, double inv_theta, BHNode *nodes, double *agg,
                           const int32_t *__restrict__ parent_leaf,
                           const int32_t *__restrict__ parent_node, int32_t *arrive) {
+    __shared__ double lagg[AGG - 1][BLK];
+    __shared__ int32_t larr[BLK];
     const int m = meta[0];
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int S0 = blockIdx.x * BLK;
+    larr[threadIdx.x] = 0;
+    __syncthreads();
+    const int s = S0 + threadIdx.x;
     if (s >= m || m < 2) return;
     const double W = *Wp;
+    auto in_blk = [&](int q) { return nodes[q].first >= S0 && nodes[q].last < S0 + BLK; };
     int p = parent_leaf[s];
+    bool intra = p >= 0 && in_blk(p);
     while (p >= 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-            return;                                      // first arriver stops
+        if (intra) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (__hip_atomic_fetch_add(&larr[p - S0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                return;                                  // first arriver stops
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+                return;
+        }
         const int32_t l = nodes[p].left, r = nodes[p].right, dl = nodes[p].delta;
         double a[2][7];                                  // sx, sy, x0, x1, y0, y1, hmin
         double c[2], rb[2];
@@ -314,6 +333,12 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
                 a[k][6] = __builtin_inf();
                 c[k] = 1.0;
                 rb[k] = __builtin_inf();
+            } else if (intra) {                          // children of an in-block node are in-block
+                const int o = ch[k] - S0;
+#pragma unroll
+                for (int f = 0; f < 7; ++f) a[k][f] = lagg[f][o];
+                c[k] = lagg[7][o];
+                rb[k] = lagg[8][o];
             } else {
                 const double *g = agg + AGG * (int64_t)ch[k];
 #pragma unroll
@@ -345,10 +370,18 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
             }
         }
         rball = rball > 0.0 ? rball * (1.0 - 1e-9) : 0.0;
-        double *g = agg + AGG * (int64_t)p;
-        st_sys(g + 0, sx); st_sys(g + 1, sy);
-        st_sys(g + 2, x0); st_sys(g + 3, x1); st_sys(g + 4, y0); st_sys(g + 5, y1);
-        st_sys(g + 6, hmin); st_sys(g + 7, cnt); st_sys(g + 8, rball);
+        const bool pintra = par >= 0 && in_blk(par);
+        if (pintra) {
+            const int o = p - S0;
+            lagg[0][o] = sx; lagg[1][o] = sy;
+            lagg[2][o] = x0; lagg[3][o] = x1; lagg[4][o] = y0; lagg[5][o] = y1;
+            lagg[6][o] = hmin; lagg[7][o] = cnt; lagg[8][o] = rball;
+        } else {
+            double *g = agg + AGG * (int64_t)p;
+            st_sys(g + 0, sx); st_sys(g + 1, sy);
+            st_sys(g + 2, x0); st_sys(g + 3, x1); st_sys(g + 4, y0); st_sys(g + 5, y1);
+            st_sys(g + 6, hmin); st_sys(g + 7, cnt); st_sys(g + 8, rball);
+        }
         BHNode &nd = nodes[p];                           // read by the traversal (next launch)
         nd.cx = cx;
         nd.cy = cy;
@@ -358,6 +391,7 @@ __global__ void bottom_up(const double2 *__restrict__ pos, const int32_t *__rest
         nd.rball = rball;
         nd.bx0 = x0; nd.bx1 = x1; nd.by0 = y0; nd.by1 = y1;
         p = par;
+        intra = pintra;
     }
 }
 
@@ -1284,8 +1318,8 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
                        t.nodes, t.parent_leaf, t.parent_node, t.arrive);
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
-    hipLaunchKernelGGL(bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
-                       t.agg, t.parent_leaf, t.parent_node, t.arrive);
+    hipLaunchKernelGGL(bottom_up<1024>, dim3(ceil_div(n, 1024)), dim3(1024), 0, st, t.pos, t.meta, t.W, inv_theta,
+                       t.nodes, t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
     hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, inv_theta,
                        bh_near_dmax(theta), t.qrec);
