@@ -874,10 +874,13 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // 0. attraction sums on the side stream (not in loss iterations: the KL
-    // terms need Z), concurrent with 1-3
+    // terms need Z), concurrent with the BH traversal (TSNE_OVERLAP=tree:
+    // already with the tree build, whose short latency-bound kernels it then
+    // stretches, e.g. morton_keys 15 -> 800 us)
     AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->scal, p.metric, ex, s->attr, s->part};
     const bool overlap = !want_loss;
-    if (overlap) {
+    static const bool with_tree = [] { const char *e = getenv("TSNE_OVERLAP"); return e && std::string(e) == "tree"; }();
+    auto side_attract = [&] {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
         TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
         if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a0, s->side));
@@ -885,9 +888,11 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_LAUNCH_CHECK();
         if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a1, s->side));
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
-    }
+    };
+    if (overlap && with_tree) side_attract();
     // 1. tree
     bh_build(ctx, s->tree, Y, p.theta);
+    if (overlap && !with_tree) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's slice of the Morton-sorted points.  With
     // several ranks the slices are cut by the previous iteration's measured
