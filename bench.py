@@ -229,7 +229,7 @@ def main():
         "knn_mfma_frac_of_peak": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF,
         "affinities_joint_s": t_aff,
         "final_loss": losses.get(max(losses)) if losses else None,
-        "roofline": {"kernel": "attract_rows (CSR attraction, TsneHelpers.scala:269-306)",
+        "roofline": {"kernel": "attract_rows<64,4,LOSS=true> (CSR attraction + KL terms, TsneHelpers.scala:269-306), timed alone in loss iterations; the non-loss launches share the CUs with the BH traversal on a side stream",
                      "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
                      "bytes_per_launch": attr_bytes, "avg_ms": attr_ms},

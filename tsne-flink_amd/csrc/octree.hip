@@ -244,19 +244,34 @@ __device__ __forceinline__ double ld_sys3(const double *p) {
     return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Bottom-up sums / boxes / hmin / rball (bhtree.hip bottom_up, one more axis).
-__global__ void bottom_up3(const double4 *__restrict__ pos, const int32_t *__restrict__ meta,
+// Bottom-up sums / boxes / hmin / rball (bhtree.hip bottom_up, one more axis;
+// the same LDS hand-off for nodes inside the workgroup's BLK leaves).
+template <int BLK>
+__global__ __launch_bounds__(BLK) void bottom_up3(const double4 *__restrict__ pos, const int32_t *__restrict__ meta,
                            const double *__restrict__ Wp, double inv_theta, OctNode *nodes, double *agg,
                            const int32_t *__restrict__ parent_leaf, const int32_t *__restrict__ parent_node,
                            int32_t *arrive) {
+    __shared__ double lagg[AGG3][BLK];
+    __shared__ int32_t larr[BLK];
     const int m = meta[0];
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int S0 = blockIdx.x * BLK;
+    larr[threadIdx.x] = 0;
+    __syncthreads();
+    const int s = S0 + threadIdx.x;
     if (s >= m || m < 2) return;
     const double W = *Wp;
+    auto in_blk = [&](int q) { return nodes[q].first >= S0 && nodes[q].last < S0 + BLK; };
     int p = parent_leaf[s];
+    bool intra = p >= 0 && in_blk(p);
     while (p >= 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+        if (intra) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (__hip_atomic_fetch_add(&larr[p - S0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                return;
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+        }
         const int32_t ch[2] = {nodes[p].left, nodes[p].right};
         const int32_t dl = nodes[p].delta;
         double a[2][10];   // sx, sy, sz, x0, x1, y0, y1, z0, z1, hmin
@@ -270,6 +285,12 @@ __global__ void bottom_up3(const double4 *__restrict__ pos, const int32_t *__res
                 a[k][9] = __builtin_inf();
                 c[k] = 1.0;
                 rb[k] = __builtin_inf();
+            } else if (intra) {
+                const int o = ch[k] - S0;
+#pragma unroll
+                for (int f = 0; f < 10; ++f) a[k][f] = lagg[f][o];
+                c[k] = lagg[10][o];
+                rb[k] = lagg[11][o];
             } else {
                 const double *g = agg + AGG3 * (int64_t)ch[k];
 #pragma unroll
@@ -301,11 +322,20 @@ __global__ void bottom_up3(const double4 *__restrict__ pos, const int32_t *__res
             }
         }
         rball = rball > 0.0 ? rball * (1.0 - 1e-9) : 0.0;
-        double *g = agg + AGG3 * (int64_t)p;
-        st_sys3(g + 0, sx); st_sys3(g + 1, sy); st_sys3(g + 2, sz);
-        st_sys3(g + 3, x0); st_sys3(g + 4, x1); st_sys3(g + 5, y0); st_sys3(g + 6, y1);
-        st_sys3(g + 7, z0); st_sys3(g + 8, z1); st_sys3(g + 9, hmin);
-        st_sys3(g + 10, cnt); st_sys3(g + 11, rball);
+        const bool pintra = par >= 0 && in_blk(par);
+        if (pintra) {
+            const int o = p - S0;
+            lagg[0][o] = sx; lagg[1][o] = sy; lagg[2][o] = sz;
+            lagg[3][o] = x0; lagg[4][o] = x1; lagg[5][o] = y0; lagg[6][o] = y1;
+            lagg[7][o] = z0; lagg[8][o] = z1; lagg[9][o] = hmin;
+            lagg[10][o] = cnt; lagg[11][o] = rball;
+        } else {
+            double *g = agg + AGG3 * (int64_t)p;
+            st_sys3(g + 0, sx); st_sys3(g + 1, sy); st_sys3(g + 2, sz);
+            st_sys3(g + 3, x0); st_sys3(g + 4, x1); st_sys3(g + 5, y0); st_sys3(g + 6, y1);
+            st_sys3(g + 7, z0); st_sys3(g + 8, z1); st_sys3(g + 9, hmin);
+            st_sys3(g + 10, cnt); st_sys3(g + 11, rball);
+        }
         OctNode &nd = nodes[p];
         nd.cx = cx; nd.cy = cy; nd.cz = cz;
         nd.cnt = (int32_t)cnt;
@@ -314,6 +344,7 @@ __global__ void bottom_up3(const double4 *__restrict__ pos, const int32_t *__res
         nd.rball = rball;
         nd.bx0 = x0; nd.bx1 = x1; nd.by0 = y0; nd.by1 = y1; nd.bz0 = z0; nd.bz1 = z1;
         p = par;
+        intra = pintra;
     }
 }
 
@@ -560,7 +591,7 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(karras3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, t.meta, t.nodes,
                        t.parent_leaf, t.parent_node, t.arrive);
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
-    hipLaunchKernelGGL(bottom_up3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
+    hipLaunchKernelGGL(bottom_up3<512>, dim3(ceil_div(n, 512)), dim3(512), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root3, dim3(1), dim3(1), 0, st, t.meta);
     TSNE_LAUNCH_CHECK();

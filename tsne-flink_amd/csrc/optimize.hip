@@ -879,10 +879,21 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // stretches, e.g. morton_keys 15 -> 800 us)
     AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->scal, p.metric, ex, s->attr, s->part};
     const bool overlap = !want_loss;
-    static const bool with_tree = [] { const char *e = getenv("TSNE_OVERLAP"); return e && std::string(e) == "tree"; }();
-    auto side_attract = [&] {
+    // TSNE_OVERLAP=bh: the side launch is issued after the BH launch (same
+    // dependency on the tree), so BH waves are dispatched first and the
+    // attraction fills the slots freed by BH's heavy-wave tail
+    static const int ov_mode = [] {
+        const char *e = getenv("TSNE_OVERLAP");
+        const std::string v = e ? e : "";
+        return v == "tree" ? 0 : v == "bh" ? 2 : 1;
+    }();
+    const bool with_tree = ov_mode == 0;
+    auto side_wait = [&] {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
         TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
+    };
+    auto side_attract = [&] {
+        if (ov_mode != 2) side_wait();
         if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a0, s->side));
         attract_launch(s->side, aa, false);
         TSNE_LAUNCH_CHECK();
@@ -892,7 +903,8 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (overlap && with_tree) side_attract();
     // 1. tree
     bh_build(ctx, s->tree, Y, p.theta);
-    if (overlap && !with_tree) side_attract();
+    if (overlap && ov_mode == 1) side_attract();
+    if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's slice of the Morton-sorted points.  With
     // several ranks the slices are cut by the previous iteration's measured
@@ -908,6 +920,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
+    if (overlap && ov_mode == 2) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. exchange + Z
     if (ctx->world > 1) {
