@@ -531,7 +531,10 @@ static void combine_launch(hipStream_t st, int64_t r0, int64_t r1, const double2
 }
 
 // Upper bound of attract_launch's block count for rows rows.
-static int64_t attract_max_blocks(int64_t rows) { return std::max<int64_t>(1, ceil_div(rows * 64, 256)); }
+// (rounded up to the XCD count like attract_grid's launch)
+static int64_t attract_max_blocks(int64_t rows) {
+    return round_up(std::max<int64_t>(1, ceil_div(rows * 64, 256)), NUM_XCD);
+}
 }  // namespace
 
 // ------------------------------------------------------------ single ops
