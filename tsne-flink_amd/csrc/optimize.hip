@@ -741,7 +741,17 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         bh_alloc(ctx, s->tree, n);
     }
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
-    TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+    {   // side stream (attraction); TSNE_SIDE_PRIO=high|low picks a stream priority
+        const char *e = getenv("TSNE_SIDE_PRIO");
+        const std::string v = e ? e : "";
+        int least = 0, greatest = 0;
+        TSNE_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        if (v == "high" || v == "low")
+            TSNE_HIP(hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, v == "high" ? greatest : least));
+        else
+            TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
+        if (getenv("TSNE_DEBUG_PRIO")) fprintf(stderr, "[prio] range least=%d greatest=%d side=%s\n", least, greatest, v.c_str());
+    }
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_attr, hipEventDisableTiming));
     TSNE_HIP(hipEventCreate(&s->ev_a0));
