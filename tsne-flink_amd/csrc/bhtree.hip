@@ -516,12 +516,18 @@ __global__ void moment_fill(const int32_t *__restrict__ meta, const int32_t *__r
 }
 
 // One wave per item (<= MOM_CHUNK points of one node): lanes accumulate the
-// scaled moments u_x^a u_y^b / (a! b!) in registers, then a fixed shuffle tree.
+// scaled moments u_x^a u_y^b / (a! b!) in registers, then a fixed reduction
+// order: LDSRED transposes 8 moments at a time through a per-wave LDS tile
+// (8 row sums per column + 3 shuffle stages, ~20 instructions per 8 moments)
+// instead of a 6-stage shuffle tree per moment.
+template <bool LDSRED>
 __global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ pos,
                                                     const BHNode *__restrict__ nodes,
                                                     const int32_t *__restrict__ off, int64_t n,
                                                     const int32_t *__restrict__ item,
                                                     double *__restrict__ part) {
+    __shared__ double red[4][64 * 9];
+    double *rw = red[threadIdx.x >> 6];
     const int total = off[n];
     const int lane = lane_id();
     const int nw = gridDim.x * (blockDim.x >> 6);
@@ -552,10 +558,26 @@ __global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ 
                 for (int b = 0; b <= MOM_DEG; ++b)
                     if (a + b <= MOM_DEG) acc[midx(a, b)] = __fma_rn(X[a], Yv[b], acc[midx(a, b)]);
         }
+        if (LDSRED) {
+            const int col = lane & 7, r0 = (lane >> 3) * 8;
 #pragma unroll
-        for (int k = 0; k < MOM_K; ++k) {
-            const double v = wave_sum(acc[k]);
-            if (lane == 0) part[(int64_t)it * MOM_K + k] = v;
+            for (int k0 = 0; k0 < MOM_K; k0 += 8) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rw[lane * 9 + j] = (k0 + j < MOM_K) ? acc[k0 + j] : 0.0;
+                double v = 0.0;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v += rw[(r0 + r) * 9 + col];
+                v += __shfl_xor(v, 8, 64);
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                if (lane < 8 && k0 + lane < MOM_K) part[(int64_t)it * MOM_K + k0 + lane] = v;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < MOM_K; ++k) {
+                const double v = wave_sum(acc[k]);
+                if (lane == 0) part[(int64_t)it * MOM_K + k] = v;
+            }
         }
     }
 }
@@ -1353,8 +1375,13 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
     const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
     hipLaunchKernelGGL(moment_fill, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
                        t.mom_item);
-    hipLaunchKernelGGL(moment_items, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n, t.mom_item,
-                       t.mom_part);
+    static const bool ldsred = [] { const char *e = getenv("TSNE_MOMRED"); return !(e && std::string(e) == "shuffle"); }();
+    if (ldsred)
+        hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n,
+                           t.mom_item, t.mom_part);
+    else
+        hipLaunchKernelGGL(moment_items<false>, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n,
+                           t.mom_item, t.mom_part);
     hipLaunchKernelGGL(moment_reduce, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
                        t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
