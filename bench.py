@@ -3,14 +3,21 @@ sqeuclidean, k = 90, perplexity 30, theta 0.5, 1000 Barnes-Hut iterations).
 
 One "step" = one optimizer iteration t of the reference schedule (tree build +
 BH repulsion + attraction + fused gains/momentum update + centring) of the
-device-resident loop; the embedding, P and all state stay in HBM.  By default
-the timed steps are the WHOLE schedule t = 1..T (T = 1000): per-iteration cost
-varies by >1000x over a run (near-exact O(N^2) BH while the embedding is tiny,
-~2 node visits per point once it has expanded: SURVEY.md section 8a row A15),
-so `value` = T / (time of the full loop) is the honest iterations/s.  Warmup
-iterations run on a snapshot of the initial state, which is restored before
-timing.  Setup (synthetic data, kNN, affinities, symmetrisation, seeded init)
-is timed separately; kNN points/s and end-to-end seconds are reported beside.
+device-resident loop; the embedding, P and all state stay in HBM.
+
+Timeline of a run:
+  setup    synthetic data on the device, kNN, affinities, symmetrisation,
+           seeded init, tsne_dev_opt_setup -- each timed;
+  warmup   W iterations (t = 1..W) on a snapshot of the initial state, with
+           the per-stage profile and BH work counters ON (they describe the
+           first W iterations of the timed window); the snapshot is restored;
+  window   `value`: EXACTLY K iterations t = 1..K timed between barriers +
+           synchronisations (no profiling inside; the attraction kernel's HIP
+           events are recorded on its own stream and read afterwards);
+  rest     the remaining iterations t = K+1..T of the schedule (per-iteration
+           cost varies by >1000x over a run: SURVEY.md 8a row A15), profiled
+           every --trace iterations -> `full_schedule_it_s` = T / (window + rest)
+           and `end_to_end_s` = setup + whole schedule + D2H of Y and the losses.
 
 Multi-GPU: launched by torch.distributed.run, one process per GPU; the
 library's own RCCL communicator carries the per-iteration all-gathers;
@@ -43,8 +50,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=0, help="timed iterations (0 = the whole schedule T)")
-    ap.add_argument("--warmup", type=int, default=3, help="untimed iterations on a restored snapshot")
+    ap.add_argument("--steps", type=int, default=20, help="timed iterations t=1..K (0 = the whole schedule T)")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed, profiled iterations on a restored snapshot")
+    ap.add_argument("--no-rest", action="store_true", help="stop after the timed window (skip t = K+1..T)")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=90)
@@ -54,6 +62,7 @@ def parse():
     ap.add_argument("--trace", type=int, default=50, help="profile every N-th timed iteration (0 = off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
+    ap.add_argument("--cpu-knn-sample", type=int, default=32, help="queries in the CPU baseline kNN sample")
     ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as gpurun_out/Y_t<t>.npy")
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
@@ -84,6 +93,24 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def trace_entry(ctx, t, rows, Y, n):
+    ms_t, vis_t = ctx.dev_opt_profile(0)
+    per_wave = max(1, rows / 64)
+    return {"t": t, "tree_ms": ms_t[0], "bh_ms": ms_t[1], "exchange_ms": ms_t[2],
+            "attract_ms": ms_t[3], "update_ms": ms_t[4],
+            "bh_interactions": vis_t[0],
+            "bh_interactions_per_s": vis_t[0] / (ms_t[1] * 1e-3) if ms_t[1] > 0 else None,
+            "visits_per_point": vis_t[0] / max(1, rows),
+            "moment_evals_per_point": vis_t[1] / max(1, rows),
+            "dense_pairs_per_point": vis_t[2] / max(1, rows),
+            "pops_per_wave": vis_t[3] / per_wave,
+            "tile_points_per_wave": vis_t[4] / per_wave,
+            "lane_utilisation": vis_t[5] / max(1, 64 * vis_t[6]),
+            "heaviest_wave_vs_mean": vis_t[7] / max(1e-9, (vis_t[3] + vis_t[4] / 16) / per_wave),
+            "max_wave_pops": vis_t[8], "max_wave_dense_points": vis_t[9],
+            "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,6 +130,7 @@ def main():
     kk = min(k, n - 1)
     r0, r1 = T.shard_rows(n, world, rank)
     steps = a.steps if a.steps > 0 else a.iterations
+    steps = min(steps, a.iterations)
 
     # ---------------------------------------------------------- setup stages
     X = gmm(n, d, 2, dev)
@@ -113,6 +141,7 @@ def main():
     ctx.dev_knn(X, k, "sqeuclidean", r0, r1, idx, dist)
     sync_barrier(world)
     t_knn = max_over_ranks(time.perf_counter() - t0, world)
+    knn_filter_ms = float(sum(ctx.stage_ms("knn.filter")))
 
     t0 = time.perf_counter()
     rp_local = torch.arange(0, (r1 - r0) * kk + 1, kk, dtype=torch.int64, device=dev)
@@ -139,6 +168,7 @@ def main():
     e0, e1 = int(orp[r0].item()), int(orp[r1].item())      # this rank's rows of P
     sync_barrier(world)
     t_aff = max_over_ranks(time.perf_counter() - t0, world)
+    X_host = X.cpu().numpy() if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
     del X, dist, p
 
     Y = torch.zeros((n, 2), dtype=torch.float64, device=dev)
@@ -148,61 +178,88 @@ def main():
     Y[:n].copy_(torch.from_numpy(Yh))
     snap = (Y.clone(), upd.clone(), gains.clone())
     params = default_params(iterations=a.iterations, theta=a.theta)
-    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)
-
-    # ----------------------------------------------- warmup on a snapshot
-    for t in range(1, a.warmup + 1):
-        ctx.dev_opt_step(t)
-    torch.cuda.synchronize()
-    Y.copy_(snap[0]); upd.copy_(snap[1]); gains.copy_(snap[2])
-    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)   # fresh loss slots
-
-    # ------------------------------------------------------- timed steps
-    timeline = []
-    snap_at = {1, max(1, steps // 10), max(1, steps // 5), max(1, 2 * steps // 5), steps}
-    snaps = {}
     sync_barrier(world)
     t0 = time.perf_counter()
-    t_progress = t0
-    for t in range(1, steps + 1):
-        traced = a.trace and (t % a.trace == 0 or t == 1)
-        if traced:
-            ctx.dev_opt_profile(1)
-        ctx.dev_opt_step(t)
-        if traced:
-            ms_t, vis_t = ctx.dev_opt_profile(0)
-            timeline.append({"t": t, "tree_ms": ms_t[0], "bh_ms": ms_t[1], "exchange_ms": ms_t[2],
-                             "attract_ms": ms_t[3], "centre_ms": ms_t[4],
-                             "visits_per_point": vis_t[0] / max(1, r1 - r0),
-                             "moment_evals_per_point": vis_t[1] / max(1, r1 - r0),
-                             "dense_pairs_per_point": vis_t[2] / max(1, r1 - r0),
-                             "pops_per_wave": vis_t[3] / max(1, (r1 - r0) / 64),
-                             "tile_points_per_wave": vis_t[4] / max(1, (r1 - r0) / 64),
-                             "lane_utilisation": vis_t[5] / max(1, 64 * vis_t[6]),
-                             "heaviest_wave_vs_mean": vis_t[7] / max(1e-9, (vis_t[3] + vis_t[4] / 16) / max(1, (r1 - r0) / 64)),
-                             "max_wave_pops": vis_t[8], "max_wave_dense_points": vis_t[9],
-                             "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()})
-        if rank == 0 and world == 1 and not a.no_cpu_baseline and t in snap_at and traced:
-            snaps[t] = Y[:n].cpu().numpy().copy()
-        if rank == 0 and a.dump_y and t in {int(v) for v in a.dump_y.split(",")}:
-            os.makedirs("gpurun_out", exist_ok=True)
-            np.save(f"gpurun_out/Y_t{t}.npy", Y[:n].cpu().numpy())
-        if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
-            t_progress = time.perf_counter()
-            print(f"[bench] t={t}/{steps} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)
+    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)
     sync_barrier(world)
-    t_loop = max_over_ranks(time.perf_counter() - t0, world)
-    losses = ctx.dev_opt_losses()
+    t_setup = max_over_ranks(time.perf_counter() - t0, world)
 
-    value = steps / t_loop
+    # ------------------------ warmup on a snapshot: profiled (t = 1..W of the window)
+    window_profile = []
+    snap_at = sorted({1, max(1, a.iterations // 10), max(1, a.iterations // 5), max(1, 2 * a.iterations // 5),
+                      a.iterations})
+    snaps = {}
+    want_snaps = rank == 0 and world == 1 and not a.no_cpu_baseline
+    for t in range(1, min(a.warmup, a.iterations) + 1):
+        ctx.dev_opt_profile(1)
+        ctx.dev_opt_step(t)
+        window_profile.append(trace_entry(ctx, t, r1 - r0, Y, n))
+        if want_snaps and t in snap_at:
+            snaps[t] = Y[:n].cpu().numpy().copy()
+    torch.cuda.synchronize()
+    Y.copy_(snap[0]); upd.copy_(snap[1]); gains.copy_(snap[2])
+    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)   # fresh loss slots and kernel logs
+
+    # ------------------------------------------- timed window: t = 1..K, nothing traced
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    for t in range(1, steps + 1):
+        ctx.dev_opt_step(t)
+    sync_barrier(world)
+    t_window = max_over_ranks(time.perf_counter() - t0, world)
+
+    # --------------------------- rest of the schedule: t = K+1..T, profiled every --trace
+    timeline = []
+    t_rest = 0.0
+    if not a.no_rest and steps < a.iterations:
+        sync_barrier(world)
+        t0 = time.perf_counter()
+        t_progress = t0
+        for t in range(steps + 1, a.iterations + 1):
+            traced = a.trace and t % a.trace == 0
+            if traced:
+                ctx.dev_opt_profile(1)
+            ctx.dev_opt_step(t)
+            if traced:
+                timeline.append(trace_entry(ctx, t, r1 - r0, Y, n))
+            if want_snaps and t in snap_at:
+                torch.cuda.synchronize()
+                snaps[t] = Y[:n].cpu().numpy().copy()
+            if rank == 0 and a.dump_y and t in {int(v) for v in a.dump_y.split(",")}:
+                os.makedirs("gpurun_out", exist_ok=True)
+                np.save(f"gpurun_out/Y_t{t}.npy", Y[:n].cpu().numpy())
+            if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
+                t_progress = time.perf_counter()
+                print(f"[bench] t={t}/{a.iterations} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)
+        sync_barrier(world)
+        t_rest = max_over_ranks(time.perf_counter() - t0, world)
+    done = a.iterations if (not a.no_rest) else steps
+    t0 = time.perf_counter()
+    losses = ctx.dev_opt_losses()
+    Y_final = Y[:n].cpu().numpy() if rank == 0 else None
+    t_out = time.perf_counter() - t0
+
+    value = steps / t_window
     # ---- roofline of the HBM-bound gradient kernel attract_rows (stage [3])
     # bytes per launch = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr
     #   + rows*(16 own Y + 16 attr out) + n*16 (gathered Y_j, counted once)
     rows = r1 - r0
     attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 32 + n * 16
-    attr_ms = float(np.median([e["attract_ms"] for e in timeline])) if timeline else None
+    alog = ctx.dev_opt_attract_log()
+    win_alone = [ms for (t, sa, ms) in alog if sa and t <= steps]
+    all_alone = [ms for (t, sa, ms) in alog if sa]
+    win_conc = [ms for (t, sa, ms) in alog if not sa and t <= steps]
+    upd_ms = ctx.stage_ms("opt.update")
+    attr_ms = float(np.mean(win_alone)) if win_alone else (float(np.mean(all_alone)) if all_alone else None)
+    attr_src = ("t <= K (timed window)" if win_alone else "whole schedule (no loss iteration in the window)")
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
     knn_flops = 2.0 * (r1 - r0) * n * d
+    upd_bytes = 128 * rows   # N*C*(5 reads + 3 writes)*8 B, C = 2
+    upd_win = upd_ms[:steps]
+    upd_avg = float(np.mean(upd_win)) if upd_win else None
+    bh_int = [e["bh_interactions"] for e in window_profile + timeline]
+    bh_ms = [e["bh_ms"] for e in window_profile + timeline]
+    t_loop_full = t_window + t_rest
 
     out = {
         "metric": METRIC,
@@ -211,7 +268,7 @@ def main():
         "n_gpus": world,
         "steps": steps,
         "warmup": a.warmup,
-        "ms_per_step": 1e3 * t_loop / steps,
+        "ms_per_step": 1e3 * t_window / steps,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -221,30 +278,53 @@ def main():
                                f"theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}",
                    "n": n, "dim": d, "k": k, "theta": a.theta, "parallelism": f"rows{world}",
                    "nnz_P": int(nnz)},
-        "end_to_end_s": t_knn + t_aff + t_loop,
-        "loop_s": t_loop,
+        "window": f"t=1..{steps} of T={a.iterations}",
+        "full_schedule_it_s": (done / t_loop_full) if done == a.iterations else None,
+        "loop_full_s": t_loop_full if done == a.iterations else None,
+        "end_to_end_s": t_knn + t_aff + t_setup + t_loop_full + t_out,
+        "end_to_end_note": "kNN + affinities + joint + optimizer setup + every iteration run + D2H of Y and losses; "
+                           "input already in HBM (synthetic), CSV/loss-file formatting not included",
         "knn_s": t_knn,
         "knn_pts_per_s": n / t_knn,
-        "knn_mfma_tflops": knn_flops / t_knn / 1e12,
-        "knn_mfma_frac_of_peak": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF,
+        "knn_filter_ms": knn_filter_ms,
+        "knn_mfma_tflops": knn_flops / (knn_filter_ms * 1e-3) / 1e12 if knn_filter_ms > 0 else None,
+        "knn_mfma_frac_of_peak": (knn_flops / (knn_filter_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF) if knn_filter_ms > 0 else None,
+        "knn_mfma_frac_whole_knn": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF,
         "affinities_joint_s": t_aff,
+        "opt_setup_s": t_setup,
         "final_loss": losses.get(max(losses)) if losses else None,
-        "roofline": {"kernel": "attract_rows<64,4,LOSS=true> (CSR attraction + KL terms, TsneHelpers.scala:269-306), timed alone in loss iterations; the non-loss launches share the CUs with the BH traversal on a side stream",
+        "losses_sampled": {str(t): losses[t] for t in sorted(losses) if t in (10, 20, 100, 200, 500, 1000)},
+        "roofline": {"kernel": "attract_rows<64,4,LOSS=true> (CSR attraction + KL terms, TsneHelpers.scala:269-306): "
+                               "mean HIP-event time of its standalone launches (loss iterations t%10==0, alone on "
+                               "the context stream) in " + attr_src,
                      "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
-                     "bytes_per_launch": attr_bytes, "avg_ms": attr_ms},
+                     "bytes_per_launch": attr_bytes, "avg_ms": attr_ms,
+                     "launches": len(win_alone) if win_alone else len(all_alone),
+                     "avg_ms_whole_schedule": float(np.mean(all_alone)) if all_alone else None,
+                     "avg_ms_concurrent_in_window": float(np.mean(win_conc)) if win_conc else None},
+        "update_centre": {"kernels": "combine_update<1> (+ centring mean partials) + mean2_final + center_scatter",
+                          "avg_ms": upd_avg, "bytes_per_iteration": upd_bytes,
+                          "achieved_GBs": upd_bytes / (upd_avg * 1e-3) / 1e9 if upd_avg else None,
+                          "frac": upd_bytes / (upd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if upd_avg else None},
+        "bh_interactions_per_s": (sum(bh_int) / (sum(bh_ms) * 1e-3)) if sum(bh_ms) > 0 else None,
+        "bh_interactions_note": "reference-equivalent node evaluations (device counter) / BH kernel time, over the "
+                                "profiled iterations (warmup t=1..W and every --trace-th of the rest)",
+        "window_profile": window_profile,
         "timeline": timeline,
     }
-    # HBM bytes per launch of attract_rows from the committed PMC passes
-    # (profiles/r01_attract_traffic.json, scripts/gpu_pmc_attract.sh), valid for this workload
-    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_attract_traffic.json")
+    # HBM bytes per standalone launch of attract_rows in the same window, from
+    # committed PMC passes of this command (profiles/r02_attract_traffic.json)
+    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02_attract_traffic.json")
     if os.path.exists(tf) and n == 1_000_000 and d == 128 and world == 1:
         with open(tf) as fh:
             tj = json.load(fh)
-        out["roofline"]["traffic"] = tj["traffic_bytes"]
-        out["roofline"]["traffic_source"] = tj["source"] + "; " + tj["window"] + "; " + tj["note"]
+        key = f"steps{steps}"
+        if key in tj.get("per_window", {}):
+            out["roofline"]["traffic"] = tj["per_window"][key]["traffic_bytes"]
+            out["roofline"]["traffic_source"] = tj["source"] + "; " + tj["per_window"][key]["note"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps)
+        out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps, X_host, (orp, oc, ov))
     if rank == 0 and a.locality:
         locality_report(Y[:n], orp, oc, n)
     if rank == 0:
@@ -274,18 +354,40 @@ def locality_report(Y, rp, col, n):
     print(f"[locality] quantiles 50/75/90/99%: {torch.quantile(sample, qs).tolist()}", file=sys.stderr)
 
 
-def cpu_baseline(snaps, a, n, steps):
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may run on
+    (nproc), capped by OMP_NUM_THREADS where the box sets the CPU share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
+
+
+def cpu_baseline(snaps, a, n, steps, X_host, P_dev):
     """The oracle (C fp64 restatement of the reference, OpenMP) timed on a
-    bounded sample of the same run: at each embedding snapshot taken from the
-    GPU trajectory (t in snaps), the reference quadtree build of all n points
-    + BH repulsion of `cpu_sample` random queries, extrapolated to n queries;
-    the per-iteration cost is held piecewise constant between snapshots and
-    integrated over the timed schedule -> iterations/s."""
+    bounded sample of the same run.  Optimizer: at embedding snapshots taken
+    from the GPU trajectory (t in snaps), the reference quadtree build of all n
+    points + BH repulsion of `cpu_sample` random queries, extrapolated to n
+    queries, plus the attraction + update of a sample of rows extrapolated to
+    n; the per-iteration cost is held piecewise constant between snapshots and
+    integrated over the timed window (`value`) and over the whole schedule.
+    kNN: the reference brute force (oracle_knn, all n candidates) for
+    `cpu_knn_sample` queries, extrapolated to n queries."""
     import oracle_ctypes as O
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     q = min(a.cpu_sample, n)
-    sel = np.random.default_rng(0).choice(n, q, replace=False)
+    rng = np.random.default_rng(0)
+    sel = rng.choice(n, q, replace=False)
     per_t = {}
+    # attraction + update of 20000 rows (one thread), extrapolated
+    rp, col, val = (x.cpu().numpy() for x in P_dev)
+    nr = min(n, 20000)
+    r0 = int(rng.integers(0, n - nr + 1))
+    Ys0 = next(iter(snaps.values())) if snaps else np.zeros((n, 2))
+    t0 = time.perf_counter()
+    g, _ = O.attraction_rows(rp, col, val, Ys0, np.zeros((n, 2)), 1.0, r0, r0 + nr, want_loss=True)
+    O.update(np.ascontiguousarray(g), Ys0[r0:r0 + nr].copy(), np.zeros((nr, 2)), np.ones((nr, 2)), 0.01, 0.8, 1000.0)
+    t_attr = (time.perf_counter() - t0) / nr * n
+    del rp, col, val
     for t, Ys in sorted(snaps.items()):
         print(f"[bench] cpu baseline sample at t={t}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
@@ -294,18 +396,28 @@ def cpu_baseline(snaps, a, n, steps):
         t0 = time.perf_counter()
         O.repulsion_queries(Ys, a.theta, Ys[sel[:1]], threads=1)
         t_build = time.perf_counter() - t0
-        per_t[t] = t_build + max(t_sample - t_build, 1e-9) / q * n
+        per_t[t] = t_build + max(t_sample - t_build, 1e-9) / q * n + t_attr
     ts = sorted(per_t)
-    total = 0.0
-    for it in range(1, steps + 1):
-        nearest = min(ts, key=lambda s: abs(s - it))
-        total += per_t[nearest]
-    return {"value": steps / total, "unit": "iterations/s", "cores": threads, "kind": "port",
-            "per_iteration_s_at": {str(t): per_t[t] for t in ts},
-            "sample": f"oracle (C fp64 reference restatement, OpenMP {threads} threads): at GPU-trajectory "
-                      f"snapshots t={ts}, reference quadtree build of all {n} points + BH repulsion of {q} "
-                      f"random queries extrapolated to {n}; piecewise-constant over t=1..{steps}; "
-                      f"attraction/update excluded (so the CPU figure is optimistic)"}
+
+    def total(t_end):
+        return sum(per_t[min(ts, key=lambda s: abs(s - it))] for it in range(1, t_end + 1))
+
+    out = {"value": steps / total(steps), "unit": "iterations/s", "cores": threads, "kind": "port",
+           "full_schedule_it_s": a.iterations / total(a.iterations),
+           "per_iteration_s_at": {str(t): per_t[t] for t in ts},
+           "sample": f"oracle (C fp64 reference restatement, OpenMP {threads} threads): at GPU-trajectory "
+                     f"snapshots t={ts}, reference quadtree build of all {n} points + BH repulsion of {q} "
+                     f"random queries extrapolated to {n}, + attraction/loss/update of {nr} rows (1 thread) "
+                     f"extrapolated; piecewise-constant over t=1..{steps} (value) and t=1..{a.iterations}"}
+    if X_host is not None:
+        qk = min(a.cpu_knn_sample, n)
+        t0 = time.perf_counter()
+        O.knn(X_host, a.k, "sqeuclidean", q0=0, q1=qk, threads=threads)
+        t_k = time.perf_counter() - t0
+        out["knn_pts_per_s"] = qk / t_k
+        out["knn_sample"] = (f"oracle_knn (exact fp64 brute force over all {n} points, {threads} threads) "
+                             f"for queries 0..{qk - 1}: {t_k:.2f} s -> points/s")
+    return out
 
 
 if __name__ == "__main__":

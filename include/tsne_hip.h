@@ -220,6 +220,20 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
  * wave, [9] most tile points of a wave.
  * enable: 1 on, 0 off, -1 leave unchanged. */
 int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out10);
+/* Kernel time of every attraction launch since tsne_dev_opt_setup (HIP
+ * events on the stream it ran on): its iteration t, standalone = 1 when it
+ * ran alone on the context stream (loss iterations, t % 10 == 0), 0 when on
+ * the side stream concurrently with the BH traversal; ms.  Synchronises on
+ * the recorded events; *count = number of launches (entries beyond cap are
+ * not written). */
+int tsne_dev_opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap,
+                             int32_t *count);
+/* Stage timers of the context (HIP events around the stage's kernels, on
+ * their stream), in ms per interval since the stage was last reset:
+ * "knn.filter" (the fp32-MFMA distance filter launches of the last kNN call),
+ * "opt.attract" (see above), "opt.update" (combine + updateEmbedding +
+ * centerEmbedding + write-back, per iteration).  *count = intervals. */
+int tsne_ctx_stage_ms(tsne_ctx *ctx, const char *stage, double *ms_out, int32_t cap, int32_t *count);
 
 #ifdef __cplusplus
 }

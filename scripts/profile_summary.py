@@ -1,0 +1,110 @@
+"""Summarise a scripts/gpu_check.sh run (gpurun_out/) into profiles/:
+
+  <tag>_rocprof_kernel_stats.csv     rocprofv3 --stats of `bench.py --steps K --warmup W` (whole schedule)
+  <tag>_attract_dispatches.json      attract_rows<..., LOSS=true> dispatch durations from the kernel trace,
+                                     mapped to iterations (the k-th standalone launch after the warmup's is
+                                     t = 10 k), averaged over the timed window t <= K and the whole schedule
+  r02_attract_traffic.json           FETCH_SIZE / WRITE_SIZE per standalone launch in the window
+                                     (separate PMC passes of `bench.py --no-rest`), corrected by the
+                                     calibration run (scripts/pmc_calib.hip)
+
+usage: python scripts/profile_summary.py <tag> [--steps K] [--warmup W]
+"""
+import argparse
+import csv
+import json
+import shutil
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+OUT = ROOT / "gpurun_out"
+PROF = ROOT / "profiles"
+
+
+def rows(p):
+    with open(p) as fh:
+        return list(csv.DictReader(fh))
+
+
+def loss_dispatches(trace_rows):
+    """Dispatches of the standalone (LOSS=true) attraction kernel, in dispatch order."""
+    sel = [r for r in trace_rows if "attract_rows<" in r["Kernel_Name"] and ", true," in r["Kernel_Name"]]
+    return sorted(sel, key=lambda r: int(r["Dispatch_Id"]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    a = ap.parse_args()
+    K, W = a.steps, a.warmup
+    warm_loss = W // 10          # loss iterations inside the warmup (t = 10, 20, ... <= W)
+
+    shutil.copy(OUT / "prof" / "prof_kernel_stats.csv", PROF / f"{a.tag}_rocprof_kernel_stats.csv")
+    tr = rows(OUT / "prof" / "prof_kernel_trace.csv")
+    ld = loss_dispatches(tr)[warm_loss:]
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in ld]
+    its = [10 * (k + 1) for k in range(len(durs))]
+    win = [d for t, d in zip(its, durs) if t <= K]
+    summary = {
+        "source": "rocprofv3 --kernel-trace --stats -- python bench.py --steps %d --warmup %d --no-cpu-baseline "
+                  "(scripts/gpu_check.sh); dispatches of attract_rows<64,4,true,0> after the warmup's" % (K, W),
+        "launches": len(durs),
+        "per_launch_ms": dict(zip(map(str, its), durs)),
+        "avg_ms_window": sum(win) / len(win) if win else None,
+        "avg_ms_whole_schedule": sum(durs) / len(durs) if durs else None,
+    }
+    (PROF / f"{a.tag}_attract_dispatches.json").write_text(json.dumps(summary, indent=1) + "\n")
+
+    # PMC: per standalone launch in the window (bench.py --no-rest: the window's launches only)
+    def per_launch(kind, counter):
+        rs = [r for r in rows(OUT / kind / "pmc_counter_collection.csv")
+              if ", true," in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        rs.sort(key=lambda r: int(r["Dispatch_Id"]))
+        return [float(r["Counter_Value"]) * 1024.0 for r in rs[warm_loss:]]   # KiB -> bytes
+    fetch = per_launch("pmc_fetch", "FETCH_SIZE")
+    write = per_launch("pmc_write", "WRITE_SIZE")
+    # calibration: FETCH_SIZE of known-byte streams and gathers
+    cal = {}
+    calp = OUT / "pmc_calib_fetch" / "pmc_counter_collection.csv"
+    if calp.exists():
+        known = 512 * 2 ** 20
+        for r in rows(calp):
+            k = r["Kernel_Name"]
+            v = float(r["Counter_Value"]) * 1024.0
+            if "read_stream<int>" in k:
+                cal.setdefault("stream_4B_per_lane", []).append(v / known)
+            elif "read_stream<double>" in k:
+                cal.setdefault("stream_8B_per_lane", []).append(v / known)
+            elif "read_stream<HIP_vector_type" in k:
+                cal.setdefault("stream_16B_per_lane", []).append(v / known)
+            elif "gather16" in k:
+                cal.setdefault("gather_16B_bytes_per_gather", []).append(v / (64 * 2 ** 20))
+        cal = {k: sum(v) / len(v) for k, v in cal.items()}
+    corr = 2.0   # every streaming width reports 1/2 of its bytes (calibration above)
+    tf = PROF / "r02_attract_traffic.json"
+    tj = json.loads(tf.read_text()) if tf.exists() else {}
+    tj.update({
+        "kernel": "attract_rows<64,4,LOSS=true>",
+        "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) -- python bench.py --steps K "
+                  "--warmup W --no-rest --no-cpu-baseline --trace 0 (scripts/gpu_check.sh)",
+        "unit": "bytes per launch",
+        "calibration": {"FETCH_SIZE_reported_over_known": cal,
+                        "note": "scripts/pmc_calib.hip: 512 MiB streams of 4/8/16-B-per-lane loads each report "
+                                "exactly 1/2 of their bytes (the guide's x2 holds for every width here); a random "
+                                "16-B gather from a 16 MiB table reports ~48 B, i.e. ~97 B of fabric traffic per "
+                                "gather after the x2 (a line per gather: the table misses the 4 MiB L2)"},
+    })
+    tj.setdefault("per_window", {})[f"steps{K}"] = {
+        "fetch_bytes_raw": fetch, "write_bytes": write,
+        "traffic_bytes": (corr * sum(fetch) / len(fetch) + sum(write) / len(write)) if fetch and write else None,
+        "note": f"window t=1..{K} (standalone launches t=10..{10 * len(fetch)}), FETCH_SIZE x2 (calibrated) + WRITE_SIZE",
+    }
+    tf.write_text(json.dumps(tj, indent=1) + "\n")
+    print(json.dumps(summary, indent=1))
+    print(json.dumps(tj["per_window"], indent=1))
+
+
+if __name__ == "__main__":
+    main()

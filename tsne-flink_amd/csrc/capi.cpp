@@ -158,6 +158,7 @@ int tsne_ctx_destroy(tsne_ctx *ctx) {
         (void)hipStreamSynchronize(ctx->stream);
         opt_destroy(ctx);
         comm_destroy(ctx);
+        ctx->timers.clear();
         ctx->ws.clear();
         if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     });
@@ -279,6 +280,27 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
         DeviceGuard g(ctx->device);
         int32_t k = opt_losses(ctx, loss_keys, loss_vals, cap);
         if (n_loss) *n_loss = k;
+    });
+}
+
+int tsne_ctx_stage_ms(tsne_ctx *ctx, const char *stage, double *ms_out, int32_t cap, int32_t *count) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(stage != nullptr, "stage is NULL");
+        const std::vector<double> v = ctx->timers.ms(stage);
+        for (size_t k = 0; k < v.size() && (int64_t)k < cap; ++k) ms_out[k] = v[k];
+        if (count) *count = (int32_t)v.size();
+    });
+}
+
+int tsne_dev_opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap,
+                             int32_t *count) {
+    return guard([&] {
+        check_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        int32_t k = opt_attract_log(ctx, iters, standalone, ms, cap);
+        if (count) *count = k;
     });
 }
 

@@ -77,7 +77,60 @@ struct Workspace {
     void clear() { bufs.clear(); }
 };
 
-struct Comm;      // RCCL communicator (comm.cpp)
+// Named kernel-stage timers: HIP event pairs recorded on the stream the
+// stage's kernels run on, read (and synchronised) only when asked for, so a
+// timed loop never waits on them.  Events are pooled and reused.
+struct StageTimers {
+    std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> rec;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t take() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventCreate failed");
+        return e;
+    }
+    void reset(const std::string &name) {
+        auto it = rec.find(name);
+        if (it == rec.end()) return;
+        for (auto &p : it->second) { pool.push_back(p.first); pool.push_back(p.second); }
+        it->second.clear();
+    }
+    // begin(): returns the index of the new interval; end() closes the last one.
+    size_t begin(const std::string &name, hipStream_t st) {
+        auto &v = rec[name];
+        v.push_back({take(), take()});
+        if (hipEventRecord(v.back().first, st) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventRecord failed");
+        return v.size() - 1;
+    }
+    void end(const std::string &name, hipStream_t st) {
+        auto &v = rec[name];
+        if (v.empty()) fail(TSNE_ERR_HIP, "stage timer " + name + " not started");
+        if (hipEventRecord(v.back().second, st) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventRecord failed");
+    }
+    // elapsed ms of every interval of `name` (synchronises on their events)
+    std::vector<double> ms(const std::string &name) {
+        std::vector<double> out;
+        auto it = rec.find(name);
+        if (it == rec.end()) return out;
+        for (auto &p : it->second) {
+            if (hipEventSynchronize(p.second) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventSynchronize failed");
+            float f = 0.f;
+            if (hipEventElapsedTime(&f, p.first, p.second) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventElapsedTime failed");
+            out.push_back(f);
+        }
+        return out;
+    }
+    void clear() {
+        for (auto &kv : rec)
+            for (auto &p : kv.second) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+        rec.clear();
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+        pool.clear();
+    }
+    ~StageTimers() { clear(); }
+};
+
+struct Comm;      // collective backend: RCCL or in-process loopback (comm.cpp)
 struct OptState;  // device-resident optimizer state (optimize.hip)
 
 }  // namespace tsne
@@ -90,6 +143,7 @@ struct tsne_ctx {
     tsne::Comm *comm = nullptr;
     tsne::Workspace ws;
     tsne::OptState *opt = nullptr;
+    tsne::StageTimers timers;
     int cu_count = 256;
 };
 
@@ -144,6 +198,7 @@ void opt_step(tsne_ctx *ctx, int32_t t);
 void opt_sync(tsne_ctx *ctx);
 int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap);
 void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits);
+int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap);
 void opt_destroy(tsne_ctx *ctx);
 
 // comm.cpp

@@ -488,9 +488,14 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     int64_t s0 = round_up(std::max<int64_t>(kk + 1, 256), TC);
     s0 = std::min<int64_t>(std::min<int64_t>(s0, CAP), n);
     hipLaunchKernelGGL(fill_i32, dim3(ceil_div(nq, 256)), dim3(256), 0, st, cnt, nq, (int32_t)s0);
+    // "knn.filter": the MFMA filter launches alone (their sum is the kNN's
+    // dense-contraction time, tsne_ctx_stage_ms)
+    ctx->timers.reset("knn.filter");
+    ctx->timers.begin("knn.filter", st);
     hipLaunchKernelGGL(knn_filter<0>, dim3(ceil_div(s0, TC), qtiles), dim3(256), 0, st, X32, norm32,
                        dpad, q0, q1, (int64_t)0, s0, dot_scale, tau, cnt, cand_d, cand_j, flags,
                        (int32_t)CAP);
+    ctx->timers.end("knn.filter", st);
     TSNE_LAUNCH_CHECK();
     auto compact = [&]() {
         hipLaunchKernelGGL(knn_compact<CAP>, dim3(ceil_div(nq, 4)), dim3(256), 0, st, nq, kk, norm32,
@@ -501,9 +506,11 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     int64_t seen = s0;
     while (seen < n) {
         int64_t r = std::min<int64_t>(seen, n - seen);
+        ctx->timers.begin("knn.filter", st);
         hipLaunchKernelGGL(knn_filter<1>, dim3(ceil_div(r, TC), qtiles), dim3(256), 0, st, X32,
                            norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d,
                            cand_j, flags, (int32_t)CAP);
+        ctx->timers.end("knn.filter", st);
         TSNE_LAUNCH_CHECK();
         compact();
         seen += r;

@@ -71,7 +71,12 @@ struct OptState {
     // iterations they run on a second stream concurrently with the tree
     // build and the BH traversal (latency-bound kernels that leave CUs idle).
     hipStream_t side = nullptr;
-    hipEvent_t ev_y = nullptr, ev_attr = nullptr, ev_a0 = nullptr, ev_a1 = nullptr;
+    hipEvent_t ev_y = nullptr, ev_attr = nullptr;
+    // per launch of the attraction kernel (ctx->timers "opt.attract"): its
+    // iteration and whether it ran alone on the main stream (loss iterations)
+    // or on the side stream concurrently with the BH traversal
+    std::vector<std::pair<int32_t, int32_t>> attract_iter;
+    double *mpart = nullptr;  // centring mean: block partials of combine_update
     double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits[10] = {};
 };
@@ -219,34 +224,83 @@ __global__ __launch_bounds__(256) void attract_rows(
 // grad = attr - F / Z (TsneHelpers.scala:311-317); MODE 0 writes it, MODE 1
 // applies updateEmbedding (TsneHelpers.scala:341-369) -> Ynew.  One thread
 // per row, all accesses coalesced except F[inv[i]] (near-identity gather).
+// With `mpart` (MODE 1) each block also writes the sum of its rows' Ynew
+// (x, y) to mpart[2 * block]: the centring mean's partials, fused into the
+// update so that centerEmbedding costs one more pass (center_scatter).
 template <int MODE>
 __global__ __launch_bounds__(256) void combine_update(
     int64_t r0, int64_t r1, const double2 *__restrict__ attr, const int32_t *__restrict__ inv,
     const double2 *__restrict__ F, const double *__restrict__ scal, const double *__restrict__ Y,
     double *__restrict__ grad, double *__restrict__ Ynew, double *__restrict__ upd, double *__restrict__ gains,
-    double min_gain, double mom, double lr) {
+    double min_gain, double mom, double lr, double *__restrict__ mpart) {
+    __shared__ double sm[2][4];
     const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= r1) return;
-    const double Z = scal[0];
-    const double2 at = attr[i - r0];
-    const double2 f = F[inv[i]];
-    const double gx = at.x - f.x / Z, gy = at.y - f.y / Z;  // attrForce - repForce / sumQ
-    if (MODE == 0) {
-        grad[2 * i] = gx;
-        grad[2 * i + 1] = gy;
-        return;
-    }
-    const double g[2] = {gx, gy};
+    const bool live = i < r1;
+    double yn[2] = {0.0, 0.0};
+    if (live) {
+        const double Z = scal[0];
+        const double2 at = attr[i - r0];
+        const double2 f = F[inv[i]];
+        const double gx = at.x - f.x / Z, gy = at.y - f.y / Z;  // attrForce - repForce / sumQ
+        if (MODE == 0) {
+            grad[2 * i] = gx;
+            grad[2 * i + 1] = gy;
+        } else {
+            const double g[2] = {gx, gy};
+            const double2 u2 = *reinterpret_cast<const double2 *>(upd + 2 * i);
+            const double2 g2 = *reinterpret_cast<const double2 *>(gains + 2 * i);
+            const double2 y2 = *reinterpret_cast<const double2 *>(Y + 2 * i);
+            const double uu[2] = {u2.x, u2.y}, gg[2] = {g2.x, g2.y}, yy[2] = {y2.x, y2.y};
+            double un[2], gn[2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const int64_t o = 2 * i + c;
-        const double u = upd[o], gn0 = gains[o];
-        const double gn = ((g[c] > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain) : jmax(gn0 + 0.2, min_gain);
-        const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g[c]));
-        gains[o] = gn;
-        upd[o] = un;
-        Ynew[o] = __dadd_rn(un, Y[o]);
+            for (int c = 0; c < 2; ++c) {
+                gn[c] = ((g[c] > 0.0) == (uu[c] > 0.0)) ? jmax(gg[c] * 0.8, min_gain) : jmax(gg[c] + 0.2, min_gain);
+                un[c] = __dsub_rn(__dmul_rn(mom, uu[c]), __dmul_rn(__dmul_rn(lr, gn[c]), g[c]));
+                yn[c] = __dadd_rn(un[c], yy[c]);
+            }
+            *reinterpret_cast<double2 *>(gains + 2 * i) = make_double2(gn[0], gn[1]);
+            *reinterpret_cast<double2 *>(upd + 2 * i) = make_double2(un[0], un[1]);
+            *reinterpret_cast<double2 *>(Ynew + 2 * i) = make_double2(yn[0], yn[1]);
+        }
     }
+    if (MODE == 1 && mpart) {
+        const double sx = wave_sum(yn[0]), sy = wave_sum(yn[1]);
+        if (lane_id() == 0) { sm[0][threadIdx.x >> 6] = sx; sm[1][threadIdx.x >> 6] = sy; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            mpart[2 * blockIdx.x] = (sm[0][0] + sm[0][1]) + (sm[0][2] + sm[0][3]);
+            mpart[2 * blockIdx.x + 1] = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
+        }
+    }
+}
+
+// mean[c] = (sum of the nb block partials of component c, fixed order) / n
+__global__ __launch_bounds__(256) void mean2_final(const double *__restrict__ mpart, int64_t nb, double n,
+                                                   double *__restrict__ mean) {
+    __shared__ double sm[2][4];
+    double s[2] = {0.0, 0.0};
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) { s[0] += mpart[2 * b]; s[1] += mpart[2 * b + 1]; }
+    s[0] = wave_sum(s[0]);
+    s[1] = wave_sum(s[1]);
+    if (lane_id() == 0) { sm[0][threadIdx.x >> 6] = s[0]; sm[1][threadIdx.x >> 6] = s[1]; }
+    __syncthreads();
+    if (threadIdx.x < 2) mean[threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3])) / n;
+}
+
+// centerEmbedding (TsneHelpers.scala:320-329) fused with the write-back of
+// the caller's embedding in the original point order: Y = Ynew - mean,
+// Yu[orig[i]] = Y[i].
+__global__ __launch_bounds__(256) void center_scatter(const double *__restrict__ Ynew, const int32_t *__restrict__ orig,
+                                                      int64_t n, const double *__restrict__ mean,
+                                                      double *__restrict__ Y, double *__restrict__ Yu) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double2 v = *reinterpret_cast<const double2 *>(Ynew + 2 * i);
+    const double2 y = make_double2(v.x - mean[0], v.y - mean[1]);
+    *reinterpret_cast<double2 *>(Y + 2 * i) = y;
+    const int64_t o = orig[i];   // the caller's buffer: 8-byte alignment only
+    Yu[2 * o] = y.x;
+    Yu[2 * o + 1] = y.y;
 }
 
 __global__ void center_apply(const double *__restrict__ src, int64_t n, int32_t c,
@@ -524,10 +578,11 @@ static int64_t attract_launch(hipStream_t st, const AttractArgs &a, bool loss) {
 template <int MODE>
 static void combine_launch(hipStream_t st, int64_t r0, int64_t r1, const double2 *attr, const int32_t *inv,
                            const double2 *F, const double *scal, const double *Y, double *grad, double *Ynew,
-                           double *upd, double *gains, double min_gain, double mom, double lr) {
+                           double *upd, double *gains, double min_gain, double mom, double lr,
+                           double *mpart = nullptr) {
     if (r1 <= r0) return;
     hipLaunchKernelGGL(combine_update<MODE>, dim3(ceil_div(r1 - r0, 256)), dim3(256), 0, st, r0, r1, attr, inv, F,
-                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr);
+                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr, mpart);
 }
 
 // Upper bound of attract_launch's block count for rows rows.
@@ -647,7 +702,7 @@ void opt_destroy(tsne_ctx *ctx) {
     OptState *s = ctx->opt;
     for (auto &e : s->ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {s->ev_y, s->ev_attr, s->ev_a0, s->ev_a1})
+    for (hipEvent_t e : {s->ev_y, s->ev_attr})
         if (e) (void)hipEventDestroy(e);
     if (s->side) {
         (void)hipStreamSynchronize(s->side);
@@ -724,6 +779,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->scal = ws.get<double>("opt.scal", 8);
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(s->chunk)));
     s->part2 = ws.get<double>("opt.part2", NPART);
+    s->mpart = ws.get<double>("opt.mpart", 2 * ceil_div(s->chunk, 256) + 2);
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
@@ -754,8 +810,8 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     }
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_attr, hipEventDisableTiming));
-    TSNE_HIP(hipEventCreate(&s->ev_a0));
-    TSNE_HIP(hipEventCreate(&s->ev_a1));
+    ctx->timers.reset("opt.attract");
+    ctx->timers.reset("opt.update");
     TSNE_LAUNCH_CHECK();
 }
 
@@ -817,16 +873,13 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     }
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
-    if (s->profile) {
-        TSNE_HIP(hipEventRecord(s->ev[3], st));
-        TSNE_HIP(hipEventRecord(s->ev_a0, st));
-    }
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
+    ctx->timers.begin("opt.attract", st);
     const int64_t blocks = attract3_launch(st, s->rp[0], s->col[0], s->val[0], s->r0, s->r1, Y, s->scal, p.metric,
                                            ex, s->attr3, s->part, want_loss);
-    if (s->profile) {
-        TSNE_HIP(hipEventRecord(s->ev_a1, st));
-        TSNE_HIP(hipEventRecord(s->ev[4], st));
-    }
+    ctx->timers.end("opt.attract", st);
+    s->attract_iter.push_back({t, 1});
+    if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     if (s->r1 > s->r0)
         hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->r1 - s->r0, 256)), dim3(256), 0, st, s->r0, s->r1,
                            s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[0], s->gains[0],
@@ -855,10 +908,10 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
         TSNE_HIP(hipEventSynchronize(s->ev[5]));
         for (int k = 0; k < 5; ++k) {
             float ms = 0.f;
-            if (k == 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev_a0, s->ev_a1));
-            else TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+            if (k != 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
+        s->last_ms[3] = ctx->timers.ms("opt.attract").back();
         for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
     }
 }
@@ -907,10 +960,11 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     };
     auto side_attract = [&] {
         if (ov_mode != 2) side_wait();
-        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a0, s->side));
+        ctx->timers.begin("opt.attract", s->side);
         attract_launch(s->side, aa, false);
         TSNE_LAUNCH_CHECK();
-        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a1, s->side));
+        ctx->timers.end("opt.attract", s->side);
+        s->attract_iter.push_back({t, 0});
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
     if (overlap && with_tree) side_attract();
@@ -950,14 +1004,19 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (overlap) {
         TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     } else {
-        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a0, st));
+        ctx->timers.begin("opt.attract", st);
         blocks = attract_launch(st, aa, true);
         TSNE_LAUNCH_CHECK();
-        if (s->profile) TSNE_HIP(hipEventRecord(s->ev_a1, st));
+        ctx->timers.end("opt.attract", st);
+        s->attract_iter.push_back({t, 1});
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
+    // update + centre: combine_update (with the mean's block partials when one
+    // rank holds every row), mean, centre + write-back of the caller's Y
+    ctx->timers.begin("opt.update", st);
+    const bool fused_mean = ctx->world == 1;
     combine_launch<1>(st, s->r0, s->r1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
-                      s->gains[c], p.min_gain, mom, p.learning_rate);
+                      s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
     if (want_loss) {
         hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
         hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
@@ -969,14 +1028,19 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         }
     }
     // 5. exchange + 6. centre
-    if (ctx->world > 1) comm_allgather_bytes(ctx, s->Ynew + 2 * s->r0, s->Ynew, sizeof(double) * 2 * s->chunk);
-    for (int k = 0; k < 2; ++k) {
-        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 2, k, s->part);
-        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
+    if (fused_mean) {
+        hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->r1 - s->r0, 256), (double)n,
+                           s->scal + 2);
+    } else {
+        comm_allgather_bytes(ctx, s->Ynew + 2 * s->r0, s->Ynew, sizeof(double) * 2 * s->chunk);
+        for (int k = 0; k < 2; ++k) {
+            hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 2, k, s->part);
+            hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
+        }
     }
-    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 2, 256)), dim3(256), 0, st, s->Ynew, n, 2, s->scal + 2, Y);
-    // the caller's Y, original order
-    hipLaunchKernelGGL(scatter_to_user, dim3(ceil_div(n, 256)), dim3(256), 0, st, Y, s->orig[c], n, s->Yu);
+    hipLaunchKernelGGL(center_scatter, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Ynew, s->orig[c], n, s->scal + 2,
+                       Y, s->Yu);
+    ctx->timers.end("opt.update", st);
     TSNE_LAUNCH_CHECK();
     if (t % RELABEL_EVERY == 0) relabel(ctx, s);
     if (s->profile) {
@@ -984,10 +1048,10 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipEventSynchronize(s->ev[5]));
         for (int k = 0; k < 5; ++k) {   // [3]: the attraction kernel alone, on its own stream
             float ms = 0.f;
-            if (k == 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev_a0, s->ev_a1));
-            else TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+            if (k != 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
             s->last_ms[k] = ms;
         }
+        s->last_ms[3] = ctx->timers.ms("opt.attract").back();
         unsigned long long v[16] = {};
         TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
         for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
@@ -1029,6 +1093,20 @@ int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap) {
             if (vals) vals[k] = h[i];
         }
         ++k;
+    }
+    return k;
+}
+
+int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap) {
+    OptState *s = ctx->opt;
+    TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    const std::vector<double> v = ctx->timers.ms("opt.attract");
+    TSNE_REQUIRE(v.size() == s->attract_iter.size(), "attraction timer log out of step");
+    const int32_t k = (int32_t)v.size();
+    for (int32_t e = 0; e < k && e < cap; ++e) {
+        if (iters) iters[e] = s->attract_iter[e].first;
+        if (standalone) standalone[e] = s->attract_iter[e].second;
+        if (ms) ms[e] = v[e];
     }
     return k;
 }

@@ -22,6 +22,28 @@ def _f64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
 
 
+def _csr(row_ptr, col, P, n):
+    """CSR arrays in the ABI's types.  The caller must keep the returned arrays
+    referenced until the library call returns: a converted temporary passed
+    straight into _ptr() would be freed before the library reads it."""
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    cl = np.ascontiguousarray(col, dtype=np.int32)
+    pv = np.ascontiguousarray(P, dtype=np.float64)
+    if rp.shape != (n + 1,):
+        raise ValueError("row_ptr has shape %s, expected (%d,)" % (rp.shape, n + 1))
+    if cl.shape != (int(rp[-1]),) or pv.shape != cl.shape:
+        raise ValueError("col / P must hold row_ptr[n] = %d entries" % int(rp[-1]))
+    return rp, cl, pv
+
+
+def _inout(n, c, **arrays):
+    """Arrays the library writes in place must already be float64, C-contiguous, n x c."""
+    for name, a in arrays.items():
+        if not (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous
+                and a.shape == (n, c)):
+            raise ValueError("%s must be a C-contiguous float64 array of shape (%d, %d)" % (name, n, c))
+
+
 def default_params(**kw):
     p = Params()
     lib().tsne_params_default(C.byref(p))
@@ -132,11 +154,11 @@ class Context:
         is 2 (quadtree) or 3 (the octree extension, tsne_gradient_c)."""
         Y = _f64(Y)
         n, c = Y.shape
+        rp, cl, pv = _csr(row_ptr, col, P, n)   # converted copies stay referenced across the call
         grad = np.zeros((n, c))
         z = C.c_double()
         loss = C.c_double()
-        check(lib().tsne_gradient_c(self._h, _ptr(np.ascontiguousarray(row_ptr, np.int64)),
-                                    _ptr(np.ascontiguousarray(col, np.int32)), _ptr(_f64(P)), n, c,
+        check(lib().tsne_gradient_c(self._h, _ptr(rp), _ptr(cl), _ptr(pv), n, c,
                                     _ptr(Y), METRICS[metric], theta, exaggeration, _ptr(grad),
                                     C.byref(z), C.byref(loss) if want_loss else None))
         return grad, z.value, (loss.value if want_loss else None)
@@ -144,16 +166,17 @@ class Context:
     def updateEmbedding(self, grad, Y, upd, gains, min_gain, momentum, learning_rate):
         """TsneHelpers.scala:341-369, in place on Y / upd / gains."""
         n, c = Y.shape
+        _inout(n, c, Y=Y, upd=upd, gains=gains)
         g = _f64(grad)
-        for a in (Y, upd, gains):
-            assert a.dtype == np.float64 and a.flags.c_contiguous
+        if g.shape != (n, c):
+            raise ValueError("grad has shape %s, expected %s" % (g.shape, (n, c)))
         check(lib().tsne_update_embedding(self._h, n, c, _ptr(g), _ptr(Y), _ptr(upd), _ptr(gains),
                                           min_gain, momentum, learning_rate))
 
     def centerEmbedding(self, Y):
         """TsneHelpers.scala:320-329, in place."""
-        assert Y.dtype == np.float64 and Y.flags.c_contiguous
         n, c = Y.shape
+        _inout(n, c, Y=Y)
         check(lib().tsne_center_embedding(self._h, n, c, _ptr(Y)))
 
     def initWorkingSet(self, n, n_components=2, seed=0):
@@ -169,12 +192,13 @@ class Context:
         n = Y.shape[0]
         if Y.shape[1] != params.n_components:
             raise ValueError("Y has %d columns, params.n_components is %d" % (Y.shape[1], params.n_components))
+        _inout(n, params.n_components, Y=Y, upd=upd, gains=gains)   # written in place by the library
+        rp, cl, pv = _csr(row_ptr, col, P, n)   # converted copies stay referenced across the call
         cap = params.iterations // 10 + 1
         keys = np.zeros(cap, dtype=np.int32)
         vals = np.zeros(cap)
         nl = C.c_int32()
-        check(lib().tsne_optimize(self._h, C.byref(params), _ptr(np.ascontiguousarray(row_ptr, np.int64)),
-                                  _ptr(np.ascontiguousarray(col, np.int32)), _ptr(_f64(P)), n, _ptr(Y),
+        check(lib().tsne_optimize(self._h, C.byref(params), _ptr(rp), _ptr(cl), _ptr(pv), n, _ptr(Y),
                                   _ptr(upd), _ptr(gains), _ptr(keys), _ptr(vals), cap, C.byref(nl)))
         return dict(zip(keys[:nl.value].tolist(), vals[:nl.value].tolist()))
 
@@ -213,6 +237,25 @@ class Context:
     def dev_balance_cuts(self, bcost, n, world, bounds):
         """tsne_dev_balance_cuts on device tensors (uint64/int64 bucket costs, int64 bounds[world+1])."""
         check(lib().tsne_dev_balance_cuts(self._h, _ptr(bcost), n, world, _ptr(bounds)))
+
+    def dev_opt_attract_log(self):
+        """-> list of (iteration, standalone, ms) for every attraction launch since setup."""
+        cnt = C.c_int32()
+        check(lib().tsne_dev_opt_attract_log(self._h, None, None, None, 0, C.byref(cnt)))
+        k = cnt.value
+        it = np.zeros(max(k, 1), dtype=np.int32)
+        sa = np.zeros(max(k, 1), dtype=np.int32)
+        ms = np.zeros(max(k, 1))
+        check(lib().tsne_dev_opt_attract_log(self._h, _ptr(it), _ptr(sa), _ptr(ms), k, C.byref(cnt)))
+        return [(int(it[e]), int(sa[e]), float(ms[e])) for e in range(k)]
+
+    def stage_ms(self, stage):
+        """Per-interval kernel times (ms) of a stage timer (tsne_ctx_stage_ms)."""
+        cnt = C.c_int32()
+        check(lib().tsne_ctx_stage_ms(self._h, stage.encode(), None, 0, C.byref(cnt)))
+        out = np.zeros(max(cnt.value, 1))
+        check(lib().tsne_ctx_stage_ms(self._h, stage.encode(), _ptr(out), cnt.value, C.byref(cnt)))
+        return out[:cnt.value].tolist()
 
     def dev_opt_profile(self, enable=-1):
         """-> (stage ms[5], BH counters [visits, moment evaluations, dense pair terms,
