@@ -86,6 +86,17 @@ int tsne_dev_balance_cuts(tsne_ctx *ctx, const uint64_t *d_bcost, int64_t n, int
 
 /* ---------------------------------------------------------------- context */
 int tsne_ctx_create(int32_t device, tsne_ctx **out);
+/* One caller, several GPUs (SURVEY.md 8b "Threading": a Flink operator at
+ * parallelism 1 drives the node).  Creates one rank context per entry of
+ * devices[0..ndev) and their communicator: RCCL (ncclCommInitAll, over xGMI)
+ * when all devices are distinct, an in-process loopback when all are the same
+ * device (ndev ranks sharing one GPU -- executes the multi-GPU code path on a
+ * single GPU, for testing).  On the returned handle tsne_knn splits the query
+ * rows and tsne_optimize shards the rows of P and the BH queries over the
+ * ranks, one host thread per rank, results written to the caller's buffers
+ * once; every other host-buffer operator, and the tsne_dev_* calls, run on
+ * the first device.  Destroy with tsne_ctx_destroy. */
+int tsne_ctx_create_multi(const int32_t *devices, int32_t ndev, tsne_ctx **out);
 int tsne_ctx_destroy(tsne_ctx *ctx);
 /* Enqueue on a caller-owned hipStream_t (e.g. torch's current stream). NULL = own stream. */
 int tsne_ctx_set_stream(tsne_ctx *ctx, void *hip_stream);
@@ -95,13 +106,30 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
 /* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls
  * tsne_comm_unique_id and ships the bytes to the other ranks out of band
  * (torch.distributed / MPI / a file); every rank then calls
- * tsne_ctx_init_comm.  Afterwards tsne_knn shards query rows and
- * tsne_optimize / tsne_dev_opt_* shard P rows and BH queries; results are
- * replicated on every rank. */
+ * tsne_ctx_init_comm.  Afterwards tsne_optimize / tsne_dev_opt_* shard the
+ * rows of P and the BH queries (each rank owns a range of internal labels,
+ * re-cut by measured BH cost when the labels are renumbered); per iteration
+ * only the updated embedding slices (all-gather) and Z (all-reduce) cross
+ * ranks.  Results are replicated on every rank.  (tsne_knn takes explicit
+ * query ranges per rank.) */
 int tsne_comm_unique_id(uint8_t id_out[TSNE_UNIQUE_ID_BYTES]);
 int tsne_ctx_init_comm(tsne_ctx *ctx, int32_t rank, int32_t world,
                        const uint8_t id[TSNE_UNIQUE_ID_BYTES]);
 int tsne_ctx_rank(tsne_ctx *ctx, int32_t *rank, int32_t *world);
+
+/* Collectives supplied by the host dataflow instead of RCCL (e.g. carried by
+ * the JVM's own network stack across nodes, or torch.distributed in tests).
+ * Each operates in place on a HOST buffer and returns 0 on success; every
+ * rank calls them in the same order.  allgatherv: rank r's bytes
+ * [off[r], off[r+1]) of buf (off has world + 1 entries) must reach every
+ * rank's buf. */
+typedef struct {
+    int (*allreduce_sum_f64)(void *user, double *buf, int64_t count);
+    int (*allreduce_sum_u64)(void *user, uint64_t *buf, int64_t count);
+    int (*allgatherv)(void *user, void *buf, const int64_t *off);
+} tsne_comm_ops;
+int tsne_ctx_init_comm_callbacks(tsne_ctx *ctx, int32_t rank, int32_t world, const tsne_comm_ops *ops,
+                                 void *user);
 
 /* ------------------------------------------------- host-buffer operators */
 
@@ -190,15 +218,18 @@ int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const i
                                 int32_t *d_out_col, double *d_out_val, int64_t *nnz_out);
 
 /* Device-resident optimizer.  setup copies the FULL P (every rank holds it;
- * rank r computes rows [r*ceil(n/world), ...) of the optimizer's internal
- * point labels) and the working set (Y, upd, gains: n x n_components, original point
- * order) into its own state and allocates the workspace; step runs global
- * iteration t (1-based) with the reference phase schedule and rewrites the
- * caller's Y (original order) at the end of every step; sync also writes
- * back upd and gains.  Losses for t % 10 == 0 stay on the device and are read
- * by tsne_dev_opt_losses.  Internally the points are relabelled into Morton
- * order every 25 iterations (cache locality of the CSR attraction; 2-D only).
- * n_components = 3 runs the octree extension (see tsne_gradient_c). */
+ * rank r computes the rows of its range of the optimizer's internal point
+ * labels) and the working set (Y, upd, gains: n x n_components, original
+ * point order) into its own state and allocates the workspace; step runs
+ * global iteration t (1-based) with the reference phase schedule and
+ * rewrites the caller's Y (original order) at the end of every step; sync
+ * also writes back upd and gains.  Losses for t % 10 == 0 stay on the device
+ * and are read by tsne_dev_opt_losses.  Internal labels (2-D): P's graph
+ * order at setup (connected components, BFS level), then every 25
+ * iterations the Morton order of the embedding when it keeps more of P's
+ * edges local -- cache locality of the CSR attraction's gathers; results do
+ * not depend on the labelling beyond summation order.  n_components = 3 runs
+ * the octree extension (see tsne_gradient_c). */
 int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *d_row_ptr,
                        const int32_t *d_col, const double *d_P, int64_t n, double *d_Y,
                        double *d_upd, double *d_gains);

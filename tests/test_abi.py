@@ -69,3 +69,17 @@ def test_no_device_fails_loudly():
     with pytest.raises(T.TsneError) as e:
         T.Context(0)
     assert e.value.status == -7
+
+
+def test_create_multi_argument_errors():
+    """tsne_ctx_create_multi validates the device list before touching a GPU."""
+    import ctypes as C
+    import numpy as np
+    L = T.lib()
+    h = C.c_void_p()
+    for devs in ([0, 0, 1], [1, 2, 1]):
+        d = np.array(devs, dtype=np.int32)
+        rc = L.tsne_ctx_create_multi(d.ctypes.data_as(C.c_void_p), len(devs), C.byref(h))
+        assert rc == -1 and b"distinct" in L.tsne_last_error()
+    rc = L.tsne_ctx_create_multi(None, 0, C.byref(h))
+    assert rc == -1

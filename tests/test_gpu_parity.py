@@ -296,6 +296,26 @@ def test_optimize_loss_matches_oracle(ctx):
     assert abs(lg[200] - mu) <= 4.0 * sd + 0.01 * abs(mu), (lg[200], final)
 
 
+def test_host_api_converts_csr_types(ctx):
+    """int32 row_ptr, int64 col and float32 P are converted by the binding (and
+    the converted copies stay alive across the library call)."""
+    n = 500
+    rp, col, val = random_problem(n, 10, seed=61)
+    val32 = val.astype(np.float32)
+    Y0 = np.random.default_rng(4).normal(size=(n, 2)) * 1e-2
+    g_ref, z_ref, _ = ctx.gradient(rp, col, val32.astype(np.float64), Y0, 0.5)
+    g, z, _ = ctx.gradient(rp.astype(np.int32), col.astype(np.int64), val32, Y0, 0.5)
+    assert np.array_equal(g, g_ref) and z == z_ref
+    p = default_params(iterations=15, theta=0.5)
+    Ya, ua, ga = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    la = ctx.optimize(rp, col, val32.astype(np.float64), Ya, ua, ga, p)
+    Yb, ub, gb = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lb = ctx.optimize(list(rp), col.astype(np.int16), val32, Yb, ub, gb, p)
+    assert np.array_equal(Ya, Yb) and la == lb
+    with pytest.raises(ValueError):
+        ctx.optimize(rp, col, val, Y0.astype(np.float32), ua, ga, p)
+
+
 def test_unsupported_components(ctx):
     rp, col, val = triples_to_csr(G["denseJointProbabilitiesResults"], 10)
     Y = np.zeros((10, 4))

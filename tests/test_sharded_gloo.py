@@ -1,17 +1,18 @@
-"""The N>1 decomposition on CPU: world_size 2 over gloo.
+"""The N>1 decomposition on CPU: world_size 2/3 over gloo.
 
-libtsne_hip's multi-GPU iteration (optimize.hip) is: every rank builds the
-same tree from the full Y; rank r computes BH repulsion for its slice of the
-Morton-sorted points, the slices cut by the previous iteration's measured
-per-bucket cost (tsne_balance_cuts: identical cuts on every rank after an
-all-reduce of the bucket costs); the zero-filled (F, z) buffers are
-all-reduced; Z is summed locally; rank r runs attraction + update for its
-rows of P (tsne_shard_rows); the updated Y slices are all-gathered; every
-rank centres.  This test replays exactly that decomposition with the oracle
-as the compute (a per-query force-magnitude cost) and torch.distributed
+libtsne_hip's multi-GPU iteration (optimize.hip, world > 1): rank r owns a
+range of point labels = rows of P (cost-balanced cuts, re-cut from measured
+per-bucket costs when the labels are renumbered: tsne_balance_cuts, identical
+on every rank after an all-reduce of the costs); every rank builds the same
+tree from the full Y and computes BH repulsion for ITS OWN points only; Z is
+the all-reduce of the ranks' partial sums (one double); rank r runs attraction
++ update for its rows; the updated Y slices are all-gathered (ragged: one
+broadcast per rank); every rank centres; the loss every 10th iteration is one
+more all-reduce.  No per-point force crosses ranks.  This test replays exactly
+that decomposition with the oracle as the compute and torch.distributed
 (gloo) as the exchange, and checks it reproduces the single-process reference
-iteration.  The slicing comes from the library's own host logic, which needs
-no GPU.
+iteration.  (The library's own world > 1 step runs in tests/test_gpu_multi.py,
+with loopback ranks and with gloo-carried collectives.)
 """
 import os
 import socket
@@ -36,11 +37,6 @@ def _problem(n=300, k=20, seed=3):
     return P, Y
 
 
-def _sorted_order(Y):
-    # any fixed permutation shared by all ranks stands in for the Morton order
-    return np.lexsort((Y[:, 1], Y[:, 0]))
-
-
 def _worker(rank, world, port, T, out_path):
     import sys
     from pathlib import Path
@@ -54,58 +50,61 @@ def _worker(rank, world, port, T, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     (rp, col, val), Y = _problem()
     n = Y.shape[0]
-    r0, r1 = TA.shard_rows(n, world, rank)
-    chunk = -(-n // world)
     upd, gains = np.zeros_like(Y), np.ones_like(Y)
     losses = {}
     BUCKET = 16
     cut_log = []
     nb = -(-n // BUCKET)
-    bounds = np.array([min(n, chunk * r) for r in range(world + 1)], dtype=np.int64)
+    own = np.array([min(n, -(-n // world) * r) for r in range(world + 1)], dtype=np.int64)
     for t in range(1, T + 1):
         ex = 4.0 if t <= 101 else 1.0
         mom = 0.5 if t <= 20 else 0.8
-        # BH for this rank's cost-balanced slice of the sorted order
-        order = _sorted_order(Y)
-        b0, b1 = int(bounds[rank]), int(bounds[rank + 1])
-        sl = order[b0:b1]
-        full = np.zeros((n, 3))
-        cost = np.zeros(nb, dtype=np.uint64)
-        if b1 > b0:
-            rep_s, z_s = Ow.repulsion_queries(Y, 0.5, Y[sl])
-            full[b0:b1, :2] = rep_s
-            full[b0:b1, 2] = z_s
-            # any per-query cost measured on the slice will do; the library uses its wave pops
-            vis = (1 + 100.0 * np.abs(rep_s).sum(1) / max(1e-300, np.abs(rep_s).sum(1).max())).astype(np.uint64)
-            np.add.at(cost, np.arange(b0, b1) // BUCKET, vis)
-        ft = torch.from_numpy(full)
-        dist.all_reduce(ft)                                    # zero-filled slices: exact sum
-        full = ft.numpy()
-        ct = torch.from_numpy(cost.astype(np.int64))
-        dist.all_reduce(ct)
-        bounds = TA.balance_cuts(ct.numpy().astype(np.uint64), n, world, bucket=BUCKET)
-        if rank == 0:
-            cut_log.append(bounds.tolist())
+        r0, r1 = int(own[rank]), int(own[rank + 1])
+        # BH for this rank's own points only
         rep = np.zeros((n, 2))
-        z = np.zeros(n)
-        rep[order] = full[:, :2]
-        z[order] = full[:, 2]
-        Z = z.sum()
+        cost = np.zeros(nb, dtype=np.uint64)
+        zpart = np.zeros(1)
+        if r1 > r0:
+            rep_s, z_s = Ow.repulsion_queries(Y, 0.5, Y[r0:r1])
+            rep[r0:r1] = rep_s
+            zpart[0] = z_s.sum()
+            # any per-query cost measured on the slice will do; the library uses its wave times
+            vis = (1 + 100.0 * np.abs(rep_s).sum(1) / max(1e-300, np.abs(rep_s).sum(1).max())).astype(np.uint64)
+            np.add.at(cost, np.arange(r0, r1) // BUCKET, vis)
+        zt = torch.from_numpy(zpart)
+        dist.all_reduce(zt)                                    # the only per-iteration all-reduce
+        Z = float(zt.item())
         g, lpart = Ow.attraction_rows(rp, col, val, Y, rep, Z, r0, r1, exaggeration=ex,
                                       want_loss=(t % 10 == 0))
         Yr, ur, gr = Y[r0:r1].copy(), upd[r0:r1].copy(), gains[r0:r1].copy()
         Ow.update(np.ascontiguousarray(g), Yr, ur, gr, 0.01, mom, 200.0)
         upd[r0:r1], gains[r0:r1] = ur, gr
-        ybuf = np.zeros((chunk, 2))
-        ybuf[: r1 - r0] = Yr
-        gy = [torch.zeros(chunk, 2, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(gy, torch.from_numpy(ybuf))
-        Y = np.ascontiguousarray(torch.cat(gy).numpy()[:n])
+        Ynew = Y.copy()
+        Ynew[r0:r1] = Yr
+        for r in range(world):                                 # ragged all-gather: one broadcast per rank
+            seg = torch.from_numpy(np.ascontiguousarray(Ynew[own[r]:own[r + 1]]))
+            if seg.numel():
+                dist.broadcast(seg, src=r)
+                Ynew[own[r]:own[r + 1]] = seg.numpy()
+        Y = Ynew
         Ow.center(Y)
         if t % 10 == 0:
             lt = torch.tensor([lpart], dtype=torch.float64)
             dist.all_reduce(lt)
             losses[t] = float(lt.item())
+            # re-cut the ownership by the measured costs (the library does this at
+            # its relabels); the rows' momentum / gains follow their new owner
+            ct = torch.from_numpy(cost.astype(np.int64))
+            dist.all_reduce(ct)
+            for r in range(world):
+                for a in (upd, gains):
+                    seg = torch.from_numpy(np.ascontiguousarray(a[own[r]:own[r + 1]]))
+                    if seg.numel():
+                        dist.broadcast(seg, src=r)
+                        a[own[r]:own[r + 1]] = seg.numpy()
+            own = TA.balance_cuts(ct.numpy().astype(np.uint64), n, world, bucket=BUCKET)
+            if rank == 0:
+                cut_log.append(own.tolist())
     if rank == 0:
         np.savez(out_path, Y=Y, keys=np.array(sorted(losses)), vals=np.array([losses[k] for k in sorted(losses)]),
                  cuts=np.array(cut_log))
@@ -157,9 +156,9 @@ def test_balance_cuts_rule():
 
 
 def _worker3(rank, world, port, T, out_path):
-    """The 3-D (octree) decomposition of optimize.hip opt_step3: equal-count
-    slices of the sorted order for BH, all-reduced (F, z), rows of P by
-    tsne_shard_rows, all-gathered Y slices, local centring."""
+    """The 3-D (octree) decomposition of optimize.hip opt_step3: equal label
+    ranges (= rows of P, no relabelling), BH for the rank's own points, Z
+    all-reduced, ragged all-gather of the Y slices, local centring."""
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parent.parent
@@ -174,36 +173,33 @@ def _worker3(rank, world, port, T, out_path):
     Y = np.random.default_rng(8).normal(size=(rp.shape[0] - 1, 3)) * 1e-2
     n = Y.shape[0]
     r0, r1 = TA.shard_rows(n, world, rank)
-    chunk = -(-n // world)
     upd, gains = np.zeros_like(Y), np.ones_like(Y)
     losses = {}
     for t in range(1, T + 1):
         ex = 4.0 if t <= 101 else 1.0
         mom = 0.5 if t <= 20 else 0.8
-        order = np.lexsort((Y[:, 2], Y[:, 1], Y[:, 0]))
-        b0, b1 = min(n, chunk * rank), min(n, chunk * (rank + 1))
-        full = np.zeros((n, 4))
-        if b1 > b0:
-            rep_s, z_s = Ow.repulsion3_queries(Y, 0.5, Y[order[b0:b1]])
-            full[b0:b1, :3] = rep_s
-            full[b0:b1, 3] = z_s
-        ft = torch.from_numpy(full)
-        dist.all_reduce(ft)
-        full = ft.numpy()
         rep = np.zeros((n, 3))
-        z = np.zeros(n)
-        rep[order] = full[:, :3]
-        z[order] = full[:, 3]
-        Z = z.sum()
+        zpart = np.zeros(1)
+        if r1 > r0:
+            rep_s, z_s = Ow.repulsion3_queries(Y, 0.5, Y[r0:r1])
+            rep[r0:r1] = rep_s
+            zpart[0] = z_s.sum()
+        zt = torch.from_numpy(zpart)
+        dist.all_reduce(zt)
+        Z = float(zt.item())
         g, lpart = Ow.attraction3_rows(rp, col, val, Y, rep, Z, r0, r1, exaggeration=ex, want_loss=(t % 10 == 0))
         Yr, ur, gr = Y[r0:r1].copy(), upd[r0:r1].copy(), gains[r0:r1].copy()
         Ow.update(np.ascontiguousarray(g), Yr, ur, gr, 0.01, mom, 200.0)
         upd[r0:r1], gains[r0:r1] = ur, gr
-        ybuf = np.zeros((chunk, 3))
-        ybuf[: r1 - r0] = Yr
-        gy = [torch.zeros(chunk, 3, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(gy, torch.from_numpy(ybuf))
-        Y = np.ascontiguousarray(torch.cat(gy).numpy()[:n])
+        Ynew = Y.copy()
+        Ynew[r0:r1] = Yr
+        for r in range(world):
+            a0, a1 = TA.shard_rows(n, world, r)
+            seg = torch.from_numpy(np.ascontiguousarray(Ynew[a0:a1]))
+            if seg.numel():
+                dist.broadcast(seg, src=r)
+                Ynew[a0:a1] = seg.numpy()
+        Y = Ynew
         Ow.center(Y)
         if t % 10 == 0:
             lt = torch.tensor([lpart], dtype=torch.float64)

@@ -691,18 +691,19 @@ __device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, do
     return (MOM_ORDER + 2) * rp <= MOM_TOL * (1.0 - rho) * (1.0 - rho);
 }
 
-// Moment tasks of each query (sorted positions [s0, s1)), in traversal order,
-// added to the traversal's F and z.
+// Moment tasks of each query (query slots [g0, g1): sorted positions, or
+// qlist[slot] when a rank computes a list of them), in traversal order, added
+// to the traversal's F and z.
 __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ pos,
                                                     const BHNode *__restrict__ nodes,
                                                     const double *__restrict__ mom,
                                                     const int32_t *__restrict__ mtask,
                                                     const int32_t *__restrict__ mtask_n, int64_t g0,
-                                                    int64_t g1, const int64_t *__restrict__ dbounds,
+                                                    int64_t g1, const int32_t *__restrict__ qlist,
                                                     double2 *__restrict__ F, double *__restrict__ Z) {
-    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
-    const int64_t s = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < s0 || s >= s1) return;
+    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= g1) return;
+    const int64_t s = qlist ? (int64_t)qlist[k] : k;
     const int nt = mtask_n[s];
     if (nt == 0) return;
     const double2 q = pos[s];
@@ -855,7 +856,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
-    int64_t g1, const int64_t *__restrict__ dbounds, int xcd_chunk, double2 *__restrict__ F,
+    int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, double2 *__restrict__ F,
     double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     __shared__ int32_t sref[4][STACK];
@@ -865,11 +866,12 @@ __global__ __launch_bounds__(256) void bh_traverse(
     __shared__ uint64_t bmask[4][KPOP];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
-    const int64_t wid = blk * 4 + w;   // wave slot: queries g0 + 64 wid .. + 63, tile list wid
-    // queries [s0, s1): this rank's slice (device bounds when cost-balanced across ranks)
-    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
-    const int64_t s = g0 + wid * 64 + lane;
-    const bool valid = s >= s0 && s < s1;
+    const int64_t wid = blk * 4 + w;   // wave slot: query slots g0 + 64 wid .. + 63, tile list wid
+    // query slot k -> sorted position s (the identity, or this rank's list of
+    // its own queries in sorted order: the waves stay Morton-coherent)
+    const int64_t k = g0 + wid * 64 + lane;
+    const bool valid = k < g1;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
     if (lane == 0) ttask_n[wid] = 0;
     if (__ballot(valid) == 0) return;
     const long long t_start = COST ? clock64() : 0;
@@ -1049,7 +1051,8 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
                                                   const double *__restrict__ mom,
                                                   const TileTask *__restrict__ ttask,
                                                   const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1,
-                                                  int xcd_chunk, int32_t *__restrict__ mom_flag,
+                                                  const int32_t *__restrict__ qlist, int xcd_chunk,
+                                                  int32_t *__restrict__ mom_flag,
                                                   int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
                                                   double2 *__restrict__ F, double *__restrict__ Z,
                                                   unsigned long long *__restrict__ visits, int qmajor, int pack) {
@@ -1060,14 +1063,16 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
     const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
     if (g0 + wid * 64 >= g1) return;
-    const int64_t s = g0 + wid * 64 + lane;
+    const int64_t kq = g0 + wid * 64 + lane;
+    const bool valid = kq < g1;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
     const int nt = ttask_n[wid];
     if (nt == 0) {
-        if (s < g1) mtask_n[s] = 0;
+        if (valid) mtask_n[s] = 0;
         return;
     }
     double qx = 0.0, qy = 0.0;
-    if (s < g1) { const double2 q = pos[s]; qx = q.x; qy = q.y; }
+    if (valid) { const double2 q = pos[s]; qx = q.x; qy = q.y; }
     const bool mom_on = mom_flag[0] != 0;
     double fx = 0.0, fy = 0.0, zs = 0.0;
     int nwant = 0, ntask = 0;
@@ -1213,7 +1218,7 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
             if (dense) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)(b - a + 1); }
         }
     }
-    if (s < g1) {
+    if (valid) {
         mtask_n[s] = ntask;
         if (fx != 0.0 || fy != 0.0 || zs != 0.0) {
             const double2 f = F[s];
@@ -1388,7 +1393,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
 }
 
 void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
-                  double2 *dF, double *dz, unsigned long long *visits, const int64_t *dbounds,
+                  double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist,
                   unsigned long long *bcost) {
     if (s1 <= s0) return;
     const double near_dmax = bh_near_dmax(theta);
@@ -1408,12 +1413,13 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     const int64_t waves = ceil_div(s1 - s0, 64);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, dbounds, xcd, dF,
+                       t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd, dF,
                        dz, visits, bcost);
     hipLaunchKernelGGL(tile_apply, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.ttask, t.ttask_n, s0, s1, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor, pack);
+                       t.ttask, t.ttask_n, s0, s1, qlist, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor,
+                       pack);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.mtask, t.mtask_n, s0, s1, dbounds, dF, dz);
+                       t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

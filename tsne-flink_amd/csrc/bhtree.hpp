@@ -90,13 +90,13 @@ struct BHTree {
 void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
 // Build the tree of all n points of Y (n x 2, device).
 void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta);
-// Repulsion for sorted positions [s0, s1): F (double2) and z (sum of Q)
-// written at the sorted position; visits (nullable) += node evaluations.
-// [s0, s1) is the launch range; with dbounds (device {begin, end}) only the
-// queries inside it are computed (cost-balanced slices across ranks).  bcost
-// (nullable) accumulates each wave's cost into 256-query buckets.
+// Repulsion for the query slots [s0, s1): sorted positions, or with qlist
+// (device, ascending sorted positions: one rank's own queries) the positions
+// qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted
+// position; visits (nullable) += node evaluations; bcost (nullable)
+// accumulates each wave's cost into the 256-position bucket of its first query.
 void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
-                  double2 *dF, double *dz, unsigned long long *visits, const int64_t *dbounds = nullptr,
+                  double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist = nullptr,
                   unsigned long long *bcost = nullptr);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).
 void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int world, int64_t *bounds);

@@ -4,7 +4,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <new>
+#include <thread>
 
 #include "bhtree.hpp"
 #include "common.hpp"
@@ -36,6 +38,40 @@ template <class Fn> static int guard(Fn &&fn) {
 
 static void check_ctx(tsne_ctx *ctx) {
     if (!ctx) fail(TSNE_ERR_ARG, "context is NULL");
+}
+
+// Single-device operators on a group handle run on its first rank.
+static tsne_ctx *primary(tsne_ctx *ctx) { return ctx->group.empty() ? ctx : ctx->group[0]; }
+
+// Run fn(rank context, rank) on every rank of a group, one host thread each
+// (device made current per thread); the first failure is rethrown here after
+// the other ranks were released (loopback barrier abort) and joined.
+template <class Fn> static void run_group(tsne_ctx *g, Fn &&fn) {
+    const int world = (int)g->group.size();
+    std::vector<std::exception_ptr> err(world);
+    std::vector<std::thread> th;
+    for (int r = 0; r < world; ++r)
+        th.emplace_back([&, r] {
+            try {
+                DeviceGuard dg(g->group[r]->device);
+                fn(g->group[r], r);
+            } catch (...) {
+                err[r] = std::current_exception();
+                comm_abort(g->group[r]);
+            }
+        });
+    for (auto &t : th) t.join();
+    // report the root cause: a rank's own failure before the others' "aborted"
+    for (int pass = 0; pass < 2; ++pass)
+        for (int r = 0; r < world; ++r) {
+            if (!err[r]) continue;
+            try {
+                std::rethrow_exception(err[r]);
+            } catch (const Error &e) {
+                if (pass == 0 && e.status == TSNE_ERR_COMM) continue;
+                throw;
+            }
+        }
 }
 
 template <class T> static T *upload(tsne_ctx *ctx, const std::string &name, const T *h, size_t count) {
@@ -125,6 +161,7 @@ int tsne_balance_cuts(const uint64_t *bcost, int64_t nb, int64_t n, int32_t worl
 int tsne_dev_balance_cuts(tsne_ctx *ctx, const uint64_t *d_bcost, int64_t n, int32_t world, int64_t *d_bounds) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(d_bcost != nullptr && d_bounds != nullptr && n >= 0 && world >= 1, "bad balance arguments");
         bh_balance(ctx, reinterpret_cast<const unsigned long long *>(d_bcost), n, world, d_bounds);
@@ -151,8 +188,49 @@ int tsne_ctx_create(int32_t device, tsne_ctx **out) {
     });
 }
 
+int tsne_ctx_create_multi(const int32_t *devices, int32_t ndev, tsne_ctx **out) {
+    return guard([&] {
+        TSNE_REQUIRE(out != nullptr, "out is NULL");
+        *out = nullptr;
+        TSNE_REQUIRE(devices != nullptr && ndev >= 1 && ndev <= 64, "bad device list");
+        bool same = true, distinct = true;
+        for (int a = 0; a < ndev; ++a)
+            for (int b = a + 1; b < ndev; ++b) {
+                if (devices[a] == devices[b]) distinct = false;
+                else same = false;
+            }
+        TSNE_REQUIRE(same || distinct, "devices must be all distinct (RCCL) or all the same (loopback ranks)");
+        std::unique_ptr<tsne_ctx> g(new tsne_ctx());
+        struct Undo {
+            tsne_ctx *g;
+            ~Undo() { if (g) for (tsne_ctx *c : g->group) tsne_ctx_destroy(c); }
+        } undo{g.get()};
+        for (int r = 0; r < ndev; ++r) {
+            tsne_ctx *c = nullptr;
+            const int rc = tsne_ctx_create(devices[r], &c);
+            if (rc != TSNE_OK) throw Error(rc, g_last_error);
+            g->group.push_back(c);
+        }
+        g->device = devices[0];
+        g->cu_count = g->group[0]->cu_count;
+        comm_init_group(g->group, same && ndev > 1);
+        g->world = ndev;
+        undo.g = nullptr;
+        *out = g.release();
+    });
+}
+
 int tsne_ctx_destroy(tsne_ctx *ctx) {
     if (!ctx) return TSNE_OK;
+    if (!ctx->group.empty()) {
+        int rc = TSNE_OK;
+        for (tsne_ctx *c : ctx->group) {
+            const int r = tsne_ctx_destroy(c);
+            if (rc == TSNE_OK) rc = r;
+        }
+        delete ctx;
+        return rc;
+    }
     int rc = guard([&] {
         DeviceGuard g(ctx->device);
         (void)hipStreamSynchronize(ctx->stream);
@@ -169,6 +247,7 @@ int tsne_ctx_destroy(tsne_ctx *ctx) {
 int tsne_ctx_set_stream(tsne_ctx *ctx, void *hip_stream) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         if (ctx->own_stream && ctx->stream) {
             TSNE_HIP(hipStreamSynchronize(ctx->stream));
@@ -189,6 +268,7 @@ void *tsne_ctx_stream(tsne_ctx *ctx) { return ctx ? (void *)ctx->stream : nullpt
 int tsne_ctx_synchronize(tsne_ctx *ctx) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         sync(ctx);
     });
@@ -204,9 +284,20 @@ int tsne_comm_unique_id(uint8_t id_out[TSNE_UNIQUE_ID_BYTES]) {
 int tsne_ctx_init_comm(tsne_ctx *ctx, int32_t rank, int32_t world, const uint8_t id[TSNE_UNIQUE_ID_BYTES]) {
     return guard([&] {
         check_ctx(ctx);
+        TSNE_REQUIRE(ctx->group.empty(), "a tsne_ctx_create_multi group has its communicator already");
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(world == 1 || id != nullptr, "unique id is NULL");
         comm_init(ctx, rank, world, id);
+    });
+}
+
+int tsne_ctx_init_comm_callbacks(tsne_ctx *ctx, int32_t rank, int32_t world, const tsne_comm_ops *ops,
+                                 void *user) {
+    return guard([&] {
+        check_ctx(ctx);
+        TSNE_REQUIRE(ctx->group.empty(), "a tsne_ctx_create_multi group has its communicator already");
+        DeviceGuard g(ctx->device);
+        comm_init_callbacks(ctx, rank, world, ops, user);
     });
 }
 
@@ -224,6 +315,7 @@ int tsne_dev_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t 
                  int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         knn_device(ctx, dX, n, d, metric, k, q0, q1, d_idx, d_dist);
     });
@@ -233,6 +325,7 @@ int tsne_dev_pairwise_affinities(tsne_ctx *ctx, const int64_t *d_row_ptr, const 
                                  int64_t nrows, double perplexity, double *d_p) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         affinities_device(ctx, d_row_ptr, d_dist, nrows, perplexity, d_p);
     });
@@ -244,6 +337,7 @@ int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const i
     int64_t nnz = -1;
     int rc = guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(n >= 1, "empty matrix");
         nnz = joint_device(ctx, d_row_ptr, d_col, d_p, n, cap, d_out_row_ptr, d_out_col, d_out_val);
@@ -261,6 +355,7 @@ int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *
                        double *d_upd, double *d_gains) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         opt_setup(ctx, params, d_row_ptr, d_col, d_P, n, d_Y, d_upd, d_gains);
     });
@@ -269,6 +364,7 @@ int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *
 int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         opt_step(ctx, t);
     });
@@ -277,6 +373,7 @@ int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t) {
 int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap, int32_t *n_loss) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         int32_t k = opt_losses(ctx, loss_keys, loss_vals, cap);
         if (n_loss) *n_loss = k;
@@ -286,6 +383,7 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
 int tsne_ctx_stage_ms(tsne_ctx *ctx, const char *stage, double *ms_out, int32_t cap, int32_t *count) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(stage != nullptr, "stage is NULL");
         const std::vector<double> v = ctx->timers.ms(stage);
@@ -298,6 +396,7 @@ int tsne_dev_opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone,
                              int32_t *count) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         int32_t k = opt_attract_log(ctx, iters, standalone, ms, cap);
         if (count) *count = k;
@@ -307,6 +406,7 @@ int tsne_dev_opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone,
 int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out10) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         opt_profile(ctx, enable, ms_out5, counters_out10);
     });
@@ -318,11 +418,26 @@ int tsne_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32_t metri
              int64_t q0, int64_t q1, int32_t *idx_out, double *dist_out) {
     return guard([&] {
         check_ctx(ctx);
-        DeviceGuard g(ctx->device);
         TSNE_REQUIRE(X && idx_out && dist_out, "NULL buffer");
         TSNE_REQUIRE(n >= 2 && d >= 1 && k >= 1, "bad sizes");
         TSNE_REQUIRE(q0 >= 0 && q1 <= n && q0 <= q1, "query range out of bounds");
         const int64_t kk = std::min<int64_t>(k, n - 1);
+        if (!ctx->group.empty()) {   // query rows split evenly over the group's devices
+            const int world = (int)ctx->group.size();
+            run_group(ctx, [&](tsne_ctx *c, int r) {
+                const int64_t a = q0 + (q1 - q0) * r / world, b = q0 + (q1 - q0) * (r + 1) / world;
+                if (b == a) return;
+                double *dX = upload(c, "h.X", X, (size_t)(n * d));
+                int32_t *di = c->ws.get<int32_t>("h.knn_idx", (size_t)((b - a) * kk));
+                double *dd = c->ws.get<double>("h.knn_dist", (size_t)((b - a) * kk));
+                knn_device(c, dX, n, d, metric, k, a, b, di, dd);
+                download(c, idx_out + (a - q0) * kk, di, (size_t)((b - a) * kk));
+                download(c, dist_out + (a - q0) * kk, dd, (size_t)((b - a) * kk));
+                sync(c);
+            });
+            return;
+        }
+        DeviceGuard g(ctx->device);
         double *dX = upload(ctx, "h.X", X, (size_t)(n * d));
         int32_t *di = ctx->ws.get<int32_t>("h.knn_idx", (size_t)std::max<int64_t>(1, (q1 - q0) * kk));
         double *dd = ctx->ws.get<double>("h.knn_dist", (size_t)std::max<int64_t>(1, (q1 - q0) * kk));
@@ -337,6 +452,7 @@ int tsne_project_knn(tsne_ctx *ctx, const double *X, int64_t n, int32_t d, int32
                      int32_t iterations, const double *shifts, int32_t *idx_out, double *dist_out) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(X && idx_out && dist_out && n >= 2 && d >= 1 && iterations >= 1, "bad arguments");
         TSNE_REQUIRE(iterations == 1 || shifts, "NULL shifts");
@@ -356,6 +472,7 @@ int tsne_dev_project_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, 
                          int32_t iterations, const double *d_shifts, int32_t *d_idx, double *d_dist) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         project_knn_device(ctx, dX, n, d, metric, k, iterations, d_shifts, d_idx, d_dist);
     });
@@ -365,6 +482,7 @@ int tsne_pairwise_affinities(tsne_ctx *ctx, const int64_t *row_ptr, const double
                              double perplexity, double *p_out) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(row_ptr && nrows >= 0, "bad CSR");
         const int64_t nnz = row_ptr[nrows] - row_ptr[0];
@@ -385,6 +503,7 @@ int tsne_joint_distribution(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t
     int64_t nnz = -1;
     int rc = guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(row_ptr && n >= 1 && row_ptr[0] == 0, "bad CSR");
         const int64_t nin = row_ptr[n];
@@ -418,6 +537,7 @@ int tsne_gradient(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, con
                   double *sumq_out, double *loss_out) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(row_ptr && Y && grad_out && n >= 1 && row_ptr[0] == 0, "bad arguments");
         TSNE_REQUIRE(metric >= 0 && metric <= 2, "unknown metric");
@@ -440,6 +560,7 @@ int tsne_gradient_c(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, c
                                      loss_out);
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         if (c != 3) fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
         TSNE_REQUIRE(row_ptr && Y && grad_out && n >= 1 && row_ptr[0] == 0, "bad arguments");
@@ -460,6 +581,7 @@ int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *gra
                           double *gains, double min_gain, double momentum, double learning_rate) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(grad && Y && upd && gains && n >= 0 && c >= 1, "bad arguments");
         const size_t ne = (size_t)(n * c);
@@ -478,6 +600,7 @@ int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *gra
 int tsne_center_embedding(tsne_ctx *ctx, int64_t n, int32_t c, double *Y) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(Y && n >= 1 && c >= 1 && c <= 8, "bad arguments");
         double *dY = upload(ctx, "h.Y", Y, (size_t)(n * c));
@@ -491,6 +614,7 @@ int tsne_init_working_set(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed, do
                           double *gains) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         TSNE_REQUIRE(Y && upd && gains && n >= 0 && c >= 1, "bad arguments");
         const size_t ne = (size_t)(n * c);
@@ -510,36 +634,51 @@ int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_p
                   double *loss_vals, int32_t loss_cap, int32_t *n_loss) {
     return guard([&] {
         check_ctx(ctx);
-        DeviceGuard g(ctx->device);
         TSNE_REQUIRE(params && row_ptr && Y && upd && gains && n >= 1 && row_ptr[0] == 0, "bad arguments");
         if (params->n_components != 2 && params->n_components != 3)
             fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
         const size_t C = (size_t)params->n_components;
         const int64_t nnz = row_ptr[n];
+        TSNE_REQUIRE(nnz == 0 || (col && P), "NULL buffer");
         for (int64_t e = 0; e < nnz; ++e)
             if (col[e] < 0 || col[e] >= n) fail(TSNE_ERR_ARG, "column index out of range");
-        // the full P on every rank; each rank computes its own label slice
-        int64_t *drp = upload(ctx, "h.rp", row_ptr, (size_t)n + 1);
-        int32_t *dc = upload(ctx, "h.col", col, (size_t)nnz);
-        double *dp = upload(ctx, "h.p", P, (size_t)nnz);
-        double *dY = upload(ctx, "h.Yopt", Y, (size_t)n * C);
-        double *du = upload(ctx, "h.updopt", upd, (size_t)n * C);
-        double *dn = upload(ctx, "h.gainsopt", gains, (size_t)n * C);
-        opt_setup(ctx, params, drp, dc, dp, n, dY, du, dn);
-        for (int32_t t = 1; t <= params->iterations; ++t) opt_step(ctx, t);
-        opt_sync(ctx);
-        download(ctx, Y, dY, (size_t)n * C);
-        download(ctx, upd, du, (size_t)n * C);
-        download(ctx, gains, dn, (size_t)n * C);
-        sync(ctx);
-        int32_t k = opt_losses(ctx, loss_keys, loss_vals, loss_cap);
-        if (n_loss) *n_loss = k;
+        // every rank gets the full P and working set and runs the same
+        // iterations on its own rows; in a group (one thread per rank, shared
+        // host buffers) rank 0 writes the results back
+        auto run = [&](tsne_ctx *c, int rank) {
+            int64_t *drp = upload(c, "h.rp", row_ptr, (size_t)n + 1);
+            int32_t *dc = upload(c, "h.col", col, (size_t)nnz);
+            double *dp = upload(c, "h.p", P, (size_t)nnz);
+            double *dY = upload(c, "h.Yopt", Y, (size_t)n * C);
+            double *du = upload(c, "h.updopt", upd, (size_t)n * C);
+            double *dn = upload(c, "h.gainsopt", gains, (size_t)n * C);
+            opt_setup(c, params, drp, dc, dp, n, dY, du, dn);
+            for (int32_t t = 1; t <= params->iterations; ++t) opt_step(c, t);
+            opt_sync(c);
+            if (rank != 0) {
+                sync(c);
+                return;
+            }
+            download(c, Y, dY, (size_t)n * C);
+            download(c, upd, du, (size_t)n * C);
+            download(c, gains, dn, (size_t)n * C);
+            sync(c);
+            int32_t k = opt_losses(c, loss_keys, loss_vals, loss_cap);
+            if (n_loss) *n_loss = k;
+        };
+        if (!ctx->group.empty()) {
+            run_group(ctx, run);
+            return;
+        }
+        DeviceGuard g(ctx->device);
+        run(ctx, 0);   // one process per rank: every process writes its own host buffers
     });
 }
 
 int tsne_dev_opt_sync(tsne_ctx *ctx) {
     return guard([&] {
         check_ctx(ctx);
+        ctx = primary(ctx);
         DeviceGuard g(ctx->device);
         opt_sync(ctx);
     });

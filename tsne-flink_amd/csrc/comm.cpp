@@ -1,22 +1,186 @@
-// comm.cpp -- RCCL (over xGMI) for the row-sharded multi-GPU path: one
-// process per GPU, the unique id shipped out of band by the caller.
-// Per optimizer iteration the traffic is an all-reduce of the zero-filled
-// (F, z) buffers holding each rank's cost-balanced BH slice, an all-reduce of
-// the 256-query bucket costs (n/256 integers), the all-gather of the updated
-// embedding slices, and every 10th iteration a one-double all-reduce of the
-// loss.
+// comm.cpp -- the collectives of the row-sharded multi-GPU path, behind one
+// interface with three backends:
+//   * RCCL over xGMI: one rank per GPU (one process per GPU, the unique id
+//     shipped out of band by the caller, or one thread per GPU of a
+//     tsne_ctx_create_multi group, communicators from ncclCommInitAll);
+//   * loopback: several ranks on ONE device, one host thread each, inside one
+//     process (tsne_ctx_create_multi with a repeated device id).  Collectives
+//     meet at a host barrier and copy through the shared device memory in a
+//     fixed rank order.  It executes the library's own world > 1 code path
+//     on a single GPU, which is how the multi-GPU optimizer is tested;
+//   * callbacks: collectives on host buffers supplied by the caller
+//     (tsne_ctx_init_comm_callbacks): the host dataflow's own exchange.
+// Per optimizer iteration the traffic is the all-gather of the owned slices
+// of the updated embedding (16 B per point, ragged slices) and an all-reduce
+// of the Z normaliser (one double); every 10th iteration one more double (the
+// loss); every relabel (25 iterations) an all-reduce of the 256-query bucket
+// costs and an all-gather of the momentum / gains slices.
 #include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <mutex>
 
 #include "common.hpp"
 
 namespace tsne {
 
 struct Comm {
-    ncclComm_t comm = nullptr;
+    virtual ~Comm() = default;
+    // in place: every rank's buf becomes the element-wise sum over ranks
+    virtual void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) = 0;
+    virtual void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) = 0;
+    // in place: rank r's bytes [off[r], off[r+1]) of buf are copied to every rank
+    virtual void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) = 0;
 };
 
-static void nccl_check(ncclResult_t r, const char *what) {
+namespace {
+
+void nccl_check(ncclResult_t r, const char *what) {
     if (r != ncclSuccess) fail(TSNE_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+struct RcclComm : Comm {
+    ncclComm_t comm = nullptr;
+    ~RcclComm() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override {
+        nccl_check(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, ctx->stream), "ncclAllReduce");
+    }
+    void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override {
+        nccl_check(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm, ctx->stream), "ncclAllReduce");
+    }
+    // ragged all-gather: one in-place broadcast per root, fused into one group
+    void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
+        uint8_t *b = static_cast<uint8_t *>(buf);
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        for (int r = 0; r < ctx->world; ++r) {
+            const size_t bytes = (size_t)(off[r + 1] - off[r]);
+            if (bytes == 0) continue;
+            nccl_check(ncclBroadcast(b + off[r], b + off[r], bytes, ncclUint8, r, comm, ctx->stream), "ncclBroadcast");
+        }
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    }
+};
+
+// Shared state of the ranks of one loopback group (one device).
+struct LoopGroup {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    bool aborted = false;
+    std::vector<void *> ptr;
+    explicit LoopGroup(int w) : world(w), ptr(w, nullptr) {}
+    // all ranks meet; throws on every rank once one rank has aborted
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (aborted) fail(TSNE_ERR_COMM, "loopback group aborted by another rank");
+        const uint64_t gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen || aborted; });
+            if (generation == gen) fail(TSNE_ERR_COMM, "loopback group aborted by another rank");
+        }
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+struct LoopComm : Comm {
+    std::shared_ptr<LoopGroup> g;
+    explicit LoopComm(std::shared_ptr<LoopGroup> grp) : g(std::move(grp)) {}
+
+    // publish this rank's pointer once its stream has produced the data
+    void publish(tsne_ctx *ctx, void *p) {
+        TSNE_HIP(hipStreamSynchronize(ctx->stream));
+        g->ptr[ctx->rank] = p;
+        g->barrier();
+    }
+    template <class T> void allreduce(tsne_ctx *ctx, T *buf, size_t count) {
+        if (count == 0) return;
+        publish(ctx, buf);
+        std::vector<T> acc(count, T(0)), tmp(count);
+        for (int r = 0; r < g->world; ++r) {   // fixed rank order: identical sums on every rank
+            TSNE_HIP(hipMemcpy(tmp.data(), g->ptr[r], sizeof(T) * count, hipMemcpyDeviceToHost));
+            for (size_t e = 0; e < count; ++e) acc[e] += tmp[e];
+        }
+        g->barrier();   // every rank has read every buffer before any is overwritten
+        TSNE_HIP(hipMemcpy(buf, acc.data(), sizeof(T) * count, hipMemcpyHostToDevice));
+    }
+    void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override { allreduce(ctx, buf, count); }
+    void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override { allreduce(ctx, buf, count); }
+    void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
+        publish(ctx, buf);
+        uint8_t *b = static_cast<uint8_t *>(buf);
+        for (int r = 0; r < g->world; ++r) {
+            if (r == ctx->rank || off[r + 1] == off[r]) continue;
+            const uint8_t *src = static_cast<const uint8_t *>(g->ptr[r]);
+            TSNE_HIP(hipMemcpy(b + off[r], src + off[r], (size_t)(off[r + 1] - off[r]), hipMemcpyDeviceToDevice));
+        }
+        g->barrier();
+    }
+};
+
+// Caller-supplied collectives on host buffers (tsne_ctx_init_comm_callbacks):
+// the host dataflow's own exchange (e.g. Flink's network stack, MPI, or
+// torch.distributed/gloo in the tests) carries the library's messages.  The
+// library stages each message through host memory.
+struct CallbackComm : Comm {
+    tsne_comm_ops ops{};
+    void *user = nullptr;
+    std::vector<uint8_t> host;
+    void check(int rc, const char *what) {
+        if (rc != 0) fail(TSNE_ERR_COMM, std::string(what) + " callback returned " + std::to_string(rc));
+    }
+    template <class T> T *stage_in(tsne_ctx *ctx, const T *dev, size_t bytes) {
+        if (host.size() < bytes) host.resize(bytes);
+        if (bytes) TSNE_HIP(hipMemcpyAsync(host.data(), dev, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        TSNE_HIP(hipStreamSynchronize(ctx->stream));
+        return reinterpret_cast<T *>(host.data());
+    }
+    void stage_out(tsne_ctx *ctx, void *dev, size_t bytes) {
+        if (bytes) TSNE_HIP(hipMemcpyAsync(dev, host.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+        TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override {
+        double *h = stage_in(ctx, buf, count * sizeof(double));
+        check(ops.allreduce_sum_f64(user, h, (int64_t)count), "allreduce_sum_f64");
+        stage_out(ctx, buf, count * sizeof(double));
+    }
+    void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override {
+        uint64_t *h = reinterpret_cast<uint64_t *>(stage_in(ctx, buf, count * sizeof(uint64_t)));
+        check(ops.allreduce_sum_u64(user, h, (int64_t)count), "allreduce_sum_u64");
+        stage_out(ctx, buf, count * sizeof(uint64_t));
+    }
+    void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
+        const size_t bytes = (size_t)off[ctx->world];
+        uint8_t *h = stage_in(ctx, static_cast<uint8_t *>(buf), bytes);
+        check(ops.allgatherv(user, h, off), "allgatherv");
+        stage_out(ctx, buf, bytes);
+    }
+};
+
+}  // namespace
+
+void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops *ops, void *user) {
+    TSNE_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+    TSNE_REQUIRE(ops && ops->allreduce_sum_f64 && ops->allreduce_sum_u64 && ops->allgatherv, "incomplete comm ops");
+    comm_destroy(ctx);
+    if (world == 1) return;
+    CallbackComm *c = new CallbackComm();
+    c->ops = *ops;
+    c->user = user;
+    ctx->comm = c;
+    ctx->rank = rank;
+    ctx->world = world;
 }
 
 void comm_unique_id(uint8_t *out) {
@@ -32,43 +196,68 @@ void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id) {
     if (world == 1) { ctx->rank = 0; ctx->world = 1; return; }
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    Comm *c = new Comm();
-    ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
-    if (r != ncclSuccess) {
-        delete c;
-        nccl_check(r, "ncclCommInitRank");
-    }
-    ctx->comm = c;
+    std::unique_ptr<RcclComm> c(new RcclComm());
+    nccl_check(ncclCommInitRank(&c->comm, world, uid, rank), "ncclCommInitRank");
+    ctx->comm = c.release();
     ctx->rank = rank;
     ctx->world = world;
 }
 
-void comm_destroy(tsne_ctx *ctx) {
-    if (ctx->comm) {
-        if (ctx->comm->comm) (void)ncclCommDestroy(ctx->comm->comm);
-        delete ctx->comm;
-        ctx->comm = nullptr;
+// Communicators for the contexts of one tsne_ctx_create_multi group: RCCL
+// (ncclCommInitAll) when every device is distinct, loopback when all are the
+// same device.
+void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback) {
+    const int world = (int)subs.size();
+    if (world == 1) return;
+    if (loopback) {
+        auto g = std::make_shared<LoopGroup>(world);
+        for (int r = 0; r < world; ++r) {
+            comm_destroy(subs[r]);
+            subs[r]->comm = new LoopComm(g);
+            subs[r]->rank = r;
+            subs[r]->world = world;
+        }
+        return;
     }
+    std::vector<ncclComm_t> comms(world);
+    std::vector<int> devs(world);
+    for (int r = 0; r < world; ++r) devs[r] = subs[r]->device;
+    nccl_check(ncclCommInitAll(comms.data(), world, devs.data()), "ncclCommInitAll");
+    for (int r = 0; r < world; ++r) {
+        comm_destroy(subs[r]);
+        RcclComm *c = new RcclComm();
+        c->comm = comms[r];
+        subs[r]->comm = c;
+        subs[r]->rank = r;
+        subs[r]->world = world;
+    }
+}
+
+// A rank of a loopback group failed: release the others from the barrier.
+void comm_abort(tsne_ctx *ctx) {
+    if (auto *lc = dynamic_cast<LoopComm *>(ctx->comm)) lc->g->abort();
+}
+
+void comm_destroy(tsne_ctx *ctx) {
+    delete ctx->comm;
+    ctx->comm = nullptr;
     ctx->rank = 0;
     ctx->world = 1;
 }
 
-void comm_allgather_bytes(tsne_ctx *ctx, const void *send, void *recv, size_t bytes_per_rank) {
+void comm_allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off_bytes) {
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
-    nccl_check(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, ctx->comm->comm, ctx->stream),
-               "ncclAllGather");
+    ctx->comm->allgatherv(ctx, buf, off_bytes);
 }
 
 void comm_allreduce_sum_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) {
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
-    nccl_check(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, ctx->comm->comm, ctx->stream),
-               "ncclAllReduce");
+    ctx->comm->allreduce_u64(ctx, buf, count);
 }
 
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count) {
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
-    nccl_check(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, ctx->comm->comm, ctx->stream),
-               "ncclAllReduce");
+    ctx->comm->allreduce_f64(ctx, buf, count);
 }
 
 }  // namespace tsne

@@ -145,6 +145,9 @@ struct tsne_ctx {
     tsne::OptState *opt = nullptr;
     tsne::StageTimers timers;
     int cu_count = 256;
+    // tsne_ctx_create_multi: the per-device contexts (ranks) of a group
+    // handle; host-buffer operators fan out over them, one thread per rank
+    std::vector<tsne_ctx *> group;
 };
 
 namespace tsne {
@@ -205,7 +208,11 @@ void opt_destroy(tsne_ctx *ctx);
 void comm_unique_id(uint8_t *out);
 void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id);
 void comm_destroy(tsne_ctx *ctx);
-void comm_allgather_bytes(tsne_ctx *ctx, const void *send, void *recv, size_t bytes_per_rank);
+void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback);
+void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops *ops, void *user);
+void comm_abort(tsne_ctx *ctx);
+// in place: rank r's bytes [off_bytes[r], off_bytes[r+1]) of buf reach every rank
+void comm_allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off_bytes);
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count);
 void comm_allreduce_sum_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count);
 

@@ -398,16 +398,16 @@ __device__ __forceinline__ bool summarise3(double h, double dx, double dy, doubl
 __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ pos, const int32_t *__restrict__ dupc,
                                                     const OctNode *__restrict__ nodes,
                                                     const int32_t *__restrict__ meta, double theta, double near_dmax,
-                                                    int64_t g0, int64_t g1, const int64_t *__restrict__ dbounds,
+                                                    int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
                                                     double *__restrict__ F, double *__restrict__ Z) {
     __shared__ int32_t sref[4][STACK3];
     __shared__ uint64_t smask[4][STACK3];
     __shared__ double4 tbuf[4][64];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t wid = (int64_t)blockIdx.x * 4 + w;
-    const int64_t s0 = dbounds ? dbounds[0] : g0, s1 = dbounds ? dbounds[1] : g1;
-    const int64_t s = g0 + wid * 64 + lane;
-    const bool valid = s >= s0 && s < s1;
+    const int64_t k = g0 + wid * 64 + lane;   // query slot -> sorted position (qlist: a rank's own queries)
+    const bool valid = k < g1;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
     if (__ballot(valid) == 0) return;
     const int root = meta[1];
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
@@ -608,11 +608,11 @@ static double oct_near_dmax(double theta) {
 }
 
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF, double *dz,
-                   const int64_t *dbounds) {
+                   const int32_t *qlist) {
     if (s1 <= s0) return;
     const int64_t waves = ceil_div(s1 - s0, 64);
     hipLaunchKernelGGL(oct_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.meta, theta, oct_near_dmax(theta), s0, s1, dbounds, dF, dz);
+                       t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

@@ -45,9 +45,10 @@ struct OctTree {
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n);
 // Octree of all n points of Y (n x 3, device).
 void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta);
-// Repulsion for the sorted queries [s0, s1) (dbounds: device {begin, end}
-// overriding them, nullable): F (n x 3, sorted order) and z written there.
+// Repulsion for the query slots [s0, s1) (sorted positions, or qlist[slot]:
+// a rank's own queries, ascending): F (n x 3, sorted order) and z written
+// at the sorted position.
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF,
-                   double *dz, const int64_t *dbounds = nullptr);
+                   double *dz, const int32_t *qlist = nullptr);
 
 }  // namespace tsne

@@ -31,27 +31,43 @@ namespace tsne {
 
 struct OptState {
     tsne_params p{};
-    int64_t n = 0, chunk = 0, npad = 0, r0 = 0, r1 = 0, nnz = 0;
-    // caller buffers (original order, n x 2)
+    int C = 2;
+    int64_t n = 0, nnz = 0;
+    // caller buffers (original order, n x C)
     double *Yu = nullptr, *updu = nullptr, *gainsu = nullptr;
-    // internal (label order): full CSR P and working set, double-buffered for relabeling
-    int64_t *rp[2] = {nullptr, nullptr};
-    int32_t *col[2] = {nullptr, nullptr};
-    double *val[2] = {nullptr, nullptr};
+    // the caller's P (original point order, every rank holds it), copied once
+    int64_t *rp0 = nullptr;
+    int32_t *col0 = nullptr;
+    double *val0 = nullptr;
+    // 2-D: this rank's rows (labels [L0, L1)) with columns in labels, rebuilt
+    // from P0 at every relabel; row pointer local (rpw[r] for label L0 + r)
+    int64_t *rpw = nullptr;
+    int32_t *colw = nullptr;
+    double *valw = nullptr;
+    // labels: working set in label order (full n on every rank; upd / gains
+    // are current on a rank only for its own labels between relabels)
     double *Y[2] = {nullptr, nullptr}, *upd[2] = {nullptr, nullptr}, *gains[2] = {nullptr, nullptr};
     int32_t *orig[2] = {nullptr, nullptr};   // label -> original index
+    int32_t *lab = nullptr;                  // original index -> label
+    int cur = 0;
+    std::vector<int64_t> own;                // world + 1 label cuts (identical on every rank)
+    int64_t L0 = 0, L1 = 0;
     int64_t *rowlen = nullptr;
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
+    int32_t *qlist = nullptr, *qcnt = nullptr, *qoff = nullptr;   // world > 1: this rank's BH queries
+    void *qscan_tmp = nullptr;
+    size_t qscan_tmp_bytes = 0;
+    unsigned long long *lscore = nullptr;    // locality_score counters
+    int relabels = 0, relabel_checks = 0;
 
-    int cur = 0;
-    double *Ynew = nullptr;   // npad x 2
-    double2 *F = nullptr;     // npad, sorted order
-    double2 *attr = nullptr;  // chunk: attraction of the owned rows
-    int64_t *bounds = nullptr;             // world + 1: BH query slices (device)
-    unsigned long long *bcost = nullptr;   // 256-query bucket costs of the last traversal
-    double *z = nullptr;      // npad, sorted order
-    double *scal = nullptr;   // [0] Z, [1] loss, [2..3] mean
+    double *Ynew = nullptr;   // n x C (label order)
+    double2 *F = nullptr;     // n, sorted order
+    double2 *attr = nullptr;  // owned rows
+    unsigned long long *bcost = nullptr;   // 256-position bucket costs of the last traversal
+    int64_t *bounds = nullptr;             // world + 1 (device): cost-balanced cuts
+    double *z = nullptr;      // n, sorted order
+    double *scal = nullptr;   // [0] Z, [1] loss, [2..4] mean
     double *part = nullptr;   // reduction partials
     double *part2 = nullptr;  // second-level partials (NPART)
     double *loss = nullptr;   // per loss slot
@@ -60,16 +76,15 @@ struct OptState {
     unsigned long long *visits = nullptr;
     BHTree tree;
     // 3-D embeddings (nComponents = 3, the SURVEY.md 8f octree extension):
-    // C = 3 uses the octree, F3 (npad x 3, sorted order) and attr3 (chunk x 3);
-    // no relabelling, no side stream, equal-count BH slices across ranks.
-    int C = 2;
+    // labels stay the original indices (no relabel); owned rows are read
+    // straight from P0; F3 (n x 3, sorted order) and attr3 (owned x 3).
     OctTree otree;
     double *F3 = nullptr, *attr3 = nullptr;
     bool profile = false;
     hipEvent_t ev[6] = {};
     // The attraction sums need only Y and P (not F or Z), so outside loss
-    // iterations they run on a second stream concurrently with the tree
-    // build and the BH traversal (latency-bound kernels that leave CUs idle).
+    // iterations they run on a second stream concurrently with the BH
+    // traversal (a latency-bound kernel that leaves CUs idle).
     hipStream_t side = nullptr;
     hipEvent_t ev_y = nullptr, ev_attr = nullptr;
     // per launch of the attraction kernel (ctx->timers "opt.attract"): its
@@ -350,49 +365,165 @@ __global__ void iota_i32(int32_t *p, int64_t n) {
     if (i < n) p[i] = (int32_t)i;
 }
 
-// dst[orig[i]] = src[i] (2 components)
-__global__ void scatter_to_user(const double *__restrict__ src, const int32_t *__restrict__ orig,
-                                int64_t n, double *__restrict__ dst) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t o = orig[i];
-    dst[2 * o] = src[2 * i];
-    dst[2 * o + 1] = src[2 * i + 1];
-}
-
-// new label s <- old label idx_sorted[s]: working set, label map, row lengths
-__global__ void relabel_state(const int32_t *__restrict__ order, int64_t n,
-                              const double *__restrict__ Y0, const double *__restrict__ u0,
-                              const double *__restrict__ g0, const int32_t *__restrict__ o0,
-                              const int64_t *__restrict__ rp0, double *__restrict__ Y1,
-                              double *__restrict__ u1, double *__restrict__ g1, int32_t *__restrict__ o1,
-                              int64_t *__restrict__ len) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s > n) return;
-    if (s == n) { len[n] = 0; return; }
-    const int64_t i = order[s];
-    Y1[2 * s] = Y0[2 * i]; Y1[2 * s + 1] = Y0[2 * i + 1];
-    u1[2 * s] = u0[2 * i]; u1[2 * s + 1] = u0[2 * i + 1];
-    g1[2 * s] = g0[2 * i]; g1[2 * s + 1] = g0[2 * i + 1];
-    o1[s] = o0[i];
-    len[s] = rp0[i + 1] - rp0[i];
-}
-
-// one wave per new row: copy the old row, columns renamed old -> new label
-__global__ void relabel_rows(const int32_t *__restrict__ order, const int32_t *__restrict__ inv, int64_t n,
-                             const int64_t *__restrict__ rp0, const int32_t *__restrict__ c0,
-                             const double *__restrict__ v0, const int64_t *__restrict__ rp1,
-                             int32_t *__restrict__ c1, double *__restrict__ v1) {
-    const int64_t s = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+// new label s <- old label order[s]: working set (C components) and the label
+// maps orig1 (label -> original point) and lab (original point -> label)
+__global__ void relabel_state(const int32_t *__restrict__ order, int64_t n, int C, const double *__restrict__ Y0,
+                              const double *__restrict__ u0, const double *__restrict__ g0,
+                              const int32_t *__restrict__ o0, double *__restrict__ Y1, double *__restrict__ u1,
+                              double *__restrict__ g1, int32_t *__restrict__ o1, int32_t *__restrict__ lab) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     const int64_t i = order[s];
-    const int64_t a = rp0[i], len = rp0[i + 1] - a, b = rp1[s];
+    for (int c = 0; c < C; ++c) {
+        Y1[C * s + c] = Y0[C * i + c];
+        u1[C * s + c] = u0[C * i + c];
+        g1[C * s + c] = g0[C * i + c];
+    }
+    const int32_t o = o0[i];
+    o1[s] = o;
+    lab[o] = (int32_t)s;
+}
+
+// Row lengths of the owned labels [L0, L1) from the caller's P (original order)
+__global__ void own_rowlen(const int32_t *__restrict__ orig, const int64_t *__restrict__ rp0, int64_t L0, int64_t L1,
+                           int64_t *__restrict__ len) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > L1 - L0) return;
+    if (r == L1 - L0) { len[r] = 0; return; }
+    const int64_t o = orig[L0 + r];
+    len[r] = rp0[o + 1] - rp0[o];
+}
+
+// One wave per owned row: the caller's row of its original point, columns
+// renamed into labels (entry order kept: the attraction sums run in the
+// reference's row order whatever the labelling).
+__global__ void own_rows(const int32_t *__restrict__ orig, const int32_t *__restrict__ lab,
+                         const int64_t *__restrict__ rp0, const int32_t *__restrict__ c0,
+                         const double *__restrict__ v0, int64_t L0, int64_t L1, const int64_t *__restrict__ rpw,
+                         int32_t *__restrict__ cw, double *__restrict__ vw) {
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (r >= L1 - L0) return;
+    const int64_t o = orig[L0 + r];
+    const int64_t a = rp0[o], len = rp0[o + 1] - a, b = rpw[r];
     for (int64_t e = lane_id(); e < len; e += 64) {
-        c1[b + e] = inv[c0[a + e]];
-        v1[b + e] = v0[a + e];
+        cw[b + e] = lab[c0[a + e]];
+        vw[b + e] = v0[a + e];
     }
 }
 
+// This rank's queries: the sorted positions whose label it owns, ascending
+// (a stable compaction: flags, block counts, scan, scatter).
+__global__ void qlist_count(const int32_t *__restrict__ idx_sorted, int64_t n, int64_t L0, int64_t L1,
+                            int32_t *__restrict__ bcnt) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool f = s < n && idx_sorted[s] >= L0 && idx_sorted[s] < L1;
+    __shared__ int wc[4];
+    const int c = __popcll(__ballot(f));
+    if (lane_id() == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+__global__ void qlist_fill(const int32_t *__restrict__ idx_sorted, int64_t n, int64_t L0, int64_t L1,
+                           const int32_t *__restrict__ boff, int32_t *__restrict__ qlist) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool f = s < n && idx_sorted[s] >= L0 && idx_sorted[s] < L1;
+    __shared__ int wc[4];
+    const uint64_t bal = __ballot(f);
+    if (lane_id() == 0) wc[threadIdx.x >> 6] = __popcll(bal);
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    int base = boff[blockIdx.x];
+    for (int k = 0; k < w; ++k) base += wc[k];
+    if (f) qlist[base + __popcll(bal & lanemask_lt())] = (int32_t)s;
+}
+
+// Z partial of a rank: sum of z over its query list (fixed order per block)
+__global__ void reduce_list_partial(const double *__restrict__ z, const int32_t *__restrict__ qlist, int64_t m,
+                                    double *__restrict__ part) {
+    __shared__ double sw[4];
+    double acc = 0.0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x)
+        acc += z[qlist[k]];
+    acc = wave_sum(acc);
+    if (lane_id() == 0) sw[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (sw[0] + sw[1]) + (sw[2] + sw[3]);
+}
+
+// ---- locality of the CSR attraction's gathers (relabel decisions)
+// Connected components (minimum original index) and BFS level from that
+// root over the symmetric P: fixpoint iterations, deterministic.
+__global__ void cc_pull(const int64_t *__restrict__ rp, const int32_t *__restrict__ col, int64_t n,
+                        int32_t *__restrict__ comp, int32_t *__restrict__ changed) {
+    const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (i >= n) return;
+    int32_t m = comp[i];
+    for (int64_t e = rp[i] + lane_id(); e < rp[i + 1]; e += 64) m = min(m, comp[col[e]]);
+    m = wave_min(m);
+    if (lane_id() == 0 && m < comp[i]) {
+        atomicMin(&comp[i], m);
+        changed[0] = 1;
+    }
+}
+__global__ void cc_jump(int32_t *__restrict__ comp, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    comp[i] = comp[comp[comp[i]]];
+}
+__global__ void level_init(const int32_t *__restrict__ comp, int64_t n, int32_t *__restrict__ lev) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) lev[i] = comp[i] == (int32_t)i ? 0 : INT32_MAX;
+}
+__global__ void level_pull(const int64_t *__restrict__ rp, const int32_t *__restrict__ col, int64_t n,
+                           int32_t *__restrict__ lev, int32_t *__restrict__ changed) {
+    const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (i >= n) return;
+    int32_t m = INT32_MAX;
+    for (int64_t e = rp[i] + lane_id(); e < rp[i + 1]; e += 64) m = min(m, lev[col[e]]);
+    m = wave_min(m);
+    if (lane_id() == 0 && m != INT32_MAX && m + 1 < lev[i]) {
+        atomicMin(&lev[i], m + 1);
+        changed[0] = 1;
+    }
+}
+__global__ void graph_keys(const int32_t *__restrict__ comp, const int32_t *__restrict__ lev, int64_t n,
+                           uint64_t *__restrict__ key, int32_t *__restrict__ val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    key[i] = ((uint64_t)(uint32_t)comp[i] << 24) | (uint64_t)min(lev[i], (1 << 24) - 1);
+    val[i] = (int32_t)i;
+}
+
+// Fraction of P's edges (a fixed sample of rows) whose endpoints lie within
+// `win` labels of each other: under the current labels (cnt[0]) and under the
+// Morton order of this iteration's tree (cnt[1]: label l -> inv[l]).
+__global__ void locality_score(const int64_t *__restrict__ rp0, const int32_t *__restrict__ c0,
+                               const int32_t *__restrict__ lab, const int32_t *__restrict__ inv, int64_t n,
+                               int64_t stride, int64_t nsamp, int64_t win, unsigned long long *__restrict__ cnt) {
+    const int64_t k = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (k >= nsamp) return;
+    const int64_t o = k * stride;
+    const int64_t li = lab[o], mi = inv[li];
+    unsigned long long a = 0, b = 0;
+    for (int64_t e = rp0[o] + lane_id(); e < rp0[o + 1]; e += 64) {
+        const int64_t lj = lab[c0[e]];
+        const int64_t da = li - lj, db = mi - (int64_t)inv[lj];
+        a += (da <= win && -da <= win);
+        b += (db <= win && -db <= win);
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane_id() == 0) { atomicAdd(cnt, a); atomicAdd(cnt + 1, b); }
+}
+
+// dst[orig[i]] = src[i], c components
+__global__ void scatter_to_user_c(const double *__restrict__ src, const int32_t *__restrict__ orig, int64_t n,
+                                  int32_t c, double *__restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = orig[i];
+    for (int k = 0; k < c; ++k) dst[c * o + k] = src[c * i + k];
+}
 
 // ---- 3-D (nComponents = 3) optimizer kernels
 // q = 1 / (1 + metric(y_i, y_j)) on 3-D points (TsneHelpers.scala:293)
@@ -484,15 +615,6 @@ __global__ __launch_bounds__(256) void combine_update3(int64_t r0, int64_t r1, c
         upd[o] = un;
         Ynew[o] = __dadd_rn(un, Y[o]);
     }
-}
-
-// dst[orig[i]] = src[i], c components
-__global__ void scatter_to_user_c(const double *__restrict__ src, const int32_t *__restrict__ orig, int64_t n,
-                                  int32_t c, double *__restrict__ dst) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t o = orig[i];
-    for (int k = 0; k < c; ++k) dst[c * o + k] = src[c * i + k];
 }
 
 static int64_t attract3_blocks(int64_t rows) { return std::max<int64_t>(1, std::min<int64_t>(8192, ceil_div(rows, 4))); }
@@ -712,6 +834,107 @@ void opt_destroy(tsne_ctx *ctx) {
     ctx->opt = nullptr;
 }
 
+// cuts of [0, n) into world equal label ranges
+static std::vector<int64_t> equal_cuts(int64_t n, int world) {
+    std::vector<int64_t> c(world + 1);
+    const int64_t chunk = ceil_div(n, world);
+    for (int r = 0; r <= world; ++r) c[r] = std::min<int64_t>(n, chunk * r);
+    return c;
+}
+
+// make every rank's upd / gains current for all labels (each rank updates
+// only its own labels between relabels): ragged all-gather of the slices
+static void gather_working_set(tsne_ctx *ctx, OptState *s) {
+    if (ctx->world == 1) return;
+    const int c = s->cur;
+    std::vector<int64_t> off(ctx->world + 1);
+    for (int r = 0; r <= ctx->world; ++r) off[r] = s->own[r] * s->C * (int64_t)sizeof(double);
+    comm_allgatherv(ctx, s->upd[c], off.data());
+    comm_allgatherv(ctx, s->gains[c], off.data());
+}
+
+// this rank's rows of P in the current labels (2-D)
+static void build_own_rows(tsne_ctx *ctx, OptState *s) {
+    hipStream_t st = ctx->stream;
+    const int64_t m = s->L1 - s->L0;
+    const int32_t *orig = s->orig[s->cur];
+    hipLaunchKernelGGL(own_rowlen, dim3(ceil_div(m + 1, 256)), dim3(256), 0, st, orig, s->rp0, s->L0, s->L1, s->rowlen);
+    size_t tb = s->scan_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, s->rowlen, s->rpw, (int)(m + 1), st));
+    if (m > 0)
+        hipLaunchKernelGGL(own_rows, dim3(ceil_div(m, 4)), dim3(256), 0, st, orig, s->lab, s->rp0, s->col0, s->val0,
+                           s->L0, s->L1, s->rpw, s->colw, s->valw);
+    TSNE_LAUNCH_CHECK();
+}
+
+// world > 1: the sorted positions of this rank's labels, ascending
+static void build_qlist(tsne_ctx *ctx, OptState *s, const int32_t *idx_sorted) {
+    hipStream_t st = ctx->stream;
+    const int64_t n = s->n, nb = ceil_div(n, 256);
+    hipLaunchKernelGGL(qlist_count, dim3(nb), dim3(256), 0, st, idx_sorted, n, s->L0, s->L1, s->qcnt);
+    size_t tb = s->qscan_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(s->qscan_tmp, tb, s->qcnt, s->qoff, (int)nb, st));
+    hipLaunchKernelGGL(qlist_fill, dim3(nb), dim3(256), 0, st, idx_sorted, n, s->L0, s->L1, s->qoff, s->qlist);
+    TSNE_LAUNCH_CHECK();
+}
+
+// Renumber labels: new label j holds old label order[j] (device); new cuts.
+static void relabel(tsne_ctx *ctx, OptState *s, const int32_t *order, const std::vector<int64_t> &cuts) {
+    hipStream_t st = ctx->stream;
+    const int a = s->cur, b = 1 - a;
+    gather_working_set(ctx, s);   // full upd / gains under the old cuts
+    hipLaunchKernelGGL(relabel_state, dim3(ceil_div(s->n, 256)), dim3(256), 0, st, order, s->n, s->C, s->Y[a],
+                       s->upd[a], s->gains[a], s->orig[a], s->Y[b], s->upd[b], s->gains[b], s->orig[b], s->lab);
+    TSNE_LAUNCH_CHECK();
+    s->cur = b;
+    s->own = cuts;
+    s->L0 = cuts[ctx->rank];
+    s->L1 = cuts[ctx->rank + 1];
+    build_own_rows(ctx, s);
+    ++s->relabels;
+}
+
+// Initial labels: P's connected components (smallest original index), then
+// the BFS level from that root, then the original index -- points that
+// share neighbourhoods in P get nearby labels, so each XCD's rows gather
+// their Y_j from a few components instead of the whole embedding while the
+// embedding itself is still unrelated to P (the first ~150 iterations, before
+// the Morton relabelling below takes over).  Deterministic fixpoints.
+static void graph_order(tsne_ctx *ctx, OptState *s, int32_t *order) {
+    hipStream_t st = ctx->stream;
+    Workspace &ws = ctx->ws;
+    const int64_t n = s->n;
+    int32_t *comp = ws.get<int32_t>("opt.g.comp", n);
+    int32_t *lev = ws.get<int32_t>("opt.g.lev", n);
+    int32_t *flag = ws.get<int32_t>("opt.g.flag", 1);
+    uint64_t *key = ws.get<uint64_t>("opt.g.key", n), *key2 = ws.get<uint64_t>("opt.g.key2", n);
+    int32_t *val = ws.get<int32_t>("opt.g.val", n);
+    hipLaunchKernelGGL(iota_i32, dim3(ceil_div(n, 256)), dim3(256), 0, st, comp, n);
+    auto fixpoint = [&](auto &&pass) {
+        for (int it = 0; it < 10000; ++it) {
+            int32_t h = 0;
+            TSNE_HIP(hipMemsetAsync(flag, 0, sizeof(int32_t), st));
+            pass();
+            TSNE_HIP(hipMemcpyAsync(&h, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+            TSNE_HIP(hipStreamSynchronize(st));
+            if (!h) return;
+        }
+        fail(TSNE_ERR_HIP, "graph ordering did not converge");
+    };
+    fixpoint([&] {
+        hipLaunchKernelGGL(cc_pull, dim3(ceil_div(n, 4)), dim3(256), 0, st, s->rp0, s->col0, n, comp, flag);
+        hipLaunchKernelGGL(cc_jump, dim3(ceil_div(n, 256)), dim3(256), 0, st, comp, n);
+    });
+    hipLaunchKernelGGL(level_init, dim3(ceil_div(n, 256)), dim3(256), 0, st, comp, n, lev);
+    fixpoint([&] { hipLaunchKernelGGL(level_pull, dim3(ceil_div(n, 4)), dim3(256), 0, st, s->rp0, s->col0, n, lev, flag); });
+    hipLaunchKernelGGL(graph_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, comp, lev, n, key, val);
+    size_t tb = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, val, order, (int)n, 0, 64, st));
+    void *tmp = ws.get<uint8_t>("opt.g.tmp", tb);
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key2, val, order, (int)n, 0, 64, st));
+    TSNE_LAUNCH_CHECK();
+}
+
 void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, const int32_t *d_col,
                const double *d_P, int64_t n, double *dY, double *dupd, double *dgains) {
     TSNE_REQUIRE(p != nullptr, "params is NULL");
@@ -719,6 +942,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
     TSNE_REQUIRE(n >= 1, "empty embedding");
     TSNE_REQUIRE(p->metric >= 0 && p->metric <= 2, "unknown metric");
+    TSNE_REQUIRE(n < (int64_t)INT32_MAX, "n must fit int32 point ids");
     hipStream_t st = ctx->stream;
     opt_destroy(ctx);
     OptState *s = new OptState();
@@ -726,11 +950,8 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->p = *p;
     s->C = p->n_components;
     const int C = s->C;
+    const int world = ctx->world;
     s->n = n;
-    s->chunk = ceil_div(n, ctx->world);
-    s->npad = s->chunk * ctx->world;
-    s->r0 = std::min<int64_t>(n, s->chunk * ctx->rank);
-    s->r1 = std::min<int64_t>(n, s->r0 + s->chunk);
     s->Yu = dY;
     s->updu = dupd;
     s->gainsu = dgains;
@@ -739,62 +960,83 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     TSNE_HIP(hipStreamSynchronize(st));
     s->nnz = nnz;
     Workspace &ws = ctx->ws;
+    s->rp0 = ws.get<int64_t>("opt.rp0", n + 1);
+    s->col0 = ws.get<int32_t>("opt.col0", nnz + 1);
+    s->val0 = ws.get<double>("opt.val0", nnz + 1);
+    TSNE_HIP(hipMemcpyAsync(s->rp0, d_row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->col0, d_col, sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, st));
+    TSNE_HIP(hipMemcpyAsync(s->val0, d_P, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
     for (int b = 0; b < 2; ++b) {
         const std::string k = std::to_string(b);
-        s->rp[b] = ws.get<int64_t>("opt.rp" + k, n + 1);
-        s->col[b] = ws.get<int32_t>("opt.col" + k, nnz + 1);
-        s->val[b] = ws.get<double>("opt.val" + k, nnz + 1);
-        s->Y[b] = ws.get<double>("opt.Y" + k, C * s->npad);
-        s->upd[b] = ws.get<double>("opt.upd" + k, C * s->npad);
-        s->gains[b] = ws.get<double>("opt.gains" + k, C * s->npad);
+        s->Y[b] = ws.get<double>("opt.Y" + k, C * n);
+        s->upd[b] = ws.get<double>("opt.upd" + k, C * n);
+        s->gains[b] = ws.get<double>("opt.gains" + k, C * n);
         s->orig[b] = ws.get<int32_t>("opt.orig" + k, n);
     }
+    s->lab = ws.get<int32_t>("opt.lab", n);
     s->cur = 0;
-    TSNE_HIP(hipMemcpyAsync(s->rp[0], d_row_ptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, st));
-    TSNE_HIP(hipMemcpyAsync(s->col[0], d_col, sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, st));
-    TSNE_HIP(hipMemcpyAsync(s->val[0], d_P, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
-    TSNE_HIP(hipMemsetAsync(s->Y[0], 0, sizeof(double) * C * s->npad, st));
     TSNE_HIP(hipMemcpyAsync(s->Y[0], dY, sizeof(double) * C * n, hipMemcpyDeviceToDevice, st));
     TSNE_HIP(hipMemcpyAsync(s->upd[0], dupd, sizeof(double) * C * n, hipMemcpyDeviceToDevice, st));
     TSNE_HIP(hipMemcpyAsync(s->gains[0], dgains, sizeof(double) * C * n, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(iota_i32, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->orig[0], n);
-    s->rowlen = ws.get<int64_t>("opt.rowlen", n + 1);
+    hipLaunchKernelGGL(iota_i32, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->lab, n);
+    s->own = equal_cuts(n, world);
+    s->L0 = s->own[ctx->rank];
+    s->L1 = s->own[ctx->rank + 1];
+    const int64_t rows_cap = n;   // owned rows (cost-balanced cuts may give one rank most of them)
+    s->rowlen = ws.get<int64_t>("opt.rowlen", rows_cap + 1);
     size_t tb = 0;
-    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->rowlen, s->rp[1], (int)(n + 1), st));
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, s->rowlen, s->rowlen, (int)(rows_cap + 1), st));
     s->scan_tmp_bytes = tb;
     s->scan_tmp = ws.get<uint8_t>("opt.scan_tmp", tb);
-
-    s->Ynew = ws.get<double>("opt.Ynew", C * s->npad);
-    s->F = ws.get<double2>("opt.F", s->npad);
-    s->attr = ws.get<double2>("opt.attr", s->chunk);
-    s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
-    s->bounds = ws.get<int64_t>("opt.bounds", ctx->world + 1);
-    {
-        std::vector<int64_t> b0(ctx->world + 1);
-        for (int r = 0; r <= ctx->world; ++r) b0[r] = std::min<int64_t>(n, s->chunk * r);
-        TSNE_HIP(hipMemcpyAsync(s->bounds, b0.data(), sizeof(int64_t) * b0.size(), hipMemcpyHostToDevice, st));
-        TSNE_HIP(hipStreamSynchronize(st));
-    }
-    s->z = ws.get<double>("opt.z", s->npad);
+    s->Ynew = ws.get<double>("opt.Ynew", C * n);
+    s->attr = ws.get<double2>("opt.attr", rows_cap);
+    s->F = ws.get<double2>("opt.F", n);
+    s->z = ws.get<double>("opt.z", n);
     s->scal = ws.get<double>("opt.scal", 8);
-    s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(s->chunk)));
+    s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(rows_cap)));
     s->part2 = ws.get<double>("opt.part2", NPART);
-    s->mpart = ws.get<double>("opt.mpart", 2 * ceil_div(s->chunk, 256) + 2);
+    s->mpart = ws.get<double>("opt.mpart", 2 * ceil_div(rows_cap, 256) + 2);
+    s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
+    s->bounds = ws.get<int64_t>("opt.bounds", world + 1);
+    s->lscore = ws.get<unsigned long long>("opt.lscore", 2);
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
     s->visits = ws.get<unsigned long long>("opt.visits", 16);
-    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * C * s->npad, st));
-    TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * s->npad, st));
-    TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * s->npad, st));
+    if (world > 1) {
+        const int64_t nb = ceil_div(n, 256);
+        s->qlist = ws.get<int32_t>("opt.qlist", n);
+        s->qcnt = ws.get<int32_t>("opt.qcnt", nb);
+        s->qoff = ws.get<int32_t>("opt.qoff", nb);
+        size_t qb = 0;
+        TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, qb, s->qcnt, s->qoff, (int)nb, st));
+        s->qscan_tmp_bytes = qb;
+        s->qscan_tmp = ws.get<uint8_t>("opt.qscan_tmp", qb);
+    }
+    TSNE_HIP(hipMemsetAsync(s->Ynew, 0, sizeof(double) * C * n, st));
+    TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * n, st));
+    TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * n, st));
     if (C == 3) {
         oct_alloc(ctx, s->otree, n);
-        s->F3 = ws.get<double>("opt.F3", 3 * (size_t)s->npad);
-        s->attr3 = ws.get<double>("opt.attr3", 3 * (size_t)s->chunk);
-        s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract3_blocks(s->chunk)));
-        TSNE_HIP(hipMemsetAsync(s->F3, 0, sizeof(double) * 3 * s->npad, st));
+        s->F3 = ws.get<double>("opt.F3", 3 * (size_t)n);
+        s->attr3 = ws.get<double>("opt.attr3", 3 * (size_t)rows_cap);
+        s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract3_blocks(rows_cap)));
+        TSNE_HIP(hipMemsetAsync(s->F3, 0, sizeof(double) * 3 * n, st));
     } else {
         bh_alloc(ctx, s->tree, n);
+        s->rpw = ws.get<int64_t>("opt.rpw", rows_cap + 1);
+        s->colw = ws.get<int32_t>("opt.colw", nnz + 1);
+        s->valw = ws.get<double>("opt.valw", nnz + 1);
+        // initial labels in P's graph order (TSNE_GRAPH_ORDER=0: the original order)
+        static const bool gorder = [] { const char *e = getenv("TSNE_GRAPH_ORDER"); return !(e && e[0] == '0'); }();
+        if (gorder && n >= 2) {
+            int32_t *order = ws.get<int32_t>("opt.g.order", n);
+            graph_order(ctx, s, order);
+            relabel(ctx, s, order, s->own);
+        } else {
+            build_own_rows(ctx, s);
+        }
     }
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
     {   // side stream (attraction); TSNE_SIDE_PRIO=high|low picks a stream priority
@@ -806,7 +1048,6 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
             TSNE_HIP(hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, v == "high" ? greatest : least));
         else
             TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-        if (getenv("TSNE_DEBUG_PRIO")) fprintf(stderr, "[prio] range least=%d greatest=%d side=%s\n", least, greatest, v.c_str());
     }
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_attr, hipEventDisableTiming));
@@ -815,36 +1056,65 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     TSNE_LAUNCH_CHECK();
 }
 
-// make every rank's copy of upd / gains current (each rank updates only its labels)
-static void gather_working_set(tsne_ctx *ctx, OptState *s) {
-    if (ctx->world == 1) return;
-    const int c = s->cur;
-    const int C = s->C;
-    comm_allgather_bytes(ctx, s->upd[c] + C * s->r0, s->upd[c], sizeof(double) * C * s->chunk);
-    comm_allgather_bytes(ctx, s->gains[c] + C * s->r0, s->gains[c], sizeof(double) * C * s->chunk);
-}
-
-// renumber labels into the Morton order of this iteration's tree
-static void relabel(tsne_ctx *ctx, OptState *s) {
+// Z = sum of z over all queries: locally (one rank) or this rank's partial
+// over its query list + an all-reduce of one double
+static void reduce_Z(tsne_ctx *ctx, OptState *s, const double *z) {
     hipStream_t st = ctx->stream;
-    const int64_t n = s->n;
-    const int a = s->cur, b = 1 - a;
-    gather_working_set(ctx, s);
-    hipLaunchKernelGGL(relabel_state, dim3(ceil_div(n + 1, 256)), dim3(256), 0, st, s->tree.idx_sorted, n,
-                       s->Y[a], s->upd[a], s->gains[a], s->orig[a], s->rp[a], s->Y[b], s->upd[b], s->gains[b],
-                       s->orig[b], s->rowlen);
-    size_t tb = s->scan_tmp_bytes;
-    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(s->scan_tmp, tb, s->rowlen, s->rp[b], (int)(n + 1), st));
-    hipLaunchKernelGGL(relabel_rows, dim3(ceil_div(n, 4)), dim3(256), 0, st, s->tree.idx_sorted, s->tree.inv, n,
-                       s->rp[a], s->col[a], s->val[a], s->rp[b], s->col[b], s->val[b]);
-    // (Sorting each relabelled row by column was measured: no change in the
-    // attraction's time, +5 ms per relabel -- not done.)
-    TSNE_LAUNCH_CHECK();
-    s->cur = b;
+    if (ctx->world == 1) {
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, z, s->n, 1, 0, s->part2);
+    } else {
+        hipLaunchKernelGGL(reduce_list_partial, dim3(NPART), dim3(256), 0, st, z, s->qlist, s->L1 - s->L0, s->part2);
+    }
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal, 0.0);
+    if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal, 1);
 }
 
-// One iteration of the 3-D (octree) optimizer: the opt_step sequence without
-// relabelling or the side stream; BH slices are the equal-count cuts of setup.
+// loss of this iteration (all ranks' partial sums) into its slot
+static void record_loss(tsne_ctx *ctx, OptState *s, int32_t t, int64_t blocks) {
+    hipStream_t st = ctx->stream;
+    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
+    if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
+    const int slot = t / 10 - 1;
+    if (slot >= 0 && slot < s->loss_slots) {
+        TSNE_HIP(hipMemcpyAsync(s->loss + slot, s->scal + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
+        s->loss_written[slot] = t;
+    }
+}
+
+// the updated embedding of every rank's labels on every rank
+static void gather_Ynew(tsne_ctx *ctx, OptState *s) {
+    std::vector<int64_t> off(ctx->world + 1);
+    for (int r = 0; r <= ctx->world; ++r) off[r] = s->own[r] * s->C * (int64_t)sizeof(double);
+    comm_allgatherv(ctx, s->Ynew, off.data());
+}
+
+static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
+    TSNE_HIP(hipEventRecord(s->ev[5], ctx->stream));
+    TSNE_HIP(hipEventSynchronize(s->ev[5]));
+    for (int k = 0; k < 5; ++k) {   // [3]: the attraction kernel alone, on its own stream
+        float ms = 0.f;
+        if (k != 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+        s->last_ms[k] = ms;
+    }
+    s->last_ms[3] = ctx->timers.ms("opt.attract").back();
+    if (s->C == 3) {
+        for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
+        return;
+    }
+    unsigned long long v[16] = {};
+    TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
+    static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
+    if (dbg)
+        fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu\n", t,
+                v[10], v[11], v[12], v[1], v[2]);
+}
+
+// One iteration of the 3-D (octree) optimizer: labels are the original
+// indices, rank r owns rows [L0, L1) of P0 and computes BH for exactly those
+// points (its query list in octree order); only Z, the loss and the updated
+// embedding cross ranks.
 static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     hipStream_t st = ctx->stream;
     const tsne_params &p = s->p;
@@ -860,60 +1130,68 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     oct_build(ctx, s->otree, Y, p.theta);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     if (ctx->world > 1) {
-        TSNE_HIP(hipMemsetAsync(s->F3, 0, sizeof(double) * 3 * n, st));
-        TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * n, st));
-        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z, s->bounds + ctx->rank);
+        build_qlist(ctx, s, s->otree.idx_sorted);
+        oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist);
     } else {
         oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z);
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
-    if (ctx->world > 1) {
-        comm_allreduce_sum_f64(ctx, s->F3, 3 * (size_t)n);
-        comm_allreduce_sum_f64(ctx, s->z, (size_t)n);
-    }
-    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
-    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
+    reduce_Z(ctx, s, s->z);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     ctx->timers.begin("opt.attract", st);
-    const int64_t blocks = attract3_launch(st, s->rp[0], s->col[0], s->val[0], s->r0, s->r1, Y, s->scal, p.metric,
-                                           ex, s->attr3, s->part, want_loss);
+    const int64_t blocks = attract3_launch(st, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex,
+                                           s->attr3, s->part, want_loss);
     ctx->timers.end("opt.attract", st);
     s->attract_iter.push_back({t, 1});
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
-    if (s->r1 > s->r0)
-        hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->r1 - s->r0, 256)), dim3(256), 0, st, s->r0, s->r1,
+    ctx->timers.begin("opt.update", st);
+    if (s->L1 > s->L0)
+        hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->L1 - s->L0, 256)), dim3(256), 0, st, s->L0, s->L1,
                            s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[0], s->gains[0],
                            p.min_gain, mom, p.learning_rate);
     TSNE_LAUNCH_CHECK();
-    if (want_loss) {
-        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
-        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
-        if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
-        const int slot = t / 10 - 1;
-        if (slot >= 0 && slot < s->loss_slots) {
-            TSNE_HIP(hipMemcpyAsync(s->loss + slot, s->scal + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
-            s->loss_written[slot] = t;
-        }
-    }
-    if (ctx->world > 1) comm_allgather_bytes(ctx, s->Ynew + 3 * s->r0, s->Ynew, sizeof(double) * 3 * s->chunk);
+    if (want_loss) record_loss(ctx, s, t, blocks);
+    if (ctx->world > 1) gather_Ynew(ctx, s);
     for (int k = 0; k < 3; ++k) {
-        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 3, k, s->part);
-        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
+        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 3, k, s->part2);
+        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 2 + k, (double)n);
     }
     hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, 3, s->scal + 2, Y);
     TSNE_HIP(hipMemcpyAsync(s->Yu, Y, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st));
+    ctx->timers.end("opt.update", st);
     TSNE_LAUNCH_CHECK();
-    if (s->profile) {
-        TSNE_HIP(hipEventRecord(s->ev[5], st));
-        TSNE_HIP(hipEventSynchronize(s->ev[5]));
-        for (int k = 0; k < 5; ++k) {
-            float ms = 0.f;
-            if (k != 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
-            s->last_ms[k] = ms;
-        }
-        s->last_ms[3] = ctx->timers.ms("opt.attract").back();
-        for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
+    if (s->profile) finish_profile(ctx, s, t);
+}
+
+// Relabel check (every RELABEL_EVERY iterations, 2-D): renumber the labels
+// into this iteration's Morton order when that order keeps more of P's edges
+// within a window of labels than the current one (identical decision on
+// every rank: the score reads only replicated data).  With several ranks the
+// new cuts balance the BH cost measured in this iteration (all-reduced
+// 256-position bucket costs); the qlist waves of the NEXT iterations follow.
+static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
+    hipStream_t st = ctx->stream;
+    const int64_t n = s->n;
+    const int64_t nsamp = std::min<int64_t>(n, 1 << 16), stride = std::max<int64_t>(1, n / nsamp);
+    const int64_t win = std::max<int64_t>(64, n / 64);
+    TSNE_HIP(hipMemsetAsync(s->lscore, 0, 2 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(locality_score, dim3(ceil_div(nsamp, 4)), dim3(256), 0, st, s->rp0, s->col0, s->lab,
+                       s->tree.inv, n, stride, nsamp, win, s->lscore);
+    unsigned long long sc[2] = {0, 0};
+    TSNE_HIP(hipMemcpyAsync(sc, s->lscore, sizeof(sc), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    ++s->relabel_checks;
+    static const int mode = [] { const char *e = getenv("TSNE_RELABEL"); return e ? atoi(e) : 1; }();   // 0 never, 2 always
+    const bool go = mode == 2 || (mode == 1 && sc[1] > sc[0]);
+    if (!go) return;
+    std::vector<int64_t> cuts = s->own;
+    if (ctx->world > 1) {
+        comm_allreduce_sum_u64(ctx, s->bcost, (size_t)ceil_div(n, 256));
+        bh_balance(ctx, s->bcost, n, ctx->world, s->bounds);
+        TSNE_HIP(hipMemcpyAsync(cuts.data(), s->bounds, sizeof(int64_t) * (ctx->world + 1), hipMemcpyDeviceToHost, st));
+        TSNE_HIP(hipStreamSynchronize(st));
     }
+    relabel(ctx, s, s->tree.idx_sorted, cuts);
 }
 
 void opt_step(tsne_ctx *ctx, int32_t t) {
@@ -932,28 +1210,26 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const double ex = (t <= n1 + n2) ? p.early_exaggeration : 1.0;
     const double mom = (t <= n1) ? p.initial_momentum : p.final_momentum;
     const int want_loss = (t % 10 == 0);
+    const bool check_relabel = t % RELABEL_EVERY == 0;
     const int64_t n = s->n;
-    const int c = s->cur;
-    double *Y = s->Y[c];
+    const int world = ctx->world;
+    double *Y = s->Y[s->cur];
     if (s->profile) {
         TSNE_HIP(hipMemsetAsync(s->visits, 0, 16 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
+    // attraction over this rank's rows (row pointer local to L0)
+    AttractArgs aa{s->rpw - s->L0, s->colw, s->valw, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr, s->part};
     // 0. attraction sums on the side stream (not in loss iterations: the KL
     // terms need Z), concurrent with the BH traversal (TSNE_OVERLAP=tree:
     // already with the tree build, whose short latency-bound kernels it then
     // stretches, e.g. morton_keys 15 -> 800 us)
-    AttractArgs aa{s->rp[c], s->col[c], s->val[c], s->r0, s->r1, Y, s->scal, p.metric, ex, s->attr, s->part};
     const bool overlap = !want_loss;
-    // TSNE_OVERLAP=bh: the side launch is issued after the BH launch (same
-    // dependency on the tree), so BH waves are dispatched first and the
-    // attraction fills the slots freed by BH's heavy-wave tail
     static const int ov_mode = [] {
         const char *e = getenv("TSNE_OVERLAP");
         const std::string v = e ? e : "";
         return v == "tree" ? 0 : v == "bh" ? 2 : 1;
     }();
-    const bool with_tree = ov_mode == 0;
     auto side_wait = [&] {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
         TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
@@ -967,37 +1243,28 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         s->attract_iter.push_back({t, 0});
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
-    if (overlap && with_tree) side_attract();
-    // 1. tree
+    if (overlap && ov_mode == 0) side_attract();
+    // 1. tree (identical on every rank)
     bh_build(ctx, s->tree, Y, p.theta);
     if (overlap && ov_mode == 1) side_attract();
     if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
-    // 2. repulsion for this rank's slice of the Morton-sorted points.  With
-    // several ranks the slices are cut by the previous iteration's measured
-    // cost (bucket costs all-reduced, identical cuts on every rank), and the
-    // (F, z) slices are combined by an all-reduce over zero-filled buffers.
-    const int64_t nb = ceil_div(n, 256);
-    if (ctx->world > 1) {
-        TSNE_HIP(hipMemsetAsync(s->F, 0, sizeof(double2) * n, st));
-        TSNE_HIP(hipMemsetAsync(s->z, 0, sizeof(double) * n, st));
-        TSNE_HIP(hipMemsetAsync(s->bcost, 0, sizeof(unsigned long long) * nb, st));
-        bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr,
-                     s->bounds + ctx->rank, s->bcost);
+    // 2. repulsion for this rank's points: all of them, or its query list
+    // (its labels' sorted positions, ascending: the waves stay Morton-local);
+    // bucket costs only where a relabel may re-cut the ownership
+    unsigned long long *bcost = (world > 1 && check_relabel) ? s->bcost : nullptr;
+    if (bcost) TSNE_HIP(hipMemsetAsync(bcost, 0, sizeof(unsigned long long) * ceil_div(n, 256), st));
+    if (world > 1) {
+        build_qlist(ctx, s, s->tree.idx_sorted);
+        bh_repulsion(ctx, s->tree, p.theta, 0, s->L1 - s->L0, s->F, s->z, s->profile ? s->visits : nullptr, s->qlist,
+                     bcost);
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
     if (overlap && ov_mode == 2) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
-    // 3. exchange + Z
-    if (ctx->world > 1) {
-        comm_allreduce_sum_f64(ctx, reinterpret_cast<double *>(s->F), 2 * (size_t)n);
-        comm_allreduce_sum_f64(ctx, s->z, (size_t)n);
-        comm_allreduce_sum_u64(ctx, s->bcost, (size_t)nb);
-        bh_balance(ctx, s->bcost, n, ctx->world, s->bounds);
-    }
-    hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->z, n, 1, 0, s->part);
-    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal, 0.0);
+    // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
+    reduce_Z(ctx, s, s->z);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 4. attraction (loss iterations: here, after Z) + update for owned rows
     int64_t blocks = 0;
@@ -1014,52 +1281,28 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // update + centre: combine_update (with the mean's block partials when one
     // rank holds every row), mean, centre + write-back of the caller's Y
     ctx->timers.begin("opt.update", st);
-    const bool fused_mean = ctx->world == 1;
-    combine_launch<1>(st, s->r0, s->r1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
+    const bool fused_mean = world == 1;
+    const int c = s->cur;
+    combine_launch<1>(st, s->L0, s->L1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
                       s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
-    if (want_loss) {
-        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
-        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
-        if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
-        const int slot = t / 10 - 1;
-        if (slot >= 0 && slot < s->loss_slots) {
-            TSNE_HIP(hipMemcpyAsync(s->loss + slot, s->scal + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
-            s->loss_written[slot] = t;
-        }
-    }
-    // 5. exchange + 6. centre
+    if (want_loss) record_loss(ctx, s, t, blocks);
+    // 5. exchange (all-gather of the owned slices) + 6. centre
     if (fused_mean) {
-        hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->r1 - s->r0, 256), (double)n,
+        hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256), (double)n,
                            s->scal + 2);
     } else {
-        comm_allgather_bytes(ctx, s->Ynew + 2 * s->r0, s->Ynew, sizeof(double) * 2 * s->chunk);
+        gather_Ynew(ctx, s);
         for (int k = 0; k < 2; ++k) {
-            hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 2, k, s->part);
-            hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part, NPART, s->scal + 2 + k, (double)n);
+            hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 2, k, s->part2);
+            hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 2 + k, (double)n);
         }
     }
     hipLaunchKernelGGL(center_scatter, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Ynew, s->orig[c], n, s->scal + 2,
                        Y, s->Yu);
     ctx->timers.end("opt.update", st);
     TSNE_LAUNCH_CHECK();
-    if (t % RELABEL_EVERY == 0) relabel(ctx, s);
-    if (s->profile) {
-        TSNE_HIP(hipEventRecord(s->ev[5], st));
-        TSNE_HIP(hipEventSynchronize(s->ev[5]));
-        for (int k = 0; k < 5; ++k) {   // [3]: the attraction kernel alone, on its own stream
-            float ms = 0.f;
-            if (k != 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
-            s->last_ms[k] = ms;
-        }
-        s->last_ms[3] = ctx->timers.ms("opt.attract").back();
-        unsigned long long v[16] = {};
-        TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
-        for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
-        static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
-        if (dbg)
-            fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu\n", t,
-                    v[10], v[11], v[12], v[1], v[2]);
-    }
+    if (check_relabel) maybe_relabel(ctx, s);
+    if (s->profile) finish_profile(ctx, s, t);
 }
 
 // Write upd / gains (and Y) back to the caller's buffers in the original order.

@@ -24,6 +24,13 @@ class Params(C.Structure):
                 ("theta", C.c_double), ("min_gain", C.c_double)]
 
 
+class CommOps(C.Structure):
+    """tsne_comm_ops: host-buffer collectives supplied by the caller."""
+    _fields_ = [("allreduce_sum_f64", C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64)),
+                ("allreduce_sum_u64", C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.c_int64)),
+                ("allgatherv", C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64)))]
+
+
 P = C.c_void_p
 I32, I64, D, U64 = C.c_int32, C.c_int64, C.c_double, C.c_uint64
 PI32, PI64, PD = C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_double)
@@ -38,6 +45,7 @@ SIGNATURES = {
     "tsne_balance_cuts": (C.c_int, [P, I64, I64, I32, I32, P]),
     "tsne_dev_balance_cuts": (C.c_int, [P, P, I64, I32, P]),
     "tsne_ctx_create": (C.c_int, [I32, C.POINTER(P)]),
+    "tsne_ctx_create_multi": (C.c_int, [P, I32, C.POINTER(P)]),
     "tsne_ctx_destroy": (C.c_int, [P]),
     "tsne_ctx_set_stream": (C.c_int, [P, P]),
     "tsne_ctx_stream": (P, [P]),
@@ -45,6 +53,7 @@ SIGNATURES = {
     "tsne_comm_unique_id": (C.c_int, [C.c_char_p]),
     "tsne_ctx_init_comm": (C.c_int, [P, I32, I32, C.c_char_p]),
     "tsne_ctx_rank": (C.c_int, [P, PI32, PI32]),
+    "tsne_ctx_init_comm_callbacks": (C.c_int, [P, I32, I32, P, P]),
     "tsne_knn": (C.c_int, [P, P, I64, I32, I32, I32, I64, I64, P, P]),
     "tsne_pairwise_affinities": (C.c_int, [P, P, P, I64, D, P]),
     "tsne_project_knn": (C.c_int, [P, P, I64, I32, I32, I32, I32, P, P, P]),

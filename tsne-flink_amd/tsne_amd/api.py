@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import METRICS, UNIQUE_ID_BYTES, Params, check, lib
+from ._lib import METRICS, UNIQUE_ID_BYTES, CommOps, Params, check, lib
 
 
 def _ptr(a):
@@ -61,6 +61,21 @@ class Context:
         self._h = C.c_void_p()
         check(lib().tsne_ctx_create(device, C.byref(self._h)))
 
+    @classmethod
+    def multi(cls, devices):
+        """tsne_ctx_create_multi: one handle over several ranks (distinct GPUs over
+        RCCL, or the same GPU repeated = in-process loopback ranks)."""
+        self = cls.__new__(cls)
+        self._h = C.c_void_p()
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        check(lib().tsne_ctx_create_multi(_ptr(devs), len(devs), C.byref(self._h)))
+        return self
+
+    def rank_world(self):
+        r, w = C.c_int32(), C.c_int32()
+        check(lib().tsne_ctx_rank(self._h, C.byref(r), C.byref(w)))
+        return r.value, w.value
+
     def close(self):
         if self._h:
             lib().tsne_ctx_destroy(self._h)
@@ -91,6 +106,39 @@ class Context:
 
     def init_comm(self, rank, world, uid):
         check(lib().tsne_ctx_init_comm(self._h, rank, world, uid))
+
+    def init_comm_callbacks(self, rank, world, allreduce_sum, allgatherv):
+        """tsne_ctx_init_comm_callbacks: the library's collectives carried by the
+        caller.  allreduce_sum(ndarray) sums a float64 / uint64 array over the ranks
+        in place; allgatherv(ndarray_u8, offsets) makes rank r's bytes
+        [off[r], off[r+1]) reach every rank, in place."""
+        def f64(_, buf, count):
+            try:
+                allreduce_sum(np.ctypeslib.as_array(buf, shape=(count,)))
+                return 0
+            except Exception:   # noqa: BLE001 -- reported to the library as a failed collective
+                return 1
+
+        def u64(_, buf, count):
+            try:
+                allreduce_sum(np.ctypeslib.as_array(buf, shape=(count,)))
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+
+        def agv(_, buf, off):
+            try:
+                o = np.ctypeslib.as_array(off, shape=(world + 1,)).copy()
+                allgatherv(np.ctypeslib.as_array(C.cast(buf, C.POINTER(C.c_uint8)), shape=(int(o[-1]),)), o)
+                return 0
+            except Exception:   # noqa: BLE001
+                return 1
+        ops = CommOps()
+        ops.allreduce_sum_f64 = CommOps._fields_[0][1](f64)
+        ops.allreduce_sum_u64 = CommOps._fields_[1][1](u64)
+        ops.allgatherv = CommOps._fields_[2][1](agv)
+        self._comm_ops = ops   # the callbacks must outlive the context's use of them
+        check(lib().tsne_ctx_init_comm_callbacks(self._h, rank, world, C.byref(ops), None))
 
     def set_stream(self, stream_ptr):
         check(lib().tsne_ctx_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
