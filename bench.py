@@ -70,12 +70,11 @@ def parse():
 
 
 def gmm(n, d, seed, device):
-    """C3 generator: 10 centres ~ N(0, 5^2 I), within-blob N(0, I), fp32-rounded."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    centers = torch.randn(10, d, generator=g, device=device, dtype=torch.float64) * 5.0
-    lab = torch.randint(0, 10, (n,), generator=g, device=device)
-    X = centers[lab] + torch.randn(n, d, generator=g, device=device, dtype=torch.float64)
-    return X.float().double().contiguous()
+    """C3 generator (tests/configs.py c3_torch): 10 centres ~ N(0, 5^2 I),
+    within-blob N(0, I), fp32-rounded -- the same data the full-size parity
+    test (tests/test_gpu_configs.py) checks."""
+    import configs
+    return configs.c3_torch(n, d, seed, device)
 
 
 def sync_barrier(world):

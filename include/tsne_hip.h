@@ -179,6 +179,14 @@ int tsne_gradient(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, con
 int tsne_gradient_c(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, const double *P, int64_t n,
                     int32_t c, const double *Y, int32_t metric, double theta, double exaggeration,
                     double *grad_out, double *sumq_out, double *loss_out);
+/* QuadTree.computeRepulsiveForce (QuadTree.scala:123-152; tree built as in
+ * TsneHelpers.scala:227-256) for every point: F_out (n x c, the repulsive
+ * force sum before the 1/Z normalisation) and z_out (n, the point's sumQ
+ * contribution; Z = their sum, TsneHelpers.scala:266), original order.
+ * c = 2, or 3 for the octree extension. */
+int tsne_repulsion(tsne_ctx *ctx, const double *Y, int64_t n, int32_t c, double theta, double *F_out,
+                   double *z_out);
+
 /* updateEmbedding (TsneHelpers.scala:341-369), in place on Y, upd, gains. */
 int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *grad, double *Y,
                           double *upd, double *gains, double min_gain, double momentum,
@@ -209,6 +217,8 @@ int tsne_dev_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t 
                  int32_t k, int64_t q0, int64_t q1, int32_t *d_idx, double *d_dist);
 int tsne_dev_project_knn(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metric, int32_t k,
                          int32_t iterations, const double *d_shifts, int32_t *d_idx, double *d_dist);
+int tsne_dev_repulsion(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, double theta, double *d_F,
+                       double *d_z);
 int tsne_dev_pairwise_affinities(tsne_ctx *ctx, const int64_t *d_row_ptr, const double *d_dist,
                                  int64_t nrows, double perplexity, double *d_p);
 /* Fixed-k conditional rows (row i = entries [i*k, (i+1)*k)), symmetrised into

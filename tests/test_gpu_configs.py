@@ -1,0 +1,247 @@
+"""Every BASELINE.json config at its full size, against the oracle.
+
+Full-size runs are checked where the oracle finishes in seconds -- sampled
+query rows / gradient rows of the real pipeline, plus size-independent
+identities -- and end to end where the whole problem is small (C1):
+
+  C1  2,000 x 50, perplexity 30, 300 iterations, theta 0.25, lr 1000: the
+      native CLI end to end (COO file in, CSV + loss file out) against the
+      oracle pipeline from the same seeded Y0 (loss keys, early KL at 1 %, the
+      final KL inside the oracle's own perturbation ensemble: DESIGN.md 4);
+  C2  70,000 x 784 MNIST-shaped, theta 0.5, T = 1000;
+  C3  1,000,000 x 128 GMM, theta 0.5, T = 1000 (the bench workload);
+  C4  500,000 x 300 sparse, cosine, nComponents 3 (octree extension);
+      each: kNN rows bit-exact (256 contiguous query rows vs oracle_knn),
+      affinity rows at 1e-12, joint rows (pattern exact, values 1e-13
+      relative) against a restatement of jointDistribution on the sampled
+      rows, and at snapshots of the real optimizer trajectory the per-point
+      repulsion (z at BH_NEAR_TOL = 1e-6 relative, the gradient of a row block
+      at 1e-4 x max|grad|: north_star), Z == sum of the per-point z, and the
+      KL loss over all rows at 1e-9 (the oracle's attraction + loss with the
+      same Z).
+"""
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import configs as CF
+import oracle_ctypes as O
+import tsne_amd as T
+from tsne_amd.api import default_params
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+CLI = ROOT / "tsne-flink_amd" / "tsne_hip"
+THREADS = 16
+NEAR_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+def exaggeration(t, T_=1000):
+    return 4.0 if t <= min(T_, 20) + min(max(T_ - 20, 0), 81) else 1.0
+
+
+# ------------------------------------------------------------------ helpers
+def check_knn_rows(X_host, idx, dist, k, metric, q0, nq=256):
+    oi, od = O.knn(X_host, k, metric, q0=q0, q1=q0 + nq, threads=THREADS)
+    assert np.array_equal(idx[q0:q0 + nq], oi), "kNN ids"
+    assert np.array_equal(np.isnan(dist[q0:q0 + nq]), np.isnan(od))
+    assert np.array_equal(np.nan_to_num(dist[q0:q0 + nq]), np.nan_to_num(od)), "kNN distances"
+
+
+def check_affinity_rows(dist, p, perplexity, rows):
+    k = dist.shape[1]
+    rp = np.arange(0, len(rows) * k + 1, k, dtype=np.int64)
+    po, _ = O.affinities(rp, dist[rows].ravel(), perplexity)
+    assert np.abs(p[rows].ravel() - po).max() <= 1e-12
+
+
+def check_joint_rows(idx, p, orp, oc, ov, rows):
+    """jointDistribution (TsneHelpers.scala:182-196) restated for single rows:
+    J_ij = p_j|i + p_i|j over the union pattern, P = J / sum(J), sum(J) = 2 sum(p)."""
+    tot = 2.0 * p.sum()
+    flat_i = idx.ravel()
+    for i in rows:
+        want = {}
+        for j, v in zip(idx[i].tolist(), p[i].tolist()):
+            want[j] = want.get(j, 0.0) + v
+        for e in np.nonzero(flat_i == i)[0].tolist():
+            j = e // idx.shape[1]
+            want[j] = want.get(j, 0.0) + p.ravel()[e]
+        a, b = orp[i], orp[i + 1]
+        got = dict(zip(oc[a:b].tolist(), ov[a:b].tolist()))
+        assert set(got) == set(want), i
+        assert list(oc[a:b]) == sorted(want), i          # rows sorted by column
+        for j, v in want.items():
+            assert abs(got[j] - v / tot) <= 1e-13 * (v / tot), (i, j)
+
+
+def check_gradient_snapshot(ctx, P, Y, theta, ex, metric, r0, nr, c=2, loss=True):
+    rp, col, val = P
+    n = Y.shape[0]
+    F, z = ctx.repulsion(Y, theta)
+    g, Z, L = ctx.gradient(rp, col, val, Y, theta, metric, exaggeration=ex, want_loss=loss)
+    assert abs(Z - z.sum()) <= 1e-12 * Z, (Z, z.sum())
+    Q = np.ascontiguousarray(Y[r0:r0 + nr])
+    if c == 2:
+        rep_o, z_o = O.repulsion_queries(Y, theta, Q, threads=THREADS)
+    else:
+        rep_o, z_o = O.repulsion3_queries(Y, theta, Q, threads=THREADS)
+    assert np.abs(z[r0:r0 + nr] - z_o).max() <= NEAR_TOL * z_o.max(), "per-point z"
+    rep = np.zeros((n, c))
+    rep[r0:r0 + nr] = rep_o
+    attr = O.attraction_rows if c == 2 else O.attraction3_rows
+    g_o, _ = attr(rp, col, val, Y, rep, Z, r0, r0 + nr, metric=metric, exaggeration=ex)
+    assert np.abs(g[r0:r0 + nr] - g_o).max() <= 1e-4 * np.abs(g_o).max(), "gradient rows"
+    if loss:
+        _, l_o = attr(rp, col, val, Y, np.zeros((n, c)), Z, 0, n, metric=metric, exaggeration=ex, want_loss=True)
+        assert abs(L - l_o) <= 1e-9 * abs(l_o), (L, l_o)
+
+
+def pipeline(ctx, Xd, k, metric, perplexity):
+    """kNN -> affinities -> joint on the device (the bench's path); host copies."""
+    n = Xd.shape[0]
+    kk = min(k, n - 1)
+    dev = Xd.device
+    idx = torch.empty((n, kk), dtype=torch.int32, device=dev)
+    dist = torch.empty((n, kk), dtype=torch.float64, device=dev)
+    ctx.dev_knn(Xd, k, metric, 0, n, idx, dist)
+    rp = torch.arange(0, n * kk + 1, kk, dtype=torch.int64, device=dev)
+    p = torch.empty_like(dist)
+    ctx.dev_affinities(rp, dist, n, perplexity, p)
+    cap = 2 * n * kk
+    orp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    oc = torch.empty(cap, dtype=torch.int32, device=dev)
+    ov = torch.empty(cap, dtype=torch.float64, device=dev)
+    nnz = ctx.dev_joint(rp, idx, p, n, cap, orp, oc, ov)
+    ctx.synchronize()
+    host = dict(idx=idx.cpu().numpy(), dist=dist.cpu().numpy(), p=p.cpu().numpy(),
+                P=(orp.cpu().numpy(), oc[:nnz].cpu().numpy(), ov[:nnz].cpu().numpy()))
+    return host, (orp, oc[:nnz], ov[:nnz])
+
+
+def run_schedule(ctx, Pd, n, c, params, snaps, seed=0, stop=None):
+    """The device optimizer over the real schedule; host copies of Y after the
+    iterations in `snaps`."""
+    dev = Pd[0].device
+    Yh, uh, gh = ctx.initWorkingSet(n, c, seed=seed)
+    Y = torch.from_numpy(Yh).to(dev)
+    u = torch.from_numpy(uh).to(dev)
+    g = torch.from_numpy(gh).to(dev)
+    ctx.dev_opt_setup(params, *Pd, n, Y, u, g)
+    out = {}
+    for t in range(1, (stop or params.iterations) + 1):
+        ctx.dev_opt_step(t)
+        if t in snaps:
+            ctx.synchronize()
+            out[t] = Y.cpu().numpy().copy()
+    return out, ctx.dev_opt_losses()
+
+
+def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, grad_rows, q0, stop=None):
+    n = Xd.shape[0]
+    host, Pd = pipeline(ctx, Xd, k, metric, perplexity)
+    check_knn_rows(X_host, host["idx"], host["dist"], k, metric, q0)
+    rows = np.arange(q0, q0 + 64)
+    check_affinity_rows(host["dist"], host["p"], perplexity, rows)
+    check_joint_rows(host["idx"], host["p"], *host["P"], rows[:16])
+    del host["idx"], host["dist"], host["p"]
+    params = default_params(iterations=T_, theta=theta, metric=metric, n_components=c)
+    Ys, losses = run_schedule(ctx, Pd, n, c, params, set(snaps), stop=stop)
+    for t, nr in snaps.items():
+        r0 = grad_rows
+        check_gradient_snapshot(ctx, host["P"], Ys[t], theta, exaggeration(t + 1, T_), metric, r0, nr, c=c,
+                                loss=(t == max(snaps)))
+    return losses
+
+
+# ------------------------------------------------------------------- C1
+def parse_loss_file(text):
+    return {int(k): float(v) for k, v in re.findall(r"(\d+)=([-+0-9.eE]+|NaN)", text)}
+
+
+def test_c1_cli_end_to_end_matches_oracle(ctx, tmp_path):
+    """configs[0]: the reference's CPU-runnable case, through the native CLI
+    with Tsne.main's flags and file formats."""
+    X = CF.c1()
+    n, d = X.shape
+    (tmp_path / "in.csv").write_text(CF.to_coo_lines(X))
+    r = subprocess.run([str(CLI), "--input", "in.csv", "--output", "out.csv", "--dimension", str(d),
+                        "--knnMethod", "bruteforce", "--metric", "sqeuclidean", "--perplexity", "30",
+                        "--iterations", "300", "--loss", "loss.txt"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = np.array([[float(v) for v in l.split(",")] for l in (tmp_path / "out.csv").read_text().splitlines()])
+    assert np.array_equal(out[:, 0], np.arange(n))
+    lg = parse_loss_file((tmp_path / "loss.txt").read_text())
+    # the oracle pipeline from the same Y0 (the CLI's --randomState 0 stream)
+    oi, od = O.knn(X, 90, threads=THREADS)
+    rp = np.arange(0, n * 90 + 1, 90, dtype=np.int64)
+    po, _ = O.affinities(rp, od.ravel(), 30.0)
+    P = O.joint(rp, oi.ravel(), po, n)
+    Y0, _, _ = ctx.initWorkingSet(n, 2, seed=0)
+    runs = []
+    for s in range(8):
+        Yo = Y0 * (1 + (0.0 if s == 0 else 1e-15) * np.random.default_rng(s).normal(size=Y0.shape))
+        runs.append(O.optimize(*P, Yo, np.zeros_like(Y0), np.ones_like(Y0), learning_rate=1000.0, iterations=300,
+                               theta=0.25, threads=THREADS))
+    lo = runs[0]
+    assert sorted(lg) == sorted(lo) == list(range(10, 301, 10))
+    for t in (10, 20, 30, 40, 50):
+        assert abs(lg[t] - lo[t]) <= 0.01 * abs(lo[t]), (t, lg[t], lo[t])
+    final = np.array([r_[300] for r_ in runs])
+    mu, sd = final.mean(), final.std()
+    assert abs(lg[300] - mu) <= 4.0 * sd + 0.01 * abs(mu), (lg[300], final)
+
+
+def test_c1_library_stages_match_oracle(ctx):
+    X = CF.c1()
+    n = X.shape[0]
+    gi, gd = ctx.kNearestNeighbors(X, 90)
+    oi, od = O.knn(X, 90, threads=THREADS)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+    rp = np.arange(0, n * 90 + 1, 90, dtype=np.int64)
+    p = ctx.pairwiseAffinities(rp, gd.ravel(), 30.0)
+    po, _ = O.affinities(rp, od.ravel(), 30.0)
+    assert np.abs(p - po).max() <= 1e-12
+    a = ctx.jointDistribution(rp, gi.ravel(), p, n)
+    b = O.joint(rp, oi.ravel(), po, n)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.abs(a[2] - b[2]).max() <= 1e-15
+
+
+# ------------------------------------------------------------------- C2
+def test_c2_mnist_shaped_full_size(ctx):
+    X = CF.c2()
+    Xd = torch.from_numpy(X).cuda()
+    losses = full_config(ctx, Xd, X, 90, "sqeuclidean", 30.0, 0.5, 1000, 2,
+                         snaps={1: 32, 100: 64, 300: 64, 1000: 64}, grad_rows=40_000, q0=12_345)
+    assert sorted(losses) == list(range(10, 1001, 10))
+    assert all(np.isfinite(v) for v in losses.values())
+
+
+# ------------------------------------------------------------------- C3
+def test_c3_gmm_1m_full_size(ctx):
+    Xd = CF.c3_torch()
+    X = Xd.cpu().numpy()
+    losses = full_config(ctx, Xd, X, 90, "sqeuclidean", 30.0, 0.5, 1000, 2,
+                         snaps={1: 16, 200: 64, 400: 64, 1000: 64}, grad_rows=654_321, q0=123_456)
+    assert sorted(losses) == list(range(10, 1001, 10))
+    assert all(np.isfinite(v) for v in losses.values())
+
+
+# ------------------------------------------------------------------- C4
+def test_c4_sparse_cosine_3d_full_size(ctx):
+    X = CF.c4()
+    Xd = torch.from_numpy(X).cuda()
+    full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 3: 16}, grad_rows=250_000,
+                q0=77_777, stop=3)

@@ -577,6 +577,36 @@ int tsne_gradient_c(tsne_ctx *ctx, const int64_t *row_ptr, const int32_t *col, c
     });
 }
 
+int tsne_repulsion(tsne_ctx *ctx, const double *Y, int64_t n, int32_t c, double theta, double *F_out,
+                   double *z_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        ctx = primary(ctx);
+        DeviceGuard g(ctx->device);
+        if (c != 2 && c != 3) fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
+        TSNE_REQUIRE(Y && F_out && z_out && n >= 1, "bad arguments");
+        double *dY = upload(ctx, "h.Y", Y, (size_t)n * c);
+        double *dF = ctx->ws.get<double>("h.repF", (size_t)n * c);
+        double *dz = ctx->ws.get<double>("h.repz", (size_t)n);
+        repulsion_device(ctx, dY, n, c, theta, dF, dz);
+        download(ctx, F_out, dF, (size_t)n * c);
+        download(ctx, z_out, dz, (size_t)n);
+        sync(ctx);
+    });
+}
+
+int tsne_dev_repulsion(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, double theta, double *d_F,
+                       double *d_z) {
+    return guard([&] {
+        check_ctx(ctx);
+        ctx = primary(ctx);
+        DeviceGuard g(ctx->device);
+        if (c != 2 && c != 3) fail(TSNE_ERR_UNSUPPORTED, "n_components must be 2 (quadtree) or 3 (octree extension)");
+        TSNE_REQUIRE(dY && d_F && d_z && n >= 1, "bad arguments");
+        repulsion_device(ctx, dY, n, c, theta, d_F, d_z);
+    });
+}
+
 int tsne_update_embedding(tsne_ctx *ctx, int64_t n, int32_t c, const double *grad, double *Y, double *upd,
                           double *gains, double min_gain, double momentum, double learning_rate) {
     return guard([&] {

@@ -190,6 +190,8 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
                      double theta, double exaggeration, double *d_grad, double *h_sumq,
                      double *h_loss);
 
+void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, double theta, double *dF,
+                      double *dz);
 void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col, const double *d_P, int64_t n,
                       const double *dY, int32_t metric, double theta, double exaggeration, double *d_grad,
                       double *h_sumq, double *h_loss);

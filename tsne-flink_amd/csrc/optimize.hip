@@ -782,6 +782,43 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     if (h_loss) *h_loss = hs[1];
 }
 
+// per-point results from sorted order back to the original order
+__global__ void unsort_fz(const int32_t *__restrict__ inv, int64_t n, int c, const double *__restrict__ Fs,
+                          const double *__restrict__ zs, double *__restrict__ Fo, double *__restrict__ zo) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t si = inv[i];
+    for (int k = 0; k < c; ++k) Fo[c * i + k] = Fs[c * si + k];
+    zo[i] = zs[si];
+}
+
+// QuadTree.computeRepulsiveForce (QuadTree.scala:123-152) for every point of
+// Y against the tree of all of them (c = 2), or the octree extension (c = 3):
+// F (n x c) and z (sumQ contribution) per point, original order.
+void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, double theta, double *dF,
+                      double *dz) {
+    TSNE_REQUIRE(n >= 1, "empty embedding");
+    hipStream_t st = ctx->stream;
+    double *Fs = ctx->ws.get<double>("rep.F", (size_t)c * n);
+    double *zs = ctx->ws.get<double>("rep.z", n);
+    const int32_t *inv;
+    if (c == 2) {
+        BHTree t;
+        bh_alloc(ctx, t, n);
+        bh_build(ctx, t, dY, theta);
+        bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, nullptr);
+        inv = t.inv;
+    } else {
+        OctTree t;
+        oct_alloc(ctx, t, n);
+        oct_build(ctx, t, dY, theta);
+        oct_repulsion(ctx, t, theta, 0, n, Fs, zs);
+        inv = t.inv;
+    }
+    hipLaunchKernelGGL(unsort_fz, dim3(ceil_div(n, 256)), dim3(256), 0, st, inv, n, c, Fs, zs, dF, dz);
+    TSNE_LAUNCH_CHECK();
+}
+
 // 3-D gradient (octree): same contract as gradient_device, Y / grad n x 3.
 void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col, const double *d_P, int64_t n,
                       const double *dY, int32_t metric, double theta, double exaggeration, double *d_grad,

@@ -62,6 +62,8 @@ SIGNATURES = {
     "tsne_gradient": (C.c_int, [P, P, P, P, I64, P, I32, D, D, P, PD, PD]),
     "tsne_gradient_c": (C.c_int, [P, P, P, P, I64, I32, P, I32, D, D, P, PD, PD]),
     "tsne_update_embedding": (C.c_int, [P, I64, I32, P, P, P, P, D, D, D]),
+    "tsne_repulsion": (C.c_int, [P, P, I64, I32, D, P, P]),
+    "tsne_dev_repulsion": (C.c_int, [P, P, I64, I32, D, P, P]),
     "tsne_center_embedding": (C.c_int, [P, I64, I32, P]),
     "tsne_init_working_set": (C.c_int, [P, I64, I32, U64, P, P, P]),
     "tsne_optimize": (C.c_int, [P, C.POINTER(Params), P, P, P, I64, P, P, P, P, P, I32, PI32]),

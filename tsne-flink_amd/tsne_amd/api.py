@@ -211,6 +211,20 @@ class Context:
                                     C.byref(z), C.byref(loss) if want_loss else None))
         return grad, z.value, (loss.value if want_loss else None)
 
+    def repulsion(self, Y, theta):
+        """QuadTree.computeRepulsiveForce (QuadTree.scala:123-152) for every point
+        -> (F[n, c], z[n]); c = Y.shape[1] is 2 or 3 (octree extension)."""
+        Y = _f64(Y)
+        n, c = Y.shape
+        F = np.zeros((n, c))
+        z = np.zeros(n)
+        check(lib().tsne_repulsion(self._h, _ptr(Y), n, c, theta, _ptr(F), _ptr(z)))
+        return F, z
+
+    def dev_repulsion(self, dY, theta, dF, dz):
+        n, c = dY.shape
+        check(lib().tsne_dev_repulsion(self._h, _ptr(dY), n, c, theta, _ptr(dF), _ptr(dz)))
+
     def updateEmbedding(self, grad, Y, upd, gains, min_gain, momentum, learning_rate):
         """TsneHelpers.scala:341-369, in place on Y / upd / gains."""
         n, c = Y.shape
