@@ -50,6 +50,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
+                    help="c3: 1M x 128 GMM (the metric's workload); c5: 50,000-point precomputed distance matrix "
+                         "(--inputDistanceMatrix: affinities + joint + optimizer, no kNN)")
     ap.add_argument("--steps", type=int, default=20, help="timed iterations t=1..K (0 = the whole schedule T)")
     ap.add_argument("--warmup", type=int, default=5, help="untimed, profiled iterations on a restored snapshot")
     ap.add_argument("--no-rest", action="store_true", help="stop after the timed window (skip t = K+1..T)")
@@ -110,28 +113,11 @@ def trace_entry(ctx, t, rows, Y, n):
             "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
-    ctx = T.Context(local)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    if world > 1:
-        obj = [T.Context.unique_id() if rank == 0 else None]
-        torch.distributed.broadcast_object_list(obj, src=0)
-        ctx.init_comm(rank, world, obj[0])
+def setup_c3(ctx, a, dev, world, rank, r0, r1):
+    """C3: device-generated GMM -> kNN (query rows of this rank) -> affinities
+    -> (all-gather of the conditional graph) -> symmetrised P on every rank."""
     n, d, k = a.n, a.dim, a.k
     kk = min(k, n - 1)
-    r0, r1 = T.shard_rows(n, world, rank)
-    steps = a.steps if a.steps > 0 else a.iterations
-    steps = min(steps, a.iterations)
-
-    # ---------------------------------------------------------- setup stages
     X = gmm(n, d, 2, dev)
     sync_barrier(world)
     t0 = time.perf_counter()
@@ -169,7 +155,83 @@ def main():
     t_aff = max_over_ranks(time.perf_counter() - t0, world)
     X_host = X.cpu().numpy() if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
     del X, dist, p
+    return orp, oc, ov, nnz, e0, e1, t_knn, knn_filter_ms, t_aff, X_host
 
+
+def setup_c5(ctx, a, dev, world):
+    """C5 (BASELINE configs[4]): a 50,000-point C3-style GMM in 64-D (seed 4,
+    tests/configs.py c5_points) whose full sqeuclidean distance matrix,
+    diagonal excluded, is the input (Tsne.readDistanceMatrix: every (i, j, d)
+    line is a neighbour, Tsne.scala:69-70,155-159) -- 2.5e9 entries, built on
+    the device; affinities (workgroup per 49,999-entry row) + joint (64-bit
+    offsets).  Every rank builds the same P."""
+    import configs
+    n = a.n
+    Xd = torch.from_numpy(configs.c5_points(n, a.dim, 4)).to(dev)
+    sq = (Xd * Xd).sum(1)
+    m = n - 1
+    dist = torch.empty((n, m), dtype=torch.float64, device=dev)
+    col = torch.empty((n, m), dtype=torch.int32, device=dev)
+    ar = torch.arange(n, device=dev, dtype=torch.int32)
+    for b0 in range(0, n, 1024):
+        b1 = min(n, b0 + 1024)
+        D = (sq[b0:b1, None] + sq[None, :] - 2.0 * (Xd[b0:b1] @ Xd.T)).clamp_(min=0.0)
+        keep = torch.ones((b1 - b0, n), dtype=torch.bool, device=dev)
+        keep[torch.arange(b1 - b0, device=dev), torch.arange(b0, b1, device=dev)] = False
+        dist[b0:b1] = D[keep].view(b1 - b0, m)
+        col[b0:b1] = ar.expand(b1 - b0, n)[keep].view(b1 - b0, m)
+        del D, keep
+    rp = torch.arange(0, n * m + 1, m, dtype=torch.int64, device=dev)
+    sync_barrier(world)
+    t0 = time.perf_counter()
+    p = torch.empty_like(dist)
+    ctx.dev_affinities(rp, dist, n, a.perplexity, p)
+    del dist
+    cap = n * m
+    orp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    oc = torch.empty(cap, dtype=torch.int32, device=dev)
+    ov = torch.empty(cap, dtype=torch.float64, device=dev)
+    nnz = ctx.dev_joint(rp, col, p, n, cap, orp, oc, ov)
+    sync_barrier(world)
+    t_aff = max_over_ranks(time.perf_counter() - t0, world)
+    del p, col
+    torch.cuda.empty_cache()
+    return orp, oc, ov, nnz, t_aff
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    ctx = T.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    if world > 1:
+        obj = [T.Context.unique_id() if rank == 0 else None]
+        torch.distributed.broadcast_object_list(obj, src=0)
+        ctx.init_comm(rank, world, obj[0])
+    if a.config == "c5":
+        if a.n == 1_000_000:
+            a.n = 50_000
+        a.dim = 64
+    n, d, k = a.n, a.dim, a.k
+    kk = min(k, n - 1)
+    r0, r1 = T.shard_rows(n, world, rank)
+    steps = a.steps if a.steps > 0 else a.iterations
+    steps = min(steps, a.iterations)
+
+    # ---------------------------------------------------------- setup stages
+    if a.config == "c5":
+        orp, oc, ov, nnz, t_aff = setup_c5(ctx, a, dev, world)
+        t_knn, knn_filter_ms, X_host = 0.0, 0.0, None
+        e0, e1 = 0, nnz
+        kk = n - 1
+    else:
+        orp, oc, ov, nnz, e0, e1, t_knn, knn_filter_ms, t_aff, X_host = setup_c3(ctx, a, dev, world, rank, r0, r1)
     Y = torch.zeros((n, 2), dtype=torch.float64, device=dev)
     upd = torch.zeros_like(Y)
     gains = torch.ones_like(Y)
@@ -272,9 +334,15 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)",
-        "config": {"workload": f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, "
-                               f"theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}",
+        "data": ("synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)"
+                 if a.config == "c3" else
+                 "full sqeuclidean distance matrix (diagonal excluded) of a synthetic 10-blob 64-D Gaussian "
+                 "mixture (seed 4), seeded Y0 ~ N(0, 1e-4^2)"),
+        "config": {"workload": (f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, "
+                                f"theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}")
+                   if a.config == "c3" else
+                   (f"C5: {n}-point precomputed distance matrix ({n}x{n - 1} entries), perplexity "
+                    f"{a.perplexity}, theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}"),
                    "n": n, "dim": d, "k": k, "theta": a.theta, "parallelism": f"rows{world}",
                    "nnz_P": int(nnz)},
         "window": f"t=1..{steps} of T={a.iterations}",
@@ -284,11 +352,11 @@ def main():
         "end_to_end_note": "kNN + affinities + joint + optimizer setup + every iteration run + D2H of Y and losses; "
                            "input already in HBM (synthetic), CSV/loss-file formatting not included",
         "knn_s": t_knn,
-        "knn_pts_per_s": n / t_knn,
+        "knn_pts_per_s": n / t_knn if t_knn > 0 else None,
         "knn_filter_ms": knn_filter_ms,
         "knn_mfma_tflops": knn_flops / (knn_filter_ms * 1e-3) / 1e12 if knn_filter_ms > 0 else None,
         "knn_mfma_frac_of_peak": (knn_flops / (knn_filter_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF) if knn_filter_ms > 0 else None,
-        "knn_mfma_frac_whole_knn": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF,
+        "knn_mfma_frac_whole_knn": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF if t_knn > 0 else None,
         "affinities_joint_s": t_aff,
         "opt_setup_s": t_setup,
         "final_loss": losses.get(max(losses)) if losses else None,
@@ -322,6 +390,11 @@ def main():
         if key in tj.get("per_window", {}):
             out["roofline"]["traffic"] = tj["per_window"][key]["traffic_bytes"]
             out["roofline"]["traffic_source"] = tj["source"] + "; " + tj["per_window"][key]["note"]
+    if a.config == "c5":
+        out["metric"] = "t-SNE iterations/sec at the 50k precomputed-distance-matrix config (C5); affinities+joint s"
+        for key in ("knn_s", "knn_pts_per_s", "knn_filter_ms", "knn_mfma_tflops", "knn_mfma_frac_of_peak",
+                    "knn_mfma_frac_whole_knn"):
+            out.pop(key, None)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps, X_host, (orp, oc, ov))
     if rank == 0 and a.locality:
@@ -379,7 +452,7 @@ def cpu_baseline(snaps, a, n, steps, X_host, P_dev):
     per_t = {}
     # attraction + update of 20000 rows (one thread), extrapolated
     rp, col, val = (x.cpu().numpy() for x in P_dev)
-    nr = min(n, 20000)
+    nr = int(min(n, 20000, max(16, 2e7 / max(1.0, len(val) / n))))   # ~2e7 entries at most
     r0 = int(rng.integers(0, n - nr + 1))
     Ys0 = next(iter(snaps.values())) if snaps else np.zeros((n, 2))
     t0 = time.perf_counter()

@@ -73,3 +73,30 @@ def to_coo_lines(X):
     i, j = np.nonzero(X)
     v = X[i, j].tolist()
     return "".join(f"{a},{b},{c!r}\n" for a, b, c in zip(i.tolist(), j.tolist(), v))
+
+
+def c5_matrix(n=5000, d=64, seed=4, diagonal=False):
+    """C5's input as CSR rows in file order: row i = (i, j, sqeuclidean(x_i, x_j))
+    for every j (j != i unless `diagonal`), as Tsne.readDistanceMatrix feeds
+    them to the affinities (Tsne.scala:69-70, 155-159).  Distances from the
+    norm expansion, clamped at 0 (any values do: they are the input)."""
+    X = c5_points(n, d, seed)
+    sq = (X * X).sum(1)
+    D = np.maximum(sq[:, None] + sq[None, :] - 2.0 * (X @ X.T), 0.0)
+    if diagonal:
+        np.fill_diagonal(D, 0.0)
+        col = np.tile(np.arange(n, dtype=np.int32), n)
+        return np.arange(0, n * n + 1, n, dtype=np.int64), col, D.ravel()
+    mask = ~np.eye(n, dtype=bool)
+    col = np.nonzero(mask)[1].astype(np.int32)
+    return np.arange(0, n * (n - 1) + 1, n - 1, dtype=np.int64), col, D[mask]
+
+
+def support(P):
+    """The entries of a CSR P with P_ij > 0 (the KL over them is finite)."""
+    rp, col, val = P
+    keep = val > 0.0
+    rows = np.repeat(np.arange(len(rp) - 1), np.diff(rp))[keep]
+    nrp = np.zeros(len(rp), dtype=np.int64)
+    np.add.at(nrp, rows + 1, 1)
+    return np.cumsum(nrp), col[keep], val[keep]

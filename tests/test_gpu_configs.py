@@ -11,7 +11,14 @@ identities -- and end to end where the whole problem is small (C1):
   C2  70,000 x 784 MNIST-shaped, theta 0.5, T = 1000;
   C3  1,000,000 x 128 GMM, theta 0.5, T = 1000 (the bench workload);
   C4  500,000 x 300 sparse, cosine, nComponents 3 (octree extension);
-      each: kNN rows bit-exact (256 contiguous query rows vs oracle_knn),
+  C5  precomputed distance matrix (--inputDistanceMatrix): the CLI end to end
+      at 2,000 points (with and without the diagonal) and the library at
+      5,000 points against the oracle (the 50,000-point run is a bench mode:
+      bench.py --config c5).  Dense rows underflow to p = 0, so the
+      reference's KL is NaN (0 ln 0, TsneHelpers.scala:300) -- reproduced
+      exactly (same loss keys, NaN at the same iterations); the KL over the
+      support P > 0 is compared instead;
+  C2-C4 each: kNN rows bit-exact (256 contiguous query rows vs oracle_knn),
       affinity rows at 1e-12, joint rows (pattern exact, values 1e-13
       relative) against a restatement of jointDistribution on the sampled
       rows, and at snapshots of the real optimizer trajectory the per-point
@@ -245,3 +252,78 @@ def test_c4_sparse_cosine_3d_full_size(ctx):
     Xd = torch.from_numpy(X).cuda()
     full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 3: 16}, grad_rows=250_000,
                 q0=77_777, stop=3)
+
+
+# ------------------------------------------------------------------- C5
+def test_c5_cli_distance_matrix_end_to_end(ctx, tmp_path):
+    """--inputDistanceMatrix through the native CLI (2,000 points, every
+    off-diagonal pair and, second pass, the diagonal too)."""
+    n = 2000
+    for diag in (False, True):
+        rp, col, d = CF.c5_matrix(n, diagonal=diag)
+        rows = np.repeat(np.arange(n), np.diff(rp))
+        (tmp_path / "dm.csv").write_text("".join(f"{a},{b},{c!r}\n" for a, b, c in
+                                                 zip(rows.tolist(), col.tolist(), d.tolist())))
+        r = subprocess.run([str(CLI), "--input", "dm.csv", "--output", "out.csv", "--dimension", "64",
+                            "--knnMethod", "bruteforce", "--inputDistanceMatrix", "--perplexity", "30",
+                            "--iterations", "60", "--theta", "0.5", "--loss", "loss.txt"], cwd=tmp_path,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        Yc = np.array([[float(v) for v in l.split(",")[1:]] for l in (tmp_path / "out.csv").read_text().splitlines()])
+        lc = parse_loss_file((tmp_path / "loss.txt").read_text())
+        po, _ = O.affinities(rp, d, 30.0)
+        P = O.joint(rp, col, po, n)
+        Y0, _, _ = ctx.initWorkingSet(n, 2, seed=0)
+        Yo = Y0.copy()
+        lo = O.optimize(*P, Yo, np.zeros_like(Y0), np.ones_like(Y0), iterations=60, theta=0.5, threads=THREADS)
+        assert sorted(lc) == sorted(lo)
+        assert [np.isnan(lc[t]) for t in sorted(lc)] == [np.isnan(lo[t]) for t in sorted(lo)]
+        S = CF.support(P)
+        _, _, kl_c = ctx.gradient(*S, Yc, 0.5, want_loss=True)
+        _, _, kl_o = ctx.gradient(*S, Yo, 0.5, want_loss=True)
+        assert abs(kl_c - kl_o) <= 0.01 * abs(kl_o), (diag, kl_c, kl_o)
+
+
+def test_c5_distance_matrix_5k_matches_oracle(ctx):
+    n = 5000
+    rp, col, d = CF.c5_matrix(n)
+    p = ctx.pairwiseAffinities(rp, d, 30.0)            # workgroup-per-row beta search
+    po, _ = O.affinities(rp, d, 30.0)
+    assert np.abs(p - po).max() <= 1e-12
+    a = ctx.jointDistribution(rp, col, p, n)            # sorted, all mutual: no sort passes
+    P = O.joint(rp, col, po, n)
+    assert np.array_equal(a[0], P[0]) and np.array_equal(a[1], P[1]) and np.abs(a[2] - P[2]).max() <= 1e-15
+    assert (P[2] == 0).any()                           # underflowed affinities: the reference's KL is NaN
+    S = CF.support(P)
+    Y0, _, _ = ctx.initWorkingSet(n, 2, seed=4)
+    T_ = 60
+    prm = default_params(iterations=T_, theta=0.5)
+    snaps = {1, 30, 60}
+    dev = torch.device("cuda", 0)
+    Pd = tuple(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in P)
+    Y = torch.from_numpy(Y0.copy()).to(dev)
+    u = torch.zeros_like(Y)
+    g = torch.ones_like(Y)
+    ctx.dev_opt_setup(prm, *Pd, n, Y, u, g)
+    for t in range(1, T_ + 1):
+        ctx.dev_opt_step(t)
+        if t in snaps:   # per-iteration gradient parity at the trajectory's own states
+            ctx.synchronize()
+            Yt = Y.cpu().numpy()
+            ex = exaggeration(t + 1, T_)
+            gg, Zg, Lg = ctx.gradient(*P, Yt, 0.5, exaggeration=ex, want_loss=True)
+            r = O.gradient(*P, Yt, 0.5, exaggeration=ex, want_loss=True, threads=THREADS)
+            assert np.abs(gg - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max(), t
+            assert abs(Zg - r["Z"]) <= NEAR_TOL * r["Z"], t
+            assert np.isnan(Lg) and np.isnan(r["loss"])
+            _, _, kg = ctx.gradient(*S, Yt, 0.5, exaggeration=ex, want_loss=True)
+            ro = O.gradient(*S, Yt, 0.5, exaggeration=ex, want_loss=True, threads=THREADS)
+            assert abs(kg - ro["loss"]) <= 1e-9 * abs(ro["loss"]), t
+    lg = ctx.dev_opt_losses()
+    Yo = Y0.copy()
+    lo = O.optimize(*P, Yo, np.zeros_like(Y0), np.ones_like(Y0), iterations=T_, theta=0.5, threads=THREADS)
+    assert sorted(lg) == sorted(lo) == list(range(10, T_ + 1, 10))
+    assert all(np.isnan(lg[t]) and np.isnan(lo[t]) for t in lg)
+    _, _, kg = ctx.gradient(*S, Y.cpu().numpy(), 0.5, want_loss=True)
+    _, _, ko = ctx.gradient(*S, Yo, 0.5, want_loss=True)
+    assert abs(kg - ko) <= 0.01 * abs(ko), (kg, ko)

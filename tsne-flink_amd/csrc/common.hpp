@@ -75,6 +75,11 @@ struct Workspace {
         return static_cast<T *>(b->ensure(count * sizeof(T)));
     }
     void clear() { bufs.clear(); }
+    // free every buffer whose name starts with prefix (large one-time temporaries)
+    void release_prefix(const std::string &prefix) {
+        for (auto it = bufs.begin(); it != bufs.end();)
+            it = it->first.compare(0, prefix.size(), prefix) == 0 ? bufs.erase(it) : std::next(it);
+    }
 };
 
 // Named kernel-stage timers: HIP event pairs recorded on the stream the

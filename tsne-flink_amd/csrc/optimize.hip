@@ -1209,7 +1209,10 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
 static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     hipStream_t st = ctx->stream;
     const int64_t n = s->n;
-    const int64_t nsamp = std::min<int64_t>(n, 1 << 16), stride = std::max<int64_t>(1, n / nsamp);
+    // a fixed sample of rows, ~1 << 22 entries at most (dense rows: fewer rows)
+    const int64_t avg = std::max<int64_t>(1, s->nnz / std::max<int64_t>(1, n));
+    const int64_t nsamp = std::max<int64_t>(1, std::min<int64_t>({n, 1 << 16, (1 << 22) / avg}));
+    const int64_t stride = std::max<int64_t>(1, n / nsamp);
     const int64_t win = std::max<int64_t>(64, n / 64);
     TSNE_HIP(hipMemsetAsync(s->lscore, 0, 2 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(locality_score, dim3(ceil_div(nsamp, 4)), dim3(256), 0, st, s->rp0, s->col0, s->lab,
