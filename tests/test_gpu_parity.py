@@ -203,6 +203,55 @@ def test_gradient_large_near_exact(ctx, n, scale):
         assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
+@pytest.mark.parametrize("theta,scale", [(0.0, 1.0), (0.5, 1.0), (0.25, 30.0), (0.5, 1e-3)])
+def test_gradient_duplicate_multiplicity(ctx, theta, scale):
+    """Exact duplicate embedding points (QuadTree.scala:52-61): a leaf holding
+    c copies re-inserts ONE when it splits, so cells created after a group's
+    first copy count fewer copies, depending on the insertion (row) order.
+    Groups of 2..7 copies at early, late and interleaved rows."""
+    n = 600
+    rp, col, val = random_problem(n, 12, seed=71)
+    rng = np.random.default_rng(int(theta * 100) + int(scale))
+    Y = rng.normal(size=(n, 2)) * scale
+    groups = [[3, 4], [10, 300, 590], [50, 51, 52, 53, 598, 599], [7, 100, 200, 300 + 1, 400, 500, 595],
+              [595 - 300, 2]]
+    for g in groups:
+        Y[g] = Y[g[0]]
+    g_, Z, loss = ctx.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
+    r = O.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
+    tol = 1e-12 if theta == 0.0 else 1e-6
+    assert np.abs(g_ - r["grad"]).max() <= tol * np.abs(r["grad"]).max()
+    assert abs(Z - r["Z"]) <= tol * r["Z"]
+    F, z = ctx.repulsion(Y, theta)
+    assert np.abs(z - r["zi"]).max() <= tol * r["zi"].max()
+    assert np.abs(F - r["rep"]).max() <= tol * np.abs(r["rep"]).max()
+
+
+def test_optimize_duplicates_device_path_matches_oracle(ctx):
+    """Duplicates inside the device optimizer (relabelled labels: insertion
+    rows are the original indices): one step against the oracle."""
+    import torch
+    n = 500
+    rp, col, val = random_problem(n, 12, seed=72)
+    Y0 = np.random.default_rng(11).normal(size=(n, 2)) * 1e-2
+    for g in ([5, 6, 400], [100, 20, 499, 250]):
+        Y0[g] = Y0[g[0]]
+    p = default_params(iterations=30, theta=0.5)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    dY, du, dg = t(Y0, torch.float64), torch.zeros((n, 2), dtype=torch.float64, device=dev), \
+        torch.ones((n, 2), dtype=torch.float64, device=dev)
+    ctx.dev_opt_setup(p, t(rp, torch.int64), t(col, torch.int32), t(val, torch.float64), n, dY, du, dg)
+    ctx.dev_opt_step(1)
+    ctx.dev_opt_sync()
+    ctx.synchronize()
+    gr = O.gradient(rp, col, val, Y0, 0.5, exaggeration=p.early_exaggeration)["grad"]
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    O.update(gr, Yo, uo, go, p.min_gain, p.initial_momentum, p.learning_rate)
+    O.center(Yo)
+    assert np.abs(dY.cpu().numpy() - Yo).max() <= 1e-6 * np.abs(Yo).max()
+
+
 def test_gradient_points_outside_root_and_duplicates(ctx):
     # n = 2 on one side: W = range < |x| drops points from the reference tree
     n = 400

@@ -18,11 +18,13 @@
 //  * leaves always interact directly; a leaf equal to the query contributes
 //    nothing (QuadTree.scala:128); points outside the root cell are not in
 //    the tree but still get a force (they are queries).
-// Known deviations (documented in DESIGN.md): exact duplicate embedding
-// points are counted with full multiplicity (the reference resets the
-// multiplicity to 1 each time a duplicate's leaf is split); cells deeper
-// than 31 levels are not split further (keys tie: all points interact
-// directly); centres of mass are summed in tree order, not insertion order.
+//  * exact duplicate embedding points get the reference's multiplicities
+//    (dup_* kernels below: a leaf holding c copies re-inserts ONE of them
+//    when it splits, QuadTree.scala:52-61), replayed from insertion rows.
+// Known deviations (documented in DESIGN.md): cells deeper than 31 levels
+// are not split further (keys tie: all points interact directly; duplicate
+// groups sharing such a cell with other points keep full multiplicity);
+// centres of mass are summed in tree order, not insertion order.
 #include <hipcub/hipcub.hpp>
 
 #include "bhtree.hpp"
@@ -109,6 +111,7 @@ __global__ void bbox_final(const double *__restrict__ part, int nb, double *__re
         *W = a > c ? a : c;  // scala.math.max(maxX - minX, maxY - minY)
         meta[0] = 0;
         meta[2] = 0;
+        meta[3] = 0;         // root replaced by its virtual chain top (duplicates, dup_apply)
     }
 }
 
@@ -229,11 +232,13 @@ __device__ __forceinline__ int kdelta(const uint64_t *__restrict__ k, int m, int
 // Karras (2012) binary radix tree over the m in-root points.
 __global__ void karras_build(const uint64_t *__restrict__ k, int64_t n, const int32_t *__restrict__ meta,
                              BHNode *__restrict__ nodes, int32_t *__restrict__ parent_leaf,
-                             int32_t *__restrict__ parent_node, int32_t *__restrict__ arrive) {
+                             int32_t *__restrict__ parent_node, int32_t *__restrict__ arrive,
+                             int32_t *__restrict__ arrive2) {
     const int m = meta[0];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m - 1) return;
     arrive[i] = 0;
+    arrive2[i] = 0;
     const int dr = kdelta(k, m, i, i + 1), dl = kdelta(k, m, i, i - 1);
     const int d = (dr > dl) ? 1 : -1;
     const int dmin = d > 0 ? dl : dr;
@@ -436,21 +441,199 @@ __device__ __forceinline__ void pair_force(double qx, double qy, double px, doub
 // Number of points whose coordinates equal pos[s] exactly (itself included);
 // they sit in the same equal-key run of the sorted order.
 __global__ void dup_count(const double2 *__restrict__ pos, const uint64_t *__restrict__ keys, int64_t n,
-                          int32_t *__restrict__ dupc) {
+                          int32_t *__restrict__ dupc, int32_t *__restrict__ vid, int32_t *__restrict__ dflag) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     const double2 q = pos[s];
     const uint64_t k = keys[s];
     int32_t c = 1;
+    int64_t first = s;   // value id: the first sorted position holding this exact point
     for (int64_t t = s - 1; t >= 0 && keys[t] == k; --t) {
         const double2 p = pos[t];
-        c += (p.x == q.x && p.y == q.y);
+        if (p.x == q.x && p.y == q.y) { ++c; first = t; }
     }
     for (int64_t t = s + 1; t < n && keys[t] == k; ++t) {
         const double2 p = pos[t];
         c += (p.x == q.x && p.y == q.y);
     }
     dupc[s] = c;
+    vid[s] = (int32_t)first;
+    if (c > 1) dflag[0] = 1;
+}
+
+// ---- Exact duplicates (QuadTree.scala:52-61).  The reference keeps one
+// leaf per distinct point and counts every copy on the way down, but when a
+// leaf holding c copies of v splits (a different point arrived) it re-inserts
+// v ONCE into the new child: cells created after the first copy of v was
+// inserted count only 1 + the copies inserted after their creation.  A cell
+// is created when its parent cell splits, i.e. at the row t2(parent) of the
+// first point in the parent's cell whose value differs from the value of the
+// parent cell's first point.  So for a duplicate group of m copies (rows
+// r_1 < ... < r_m) and a cell X on its path with parent cell P:
+// count_v(X) = m - max(0, #{r_i < t2(P)} - 1)  (the root: m), and the leaf
+// of v (the quad child of the deepest cell R that also holds other points)
+// has multiplicity m - max(0, #{r_i < t2(R)} - 1).  Only work when some
+// point has a duplicate (dflag); no tile or moment ever covers such a group
+// (the cells above it are traversed the reference's way).
+
+// t2 per binary node from (first row, its value id, t2) of the two children:
+// the union's first value is the earlier child's; its second distinct value
+// arrives at the earlier of that child's t2 and the other child's first row
+// (different value) or t2 (same value).
+__global__ void dup_bottom_up(const int32_t *__restrict__ meta, const int32_t *__restrict__ dflag,
+                              const int32_t *__restrict__ idx_sorted, const int32_t *__restrict__ rowmap,
+                              const int32_t *__restrict__ vid, const BHNode *__restrict__ nodes,
+                              const int32_t *__restrict__ parent_leaf, const int32_t *__restrict__ parent_node,
+                              int32_t *arrive2, int32_t *rmin, int32_t *rvid, int32_t *rt2) {
+    const int m = meta[0];
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!dflag[0] || s >= m || m < 2) return;
+    auto leaf = [&](int q, int &r, int &v, int &t) {
+        const int32_t l = idx_sorted[q];
+        r = rowmap ? rowmap[l] : l;
+        v = vid[q];
+        t = INT32_MAX;
+    };
+    auto ld = [](const int32_t *p) { return __hip_atomic_load(const_cast<int32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    auto st = [](int32_t *p, int32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    int p = parent_leaf[s];
+    while (p >= 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(&arrive2[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+        int r[2], v[2], t[2];
+        const int32_t ch[2] = {nodes[p].left, nodes[p].right};
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (ch[k] < 0) leaf(~ch[k], r[k], v[k], t[k]);
+            else { r[k] = ld(rmin + ch[k]); v[k] = ld(rvid + ch[k]); t[k] = ld(rt2 + ch[k]); }
+        }
+        const int a = r[0] < r[1] ? 0 : 1, b = 1 - a;   // a: the child holding the earlier first row
+        const int other = v[b] != v[a] ? r[b] : t[b];
+        st(rmin + p, r[a]);
+        st(rvid + p, v[a]);
+        st(rt2 + p, min(t[a], other));
+        p = parent_node[p];
+    }
+}
+
+__device__ __forceinline__ bool real_cell(const BHNode &nd) { return nd.h >= 0.0; }
+
+// One thread per pure duplicate group (the first of m >= 2 exact copies that
+// form a whole equal-key run): leaf multiplicity of its tie node, count / sum
+// corrections and no-tile marks of the real cells above it.
+__global__ void dup_fixup(const int32_t *__restrict__ meta, const int32_t *__restrict__ dflag,
+                          const double2 *__restrict__ pos, const uint64_t *__restrict__ keys,
+                          const int32_t *__restrict__ dupc, const int32_t *__restrict__ idx_sorted,
+                          const int32_t *__restrict__ rowmap, const BHNode *__restrict__ nodes,
+                          const int32_t *__restrict__ parent_leaf, const int32_t *__restrict__ parent_node,
+                          const int32_t *__restrict__ rt2, int32_t *__restrict__ cntcorr, double *__restrict__ sumcorr,
+                          int32_t *__restrict__ tiecnt, int32_t *__restrict__ notile, int32_t *__restrict__ vflag,
+                          int32_t *__restrict__ vcnt, double *__restrict__ vsum) {
+    const int mroot = meta[0];
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!dflag[0] || s >= mroot || dupc[s] < 2) return;
+    const double2 q = pos[s];
+    if (s > 0 && pos[s - 1].x == q.x && pos[s - 1].y == q.y) return;   // not the group's first
+    const int m = dupc[s], kb = s + m - 1;
+    if (kb >= mroot) return;
+    for (int u = s; u <= kb; ++u)
+        if (pos[u].x != q.x || pos[u].y != q.y) return;                 // copies not contiguous: impure run
+    if ((s > 0 && keys[s - 1] == keys[s]) || (kb + 1 < mroot && keys[kb + 1] == keys[s])) return;
+    // the group's node: climb from its first leaf until the node spans [s, kb]
+    int g = parent_leaf[s];
+    while (g >= 0 && !(nodes[g].first == s && nodes[g].last == kb)) g = parent_node[g];
+    if (g < 0 || g == 0) return;                                         // every point identical: root tie
+    auto copies_before = [&](int t2) {
+        int c = 0;
+        for (int u = s; u <= kb; ++u) {
+            const int32_t l = idx_sorted[u];
+            c += (rowmap ? rowmap[l] : l) < t2;
+        }
+        return c;
+    };
+    auto real_above = [&](int x) {   // the nearest real cell strictly above binary node x, -1 if none
+        int y = parent_node[x];
+        while (y >= 0 && !real_cell(nodes[y])) y = parent_node[y];
+        return y;
+    };
+    int R = real_above(g);
+    if (R < 0) return;
+    tiecnt[g] = m - max(0, copies_before(rt2[R]) - 1);   // the leaf: R's quad child, created at t2(R)
+    // Real node X = the DEEPEST cell C_k of a chain C_1 > ... > C_k of
+    // reference cells holding the same points (our binary node exists only
+    // where they split).  C_1 (a quad child of the real cell P above) was
+    // created at t2(P); C_2..C_k at t2(C_1) = t2(X), in one cascade.
+    for (int X = R; X >= 0;) {
+        notile[X] = 1;
+        const int P = real_above(X);
+        const int lx = nodes[X].delta >> 1;
+        const int deep = max(0, copies_before(rt2[X]) - 1);
+        int top, node_corr;
+        bool chain;
+        if (P < 0) {   // the root: C_1 is the reference root cell, which holds every copy
+            top = 0;
+            chain = lx > 0;
+        } else {
+            top = max(0, copies_before(rt2[P]) - 1);
+            chain = lx > (nodes[P].delta >> 1) + 1;
+        }
+        node_corr = chain ? deep : top;
+        if (node_corr > 0) {
+            atomicAdd(&cntcorr[X], node_corr);
+            atomicAdd(&sumcorr[2 * X], node_corr * q.x);
+            atomicAdd(&sumcorr[2 * X + 1], node_corr * q.y);
+        }
+        if (chain) {   // the chain top's own count: a virtual record when it differs
+            if (top > 0) {
+                atomicAdd(&vcnt[X], top);
+                atomicAdd(&vsum[2 * X], top * q.x);
+                atomicAdd(&vsum[2 * X + 1], top * q.y);
+            }
+            if (top != deep) vflag[X] = 1;
+        }
+        X = P;
+    }
+}
+
+__global__ void dup_clear(const int32_t *__restrict__ meta, const int32_t *__restrict__ dflag, int32_t *__restrict__ cntcorr,
+                          double *__restrict__ sumcorr, int32_t *__restrict__ tiecnt, int32_t *__restrict__ notile,
+                          int32_t *__restrict__ vflag, int32_t *__restrict__ vcnt, double *__restrict__ vsum) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!dflag[0] || i >= meta[0]) return;
+    cntcorr[i] = 0;
+    sumcorr[2 * i] = 0.0;
+    sumcorr[2 * i + 1] = 0.0;
+    tiecnt[i] = 0;
+    notile[i] = 0;
+    vflag[i] = 0;
+    vcnt[i] = 0;
+    vsum[2 * i] = 0.0;
+    vsum[2 * i + 1] = 0.0;
+}
+
+// corrected counts / centres of mass of the cells above duplicate groups
+__global__ void dup_apply(int32_t *__restrict__ meta, const int32_t *__restrict__ dflag,
+                          const int32_t *__restrict__ cntcorr, const double *__restrict__ sumcorr,
+                          const int32_t *__restrict__ vflag, const int32_t *__restrict__ vcnt,
+                          const double *__restrict__ vsum, int32_t *__restrict__ vcntf, double *__restrict__ vcom,
+                          BHNode *__restrict__ nodes) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (!dflag[0] || i >= meta[0] - 1 || (cntcorr[i] == 0 && !vflag[i])) return;
+    BHNode &nd = nodes[i];
+    const double c0 = nd.cnt, x0 = nd.cx * c0, y0 = nd.cy * c0;   // all copies
+    if (vflag[i]) {   // the chain top C_1
+        if (i == meta[1]) meta[3] = 1;   // the root's chain: the reference root cell holds every copy
+        const int32_t ct = nd.cnt - vcnt[i];
+        vcntf[i] = ct;
+        vcom[2 * i] = (x0 - vsum[2 * i]) / ct;
+        vcom[2 * i + 1] = (y0 - vsum[2 * i + 1]) / ct;
+    }
+    if (cntcorr[i] != 0) {
+        const double c1 = nd.cnt - cntcorr[i];
+        nd.cx = (x0 - sumcorr[2 * i]) / c1;
+        nd.cy = (y0 - sumcorr[2 * i + 1]) / c1;
+        nd.cnt -= cntcorr[i];
+    }
 }
 
 
@@ -754,19 +937,39 @@ __device__ __forceinline__ void cell_force(double dx, double dy, double D, int32
 // Slots of transparent nodes receive don't-care bytes: only real cells are
 // ever pushed (and their records read) by the traversal.
 constexpr int QREC_BLK = 256;
+struct DupView {   // duplicate-multiplicity data for build_qrec (nullptr members when there is none)
+    const int32_t *tiecnt, *notile, *vflag, *vcntf;
+    const double *vcom;
+    int32_t virt;   // record index offset of the virtual chain tops (= n)
+};
 __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos, int i,
-                               double inv_theta, double near_dmax, QRec &r);
+                               double inv_theta, double near_dmax, const DupView &dv, QRec &r);
 __global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict__ nodes,
                                                        const double2 *__restrict__ pos,
                                                        const int32_t *__restrict__ meta, double inv_theta,
-                                                       double near_dmax, QRec *__restrict__ qrec) {
+                                                       double near_dmax, const int32_t *__restrict__ dflag,
+                                                       DupView dv, QRec *__restrict__ qrec) {
     __shared__ QRec srec_out[QREC_BLK];
     const int m = meta[0];
     const int b0 = blockIdx.x * QREC_BLK;
     const int nrec = min(QREC_BLK, m - 1 - b0);   // uniform over the workgroup
     if (nrec <= 0) return;
     const int i = b0 + threadIdx.x;
-    if (threadIdx.x < nrec) build_qrec_one(nodes, pos, i, inv_theta, near_dmax, srec_out[threadIdx.x]);
+    const bool dups = dflag[0] != 0;
+    if (!dups) dv = DupView{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+    if (threadIdx.x < nrec) {
+        build_qrec_one(nodes, pos, i, inv_theta, near_dmax, dv, srec_out[threadIdx.x]);
+        if (dups && dv.vflag[i]) {   // node i's chain top C_1: one child, node i itself (cells C_2..C_k)
+            const BHNode &nd = nodes[i];
+            QRec v;
+            v.cx = dv.vcom[2 * i]; v.cy = dv.vcom[2 * i + 1]; v.rball = 0.0; v.hmin = nd.hmin;
+            v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
+            v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
+            v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.ch[0] = nd.h; v.cref[0] = i; v.ccnt[0] = nd.cnt;
+            for (int k = 1; k < 4; ++k) { v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.ch[k] = QCH_LEAF; v.cref[k] = 0; v.ccnt[k] = 0; }
+            qrec[dv.virt + i] = v;
+        }
+    }
     __syncthreads();
     constexpr int V = sizeof(QRec) / 16;
     const uint4 *src = reinterpret_cast<const uint4 *>(srec_out);
@@ -775,7 +978,8 @@ __global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict_
 }
 
 __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos, int i,
-                               double inv_theta, double near_dmax, QRec &r) {
+                               double inv_theta, double near_dmax, const DupView &dv, QRec &r) {
+    const int32_t *tiecnt = dv.tiecnt, *notile = dv.notile;
     const BHNode &nd = nodes[i];
     if (nd.h < 0.0) return;                 // transparent or key tie: no record
     r.cx = nd.cx; r.cy = nd.cy; r.rball = nd.rball; r.hmin = nd.hmin;
@@ -793,6 +997,13 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
             const BHNode &cn = nodes[c];
             r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; r.ch[nc] = cn.delta >= 62 ? QCH_TIE : cn.h;
             r.cref[nc] = c; r.ccnt[nc] = cn.cnt;
+            if (cn.delta >= 62 && tiecnt && tiecnt[c] > 0) {   // pure duplicate group: one leaf, its multiplicity
+                const double2 p = pos[cn.first];
+                r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ch[nc] = QCH_MULTI; r.ccnt[nc] = tiecnt[c];
+            } else if (cn.delta < 62 && dv.vflag && dv.vflag[c]) {   // the chain top C_1 of real node c
+                r.ccx[nc] = dv.vcom[2 * c]; r.ccy[nc] = dv.vcom[2 * c + 1]; r.ch[nc] = 0.5 * nd.h;
+                r.cref[nc] = dv.virt + c; r.ccnt[nc] = dv.vcntf[c];
+            }
         }
         ++nc;
     };
@@ -814,7 +1025,8 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     // max corner distance is at least the squared half-diagonal, so if that
     // exceeds both hmin / theta and near_dmax (and rball = 0) no query can.
     const double hx = 0.5 * (nd.bx1 - nd.bx0), hy = 0.5 * (nd.by1 - nd.by0);
-    const bool tile_possible = nd.rball > 0.0 || (hx * hx + hy * hy) * (1.0 - 1e-9) <= fmax(nd.hmin * inv_theta, near_dmax);
+    const bool tile_possible = (nd.rball > 0.0 || (hx * hx + hy * hy) * (1.0 - 1e-9) <= fmax(nd.hmin * inv_theta, near_dmax))
+                               && !(notile && notile[i]);   // a duplicate group below: the reference's path
     r.nch = nc | (tile_possible ? QNCH_TILE : 0);
 }
 
@@ -856,7 +1068,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
-    int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, double2 *__restrict__ F,
+    int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, int32_t virt, double2 *__restrict__ F,
     double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     __shared__ int32_t sref[4][STACK];
@@ -898,17 +1110,27 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 if (valid) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
             }
         } else {
+            // the root cell; with duplicates whose copies the reference root
+            // counts differently from the cells below it: its virtual record
+            // (h = W, every copy), opened into the real root node
+            double rh = rt.h, rcx = rt.cx, rcy = rt.cy;
+            int32_t rcnt = rt.cnt, rpush = root;
+            if (meta[3]) {
+                const QRec &vq = qrec[virt + root];
+                rh = ldexp(rt.h, rt.delta >> 1);
+                rcx = vq.cx; rcy = vq.cy; rcnt = vq.cnt; rpush = virt + root;
+            }
             bool open = false;
             if (valid) {
                 if (STATS) ++nvis;
-                const double dx = qx - rt.cx, dy = qy - rt.cy;
+                const double dx = qx - rcx, dy = qy - rcy;
                 const double D = __fma_rn(dx, dx, dy * dy);
-                if (summarise(rt.h, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rt.cnt, fx, fy, zs);
+                if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rcnt, fx, fy, zs);
                 else open = true;
             }
             const uint64_t om = __ballot(open);
             if (om) {
-                if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
+                if (lane == 0) { sref[w][0] = rpush; smask[w][0] = om; }
                 sp = 1;
             }
         }
@@ -981,6 +1203,12 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 const double chh = nd.ch[c];
                 if (chh == QCH_LEAF) {
                     if (act) { if (STATS) ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
+                } else if (chh == QCH_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                    if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
+                        if (STATS) ++nvis;
+                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                        cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
+                    }
                 } else if (chh == QCH_TIE) {
                     const BHNode &tn = nodes[nd.cref[c]];
                     for (int p = tn.first; p <= tn.last; ++p) {
@@ -1252,9 +1480,24 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.idx_sorted = ws.get<int32_t>("bh.idx_sorted", n);
     t.inv = ws.get<int32_t>("bh.inv", n);
     t.dupc = ws.get<int32_t>("bh.dupc", n);
+    t.vid = ws.get<int32_t>("bh.vid", n);
+    t.dflag = ws.get<int32_t>("bh.dflag", 1);
+    t.rmin = ws.get<int32_t>("bh.rmin", n);
+    t.rvid = ws.get<int32_t>("bh.rvid", n);
+    t.rt2 = ws.get<int32_t>("bh.rt2", n);
+    t.arrive2 = ws.get<int32_t>("bh.arrive2", n);
+    t.cntcorr = ws.get<int32_t>("bh.cntcorr", n);
+    t.tiecnt = ws.get<int32_t>("bh.tiecnt", n);
+    t.notile = ws.get<int32_t>("bh.notile", n);
+    t.sumcorr = ws.get<double>("bh.sumcorr", 2 * (size_t)n);
+    t.vflag = ws.get<int32_t>("bh.vflag", n);
+    t.vcnt = ws.get<int32_t>("bh.vcnt", n);
+    t.vcntf = ws.get<int32_t>("bh.vcntf", n);
+    t.vsum = ws.get<double>("bh.vsum", 2 * (size_t)n);
+    t.vcom = ws.get<double>("bh.vcom", 2 * (size_t)n);
     t.pos = ws.get<double2>("bh.pos", n);
     t.nodes = ws.get<BHNode>("bh.nodes", n);
-    t.qrec = ws.get<QRec>("bh.qrec", n);
+    t.qrec = ws.get<QRec>("bh.qrec", 2 * (size_t)n);   // [n, 2n): virtual chain-top records (duplicates)
     t.agg = ws.get<double>("bh.agg", AGG * (size_t)n);
     t.parent_leaf = ws.get<int32_t>("bh.parent_leaf", n);
     t.parent_node = ws.get<int32_t>("bh.parent_node", n);
@@ -1350,9 +1593,11 @@ double bh_near_dmax(double theta) {
     return d;
 }
 
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap) {
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
+    t.rowmap = rowmap;
+    TSNE_HIP(hipMemsetAsync(t.dflag, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
     hipLaunchKernelGGL(bbox_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
     hipLaunchKernelGGL(morton_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
@@ -1362,15 +1607,28 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta) {
                                                (int)n, 0, 64, st));
     hipLaunchKernelGGL(count_in_root, dim3(1), dim3(64), 0, st, t.keys_sorted, n, t.meta);
     hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
-    hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc);
+    hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc, t.vid,
+                       t.dflag);
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
-                       t.nodes, t.parent_leaf, t.parent_node, t.arrive);
+                       t.nodes, t.parent_leaf, t.parent_node, t.arrive, t.arrive2);
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     hipLaunchKernelGGL(bottom_up<1024>, dim3(ceil_div(n, 1024)), dim3(1024), 0, st, t.pos, t.meta, t.W, inv_theta,
                        t.nodes, t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root, dim3(1), dim3(1), 0, st, t.meta);
+    // exact duplicates: the reference's multiplicities (each kernel returns
+    // at once unless dup_count saw a duplicate)
+    hipLaunchKernelGGL(dup_bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.meta, t.dflag, t.idx_sorted, rowmap,
+                       t.vid, t.nodes, t.parent_leaf, t.parent_node, t.arrive2, t.rmin, t.rvid, t.rt2);
+    hipLaunchKernelGGL(dup_clear, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.meta, t.dflag, t.cntcorr, t.sumcorr,
+                       t.tiecnt, t.notile, t.vflag, t.vcnt, t.vsum);
+    hipLaunchKernelGGL(dup_fixup, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.meta, t.dflag, t.pos, t.keys_sorted,
+                       t.dupc, t.idx_sorted, rowmap, t.nodes, t.parent_leaf, t.parent_node, t.rt2, t.cntcorr,
+                       t.sumcorr, t.tiecnt, t.notile, t.vflag, t.vcnt, t.vsum);
+    hipLaunchKernelGGL(dup_apply, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.meta, t.dflag, t.cntcorr, t.sumcorr,
+                       t.vflag, t.vcnt, t.vsum, t.vcntf, t.vcom, t.nodes);
+    const DupView dv{t.tiecnt, t.notile, t.vflag, t.vcntf, t.vcom, (int32_t)n};
     hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, QREC_BLK)), dim3(QREC_BLK), 0, st, t.nodes, t.pos, t.meta, inv_theta,
-                       bh_near_dmax(theta), t.qrec);
+                       bh_near_dmax(theta), t.dflag, dv, t.qrec);
     // subtree moments for the all-open fast path
     hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag, n);
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 1024)), dim3(1024), 0, st, t.nodes, n, t.meta, t.mom_flag,
@@ -1413,8 +1671,8 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     const int64_t waves = ceil_div(s1 - s0, 64);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd, dF,
-                       dz, visits, bcost);
+                       t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd,
+                       (int32_t)t.n, dF, dz, visits, bcost);
     hipLaunchKernelGGL(tile_apply, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.ttask, t.ttask_n, s0, s1, qlist, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor,
                        pack);

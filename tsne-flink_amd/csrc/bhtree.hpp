@@ -39,6 +39,7 @@ struct __attribute__((aligned(16))) BHNode {
 // interact directly).
 constexpr double QCH_LEAF = -1.0;
 constexpr double QCH_TIE = -2.0;
+constexpr double QCH_MULTI = -3.0;   // a leaf holding ccnt copies of one point (reference multiplicity)
 constexpr int32_t QNCH_TILE = 0x100;   // nch flag: an all-open tile test can pass here
 struct __attribute__((aligned(16))) QRec {
     double cx, cy;              // centre of mass
@@ -57,9 +58,24 @@ struct BHTree {
     int32_t *idx = nullptr, *idx_sorted = nullptr;  // sorted position -> original row
     int32_t *inv = nullptr;                         // original row -> sorted position
     int32_t *dupc = nullptr;                        // exact duplicates of each sorted point (incl. itself)
+    // exact-duplicate multiplicities of the reference (QuadTree.scala:52-61):
+    // dflag[0] = some point has a duplicate; per binary node: first inserted
+    // row, its value id, the row at which a second distinct value arrived
+    // (t2: when the reference cell splits); count / sum corrections of real
+    // cells, the leaf multiplicity of a pure duplicate group's tie node,
+    // and a no-tile mark on the cells above such a group
+    int32_t *dflag = nullptr, *vid = nullptr, *rmin = nullptr, *rvid = nullptr, *rt2 = nullptr, *arrive2 = nullptr;
+    int32_t *cntcorr = nullptr, *tiecnt = nullptr, *notile = nullptr;
+    double *sumcorr = nullptr;
+    // a reference cell chain C_1 > ... > C_k (same points, one binary node)
+    // whose top cell counts different duplicate copies than the rest: a
+    // virtual record (qrec[n + node]) for C_1 with its own count / centre
+    int32_t *vflag = nullptr, *vcnt = nullptr, *vcntf = nullptr;
+    double *vsum = nullptr, *vcom = nullptr;
+    const int32_t *rowmap = nullptr;                // label -> insertion row (nullable: identity)
     double2 *pos = nullptr;                         // sorted positions (leaves + queries)
     BHNode *nodes = nullptr;
-    QRec *qrec = nullptr;       // per binary node id, valid for real nodes
+    QRec *qrec = nullptr;       // per binary node id, valid for real nodes; [n, 2n): virtual chain tops
     double *agg = nullptr;      // per-node bottom-up aggregates (AGG doubles)
     int32_t *parent_leaf = nullptr, *parent_node = nullptr;
     int32_t *arrive = nullptr;
@@ -88,8 +104,10 @@ struct BHTree {
 
 // Allocate (from ctx->ws) for n points.
 void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
-// Build the tree of all n points of Y (n x 2, device).
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta);
+// Build the tree of all n points of Y (n x 2, device).  rowmap (device,
+// nullable = identity) gives each point's insertion row in the reference
+// (its original index): the order that decides duplicate multiplicities.
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap = nullptr);
 // Repulsion for the query slots [s0, s1): sorted positions, or with qlist
 // (device, ascending sorted positions: one rank's own queries) the positions
 // qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted

@@ -1067,7 +1067,8 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         s->valw = ws.get<double>("opt.valw", nnz + 1);
         // initial labels in P's graph order (TSNE_GRAPH_ORDER=0: the original order)
         static const bool gorder = [] { const char *e = getenv("TSNE_GRAPH_ORDER"); return !(e && e[0] == '0'); }();
-        if (gorder && n >= 2) {
+        const bool dense_small = s->nnz / n > 1024 && n * 16 <= (2 << 20);   // see maybe_relabel
+        if (gorder && n >= 2 && !(dense_small && world == 1)) {
             int32_t *order = ws.get<int32_t>("opt.g.order", n);
             graph_order(ctx, s, order);
             relabel(ctx, s, order, s->own);
@@ -1209,6 +1210,10 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
 static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     hipStream_t st = ctx->stream;
     const int64_t n = s->n;
+    // dense rows over a small embedding (the distance-matrix mode, C5): every
+    // row gathers all of Y, which sits in one XCD's L2 (n * 16 B <= 2 MiB)
+    // whatever the labels, so a relabel (a copy of the whole P) buys nothing
+    if (ctx->world == 1 && s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
     // a fixed sample of rows, ~1 << 22 entries at most (dense rows: fewer rows)
     const int64_t avg = std::max<int64_t>(1, s->nnz / std::max<int64_t>(1, n));
     const int64_t nsamp = std::max<int64_t>(1, std::min<int64_t>({n, 1 << 16, (1 << 22) / avg}));
@@ -1285,7 +1290,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     };
     if (overlap && ov_mode == 0) side_attract();
     // 1. tree (identical on every rank)
-    bh_build(ctx, s->tree, Y, p.theta);
+    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur]);   // insertion rows = original indices
     if (overlap && ov_mode == 1) side_attract();
     if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
