@@ -747,9 +747,16 @@ __global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ 
             for (int k0 = 0; k0 < MOM_K; k0 += 8) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) rw[lane * 9 + j] = (k0 + j < MOM_K) ? acc[k0 + j] : 0.0;
+                // the other lanes' stores must have landed before the cross-lane
+                // loads (and those loads before the next round overwrites rw)
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+                __builtin_amdgcn_wave_barrier();
                 double v = 0.0;
 #pragma unroll
                 for (int r = 0; r < 8; ++r) v += rw[(r0 + r) * 9 + col];
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
                 v += __shfl_xor(v, 8, 64);
                 v += __shfl_xor(v, 16, 64);
                 v += __shfl_xor(v, 32, 64);
