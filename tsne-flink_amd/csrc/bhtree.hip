@@ -91,7 +91,7 @@ __global__ void bbox_partial(const double *__restrict__ Y, int64_t n, double *__
 
 // One 256-thread block folds the per-block partials.
 __global__ void bbox_final(const double *__restrict__ part, int nb, double *__restrict__ W,
-                           int32_t *__restrict__ meta) {
+                           int32_t *__restrict__ meta, double *__restrict__ bb) {
     __shared__ double sm[4][4];
     double mnx = __builtin_inf(), mxx = -__builtin_inf(), mny = __builtin_inf(), mxy = -__builtin_inf();
     for (int b = threadIdx.x; b < nb; b += blockDim.x) {
@@ -109,6 +109,7 @@ __global__ void bbox_final(const double *__restrict__ part, int nb, double *__re
         }
         const double a = sm[0][1] - sm[0][0], c = sm[0][3] - sm[0][2];
         *W = a > c ? a : c;  // scala.math.max(maxX - minX, maxY - minY)
+        for (int k = 0; k < 4; ++k) bb[k] = sm[0][k];
         meta[0] = 0;
         meta[2] = 0;
         meta[3] = 0;         // root replaced by its virtual chain top (duplicates, dup_apply)
@@ -1476,6 +1477,131 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
     }
 }
 
+// ---- Root-tile mode (the small-embedding phase).  When every point lies in
+// the root cell, no point has an exact duplicate, the bounding box is so
+// small that every query opens the root (4 theta max(dx, dy) < 1: a cell
+// holding all points has half-width >= max(dx, dy) / 2 and D <= dx^2 + dy^2)
+// and passes the near-exact test at it (every box corner within near_dmax),
+// the normal path makes the root one tile for every lane, evaluated from the
+// root's moments (tile_apply -> moment_apply).  This path computes that --
+// the root's moments (moment_items / moment_reduce, chunks of the points in
+// label order), the same per-query additions -- without the Morton sort, the
+// radix tree, the bottom-up aggregates, the quad records or the moments of
+// the other ~n/64 nodes.  Duplicates are found by a hash set instead of the
+// sorted order (any duplicate: the full path).
+// Exact-duplicate detection without sorting: open-addressing hash set of
+// point indices keyed by the coordinates' bits (flag[0] = 1 on a repeat).
+__device__ __forceinline__ uint64_t hash_xy(double x, double y) {
+    uint64_t h = (uint64_t)__double_as_longlong(x) * 0x9E3779B97F4A7C15ull;
+    h ^= (uint64_t)__double_as_longlong(y) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+    h ^= h >> 31;
+    h *= 0xD6E8FEB86659FD93ull;
+    return h ^ (h >> 32);
+}
+__global__ void dup_hash(const double *__restrict__ Y, int64_t n, int32_t *__restrict__ tab, uint64_t mask,
+                         int32_t *__restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = Y[2 * i], y = Y[2 * i + 1];
+    uint64_t h = hash_xy(x, y) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+        const int32_t prev = atomicCAS(&tab[h], 0, (int32_t)(i + 1));
+        if (prev == 0) return;
+        const int64_t j = prev - 1;
+        if (Y[2 * j] == x && Y[2 * j + 1] == y) { flag[0] = 1; return; }
+        h = (h + 1) & mask;
+    }
+}
+
+__global__ void root_tile_check(const int32_t *__restrict__ dflag, const double *__restrict__ bb,
+                                const double *__restrict__ Wp, int64_t n, double theta, double near_dmax,
+                                int32_t *__restrict__ status) {
+    const double W = *Wp, dx = bb[1] - bb[0], dy = bb[3] - bb[2];
+    const double amax = fmax(fmax(fabs(bb[0]), fabs(bb[1])), fmax(fabs(bb[2]), fabs(bb[3])));
+    const double ex = 6e-15 * amax;   // the traversal's rounding margin, bounded for every query in the box
+    const double dmax = ((dx + ex) * (dx + ex) + (dy + ex) * (dy + ex)) * (1.0 + 1e-11);
+    // every point inside the root cell Cell(0, 0, W) (closed, Cell.scala:31-36)
+    const bool in_root = -W <= bb[0] && bb[1] <= W && -W <= bb[2] && bb[3] <= W;
+    const bool ok = in_root && n >= MOM_MIN_POINTS && !dflag[0] && W > 0.0 && theta > 0.0 &&
+                    4.0 * theta * fmax(dx, dy) * (1.0 + 1e-12) < 1.0 && dmax <= near_dmax;
+    status[0] = ok ? 1 : 0;
+}
+
+// The root's moment items: node 0 = all m sorted points, its bounding box.
+__global__ void root_tile_prep(const double *__restrict__ bb, int64_t n, BHNode *__restrict__ nodes,
+                               int32_t *__restrict__ mom_cnt, int32_t *__restrict__ mom_off,
+                               int32_t *__restrict__ mom_list, int32_t *__restrict__ mom_item, int32_t *__restrict__ meta_w,
+                               int32_t *__restrict__ inv, int32_t *__restrict__ idx_sorted) {
+    const int m = (int)n;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        inv[i] = i;            // no sort: query / force slots are the labels
+        idx_sorted[i] = i;
+    }
+    const int K = (m + MOM_CHUNK - 1) / MOM_CHUNK;
+    for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < K; it += gridDim.x * blockDim.x) mom_item[it] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        BHNode &r = nodes[0];
+        r.first = 0; r.last = m - 1; r.cnt = m;
+        r.bx0 = bb[0]; r.bx1 = bb[1]; r.by0 = bb[2]; r.by1 = bb[3];
+        mom_cnt[0] = K;
+        mom_off[0] = 0;
+        mom_off[n] = K;
+        mom_list[0] = 0;
+        meta_w[0] = m;
+        meta_w[2] = 1;
+    }
+}
+
+// Per query: what the traversal (root tile, z -= duplicates), tile_apply
+// (moment task, or the dense leaf sum) and moment_apply write for it.
+template <bool STATS>
+__global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict__ pos, const int32_t *__restrict__ dupc,
+                                                      const BHNode *__restrict__ nodes, const double *__restrict__ mom,
+                                                      const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag,
+                                                      int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
+                                                      double2 *__restrict__ F, double *__restrict__ Z,
+                                                      unsigned long long *__restrict__ visits) {
+    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = k < g1;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : 0;
+    const int m = meta[0];
+    const BHNode &rt = nodes[0];
+    bool usem = false, want = false;
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    if (valid) {
+        const double2 q = pos[s];
+        want = moment_ok(rt.bx0, rt.bx1, rt.by0, rt.by1, q.x, q.y);
+        usem = want && mom_flag[0] != 0;
+        if (usem) {
+            double cx, cy, R;
+            box_centre(rt, cx, cy, R);
+            moment_eval(mom, q.x - cx, q.y - cy, fx, fy, zs);
+        } else {   // the exact leaf sum (only if the series bound fails: not expected here)
+            for (int p = 0; p < m; ++p) { const double2 pp = pos[p]; pair_force(q.x, q.y, pp.x, pp.y, fx, fy, zs); }
+        }
+        const double z0 = dupc ? -(double)dupc[s] : -1.0;   // no duplicates in root-tile mode: the query itself
+        if (usem) {
+            F[s] = make_double2(0.0 + fx, 0.0 + fy);
+            Z[s] = z0 + zs;
+        } else {
+            F[s] = make_double2(fx, fy);
+            Z[s] = z0 + zs;
+        }
+    }
+    const unsigned long long nw = __popcll(__ballot(want));
+    if (lane_id() == 0 && nw) atomicAdd(&mom_flag[1], (int)nw);
+    if (STATS && visits) {
+        const unsigned long long nv = __popcll(__ballot(valid)), nu = __popcll(__ballot(usem));
+        if (lane_id() == 0 && nv) {
+            atomicAdd(visits, nv * (unsigned long long)m);
+            atomicAdd(visits + 1, nu);
+            atomicAdd(visits + 2, (nv - nu) * (unsigned long long)m);
+            atomicAdd(visits + 3, 1ull);
+            atomicAdd(visits + 4, (unsigned long long)m);
+        }
+    }
+}
+
 }  // namespace
 
 void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
@@ -1535,6 +1661,9 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
     t.bbox_part = ws.get<double>("bh.bbox_part", 4 * (size_t)t.bbox_blocks);
     t.W = ws.get<double>("bh.W", 1);
+    t.bb = ws.get<double>("bh.bb", 4);
+    t.status = ws.get<int32_t>("bh.status", 4);
+    t.status_h = ctx->pinned;
     size_t tb = 0;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
                                                (int)n, 0, 64, ctx->stream));
@@ -1600,13 +1729,39 @@ double bh_near_dmax(double theta) {
     return d;
 }
 
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap) {
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap, bool root_tile_ok) {
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
     t.rowmap = rowmap;
+    t.root_tile = false;
     TSNE_HIP(hipMemsetAsync(t.dflag, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
-    hipLaunchKernelGGL(bbox_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
+    hipLaunchKernelGGL(bbox_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta, t.bb);
+    if (root_tile_ok) {   // one small read-back decides the path (the host must know which kernels to launch)
+        const uint64_t tsz = (uint64_t)1 << (64 - __builtin_clzll((uint64_t)std::max<int64_t>(2, 2 * n) - 1));
+        int32_t *tab = ctx->ws.get<int32_t>("bh.dup_hash", tsz);
+        TSNE_HIP(hipMemsetAsync(tab, 0, sizeof(int32_t) * tsz, st));
+        hipLaunchKernelGGL(dup_hash, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, tab, tsz - 1, t.dflag);
+        hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, bh_near_dmax(theta),
+                           t.status);
+        TSNE_HIP(hipMemcpyAsync(t.status_h, t.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        TSNE_HIP(hipStreamSynchronize(st));
+        if (t.status_h[0]) {
+            t.root_tile = true;
+            hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag, n);
+            hipLaunchKernelGGL(root_tile_prep, dim3(std::min<int64_t>(1024, ceil_div(n, 256))), dim3(256), 0, st, t.bb,
+                               n, t.nodes, t.mom_cnt, t.mom_off, t.mom_list, t.mom_item, t.meta, t.inv, t.idx_sorted);
+            const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
+            hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, reinterpret_cast<const double2 *>(dY),
+                               t.nodes, t.mom_off, n, t.mom_item, t.mom_part);
+            hipLaunchKernelGGL(moment_reduce, dim3(1), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
+                               t.mom_part, t.mom);
+            t.root_pos = reinterpret_cast<const double2 *>(dY);
+            TSNE_LAUNCH_CHECK();
+            return;
+        }
+        TSNE_HIP(hipMemsetAsync(t.dflag, 0, sizeof(int32_t), st));   // dup_count recomputes it
+    }
     hipLaunchKernelGGL(morton_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
     TSNE_LAUNCH_CHECK();
     size_t tb = t.sort_tmp_bytes;
@@ -1661,6 +1816,16 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist,
                   unsigned long long *bcost) {
     if (s1 <= s0) return;
+    if (t.root_tile) {
+        if (visits)
+            hipLaunchKernelGGL(root_tile_eval<true>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream,
+                               t.root_pos, nullptr, t.nodes, t.mom, t.meta, t.mom_flag, s0, s1, qlist, dF, dz, visits);
+        else
+            hipLaunchKernelGGL(root_tile_eval<false>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream,
+                               t.root_pos, nullptr, t.nodes, t.mom, t.meta, t.mom_flag, s0, s1, qlist, dF, dz, visits);
+        TSNE_LAUNCH_CHECK();
+        return;
+    }
     const double near_dmax = bh_near_dmax(theta);
     // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD block order (TSNE_BH_XCD = run
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)

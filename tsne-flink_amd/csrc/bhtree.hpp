@@ -97,6 +97,11 @@ struct BHTree {
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     double *bbox_part = nullptr, *W = nullptr;
+    double *bb = nullptr;        // bounding box of all points: x0, x1, y0, y1
+    int32_t *status = nullptr;   // [0] root-tile mode possible (see bh_root_tile)
+    int32_t *status_h = nullptr; // pinned host copy
+    bool root_tile = false;      // this build took the root-tile path (no sort: slots = labels)
+    const double2 *root_pos = nullptr;   // root-tile mode: the points in label order
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     int bbox_blocks = 0;
@@ -107,7 +112,11 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
 // Build the tree of all n points of Y (n x 2, device).  rowmap (device,
 // nullable = identity) gives each point's insertion row in the reference
 // (its original index): the order that decides duplicate multiplicities.
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap = nullptr);
+// With root_tile_ok, the build stops after the sort when every query's whole
+// tree is one near-exact subtree evaluated from the root's moments (the
+// small-embedding phase, see bh_root_tile): t.root_tile tells which.
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap = nullptr,
+              bool root_tile_ok = false);
 // Repulsion for the query slots [s0, s1): sorted positions, or with qlist
 // (device, ascending sorted positions: one rank's own queries) the positions
 // qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted

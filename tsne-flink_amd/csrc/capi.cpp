@@ -184,6 +184,7 @@ int tsne_ctx_create(int32_t device, tsne_ctx **out) {
         c->cu_count = prop.multiProcessorCount;
         TSNE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
+        TSNE_HIP(hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 64 * sizeof(int32_t)));
         *out = c.release();
     });
 }
@@ -238,6 +239,8 @@ int tsne_ctx_destroy(tsne_ctx *ctx) {
         comm_destroy(ctx);
         ctx->timers.clear();
         ctx->ws.clear();
+        if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
         if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     });
     delete ctx;

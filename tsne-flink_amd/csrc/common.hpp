@@ -149,6 +149,7 @@ struct tsne_ctx {
     tsne::Workspace ws;
     tsne::OptState *opt = nullptr;
     tsne::StageTimers timers;
+    int32_t *pinned = nullptr;   // small pinned host scratch (per-iteration read-backs)
     int cu_count = 256;
     // tsne_ctx_create_multi: the per-device contexts (ranks) of a group
     // handle; host-buffer operators fan out over them, one thread per rank

@@ -1290,7 +1290,10 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     };
     if (overlap && ov_mode == 0) side_attract();
     // 1. tree (identical on every rank)
-    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur]);   // insertion rows = original indices
+    // insertion rows = original indices; the root-tile shortcut while the
+    // embedding is small (TSNE_ROOT_TILE=0: always the full tree)
+    static const bool root_tile = [] { const char *e = getenv("TSNE_ROOT_TILE"); return !(e && e[0] == '0'); }();
+    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile);
     if (overlap && ov_mode == 1) side_attract();
     if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
