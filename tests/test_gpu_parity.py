@@ -203,6 +203,24 @@ def test_gradient_large_near_exact(ctx, n, scale):
         assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
+@pytest.mark.parametrize("n,scale,dups", [(20000, 1e-4, False), (5000, 1e-3, False), (5000, 1e-4, True)])
+def test_root_tile_mode_per_point(ctx, n, scale, dups):
+    """Root-tile mode (bhtree.hip: a small embedding's whole tree is one
+    near-exact subtree for every query -> the root's moments as polynomials,
+    no sort / tree): per-point F and z against the oracle's quadtree.  With
+    exact duplicates the hash-round check sends the build to the full path
+    (the reference's multiplicities)."""
+    rng = np.random.default_rng(n + int(1e5 * scale))
+    Y = rng.normal(size=(n, 2)) * scale
+    if dups:
+        Y[[7, 4000, 123]] = Y[7]
+        Y[[99, 98]] = Y[99]
+    F, z = ctx.repulsion(Y, 0.5)
+    rep, zi = O.repulsion(Y, 0.5, threads=8)
+    assert np.abs(z - zi).max() <= NEAR_TOL * zi.max()
+    assert np.abs(F - rep).max() <= NEAR_TOL * np.abs(rep).max()
+
+
 @pytest.mark.parametrize("theta,scale", [(0.0, 1.0), (0.5, 1.0), (0.25, 30.0), (0.5, 1e-3)])
 def test_gradient_duplicate_multiplicity(ctx, theta, scale):
     """Exact duplicate embedding points (QuadTree.scala:52-61): a leaf holding

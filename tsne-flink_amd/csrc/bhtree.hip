@@ -657,7 +657,7 @@ __device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double 
 __global__ void moment_gate(int32_t *mom_flag, int64_t n) {
     // worth building when the previous traversal had at least n / 64 eligible
     // tiles (fewer go to dense tiles, cheaper than ~1 ms of moment building)
-    mom_flag[0] = (int64_t)mom_flag[1] >= (n >> 6) + 1;
+    mom_flag[0] = mom_flag[1] >= mom_flag[2];
     mom_flag[1] = 0;
 }
 
@@ -791,16 +791,10 @@ __global__ void moment_reduce(const int32_t *__restrict__ meta, const int32_t *_
     }
 }
 
-// Subtree sums for one lane's query from the node's moments (see the header).
-// Returns z += sum 1/(1+D), (fx, fy) += sum (q - y)/(1+D)^2 over the subtree's
-// points, the query itself and its exact duplicates included (D = 0: they add
-// 1 to z and 0 to F; the traversal subtracts them).
-__device__ __forceinline__ void moment_eval(const double *mu, double vx, double vy, double &fx, double &fy,
-                                            double &zs) {
-    const double A = vx * vx + vy * vy;
+// omega_i (z) and phi_i (F) weights of S_i = sum D^i, Sx_i = sum D^i w, for
+// A = |v|^2.
+__device__ __forceinline__ void moment_weights(double A, double *om, double *ph) {
     const double B = 1.0 / (1.0 + A);
-    // omega_i (z) and phi_i (F) weights of S_i = sum D^i, Sx_i = sum D^i w
-    double om[MOM_ORDER + 1], ph[MOM_ORDER + 1];
     {
         double Ap[MOM_ORDER + 1], Bp[MOM_ORDER + 3];
         Ap[0] = 1.0; Bp[0] = 1.0;
@@ -821,6 +815,16 @@ __device__ __forceinline__ void moment_eval(const double *mu, double vx, double 
             ph[i] = (i & 1) ? sp : -sp;
         }
     }
+}
+
+// Subtree sums for one lane's query from the node's moments (see the header).
+// Returns z += sum 1/(1+D), (fx, fy) += sum (q - y)/(1+D)^2 over the subtree's
+// points, the query itself and its exact duplicates included (D = 0: they add
+// 1 to z and 0 to F; the traversal subtracts them).
+__device__ __forceinline__ void moment_eval(const double *mu, double vx, double vy, double &fx, double &fy,
+                                            double &zs) {
+    double om[MOM_ORDER + 1], ph[MOM_ORDER + 1];
+    moment_weights(vx * vx + vy * vy, om, ph);
     // shift to the query: w = u - v; X[e] = (-v_x)^e / e!
     double X[MOM_DEG + 1], Yv[MOM_DEG + 1];
     X[0] = 1.0; Yv[0] = 1.0;
@@ -863,6 +867,97 @@ __device__ __forceinline__ void moment_eval(const double *mu, double vx, double 
             }
         }
     }
+    zs += z;
+    fx += gx;
+    fy += gy;
+}
+
+// ---- The same sums as polynomials in v (root-tile mode: ONE subtree for
+// every query).  moment_eval computes z = sum_i om_i(A) Qz_i(v) with
+//   Qz_i(v) = sum_{a+b=2i, a,b even} C(i, a/2) a! b! nu(a, b),
+//   nu(a, b) = sum_{p<=a, q<=b} mu(a-p, b-q) (-v_x)^p (-v_y)^q / (p! q!),
+// a polynomial of degree 2i in (v_x, v_y); gx / gy likewise with ph_i and
+// Qx_i (a odd) / Qy_i (b odd) of degree 2i+1.  Their POLY_K coefficients
+// depend on the subtree's moments only: poly_coef computes them once, and a
+// query evaluates 3 (MOM_ORDER+1) small polynomials by Horner with uniform
+// (scalar-loaded) coefficients instead of shifting the moments itself --
+// ~40 VGPRs instead of 256 + spills.
+__host__ __device__ constexpr int poly_len(int d) { return (d + 1) * (d + 2) / 2; }
+__host__ __device__ constexpr int poly_off_z(int i) { return i == 0 ? 0 : poly_off_z(i - 1) + poly_len(2 * i - 2); }
+constexpr int POLY_X = poly_off_z(MOM_ORDER + 1);
+__host__ __device__ constexpr int poly_off_x(int i) { return i == 0 ? POLY_X : poly_off_x(i - 1) + poly_len(2 * i - 1); }
+constexpr int POLY_Y = poly_off_x(MOM_ORDER + 1);
+__host__ __device__ constexpr int poly_off_y(int i) { return POLY_Y + poly_off_x(i) - POLY_X; }
+constexpr int POLY_K = POLY_Y + (POLY_Y - POLY_X);
+static_assert(POLY_K == 345, "MOM_ORDER 4: 95 + 125 + 125 coefficients");
+
+__device__ __forceinline__ double factd(int k) {
+    double f = 1.0;
+    for (int j = 2; j <= k; ++j) f *= j;
+    return f;
+}
+
+// Coefficient c of the root polynomials from the node's moments mu (one
+// thread per coefficient; (p, q) ordered like midx within each polynomial).
+__global__ void poly_coef(const double *__restrict__ mu, double *__restrict__ coef) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= POLY_K) return;
+    int kind = 0, i = 0, r = c;   // kind 0 z, 1 x, 2 y
+    if (c >= POLY_Y) { kind = 2; r = c - POLY_Y; }
+    else if (c >= POLY_X) { kind = 1; r = c - POLY_X; }
+    for (;;) {
+        const int len = poly_len(kind == 0 ? 2 * i : 2 * i + 1);
+        if (r < len) break;
+        r -= len;
+        ++i;
+    }
+    const int d = kind == 0 ? 2 * i : 2 * i + 1;
+    int p = 0;
+    while (r >= d + 1 - p) { r -= d + 1 - p; ++p; }
+    const int q = r;
+    double s = 0.0;
+    for (int a = p; a <= d; ++a) {
+        const int b = d - a;
+        const bool ok = kind == 0 ? !(a & 1) : kind == 1 ? (a & 1) : !(a & 1);
+        if (!ok || b < q) continue;
+        const int j = kind == 1 ? (a - 1) / 2 : a / 2;
+        s += factd(i) / (factd(j) * factd(i - j)) * factd(a) * factd(b) * mu[midx(a - p, b - q)];
+    }
+    coef[c] = (((p + q) & 1) ? -s : s) / (factd(p) * factd(q));
+}
+
+template <int D>
+__device__ __forceinline__ double poly_eval(const double *__restrict__ c, double vx, double vy) {
+    double acc = 0.0;
+#pragma unroll
+    for (int p = D; p >= 0; --p) {
+        const int o = p * (D + 1) - p * (p - 1) / 2;
+        double r = c[o + D - p];
+#pragma unroll
+        for (int q = D - p - 1; q >= 0; --q) r = __fma_rn(r, vy, c[o + q]);
+        acc = p == D ? r : __fma_rn(acc, vx, r);
+    }
+    return acc;
+}
+
+template <int I>
+__device__ __forceinline__ void poly_terms(const double *__restrict__ c, double vx, double vy, const double *om,
+                                           const double *ph, double &z, double &gx, double &gy) {
+    if constexpr (I <= MOM_ORDER) {
+        z = __fma_rn(om[I], poly_eval<2 * I>(c + poly_off_z(I), vx, vy), z);
+        gx = __fma_rn(ph[I], poly_eval<2 * I + 1>(c + poly_off_x(I), vx, vy), gx);
+        gy = __fma_rn(ph[I], poly_eval<2 * I + 1>(c + poly_off_y(I), vx, vy), gy);
+        poly_terms<I + 1>(c, vx, vy, om, ph, z, gx, gy);
+    }
+}
+
+// moment_eval from the subtree's polynomial coefficients (poly_coef).
+__device__ __forceinline__ void poly_moment_eval(const double *__restrict__ coef, double vx, double vy, double &fx,
+                                                 double &fy, double &zs) {
+    double om[MOM_ORDER + 1], ph[MOM_ORDER + 1];
+    moment_weights(vx * vx + vy * vy, om, ph);
+    double z = 0.0, gx = 0.0, gy = 0.0;
+    poly_terms<0>(coef, vx, vy, om, ph, z, gx, gy);
     zs += z;
     fx += gx;
     fy += gy;
@@ -1463,7 +1558,10 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
         }
     }
     const int wwant = wave_sum(nwant);
-    if (lane == 0 && wwant) atomicAdd(&mom_flag[1], wwant);
+    // (only until the gate's threshold is reached: one memory-side atomic
+    // per wave on one word would serialise ~n / 64 of them)
+    if (lane == 0 && wwant && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
+        atomicAdd(&mom_flag[1], wwant);
     if (visits) {   // [1] moment evaluations, [2] dense pair terms; [10..12] diagnostics:
                     // tile tasks, wave-level dense points, tasks with a moment check
         const unsigned long long tm = wave_sum((unsigned long long)ntask), td = wave_sum(ndense);
@@ -1489,28 +1587,70 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
 // radix tree, the bottom-up aggregates, the quad records or the moments of
 // the other ~n/64 nodes.  Duplicates are found by a hash set instead of the
 // sorted order (any duplicate: the full path).
-// Exact-duplicate detection without sorting: open-addressing hash set of
-// point indices keyed by the coordinates' bits (flag[0] = 1 on a repeat).
-__device__ __forceinline__ uint64_t hash_xy(double x, double y) {
-    uint64_t h = (uint64_t)__double_as_longlong(x) * 0x9E3779B97F4A7C15ull;
+//
+// Exact-duplicate detection without sorting or atomics (device-scope atomics
+// execute at the memory side, ~13 G/s for one CAS per point): rounds of a
+// last-writer-wins table of 4n slots.  Round r: every open point stores its
+// index at slot h_r(point) (plain stores; one of the points sharing a slot
+// wins), then -- next kernel -- reads the slot back: the winner is done, a
+// point that finds a point with its exact coordinates raises the flag, and a
+// point that finds different coordinates stays open for the next round's
+// hash.  Two copies of one position share every slot, so they stay open
+// together until one of them wins one (found).  ~11 % of the points stay open
+// after round 0, ~0.2 % after round 1; any still open after the last round
+// raise the flag too (flag = "not shown duplicate-free": the full path, which
+// handles every case).
+constexpr int DUP_ROUNDS = 4;
+__device__ __forceinline__ uint64_t hash_xy(double x, double y, uint64_t seed) {
+    uint64_t h = ((uint64_t)__double_as_longlong(x) ^ seed) * 0x9E3779B97F4A7C15ull;
     h ^= (uint64_t)__double_as_longlong(y) + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
     h ^= h >> 31;
     h *= 0xD6E8FEB86659FD93ull;
     return h ^ (h >> 32);
 }
-__global__ void dup_hash(const double *__restrict__ Y, int64_t n, int32_t *__restrict__ tab, uint64_t mask,
-                         int32_t *__restrict__ flag) {
+__device__ __forceinline__ uint64_t dup_seed(int round) { return 0xA24BAED4963EE407ull * (uint64_t)(round + 1); }
+
+__global__ __launch_bounds__(256) void dup_store(const double2 *__restrict__ Y, int64_t n, int32_t *__restrict__ tab,
+                                                 uint64_t mask, const uint8_t *__restrict__ open, int round) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double x = Y[2 * i], y = Y[2 * i + 1];
-    uint64_t h = hash_xy(x, y) & mask;
-    for (uint64_t probe = 0; probe <= mask; ++probe) {
-        const int32_t prev = atomicCAS(&tab[h], 0, (int32_t)(i + 1));
-        if (prev == 0) return;
-        const int64_t j = prev - 1;
-        if (Y[2 * j] == x && Y[2 * j + 1] == y) { flag[0] = 1; return; }
-        h = (h + 1) & mask;
+    if (i >= n || (round > 0 && !open[i])) return;
+    const double2 p = Y[i];
+    tab[hash_xy(p.x, p.y, dup_seed(round)) & mask] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(256) void dup_probe(const double2 *__restrict__ Y, int64_t n,
+                                                 const int32_t *__restrict__ tab, uint64_t mask,
+                                                 uint8_t *__restrict__ open, int round, int32_t *__restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (round > 0 && !open[i])) return;
+    const double2 p = Y[i];
+    const int64_t w = tab[hash_xy(p.x, p.y, dup_seed(round)) & mask];
+    bool still = false;
+    if (w != i) {
+        const double2 o = Y[w];
+        if (o.x == p.x && o.y == p.y) flag[0] = 1;
+        else still = true;
     }
+    if (still && round == DUP_ROUNDS - 1) flag[0] = 1;
+    if (round == 0 || !still) open[i] = still ? 1 : 0;
+}
+
+// The root's moments from its chunk partials (root-tile mode, ~n / MOM_CHUNK
+// chunks): one block per moment, fixed strided + tree order.
+__global__ __launch_bounds__(256) void root_moment_reduce(const int32_t *__restrict__ mom_off, int64_t n,
+                                                          const double *__restrict__ part, double *__restrict__ mom) {
+    __shared__ double red[256];
+    const int k = blockIdx.x;
+    const int K = mom_off[n];
+    double s = 0.0;
+    for (int it = threadIdx.x; it < K; it += 256) s += part[(int64_t)it * MOM_K + k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) mom[k] = red[0];
 }
 
 __global__ void root_tile_check(const int32_t *__restrict__ dflag, const double *__restrict__ bb,
@@ -1531,7 +1671,8 @@ __global__ void root_tile_check(const int32_t *__restrict__ dflag, const double 
 __global__ void root_tile_prep(const double *__restrict__ bb, int64_t n, BHNode *__restrict__ nodes,
                                int32_t *__restrict__ mom_cnt, int32_t *__restrict__ mom_off,
                                int32_t *__restrict__ mom_list, int32_t *__restrict__ mom_item, int32_t *__restrict__ meta_w,
-                               int32_t *__restrict__ inv, int32_t *__restrict__ idx_sorted) {
+                               int32_t *__restrict__ inv, int32_t *__restrict__ idx_sorted,
+                               int32_t *__restrict__ mom_flag) {
     const int m = (int)n;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         inv[i] = i;            // no sort: query / force slots are the labels
@@ -1549,15 +1690,19 @@ __global__ void root_tile_prep(const double *__restrict__ bb, int64_t n, BHNode 
         mom_list[0] = 0;
         meta_w[0] = m;
         meta_w[2] = 1;
+        // every query's tile is eligible: the next full build keeps moments on
+        mom_flag[0] = 1;
+        mom_flag[1] = mom_flag[2];
     }
 }
 
-// Per query: what the traversal (root tile, z -= duplicates), tile_apply
-// (moment task, or the dense leaf sum) and moment_apply write for it.
+// Per query: what the traversal (root tile, z -= the query itself: no
+// duplicates in this mode), tile_apply (moment task, or the dense leaf sum)
+// and moment_apply write for it -- the moment sums from the root's
+// polynomial coefficients (poly_moment_eval).
 template <bool STATS>
-__global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict__ pos, const int32_t *__restrict__ dupc,
-                                                      const BHNode *__restrict__ nodes, const double *__restrict__ mom,
-                                                      const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag,
+__global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+                                                      const double *__restrict__ coef, const int32_t *__restrict__ meta,
                                                       int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
                                                       double2 *__restrict__ F, double *__restrict__ Z,
                                                       unsigned long long *__restrict__ visits) {
@@ -1566,38 +1711,37 @@ __global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict_
     const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : 0;
     const int m = meta[0];
     const BHNode &rt = nodes[0];
-    bool usem = false, want = false;
+    bool usem = false;
     double fx = 0.0, fy = 0.0, zs = 0.0;
     if (valid) {
         const double2 q = pos[s];
-        want = moment_ok(rt.bx0, rt.bx1, rt.by0, rt.by1, q.x, q.y);
-        usem = want && mom_flag[0] != 0;
+        usem = moment_ok(rt.bx0, rt.bx1, rt.by0, rt.by1, q.x, q.y);
         if (usem) {
             double cx, cy, R;
             box_centre(rt, cx, cy, R);
-            moment_eval(mom, q.x - cx, q.y - cy, fx, fy, zs);
+            poly_moment_eval(coef, q.x - cx, q.y - cy, fx, fy, zs);
+            F[s] = make_double2(0.0 + fx, 0.0 + fy);
         } else {   // the exact leaf sum (only if the series bound fails: not expected here)
             for (int p = 0; p < m; ++p) { const double2 pp = pos[p]; pair_force(q.x, q.y, pp.x, pp.y, fx, fy, zs); }
-        }
-        const double z0 = dupc ? -(double)dupc[s] : -1.0;   // no duplicates in root-tile mode: the query itself
-        if (usem) {
-            F[s] = make_double2(0.0 + fx, 0.0 + fy);
-            Z[s] = z0 + zs;
-        } else {
             F[s] = make_double2(fx, fy);
-            Z[s] = z0 + zs;
         }
+        Z[s] = -1.0 + zs;
     }
-    const unsigned long long nw = __popcll(__ballot(want));
-    if (lane_id() == 0 && nw) atomicAdd(&mom_flag[1], (int)nw);
-    if (STATS && visits) {
+    if (STATS && visits) {   // block totals, one set of atomics per block
+        __shared__ unsigned long long sv[4][2];
         const unsigned long long nv = __popcll(__ballot(valid)), nu = __popcll(__ballot(usem));
-        if (lane_id() == 0 && nv) {
-            atomicAdd(visits, nv * (unsigned long long)m);
-            atomicAdd(visits + 1, nu);
-            atomicAdd(visits + 2, (nv - nu) * (unsigned long long)m);
-            atomicAdd(visits + 3, 1ull);
-            atomicAdd(visits + 4, (unsigned long long)m);
+        if (lane_id() == 0) { sv[threadIdx.x >> 6][0] = nv; sv[threadIdx.x >> 6][1] = nu; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long bv = 0, bu = 0, bw = 0;
+            for (int w = 0; w < 4; ++w) { bv += sv[w][0]; bu += sv[w][1]; bw += sv[w][0] ? 1 : 0; }
+            if (bv) {
+                atomicAdd(visits, bv * (unsigned long long)m);
+                atomicAdd(visits + 1, bu);
+                atomicAdd(visits + 2, (bv - bu) * (unsigned long long)m);
+                atomicAdd(visits + 3, bw);
+                atomicAdd(visits + 4, bw * (unsigned long long)m);
+            }
         }
     }
 }
@@ -1645,8 +1789,8 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.mom_items_cap = n + ceil_div(n * 94, MOM_CHUNK);
     t.mom_item = ws.get<int32_t>("bh.mom_item", t.mom_items_cap);
     t.mom_part = ws.get<double>("bh.mom_part", (size_t)t.mom_items_cap * MOM_K);
-    t.mom_flag = ws.get<int32_t>("bh.mom_flag", 2);
-    const int32_t flag_init[2] = {1, INT32_MAX};   // first build: moments on
+    t.mom_flag = ws.get<int32_t>("bh.mom_flag", 3);
+    const int32_t flag_init[3] = {1, INT32_MAX, (int32_t)std::min<int64_t>(INT32_MAX, (n >> 6) + 1)};   // first build: moments on
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
@@ -1664,6 +1808,10 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.bb = ws.get<double>("bh.bb", 4);
     t.status = ws.get<int32_t>("bh.status", 4);
     t.status_h = ctx->pinned;
+    t.rcoef = ws.get<double>("bh.rcoef", POLY_K);
+    t.dup_mask = ((uint64_t)1 << (64 - __builtin_clzll((uint64_t)std::max<int64_t>(2, 4 * n) - 1))) - 1;
+    t.dup_tab = ws.get<int32_t>("bh.dup_tab", t.dup_mask + 1);
+    t.dup_open = ws.get<uint8_t>("bh.dup_open", n);
     size_t tb = 0;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted,
                                                (int)n, 0, 64, ctx->stream));
@@ -1738,25 +1886,28 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
     hipLaunchKernelGGL(bbox_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta, t.bb);
     if (root_tile_ok) {   // one small read-back decides the path (the host must know which kernels to launch)
-        const uint64_t tsz = (uint64_t)1 << (64 - __builtin_clzll((uint64_t)std::max<int64_t>(2, 2 * n) - 1));
-        int32_t *tab = ctx->ws.get<int32_t>("bh.dup_hash", tsz);
-        TSNE_HIP(hipMemsetAsync(tab, 0, sizeof(int32_t) * tsz, st));
-        hipLaunchKernelGGL(dup_hash, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, tab, tsz - 1, t.dflag);
+        const auto Y2 = reinterpret_cast<const double2 *>(dY);
+        for (int r = 0; r < DUP_ROUNDS; ++r) {
+            hipLaunchKernelGGL(dup_store, dim3(ceil_div(n, 256)), dim3(256), 0, st, Y2, n, t.dup_tab, t.dup_mask,
+                               t.dup_open, r);
+            hipLaunchKernelGGL(dup_probe, dim3(ceil_div(n, 256)), dim3(256), 0, st, Y2, n, t.dup_tab, t.dup_mask,
+                               t.dup_open, r, t.dflag);
+        }
         hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, bh_near_dmax(theta),
                            t.status);
         TSNE_HIP(hipMemcpyAsync(t.status_h, t.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         TSNE_HIP(hipStreamSynchronize(st));
         if (t.status_h[0]) {
             t.root_tile = true;
-            hipLaunchKernelGGL(moment_gate, dim3(1), dim3(1), 0, st, t.mom_flag, n);
             hipLaunchKernelGGL(root_tile_prep, dim3(std::min<int64_t>(1024, ceil_div(n, 256))), dim3(256), 0, st, t.bb,
-                               n, t.nodes, t.mom_cnt, t.mom_off, t.mom_list, t.mom_item, t.meta, t.inv, t.idx_sorted);
+                               n, t.nodes, t.mom_cnt, t.mom_off, t.mom_list, t.mom_item, t.meta, t.inv, t.idx_sorted,
+                               t.mom_flag);
             const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
-            hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, reinterpret_cast<const double2 *>(dY),
-                               t.nodes, t.mom_off, n, t.mom_item, t.mom_part);
-            hipLaunchKernelGGL(moment_reduce, dim3(1), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
-                               t.mom_part, t.mom);
-            t.root_pos = reinterpret_cast<const double2 *>(dY);
+            hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, Y2, t.nodes, t.mom_off, n,
+                               t.mom_item, t.mom_part);
+            hipLaunchKernelGGL(root_moment_reduce, dim3(MOM_K), dim3(256), 0, st, t.mom_off, n, t.mom_part, t.mom);
+            hipLaunchKernelGGL(poly_coef, dim3(ceil_div(POLY_K, 128)), dim3(128), 0, st, t.mom, t.rcoef);
+            t.root_pos = Y2;
             TSNE_LAUNCH_CHECK();
             return;
         }
@@ -1819,10 +1970,10 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     if (t.root_tile) {
         if (visits)
             hipLaunchKernelGGL(root_tile_eval<true>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream,
-                               t.root_pos, nullptr, t.nodes, t.mom, t.meta, t.mom_flag, s0, s1, qlist, dF, dz, visits);
+                               t.root_pos, t.nodes, t.rcoef, t.meta, s0, s1, qlist, dF, dz, visits);
         else
             hipLaunchKernelGGL(root_tile_eval<false>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream,
-                               t.root_pos, nullptr, t.nodes, t.mom, t.meta, t.mom_flag, s0, s1, qlist, dF, dz, visits);
+                               t.root_pos, t.nodes, t.rcoef, t.meta, s0, s1, qlist, dF, dz, visits);
         TSNE_LAUNCH_CHECK();
         return;
     }

@@ -88,7 +88,8 @@ struct BHTree {
     int32_t *mom_cnt = nullptr, *mom_off = nullptr;  // chunks per node, exclusive scan (n + 1)
     int32_t *mom_list = nullptr;                     // nodes that carry moments
     int32_t *mom_item = nullptr;                     // item -> node
-    int32_t *mom_flag = nullptr;                     // [0] moments built, [1] eligible tiles seen
+    int32_t *mom_flag = nullptr;                     // [0] moments built, [1] eligible tiles seen,
+                                                     // [2] tiles needed to build them (n / 64 + 1)
     int32_t *mtask = nullptr, *mtask_n = nullptr;    // per query: moment evaluations (node ids), count
     TileTask *ttask = nullptr;                       // per traversal wave: tile list
     int32_t *ttask_n = nullptr;
@@ -102,6 +103,10 @@ struct BHTree {
     int32_t *status_h = nullptr; // pinned host copy
     bool root_tile = false;      // this build took the root-tile path (no sort: slots = labels)
     const double2 *root_pos = nullptr;   // root-tile mode: the points in label order
+    double *rcoef = nullptr;             // root-tile mode: the root's sums as polynomials in v (POLY_K)
+    int32_t *dup_tab = nullptr;          // root-tile duplicate check: 4n-slot table
+    uint8_t *dup_open = nullptr;         // ... per point: still unresolved
+    uint64_t dup_mask = 0;
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     int bbox_blocks = 0;

@@ -639,16 +639,24 @@ static int64_t attract3_launch(hipStream_t st, const int64_t *rp, const int32_t 
 struct AttractArgs {
     const int64_t *rp; const int32_t *col; const double *val; int64_t r0, r1; const double *Y;
     const double *scal; int metric; double ex; double2 *attr; double *lpart;
+    int bpc = 0;   // blocks per CU of the persistent grid (0: 8 = every wave slot)
 };
 
-// persistent grid: 8 resident waves per SIMD, a multiple of the XCD count
-static int64_t attract_grid(int64_t rows, int lpr) {
+// persistent grid: bpc 256-thread blocks per CU (8: every wave slot), a
+// multiple of the XCD count.  The gathers are bound by the CU's outstanding
+// misses, not its waves: 3-4 blocks per CU run as fast as 8 and leave slots
+// to a concurrent tree build.
+static int64_t attract_grid(int64_t rows, int lpr, int bpc_req) {
     static const int cus = [] {
         int dev = 0, c = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
         return c;
     }();
-    const int64_t full = round_up(cus * 8, NUM_XCD);
+    // TSNE_ATTRACT_BPC: blocks per CU (experiment: < 8 leaves wave slots to
+    // concurrent kernels)
+    static const int bpc_env = [] { const char *e = getenv("TSNE_ATTRACT_BPC"); return e ? std::max(1, atoi(e)) : 0; }();
+    const int bpc = bpc_env ? bpc_env : bpc_req > 0 ? std::min(bpc_req, 8) : 8;
+    const int64_t full = round_up(cus * bpc, NUM_XCD);
     const int64_t need = round_up(std::max<int64_t>(1, ceil_div(rows * lpr, 256)), NUM_XCD);
     return std::min(full, need);
 }
@@ -656,7 +664,7 @@ static int64_t attract_grid(int64_t rows, int lpr) {
 template <int LPR, int U, int MET>
 static int64_t attract_launch_m(hipStream_t st, const AttractArgs &a, bool loss) {
     const int64_t rows = a.r1 - a.r0;
-    const int64_t blocks = attract_grid(rows, LPR);
+    const int64_t blocks = attract_grid(rows, LPR, a.bpc);
     if (loss)
         hipLaunchKernelGGL((attract_rows<LPR, U, true, MET>), dim3(blocks), dim3(256), 0, st, a.rp, a.col, a.val,
                            a.r0, a.r1, a.Y, a.scal, a.ex, a.attr, a.lpart);
@@ -749,6 +757,13 @@ void init_working_set_device(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed,
     TSNE_LAUNCH_CHECK();
 }
 
+// The root-tile shortcut of bh_build while the embedding is small
+// (TSNE_ROOT_TILE=0: always the full tree).
+static bool root_tile_enabled() {
+    static const bool on = [] { const char *e = getenv("TSNE_ROOT_TILE"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
                      const double *d_P, int64_t n, const double *dY, int32_t metric, double theta,
                      double exaggeration, double *d_grad, double *h_sumq, double *h_loss) {
@@ -756,7 +771,7 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
     hipStream_t st = ctx->stream;
     BHTree t;
     bh_alloc(ctx, t, n);
-    bh_build(ctx, t, dY, theta);
+    bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled());
     double2 *F = ctx->ws.get<double2>("grad.F", n);
     double *z = ctx->ws.get<double>("grad.z", n);
     double *part = ctx->ws.get<double>("grad.part", NPART);
@@ -805,7 +820,7 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
     if (c == 2) {
         BHTree t;
         bh_alloc(ctx, t, n);
-        bh_build(ctx, t, dY, theta);
+        bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled());
         bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, nullptr);
         inv = t.inv;
     } else {
@@ -1266,15 +1281,20 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // attraction over this rank's rows (row pointer local to L0)
     AttractArgs aa{s->rpw - s->L0, s->colw, s->valw, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr, s->part};
     // 0. attraction sums on the side stream (not in loss iterations: the KL
-    // terms need Z), concurrent with the BH traversal (TSNE_OVERLAP=tree:
-    // already with the tree build, whose short latency-bound kernels it then
-    // stretches, e.g. morton_keys 15 -> 800 us)
+    // terms need Z), concurrent with the BH traversal -- or, while the last
+    // build took the root-tile path, already with the tree build, on 3 blocks
+    // per CU (as fast as 8: miss-bound) so that the build's short kernels
+    // keep the other slots.  A full build is not overlapped: its latency-bound
+    // kernels stretch under the attraction (morton_keys 15 -> 800 us; whole
+    // schedule 8.53 -> 8.97 s).  TSNE_OVERLAP=tree / after / bh forces a mode.
     const bool overlap = !want_loss;
-    static const int ov_mode = [] {
+    static const int ov_env = [] {
         const char *e = getenv("TSNE_OVERLAP");
         const std::string v = e ? e : "";
-        return v == "tree" ? 0 : v == "bh" ? 2 : 1;
+        return v == "tree" ? 0 : v == "after" ? 1 : v == "bh" ? 2 : -1;
     }();
+    const int ov_mode = ov_env >= 0 ? ov_env : s->tree.root_tile ? 0 : 1;
+    if (overlap && ov_mode == 0 && s->tree.root_tile) aa.bpc = 3;
     auto side_wait = [&] {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
         TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
@@ -1291,9 +1311,8 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (overlap && ov_mode == 0) side_attract();
     // 1. tree (identical on every rank)
     // insertion rows = original indices; the root-tile shortcut while the
-    // embedding is small (TSNE_ROOT_TILE=0: always the full tree)
-    static const bool root_tile = [] { const char *e = getenv("TSNE_ROOT_TILE"); return !(e && e[0] == '0'); }();
-    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile);
+    // embedding is small
+    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled());
     if (overlap && ov_mode == 1) side_attract();
     if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
