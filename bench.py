@@ -66,7 +66,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
     ap.add_argument("--cpu-knn-sample", type=int, default=32, help="queries in the CPU baseline kNN sample")
-    ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as gpurun_out/Y_t<t>.npy")
+    ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as <dump-dir>/Y_t<t>.npy")
+    ap.add_argument("--dump-dir", default="gpurun_out")
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
@@ -287,8 +288,8 @@ def main():
                 torch.cuda.synchronize()
                 snaps[t] = Y[:n].cpu().numpy().copy()
             if rank == 0 and a.dump_y and t in {int(v) for v in a.dump_y.split(",")}:
-                os.makedirs("gpurun_out", exist_ok=True)
-                np.save(f"gpurun_out/Y_t{t}.npy", Y[:n].cpu().numpy())
+                os.makedirs(a.dump_dir, exist_ok=True)
+                np.save(os.path.join(a.dump_dir, f"Y_t{t}.npy"), Y[:n].cpu().numpy())
             if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
                 t_progress = time.perf_counter()
                 print(f"[bench] t={t}/{a.iterations} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)

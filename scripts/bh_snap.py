@@ -1,0 +1,49 @@
+"""Time the 2-D repulsion (tsne_dev_repulsion: tree build + BH traversal +
+tiles + moments) on embedding snapshots of the C3 schedule written by
+`bench.py --dump-y T1,T2,... --dump-dir DIR`, and print per snapshot the
+median wall time and checksums of F and z (to compare variants: equal
+checksums = equal results up to the printed digits).
+
+usage: python scripts/bh_snap.py DIR/Y_t250.npy [...] [--reps 5] [--theta 0.5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tsne-flink_amd"))
+import tsne_amd as T  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("snaps", nargs="+")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--theta", type=float, default=0.5)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    with T.Context(0) as ctx:
+        for path in a.snaps:
+            Y = torch.from_numpy(np.load(path)).to(dev, torch.float64).contiguous()
+            n = Y.shape[0]
+            F = torch.empty((n, 2), dtype=torch.float64, device=dev)
+            z = torch.empty(n, dtype=torch.float64, device=dev)
+            times = []
+            for _ in range(a.reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                ctx.dev_repulsion(Y, a.theta, F, z)
+                ctx.synchronize()
+                times.append(time.perf_counter() - t0)
+            times = sorted(times[1:])
+            print(json.dumps({"snapshot": os.path.basename(path), "n": n, "ms_median": 1e3 * times[len(times) // 2],
+                              "ms_min": 1e3 * times[0], "sum_abs_F": float(F.abs().sum()),
+                              "sum_z": float(z.sum())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -407,6 +407,16 @@ __global__ void set_root(int32_t *meta) {
     meta[1] = (m >= 2) ? 0 : (m == 1 ? ~0 : INT32_MIN);
 }
 
+// 1/x for the BH terms: v_rcp_f64 + one Newton step, within 11 ulp of the
+// IEEE quotient over the whole range (scripts/rcp_accuracy.hip: rcp alone
+// 2.5e8 ulp, one step 11, two steps 0) -- ~2e-15 relative per term, far
+// below the 1e-6 near-exact and 1e-4 gradient bars, two fp64 ops per term
+// cheaper than the correctly rounded pair of steps.
+__device__ __forceinline__ double recip_bh(double x) {
+    const double r = __builtin_amdgcn_rcp(x);
+    return __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+}
+
 // Direct interaction of one lane's query with one leaf point (QuadTree.scala:
 // 128-142 at a leaf: cumSize 1, com = the point; zero if equal to the query).
 __device__ __forceinline__ void leaf_force(double qx, double qy, double px, double py, double &fx,
@@ -414,10 +424,7 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
     if (px == qx && py == qy) return;
     const double dx = qx - px, dy = qy - py;
     const double D = __fma_rn(dx, dx, dy * dy);
-    const double x = 1.0 + D;
-    double r = __builtin_amdgcn_rcp(x);          // v_rcp_f64 + two Newton steps
-    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
-    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    const double r = recip_bh(1.0 + D);
     const double sc = r * r;
     fx = __fma_rn(sc, dx, fx);
     fy = __fma_rn(sc, dy, fy);
@@ -429,10 +436,7 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
 __device__ __forceinline__ void pair_force(double qx, double qy, double px, double py, double &fx,
                                            double &fy, double &zs) {
     const double dx = qx - px, dy = qy - py;
-    const double x = __fma_rn(dx, dx, __fma_rn(dy, dy, 1.0));
-    double r = __builtin_amdgcn_rcp(x);
-    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
-    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    const double r = recip_bh(__fma_rn(dx, dx, __fma_rn(dy, dy, 1.0)));
     const double sc = r * r;
     fx = __fma_rn(sc, dx, fx);
     fy = __fma_rn(sc, dy, fy);
@@ -1022,10 +1026,7 @@ __device__ __forceinline__ bool summarise(double h, double Df, double dx, double
 // One summarised cell (QuadTree.scala:134-142): Q = 1/(1+D), m = n Q.
 __device__ __forceinline__ void cell_force(double dx, double dy, double D, int32_t n, double &fx, double &fy,
                                            double &zs) {
-    const double x = 1.0 + D;
-    double Q = __builtin_amdgcn_rcp(x);
-    Q = __fma_rn(Q, __fma_rn(-x, Q, 1.0), Q);
-    Q = __fma_rn(Q, __fma_rn(-x, Q, 1.0), Q);
+    const double Q = recip_bh(1.0 + D);
     const double mult = (double)n * Q;
     const double sc = mult * Q;
     fx = __fma_rn(sc, dx, fx);
@@ -1130,7 +1131,12 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     const double hx = 0.5 * (nd.bx1 - nd.bx0), hy = 0.5 * (nd.by1 - nd.by0);
     const bool tile_possible = (nd.rball > 0.0 || (hx * hx + hy * hy) * (1.0 - 1e-9) <= fmax(nd.hmin * inv_theta, near_dmax))
                                && !(notile && notile[i]);   // a duplicate group below: the reference's path
-    r.nch = nc | (tile_possible ? QNCH_TILE : 0);
+    int kinds = 0;
+    for (int k = 0; k < nc; ++k) {
+        const double c = r.ch[k];
+        kinds |= (c == QCH_LEAF ? QK_LEAF : c == QCH_TIE ? QK_TIE : c == QCH_MULTI ? QK_MULTI : QK_CELL) << (QNCH_KIND + 2 * k);
+    }
+    r.nch = nc | (tile_possible ? QNCH_TILE : 0) | kinds;
 }
 
 // Traversal: one wave = 64 consecutive sorted queries sharing an LDS stack of
@@ -1172,7 +1178,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
     int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, int32_t virt, double2 *__restrict__ F,
-    double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost) {
+    double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost,
+    const int32_t *__restrict__ border, int32_t *__restrict__ wcost, int32_t *__restrict__ tcost) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
@@ -1180,16 +1187,18 @@ __global__ __launch_bounds__(256) void bh_traverse(
     __shared__ int32_t bref[4][KPOP];
     __shared__ uint64_t bmask[4][KPOP];
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t blk = border ? (int64_t)border[blockIdx.x]
+                      : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;   // wave slot: query slots g0 + 64 wid .. + 63, tile list wid
     // query slot k -> sorted position s (the identity, or this rank's list of
     // its own queries in sorted order: the waves stay Morton-coherent)
     const int64_t k = g0 + wid * 64 + lane;
     const bool valid = k < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
-    if (lane == 0) ttask_n[wid] = 0;
+    if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
     if (__ballot(valid) == 0) return;
     const long long t_start = COST ? clock64() : 0;
+    int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next block orders
     const int root = meta[1];
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
@@ -1253,6 +1262,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
         __builtin_amdgcn_wave_barrier();
+        npops += k;
         for (int r = 0; r < k; ++r) {
             if (STATS) ++wpops;
             const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
@@ -1261,8 +1271,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
             const QRec &nd = srec[w][r];
             // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
             bool tile = false;
-            const int nflags = nd.nch;
-            if (act && (nflags & QNCH_TILE)) {
+            const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
+            if ((nflags & QNCH_TILE) && act) {
                 const double cdx = qx - nd.cx, cdy = qy - nd.cy;
                 const double dc = cdx * cdx + cdy * cdy;
                 tile = dc <= nd.rball * nd.rball * (1.0 - 1e-9);
@@ -1288,6 +1298,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                         mytt[ntt] = tt;
                     }
                     ++ntt;
+                    ntilepts += b - a + 1;
                     if (STATS) wtile += (unsigned long long)(b - a + 1);
                     if (tile) {
                         if (STATS) nvis += (unsigned long long)(b - a + 1);
@@ -1303,17 +1314,17 @@ __global__ __launch_bounds__(256) void bh_traverse(
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 if (c >= nch) break;
-                const double chh = nd.ch[c];
-                if (chh == QCH_LEAF) {
+                const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
+                if (kind == QK_LEAF) {
                     if (act) { if (STATS) ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
-                } else if (chh == QCH_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                } else if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
                     if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
                         if (STATS) ++nvis;
                         const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
                         cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
                     }
-                } else if (chh == QCH_TIE) {
-                    const BHNode &tn = nodes[nd.cref[c]];
+                } else if (kind == QK_TIE) {
+                    const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
                     for (int p = tn.first; p <= tn.last; ++p) {
                         const double2 pp = pos[p];
                         if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
@@ -1324,7 +1335,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
                         if (STATS) ++nvis;
                         const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
                         const double D = __fma_rn(dx, dx, dy * dy);
-                        if (summarise(chh, D, dx, dy, th_lo, th_hi, theta))
+                        if (summarise(nd.ch[c], D, dx, dy, th_lo, th_hi, theta))
                             cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
                         else
                             open = true;
@@ -1342,7 +1353,11 @@ __global__ __launch_bounds__(256) void bh_traverse(
         F[s] = make_double2(fx, fy);
         Z[s] = zs;
     }
-    if (lane == 0) ttask_n[wid] = ntt;
+    if (lane == 0) {
+        ttask_n[wid] = ntt;
+        wcost[wid] = npops + (ntilepts >> 6);
+        tcost[wid] = ntilepts + 16 * ntt;
+    }
     if (COST && bcost) {   // cost of this wave into its first query's 256-query bucket
         // MODE 1: the wave's own run time (shader clock / 64; the slices only
         // move work between ranks, every query's sums are unchanged);
@@ -1386,12 +1401,14 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
                                                   int32_t *__restrict__ mom_flag,
                                                   int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
                                                   double2 *__restrict__ F, double *__restrict__ Z,
-                                                  unsigned long long *__restrict__ visits, int qmajor, int pack) {
+                                                  unsigned long long *__restrict__ visits, int qmajor, int pack,
+                                                  const int32_t *__restrict__ torder) {
     __shared__ double2 tbuf[4][64];
     __shared__ uint64_t sbm[4][64];
     __shared__ int smark[4][64];
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int64_t blk = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t blk = torder ? (int64_t)torder[blockIdx.x]
+                      : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
     if (g0 + wid * 64 >= g1) return;
     const int64_t kq = g0 + wid * 64 + lane;
@@ -1746,7 +1763,30 @@ __global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict_
     }
 }
 
+// Sort keys of a longest-first block order: block b's cost = its heaviest wave.
+__global__ void block_cost_keys(const int32_t *__restrict__ cost, int64_t nwaves, int64_t nblocks,
+                                int32_t *__restrict__ key, int32_t *__restrict__ val) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    int32_t c = 0;
+    for (int w = 0; w < 4; ++w)
+        if (4 * b + w < nwaves) c = max(c, cost[4 * b + w]);
+    key[b] = c;
+    val[b] = (int32_t)b;
+}
+
 }  // namespace
+
+// Longest-first order of nblocks blocks by the per-wave costs -> order.
+static void block_order(tsne_ctx *ctx, BHTree &t, const int32_t *cost, int64_t nwaves, int64_t nblocks,
+                        int32_t *order) {
+    hipStream_t st = ctx->stream;
+    hipLaunchKernelGGL(block_cost_keys, dim3(ceil_div(nblocks, 256)), dim3(256), 0, st, cost, nwaves, nblocks, t.okey,
+                       t.oval);
+    size_t tb = t.osort_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairsDescending(t.osort_tmp, tb, t.okey, t.okey2, t.oval, order,
+                                                          (int)nblocks, 0, 32, st));
+}
 
 void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     Workspace &ws = ctx->ws;
@@ -1817,6 +1857,20 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
                                                (int)n, 0, 64, ctx->stream));
     t.sort_tmp_bytes = tb;
     t.sort_tmp = ws.get<uint8_t>("bh.sort_tmp", tb);
+    const int64_t nb = ceil_div(t.tile_waves, 4);
+    t.wcost = ws.get<int32_t>("bh.wcost", t.tile_waves);
+    t.tcost = ws.get<int32_t>("bh.tcost", t.tile_waves);
+    t.okey = ws.get<int32_t>("bh.okey", nb);
+    t.okey2 = ws.get<int32_t>("bh.okey2", nb);
+    t.oval = ws.get<int32_t>("bh.oval", nb);
+    t.border = ws.get<int32_t>("bh.border", nb);
+    t.torder = ws.get<int32_t>("bh.torder", nb);
+    size_t ob = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, ob, t.okey, t.okey2, t.oval, t.border, (int)nb, 0,
+                                                          32, ctx->stream));
+    t.osort_tmp_bytes = ob;
+    t.osort_tmp = ws.get<uint8_t>("bh.osort_tmp", ob);
+    t.have_cost = false;
 }
 
 // Cost-balanced query slices for the next iteration: one 1024-thread block
@@ -1963,7 +2017,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     TSNE_LAUNCH_CHECK();
 }
 
-void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
+void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist,
                   unsigned long long *bcost) {
     if (s1 <= s0) return;
@@ -1991,14 +2045,30 @@ void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int6
     const int mode = visits ? 2 : (bcost ? 1 : 0);
     auto kern = kp >= 8 ? (mode == 2 ? bh_traverse<8, 2> : mode == 1 ? bh_traverse<8, 1> : bh_traverse<8, 0>)
                         : (mode == 2 ? bh_traverse<4, 2> : mode == 1 ? bh_traverse<4, 1> : bh_traverse<4, 0>);
-    const int64_t waves = ceil_div(s1 - s0, 64);
+    // longest-first block orders, TSNE_BH_ORDER bits: 1 traversal (by the
+    // previous traversal's wave costs), 2 tile_apply (by this traversal's
+    // tile points); default 2 -- the traversal keeps launch order, whose
+    // Morton-contiguous blocks share tree records in each XCD's L2 (full C3
+    // schedule 8.08 s in launch order vs 8.35 s longest-first)
+    static const int lpt_bits = [] { const char *e = getenv("TSNE_BH_ORDER"); return e ? atoi(e) : 2; }();
+    const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
-    hipLaunchKernelGGL(kern, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
+    const int32_t *border = nullptr, *torder = nullptr;
+    if ((lpt_bits & 1) && t.have_cost) {
+        block_order(ctx, t, t.wcost, waves, nblocks, t.border);
+        border = t.border;
+    }
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
                        t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd,
-                       (int32_t)t.n, dF, dz, visits, bcost);
-    hipLaunchKernelGGL(tile_apply, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
+                       (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost);
+    t.have_cost = true;
+    if (lpt_bits & 2) {
+        block_order(ctx, t, t.tcost, waves, nblocks, t.torder);
+        torder = t.torder;
+    }
+    hipLaunchKernelGGL(tile_apply, dim3(nblocks), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.ttask, t.ttask_n, s0, s1, qlist, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor,
-                       pack);
+                       pack, torder);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();

@@ -41,6 +41,10 @@ constexpr double QCH_LEAF = -1.0;
 constexpr double QCH_TIE = -2.0;
 constexpr double QCH_MULTI = -3.0;   // a leaf holding ccnt copies of one point (reference multiplicity)
 constexpr int32_t QNCH_TILE = 0x100;   // nch flag: an all-open tile test can pass here
+// nch bits 16 + 2c: child c's kind, wave-uniform in the traversal (scalar
+// branches instead of per-lane compares of ch[c])
+constexpr int QNCH_KIND = 16;
+constexpr int QK_CELL = 0, QK_LEAF = 1, QK_TIE = 2, QK_MULTI = 3;
 struct __attribute__((aligned(16))) QRec {
     double cx, cy;              // centre of mass
     double rball, hmin;         // all-open tests (see bottom_up)
@@ -110,6 +114,16 @@ struct BHTree {
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     int bbox_blocks = 0;
+    // longest-first block order of the traversal (by each wave's pops + tile
+    // points in the previous traversal) and of tile_apply (by this
+    // traversal's tile points): heavy waves start first instead of forming
+    // a low-occupancy tail
+    int32_t *wcost = nullptr, *tcost = nullptr;    // per wave
+    int32_t *okey = nullptr, *okey2 = nullptr, *oval = nullptr;   // per block: sort scratch
+    int32_t *border = nullptr, *torder = nullptr;  // per block: traversal / tile_apply order
+    void *osort_tmp = nullptr;
+    size_t osort_tmp_bytes = 0;
+    bool have_cost = false;
 };
 
 // Allocate (from ctx->ws) for n points.
@@ -127,7 +141,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
 // qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted
 // position; visits (nullable) += node evaluations; bcost (nullable)
 // accumulates each wave's cost into the 256-position bucket of its first query.
-void bh_repulsion(tsne_ctx *ctx, const BHTree &t, double theta, int64_t s0, int64_t s1,
+void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist = nullptr,
                   unsigned long long *bcost = nullptr);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).

@@ -1,5 +1,6 @@
 """ctypes declarations for libtsne_hip.so (include/tsne_hip.h)."""
 import ctypes as C
+import os
 from pathlib import Path
 
 PKG_ROOT = Path(__file__).resolve().parent.parent      # tsne-flink_amd/
@@ -83,7 +84,8 @@ _lib = None
 
 
 def lib_path():
-    return PKG_ROOT / "libtsne_hip.so"
+    # TSNE_HIP_LIB: another build of the same library (A/B experiments)
+    return Path(os.environ["TSNE_HIP_LIB"]) if os.environ.get("TSNE_HIP_LIB") else PKG_ROOT / "libtsne_hip.so"
 
 
 def lib():
