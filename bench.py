@@ -44,6 +44,7 @@ from tsne_amd.api import default_params  # noqa: E402
 
 METRIC = "t-SNE iterations/sec + end-to-end sec at N=1M×128 on 1/2/4/8 MI355X; kNN pts/s"
 FP32_MFMA_PEAK_TF = 157.3
+BF16_MFMA_PEAK_TF = 2500.0   # dense (MI355X_MICROARCH.md); the kNN filter's bf16x3 passes run 3 bf16 MFMAs per product
 HBM_PEAK_GBS = 8000.0
 
 
@@ -316,6 +317,7 @@ def main():
     attr_src = ("t <= K (timed window)" if win_alone else "whole schedule (no loss iteration in the window)")
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
     knn_flops = 2.0 * (r1 - r0) * n * d
+    knn_mode = "f32" if os.environ.get("TSNE_KNN_BF16", "1")[:1] == "0" else "bf16x3"
     upd_bytes = 128 * rows   # N*C*(5 reads + 3 writes)*8 B, C = 2
     upd_win = upd_ms[:steps]
     upd_avg = float(np.mean(upd_win)) if upd_win else None
@@ -356,8 +358,14 @@ def main():
         "knn_pts_per_s": n / t_knn if t_knn > 0 else None,
         "knn_filter_ms": knn_filter_ms,
         "knn_mfma_tflops": knn_flops / (knn_filter_ms * 1e-3) / 1e12 if knn_filter_ms > 0 else None,
-        "knn_mfma_frac_of_peak": (knn_flops / (knn_filter_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF) if knn_filter_ms > 0 else None,
-        "knn_mfma_frac_whole_knn": knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF if t_knn > 0 else None,
+        "knn_filter_mode": knn_mode,
+        # fraction of the MFMA pipe the filter runs on: f32-input MFMA (157.3 TF),
+        # or bf16x3 = 3 bf16 MFMA products per dot-product term (2.5 PF dense)
+        "knn_mfma_frac_of_peak": ((knn_flops / (knn_filter_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF) if knn_mode == "f32"
+                                  else (3 * knn_flops / (knn_filter_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF))
+        if knn_filter_ms > 0 else None,
+        "knn_mfma_frac_whole_knn": ((knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF) if knn_mode == "f32"
+                                    else (3 * knn_flops / t_knn / 1e12 / BF16_MFMA_PEAK_TF)) if t_knn > 0 else None,
         "affinities_joint_s": t_aff,
         "opt_setup_s": t_setup,
         "final_loss": losses.get(max(losses)) if losses else None,

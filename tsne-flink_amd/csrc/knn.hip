@@ -35,6 +35,14 @@ constexpr int KC = 32;    // k-chunk staged in LDS
 constexpr int LDSW = KC + 1;  // padded LDS row (bank-conflict free column reads)
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));   // 8 bf16: one 32x32x16 MFMA operand fragment
+
+// bf16x3 filter tiles (knn_filter_bf): 256 queries x 256 candidates per
+// 512-thread workgroup, dims staged 32 at a time (two 16-deep MFMA steps).
+constexpr int FT = 256;
+constexpr int FK = 32;
+constexpr int FROW = FK + 8;   // LDS row in bf16 elements (80 B): rows 20 banks apart
+constexpr int FTPB = 8;        // candidate tiles per workgroup (cross-tile prefetch)
 
 // ---------------------------------------------------------------- prep
 // Column partial sums for the mean (deterministic two-level reduction).
@@ -100,6 +108,25 @@ __global__ void prep_rows(const double *__restrict__ X, int64_t n, int32_t d, in
         norm32[row] = nv;
         if (metric != TSNE_METRIC_COSINE) norm64[row] = 0.0;
         atomicMax(nmax_bits, __float_as_uint(nv));  // non-negative floats order as uints
+    }
+}
+
+// fp32 -> bf16, round to nearest even (finite inputs).
+__device__ __forceinline__ unsigned short bf16_rn(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (unsigned short)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_to_f(unsigned short h) { return __uint_as_float((uint32_t)h << 16); }
+
+// X32 -> (hi, mid) bf16 pair per element: x = hi + mid + e, |e| <= 2^-16 |x|
+// (two bf16 roundings of 8 significant bits each).
+__global__ void split_bf16(const float *__restrict__ X32, int64_t count, unsigned short *__restrict__ Xh,
+                           unsigned short *__restrict__ Xm) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+        const float x = X32[i];
+        const unsigned short h = bf16_rn(x);
+        Xh[i] = h;
+        Xm[i] = bf16_rn(x - bf16_to_f(h));   // exact difference in fp32
     }
 }
 
@@ -226,6 +253,138 @@ __global__ __launch_bounds__(256) void knn_filter(
                                 cand_j[o] = (int32_t)c;
                             } else {
                                 flags[q - q0] = 1;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Threshold filter with bf16x3 products (the MFMA rate of bf16 is 16x that
+// of the f32-input MFMA): q.c ~ qh.ch + qh.cm + qm.ch over the (hi, mid)
+// splits, fp32 accumulation.  The dropped qm.cm and split-residual terms
+// are <= 3.02 * 2^-16 |q_k||c_k| each, so |d - d32| grows by at most
+// 3.02 * 2^-16 (|q|^2 + |c|^2) (+ the fp32 accumulation of 3K products):
+// knn_run's delta_coef covers both, and the exact fp64 re-rank restores
+// the exact order -- the filter only decides who is re-ranked.
+// Workgroup: 16 waves as 4 (queries) x 4 (candidates), wave tile 64 x 64 =
+// 2 x 2 MFMA 32x32 tiles (<= 128 registers: 4 waves/SIMD hide the loads);
+// each 32-dim stage is loaded into registers one stage ahead (across
+// candidate tiles too) and written to LDS between two barriers.
+__global__ __launch_bounds__(1024) void knn_filter_bf(
+    const unsigned short *__restrict__ Xh, const unsigned short *__restrict__ Xm, const float *__restrict__ norm32,
+    int32_t dpad, int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale, const float *__restrict__ tau,
+    int32_t *__restrict__ cnt, float *__restrict__ cand_d, int32_t *__restrict__ cand_j, int32_t *__restrict__ flags,
+    int32_t cap) {
+    __shared__ unsigned short sm[4][FT * FROW];   // Qh, Qm, Ch, Cm
+    __shared__ float nq_s[FT], tau_s[FT], nc_s[2][FT];
+    __shared__ int64_t qoff_s[FT];   // candidate-buffer offset of each query row (read in the rare append path)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;   // wave tile: rows 64 wr.., cols 64 wc..
+    const int64_t qb = q0 + (int64_t)blockIdx.y * FT;
+    // FTPB consecutive candidate tiles per workgroup: the next tile's first
+    // stage is loaded during the current tile's last one
+    const int64_t cfirst = c0 + (int64_t)blockIdx.x * FTPB * FT;
+    const int ntile = (int)min<int64_t>(FTPB, (c1 - cfirst + FT - 1) / FT);
+    if (tid < FT) {
+        const int64_t q = qb + tid;
+        nq_s[tid] = norm32[q];
+        tau_s[tid] = q < q1 ? tau[q - q0] : 0.f;
+        qoff_s[tid] = (q - q0) * (int64_t)cap;
+    }
+    // per-element tests in 32-bit tile coordinates (wave-uniform limits):
+    // 64-bit row offsets would be hoisted out of the tile loop and spilled
+    const int qlim = (int)min<int64_t>(FT, q1 - qb), qi0 = (int)(qb - q0);
+    // stage: 4 arrays x 256 rows x 4 pieces of 8 bf16 = 4096 x 16 B; thread
+    // tid loads piece (row tid / 4, part tid % 4) of every array (Qh, Qm, Ch,
+    // Cm) -- 32-bit element offsets (knn_run: npad * dpad < 2^32) on uniform
+    // bases
+    const int srow = tid >> 2, spart = tid & 3;
+    const uint32_t qoff = (uint32_t)(qb + srow) * (uint32_t)dpad + (uint32_t)(spart * 8);
+    uint4 pre[4];
+    auto load_stage = [&](int64_t cb, int k0) {
+        const uint32_t coff = (uint32_t)(cb + srow) * (uint32_t)dpad + (uint32_t)(spart * 8);
+        pre[0] = *reinterpret_cast<const uint4 *>(Xh + (qoff + k0));
+        pre[1] = *reinterpret_cast<const uint4 *>(Xm + (qoff + k0));
+        pre[2] = *reinterpret_cast<const uint4 *>(Xh + (coff + k0));
+        pre[3] = *reinterpret_cast<const uint4 *>(Xm + (coff + k0));
+    };
+    load_stage(cfirst, 0);
+    const int lr = lane & 31, lh = lane >> 5;
+    for (int it = 0; it < ntile; ++it) {
+        const int64_t cb = cfirst + (int64_t)it * FT;
+        float *ncb = nc_s[it & 1];
+        if (tid >= FT && tid < 2 * FT) ncb[tid - FT] = norm32[cb + (tid - FT)];
+        floatx16 acc[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[m][nn][r] = 0.f;
+        for (int k0 = 0; k0 < dpad; k0 += FK) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(&sm[i][srow * FROW + spart * 8]) = pre[i];
+            __syncthreads();
+            if (k0 + FK < dpad) load_stage(cb, k0 + FK);
+            else if (it + 1 < ntile) load_stage(cb + FT, 0);
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const int kc = st * 16 + 8 * lh;
+                bf16x8 bh[2], bm[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int crow = wc * 64 + t * 32 + lr;
+                    bh[t] = *reinterpret_cast<const bf16x8 *>(&sm[2][crow * FROW + kc]);
+                    bm[t] = *reinterpret_cast<const bf16x8 *>(&sm[3][crow * FROW + kc]);
+                }
+#pragma unroll
+                for (int m = 0; m < 2; ++m) {
+                    const int qrow = wr * 64 + m * 32 + lr;
+                    const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(&sm[0][qrow * FROW + kc]);
+                    const bf16x8 am = *reinterpret_cast<const bf16x8 *>(&sm[1][qrow * FROW + kc]);
+#pragma unroll
+                    for (int nn = 0; nn < 2; ++nn) {
+                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[nn], acc[m][nn], 0, 0, 0);
+                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[nn], acc[m][nn], 0, 0, 0);
+                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[nn], acc[m][nn], 0, 0, 0);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+        const int clim = (int)min<int64_t>(FT, c1 - cb);
+        const int64_t dqc = qb - cb;   // self pair: lc == lrow + dqc
+        const int dself = (dqc > -FT && dqc < FT) ? (int)dqc : (1 << 20);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+#pragma unroll
+            for (int nn = 0; nn < 2; ++nn) {
+                const int lc = wc * 64 + nn * 32 + lr;
+                const float ncv = ncb[lc];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int lrow = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float dv = nq_s[lrow] + ncv - dot_scale * acc[m][nn][r];
+                    const bool ok = lrow < qlim && lc < clim && lc != lrow + dself && dv <= tau_s[lrow];
+                    const uint64_t msk = __ballot(ok);
+                    if (msk) {
+                        const uint32_t mine = lh ? (uint32_t)(msk >> 32) : (uint32_t)msk;
+                        const int leader = __ffs(mine) - 1;
+                        int base = 0;
+                        if (ok && lr == leader) base = atomicAdd(&cnt[qi0 + lrow], __popc(mine));
+                        base = __shfl(base, (lh << 5) + (leader < 0 ? 0 : leader), 64);
+                        if (ok) {
+                            const int slot = base + __popc(mine & ((1u << lr) - 1u));
+                            if (slot < cap) {
+                                const int64_t o = qoff_s[lrow] + slot;
+                                cand_d[o] = dv;
+                                cand_j[o] = (int32_t)(cb + lc);
+                            } else {
+                                flags[qi0 + lrow] = 1;
                             }
                         }
                     }
@@ -446,7 +605,11 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     Workspace &ws = ctx->ws;
     const int64_t nq = q1 - q0;
     const int32_t dpad = (int32_t)round_up(d, KC);
-    const int64_t npad = round_up(n, 128);
+    // rows up to the last 256-tile of a candidate range starting anywhere
+    const int64_t npad = round_up(n, FT) + FT;
+    // bf16x3 threshold passes (TSNE_KNN_BF16=0: f32-input MFMA only)
+    static const bool bf_env = [] { const char *e = getenv("TSNE_KNN_BF16"); return !(e && e[0] == '0'); }();
+    const bool use_bf = bf_env && npad * (int64_t)round_up(d, KC) < ((int64_t)1 << 32);   // 32-bit offsets
 
     // --- prep
     double *mean = ws.get<double>("knn.mean", d);
@@ -466,13 +629,23 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     hipLaunchKernelGGL(prep_rows, dim3(ceil_div(npad, 4)), dim3(256), 0, st, dX, n, d, dpad, npad,
                        metric, mean, X32, norm32, norm64, nmax_bits);
     TSNE_LAUNCH_CHECK();
+    unsigned short *Xh = nullptr, *Xm = nullptr;
+    if (use_bf) {
+        Xh = ws.get<unsigned short>("knn.xh", (size_t)npad * dpad);
+        Xm = ws.get<unsigned short>("knn.xm", (size_t)npad * dpad);
+        hipLaunchKernelGGL(split_bf16, dim3(2048), dim3(256), 0, st, X32, npad * dpad, Xh, Xm);
+        TSNE_LAUNCH_CHECK();
+    }
     unsigned int nmax_h = 0;
     TSNE_HIP(hipMemcpyAsync(&nmax_h, nmax_bits, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
     TSNE_HIP(hipStreamSynchronize(st));
     float nmax;
     std::memcpy(&nmax, &nmax_h, sizeof(float));
     // |d32 - d64| <= (K + 8) u (|a|^2 + |b|^2) (see header); use K + 32 for slack.
-    const float delta_coef = (float)((dpad + 32) * 5.9604644775390625e-8);
+    // bf16x3 passes: + 3.02 * 2^-16 (split) and the fp32 accumulation of 3K
+    // products (3.06 K u): 2^-14 + (5K + 64) u covers both.
+    const float delta_coef = use_bf ? (float)(6.103515625e-05 + (5.0 * dpad + 64) * 5.9604644775390625e-8)
+                                    : (float)((dpad + 32) * 5.9604644775390625e-8);
     const float dot_scale = metric == TSNE_METRIC_COSINE ? 1.0f : 2.0f;
 
     // --- per-query state
@@ -507,9 +680,14 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     while (seen < n) {
         int64_t r = std::min<int64_t>(seen, n - seen);
         ctx->timers.begin("knn.filter", st);
-        hipLaunchKernelGGL(knn_filter<1>, dim3(ceil_div(r, TC), qtiles), dim3(256), 0, st, X32,
-                           norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d,
-                           cand_j, flags, (int32_t)CAP);
+        if (use_bf)
+            hipLaunchKernelGGL(knn_filter_bf, dim3(ceil_div(r, FT * FTPB), ceil_div(nq, FT)), dim3(1024), 0, st, Xh, Xm,
+                               norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d, cand_j, flags,
+                               (int32_t)CAP);
+        else
+            hipLaunchKernelGGL(knn_filter<1>, dim3(ceil_div(r, TC), qtiles), dim3(256), 0, st, X32,
+                               norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d,
+                               cand_j, flags, (int32_t)CAP);
         ctx->timers.end("knn.filter", st);
         TSNE_LAUNCH_CHECK();
         compact();
