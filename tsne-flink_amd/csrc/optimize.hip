@@ -4,23 +4,24 @@
 // Per global iteration t (1-based, TsneHelpers.scala:403-427 phases):
 //   ex  = earlyExaggeration if t <= min(T,20) + min(T-20, 81) else 1
 //   mom = initialMomentum if t <= min(T,20) else finalMomentum
-//   1. quadtree of the full Y (every rank builds the identical tree)
-//   2. BH repulsion for this rank's slice of the Morton-sorted points
-//   3. [multi-GPU] all-gather of (F, z) slices;  Z = sum z  (TsneHelpers.scala:266)
-//   4. fused kernel per owned row of P: attraction over the CSR row
-//      (q = 1/(1+metric(y_i, y_j)), TsneHelpers.scala:290-302), loss term
-//      every 10th iteration, grad = attr - F/Z (:311-317), gains/momentum/
-//      step (:341-369) -> Ynew
-//   5. [multi-GPU] all-gather of Ynew slices
+//   1. quadtree of the full Y (every rank builds the identical tree), or the
+//      root-tile shortcut while the embedding is small (bhtree.hip)
+//   2. BH repulsion for this rank's own points (its query list)
+//   3. Z = sum z (TsneHelpers.scala:266): the per-iteration all-reduce
+//   4. attraction per owned row of P over the CSR row (q = 1/(1+metric(y_i,
+//      y_j)), TsneHelpers.scala:290-302; side stream outside loss
+//      iterations), loss terms every 10th iteration, then combine_update:
+//      grad = attr - F/Z (:311-317), gains/momentum/step (:341-369) -> Ynew
+//   5. [multi-GPU] ragged all-gather of the owned Ynew slices
 //   6. centre: Y = Ynew - mean(Ynew) (:320-329)
 //
 // Internal labels.  The optimizer keeps its own copy of P (full, every rank)
-// and of the working set, indexed by internal point labels.  Every
-// RELABEL_EVERY iterations the labels are renumbered into the current Morton
-// order of the embedding (which the tree build computes anyway), so rows that
-// are consecutive in memory are spatial neighbours and the CSR attraction's
-// gathers of Y_j hit the L2 instead of streaming random lines from the MALL.
-// Rank r owns labels [r*chunk, (r+1)*chunk).  The caller's Y is rewritten in
+// and of the working set, indexed by internal point labels: P's graph order
+// at setup (connected components, BFS levels), then every RELABEL_EVERY
+// iterations the current Morton order of the embedding when that keeps more
+// of P's edges local -- rows consecutive in memory gather Y_j from nearby
+// labels, so the CSR attraction's gathers hit the L2.  Rank r owns a range of
+// labels (cost-balanced cuts at relabels).  The caller's Y is rewritten in
 // the original order after every step; upd / gains on tsne_dev_opt_sync.
 #include <hipcub/hipcub.hpp>
 
