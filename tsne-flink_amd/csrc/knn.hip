@@ -36,6 +36,7 @@ constexpr int LDSW = KC + 1;  // padded LDS row (bank-conflict free column reads
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));   // 8 bf16: one 32x32x16 MFMA operand fragment
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // bf16x3 filter tiles (knn_filter_bf): 256 queries x 256 candidates per
 // 512-thread workgroup, dims staged 32 at a time (two 16-deep MFMA steps).
@@ -43,6 +44,7 @@ constexpr int FT = 256;
 constexpr int FK = 32;
 constexpr int FROW = FK + 8;   // LDS row in bf16 elements (80 B): rows 20 banks apart
 constexpr int FTPB = 8;        // candidate tiles per workgroup (cross-tile prefetch)
+constexpr int FSQ = 64, FSC = 4;   // super-tile: query tiles x candidate groups
 
 // ---------------------------------------------------------------- prep
 // Column partial sums for the mean (deterministic two-level reduction).
@@ -275,7 +277,8 @@ __global__ __launch_bounds__(256) void knn_filter(
 // candidate tiles too) and written to LDS between two barriers.
 __global__ __launch_bounds__(1024) void knn_filter_bf(
     const unsigned short *__restrict__ Xh, const unsigned short *__restrict__ Xm, const float *__restrict__ norm32,
-    int32_t dpad, int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale, const float *__restrict__ tau,
+    int64_t npad_rows, int32_t dpad, int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale,
+    const float *__restrict__ tau,
     int32_t *__restrict__ cnt, float *__restrict__ cand_d, int32_t *__restrict__ cand_j, int32_t *__restrict__ flags,
     int32_t cap) {
     __shared__ unsigned short sm[4][FT * FROW];   // Qh, Qm, Ch, Cm
@@ -283,10 +286,23 @@ __global__ __launch_bounds__(1024) void knn_filter_bf(
     __shared__ int64_t qoff_s[FT];   // candidate-buffer offset of each query row (read in the rare append path)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 2, wc = wave & 3;   // wave tile: rows 64 wr.., cols 64 wc..
-    const int64_t qb = q0 + (int64_t)blockIdx.y * FT;
+    // Super-tile raster over a 1-D grid: FSQ query tiles x FSC candidate
+    // groups per super-tile, query tile fastest -- the XCD (block % 8) keeps
+    // the same FSQ/8 query tiles in its L2 across the super-tile's candidate
+    // groups, and each candidate group is re-read from the MALL, not HBM.
+    const int64_t nqt = (q1 - q0 + FT - 1) / FT;
+    const int64_t ncg = (c1 - c0 + (int64_t)FT * FTPB - 1) / ((int64_t)FT * FTPB);
+    const int64_t nqt_pad = (nqt + FSQ - 1) / FSQ * FSQ;
+    const int64_t b = blockIdx.x;
+    const int64_t sts = (int64_t)FSQ * FSC;
+    const int64_t st = b / sts, inner = b % sts;
+    const int64_t nst_q = nqt_pad / FSQ;
+    const int64_t qt = (st % nst_q) * FSQ + inner % FSQ, cg = (st / nst_q) * FSC + inner / FSQ;
+    if (qt >= nqt || cg >= ncg) return;   // uniform over the workgroup
+    const int64_t qb = q0 + qt * FT;
     // FTPB consecutive candidate tiles per workgroup: the next tile's first
     // stage is loaded during the current tile's last one
-    const int64_t cfirst = c0 + (int64_t)blockIdx.x * FTPB * FT;
+    const int64_t cfirst = c0 + cg * FTPB * FT;
     const int ntile = (int)min<int64_t>(FTPB, (c1 - cfirst + FT - 1) / FT);
     if (tid < FT) {
         const int64_t q = qb + tid;
@@ -302,16 +318,26 @@ __global__ __launch_bounds__(1024) void knn_filter_bf(
     // Cm) -- 32-bit element offsets (knn_run: npad * dpad < 2^32) on uniform
     // bases
     const int srow = tid >> 2, spart = tid & 3;
-    const uint32_t qoff = (uint32_t)(qb + srow) * (uint32_t)dpad + (uint32_t)(spart * 8);
-    uint4 pre[4];
-    auto load_stage = [&](int64_t cb, int k0) {
-        const uint32_t coff = (uint32_t)(cb + srow) * (uint32_t)dpad + (uint32_t)(spart * 8);
-        pre[0] = *reinterpret_cast<const uint4 *>(Xh + (qoff + k0));
-        pre[1] = *reinterpret_cast<const uint4 *>(Xm + (qoff + k0));
-        pre[2] = *reinterpret_cast<const uint4 *>(Xh + (coff + k0));
-        pre[3] = *reinterpret_cast<const uint4 *>(Xm + (coff + k0));
-    };
-    load_stage(cfirst, 0);
+    const uint32_t qoff = 2u * ((uint32_t)(qb + srow) * (uint32_t)dpad + (uint32_t)(spart * 8));   // bytes
+    // Buffer loads: 32-bit byte offsets on a uniform descriptor (knn_run:
+    // 2 npad dpad < 2^31).  Flat loads' 64-bit addresses spilled, and every
+    // spill reload's vmcnt(0) drained the stage prefetch.  Four named
+    // registers, not an array (a private array captured by a lambda was
+    // promoted to LDS).
+    const int nbytes = 2 * (int)(npad_rows * dpad);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short *>(Xh), (short)0, nbytes, 0x00020000);
+    const auto rm = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short *>(Xm), (short)0, nbytes, 0x00020000);
+    u32x4 p0, p1, p2, p3;
+#define TSNE_KNN_LOAD_STAGE(CB, K0)                                                                    \
+    do {                                                                                             \
+        const uint32_t coff_ = 2u * ((uint32_t)((CB) + srow) * (uint32_t)dpad + (uint32_t)(spart * 8)); \
+        const uint32_t k_ = 2u * (uint32_t)(K0);                                                     \
+        p0 = __builtin_amdgcn_raw_buffer_load_b128(rh, qoff + k_, 0, 0);                              \
+        p1 = __builtin_amdgcn_raw_buffer_load_b128(rm, qoff + k_, 0, 0);                              \
+        p2 = __builtin_amdgcn_raw_buffer_load_b128(rh, coff_ + k_, 0, 0);                             \
+        p3 = __builtin_amdgcn_raw_buffer_load_b128(rm, coff_ + k_, 0, 0);                             \
+    } while (0)
+    TSNE_KNN_LOAD_STAGE(cfirst, 0);
     const int lr = lane & 31, lh = lane >> 5;
     for (int it = 0; it < ntile; ++it) {
         const int64_t cb = cfirst + (int64_t)it * FT;
@@ -325,21 +351,19 @@ __global__ __launch_bounds__(1024) void knn_filter_bf(
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[m][nn][r] = 0.f;
         for (int k0 = 0; k0 < dpad; k0 += FK) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4 *>(&sm[i][srow * FROW + spart * 8]) = pre[i];
+            *reinterpret_cast<u32x4 *>(&sm[0][srow * FROW + spart * 8]) = p0;
+            *reinterpret_cast<u32x4 *>(&sm[1][srow * FROW + spart * 8]) = p1;
+            *reinterpret_cast<u32x4 *>(&sm[2][srow * FROW + spart * 8]) = p2;
+            *reinterpret_cast<u32x4 *>(&sm[3][srow * FROW + spart * 8]) = p3;
             __syncthreads();
-            if (k0 + FK < dpad) load_stage(cb, k0 + FK);
-            else if (it + 1 < ntile) load_stage(cb + FT, 0);
+            if (k0 + FK < dpad) TSNE_KNN_LOAD_STAGE(cb, k0 + FK);
+            else if (it + 1 < ntile) TSNE_KNN_LOAD_STAGE(cb + FT, 0);
 #pragma unroll
             for (int st = 0; st < 2; ++st) {
                 const int kc = st * 16 + 8 * lh;
-                bf16x8 bh[2], bm[2];
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    const int crow = wc * 64 + t * 32 + lr;
-                    bh[t] = *reinterpret_cast<const bf16x8 *>(&sm[2][crow * FROW + kc]);
-                    bm[t] = *reinterpret_cast<const bf16x8 *>(&sm[3][crow * FROW + kc]);
-                }
+                // fragments loaded per (m, nn): 16 live operand registers
+                // (B re-read once per m: the LDS has the bandwidth, the
+                // register file -- 128 per lane at 4 waves/SIMD -- does not)
 #pragma unroll
                 for (int m = 0; m < 2; ++m) {
                     const int qrow = wr * 64 + m * 32 + lr;
@@ -347,9 +371,12 @@ __global__ __launch_bounds__(1024) void knn_filter_bf(
                     const bf16x8 am = *reinterpret_cast<const bf16x8 *>(&sm[1][qrow * FROW + kc]);
 #pragma unroll
                     for (int nn = 0; nn < 2; ++nn) {
-                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[nn], acc[m][nn], 0, 0, 0);
-                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[nn], acc[m][nn], 0, 0, 0);
-                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[nn], acc[m][nn], 0, 0, 0);
+                        const int crow = wc * 64 + nn * 32 + lr;
+                        const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(&sm[2][crow * FROW + kc]);
+                        const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(&sm[3][crow * FROW + kc]);
+                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[m][nn], 0, 0, 0);
+                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[m][nn], 0, 0, 0);
+                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[m][nn], 0, 0, 0);
                     }
                 }
             }
@@ -368,6 +395,188 @@ __global__ __launch_bounds__(1024) void knn_filter_bf(
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int lrow = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float dv = nq_s[lrow] + ncv - dot_scale * acc[m][nn][r];
+                    const bool ok = lrow < qlim && lc < clim && lc != lrow + dself && dv <= tau_s[lrow];
+                    const uint64_t msk = __ballot(ok);
+                    if (msk) {
+                        const uint32_t mine = lh ? (uint32_t)(msk >> 32) : (uint32_t)msk;
+                        const int leader = __ffs(mine) - 1;
+                        int base = 0;
+                        if (ok && lr == leader) base = atomicAdd(&cnt[qi0 + lrow], __popc(mine));
+                        base = __shfl(base, (lh << 5) + (leader < 0 ? 0 : leader), 64);
+                        if (ok) {
+                            const int slot = base + __popc(mine & ((1u << lr) - 1u));
+                            if (slot < cap) {
+                                const int64_t o = qoff_s[lrow] + slot;
+                                cand_d[o] = dv;
+                                cand_j[o] = (int32_t)(cb + lc);
+                            } else {
+                                flags[qi0 + lrow] = 1;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+#undef TSNE_KNN_LOAD_STAGE
+
+// knn_filter_bf with the stages copied global -> LDS by the LDS DMA
+// (global_load_lds_dwordx4): no staging registers (the register-staged form
+// spilled at 4 waves/SIMD, and each spill reload's vmcnt(0) drained the
+// prefetch), two LDS stage buffers, stage g+1 issued before stage g is
+// waited for.  LDS rows are 64 B with the 16-B slots XOR-swizzled by row
+// bits 2..3 (conflict-free ds_read_b128 fragment reads); the DMA writes each
+// wave-instruction's 1 KB linearly, so the swizzle is applied to the global
+// source address.  One __shared__ array (a second one makes hipcc wait
+// vmcnt(0) before LDS reads); barriers are raw s_barrier with an
+// lgkmcnt(0) wait only -- __syncthreads() would wait vmcnt(0) too.
+constexpr int GROW = 32;                         // bf16 per LDS row
+constexpr int GARR = FT * GROW * 2;              // one array of a stage: 16 KB
+constexpr int GSTAGE = 4 * GARR;                 // Qh, Qm, Ch, Cm: 64 KB
+constexpr int G_NQ = 2 * GSTAGE, G_TAU = G_NQ + FT * 4, G_QOFF = G_TAU + FT * 4, G_NC = G_QOFF + FT * 8;
+constexpr int G_LDS = G_NC + FTPB * FT * 4;      // 140 KB
+__device__ __forceinline__ int gslot(int row, int part) { return part ^ ((row >> 2) & 3); }
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__global__ __launch_bounds__(1024) void knn_filter_glds(
+    const unsigned short *__restrict__ Xh, const unsigned short *__restrict__ Xm, const float *__restrict__ norm32,
+    int32_t dpad, int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale, const float *__restrict__ tau,
+    int32_t *__restrict__ cnt, float *__restrict__ cand_d, int32_t *__restrict__ cand_j, int32_t *__restrict__ flags,
+    int32_t cap) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[G_LDS];
+    float *nq_s = reinterpret_cast<float *>(lds + G_NQ);
+    float *tau_s = reinterpret_cast<float *>(lds + G_TAU);
+    int64_t *qoff_s = reinterpret_cast<int64_t *>(lds + G_QOFF);
+    float *nc_s = reinterpret_cast<float *>(lds + G_NC);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 2, wc = wave & 3;
+    // super-tile raster (see knn_filter_bf)
+    const int64_t nqt = (q1 - q0 + FT - 1) / FT;
+    const int64_t ncg = (c1 - c0 + (int64_t)FT * FTPB - 1) / ((int64_t)FT * FTPB);
+    const int64_t nqt_pad = (nqt + FSQ - 1) / FSQ * FSQ;
+    const int64_t bid = blockIdx.x, sts = (int64_t)FSQ * FSC;
+    const int64_t stn = bid / sts, inner = bid % sts, nst_q = nqt_pad / FSQ;
+    const int64_t qt = (stn % nst_q) * FSQ + inner % FSQ, cg = (stn / nst_q) * FSC + inner / FSQ;
+    if (qt >= nqt || cg >= ncg) return;
+    const int64_t qb = q0 + qt * FT;
+    const int64_t cfirst = c0 + cg * FTPB * FT;
+    const int ntile = (int)min<int64_t>(FTPB, (c1 - cfirst + FT - 1) / FT);
+    if (tid < FT) {
+        const int64_t q = qb + tid;
+        nq_s[tid] = norm32[q];
+        tau_s[tid] = q < q1 ? tau[q - q0] : 0.f;
+        qoff_s[tid] = (q - q0) * (int64_t)cap;
+    }
+    for (int i = tid; i < ntile * FT; i += 1024) nc_s[i] = norm32[cfirst + i];
+    __syncthreads();   // nothing in flight yet
+    const int qlim = (int)min<int64_t>(FT, q1 - qb), qi0 = (int)(qb - q0);
+    // this wave's DMA share of a stage: array ga, rows grb .. grb + 63 (4 x 16 rows)
+    const int ga = wave >> 2, grb = (wave & 3) * 64;
+    const unsigned short *gsrc = (ga & 1) ? Xm : Xh;
+    const int nks = dpad / FK, nstage = ntile * nks;
+
+    // The DMA is inline asm: seen by the compiler, an LDS DMA in flight
+    // makes it wait vmcnt(0) before every LDS access (it cannot tell the
+    // two stage buffers apart), draining the prefetch.  The wait for it is
+    // therefore explicit: vmcnt(4) = this wave's stage-g copies (stage
+    // g+1's four are the newer ones), then the barrier for the other waves'.
+    const uint32_t lds0 = lds_addr(lds);
+    auto issue = [&](int g, int ln) {   // stage g -> LDS buffer g & 1
+        const int drow = ln >> 2, dslot = ln & 3;
+        const int it = g / nks, k0 = (g - it * nks) * FK;
+        const int64_t rbase = ga < 2 ? qb : cfirst + (int64_t)it * FT;
+        const uint32_t dst = lds0 + (uint32_t)((g & 1) * GSTAGE + ga * GARR + grb * (GROW * 2));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int R = grb + i * 16 + drow;
+            const uint32_t e = (uint32_t)(rbase + R) * (uint32_t)dpad + (uint32_t)(k0 + 8 * gslot(R, dslot));
+            const uint64_t src = (uint64_t)(uintptr_t)(gsrc + e);
+            const uint32_t m0v = __builtin_amdgcn_readfirstlane(dst + i * 1024);
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(m0v) : "memory");
+        }
+    };
+    issue(0, lane);
+    for (int it = 0; it < ntile; ++it) {
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][nn][r] = 0.f;
+    for (int kstage = 0; kstage < nks; ++kstage) {
+        const int g = it * nks + kstage;
+        // lane-derived addresses are recomputed from an opaque copy of the
+        // lane id every stage: hoisted out of the loop they would stay live
+        // beside the 64 accumulators and spill (each spill reload's
+        // compiler-inserted vmcnt(0) would drain the stage prefetch)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int lr = ln & 31, lh = ln >> 5;
+        if (g + 1 < nstage) {
+            issue(g + 1, ln);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // this wave's stage-g copies landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_barrier" ::: "memory");                // every wave's stage-g copies landed
+        // fragment reads are ordinary LDS loads (the compiler tracks their
+        // lgkmcnt waits and the MFMA source hazards; it cannot see the DMA,
+        // so it inserts no vmcnt for it -- the asm waits above order them)
+        const unsigned short *sb = reinterpret_cast<const unsigned short *>(lds + (g & 1) * GSTAGE);
+#pragma unroll
+        for (int stp = 0; stp < 2; ++stp) {
+            const int part = 2 * stp + lh;
+            const int c0r = wc * 64 + lr, c1r = c0r + 32;
+            const int co0 = 2 * FT * GROW + c0r * GROW + 8 * gslot(c0r, part);
+            const int co1 = 2 * FT * GROW + c1r * GROW + 8 * gslot(c1r, part);
+            const bf16x8 bh0 = *reinterpret_cast<const bf16x8 *>(sb + co0);
+            const bf16x8 bm0 = *reinterpret_cast<const bf16x8 *>(sb + co0 + FT * GROW);
+            const bf16x8 bh1 = *reinterpret_cast<const bf16x8 *>(sb + co1);
+            const bf16x8 bm1 = *reinterpret_cast<const bf16x8 *>(sb + co1 + FT * GROW);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int qrow = wr * 64 + m * 32 + lr;
+                const int qo = qrow * GROW + 8 * gslot(qrow, part);
+                const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(sb + qo);
+                const bf16x8 am = *reinterpret_cast<const bf16x8 *>(sb + qo + FT * GROW);
+                acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh0, acc[m][0], 0, 0, 0);
+                acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm0, acc[m][0], 0, 0, 0);
+                acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh0, acc[m][0], 0, 0, 0);
+                acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh1, acc[m][1], 0, 0, 0);
+                acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm1, acc[m][1], 0, 0, 0);
+                acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh1, acc[m][1], 0, 0, 0);
+            }
+        }
+        // every wave is done reading buffer g & 1 before stage g + 2 is copied into it
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+        // epilogue of candidate tile it
+        const int lh = lane >> 5, lr = lane & 31;
+        const int64_t cb = cfirst + (int64_t)it * FT;
+        const float *ncb = nc_s + it * FT;
+        const int clim = (int)min<int64_t>(FT, c1 - cb);
+        const int64_t dqc = qb - cb;
+        const int dself = (dqc > -FT && dqc < FT) ? (int)dqc : (1 << 20);
+        // row / column bases made opaque here: otherwise the 64 (row, col)
+        // address and bound values of this unrolled epilogue are hoisted out
+        // of the stage loop (loop-invariant) and spilled
+        int rbase = wr * 64 + 4 * lh, cbase = wc * 64 + lr;
+        asm volatile("" : "+v"(rbase), "+v"(cbase));
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+#pragma unroll
+            for (int nn = 0; nn < 2; ++nn) {
+                const int lc = cbase + nn * 32;
+                const float ncv = ncb[lc];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int lrow = rbase + m * 32 + (r & 3) + 8 * (r >> 2);
                     const float dv = nq_s[lrow] + ncv - dot_scale * acc[m][nn][r];
                     const bool ok = lrow < qlim && lc < clim && lc != lrow + dself && dv <= tau_s[lrow];
                     const uint64_t msk = __ballot(ok);
@@ -608,8 +817,10 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     // rows up to the last 256-tile of a candidate range starting anywhere
     const int64_t npad = round_up(n, FT) + FT;
     // bf16x3 threshold passes (TSNE_KNN_BF16=0: f32-input MFMA only)
-    static const bool bf_env = [] { const char *e = getenv("TSNE_KNN_BF16"); return !(e && e[0] == '0'); }();
-    const bool use_bf = bf_env && npad * (int64_t)round_up(d, KC) < ((int64_t)1 << 32);   // 32-bit offsets
+    // TSNE_KNN_BF16: 0 f32-input MFMA only, 1 (default) bf16x3 with LDS-DMA
+    // staging, 2 bf16x3 with register staging
+    static const int bf_mode = [] { const char *e = getenv("TSNE_KNN_BF16"); return e ? atoi(e) : 1; }();
+    const bool use_bf = bf_mode != 0 && 2 * npad * (int64_t)round_up(d, KC) < ((int64_t)1 << 31);   // 32-bit offsets
 
     // --- prep
     double *mean = ws.get<double>("knn.mean", d);
@@ -680,9 +891,16 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     while (seen < n) {
         int64_t r = std::min<int64_t>(seen, n - seen);
         ctx->timers.begin("knn.filter", st);
-        if (use_bf)
-            hipLaunchKernelGGL(knn_filter_bf, dim3(ceil_div(r, FT * FTPB), ceil_div(nq, FT)), dim3(1024), 0, st, Xh, Xm,
-                               norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d, cand_j, flags,
+        if (use_bf && bf_mode == 1)
+            hipLaunchKernelGGL(knn_filter_glds,
+                               dim3(round_up(ceil_div(nq, FT), FSQ) * round_up(ceil_div(r, (int64_t)FT * FTPB), FSC)),
+                               dim3(1024), 0, st, Xh, Xm, norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt,
+                               cand_d, cand_j, flags, (int32_t)CAP);
+        else if (use_bf)
+            hipLaunchKernelGGL(knn_filter_bf,
+                               dim3(round_up(ceil_div(nq, FT), FSQ) * round_up(ceil_div(r, (int64_t)FT * FTPB), FSC)),
+                               dim3(1024), 0, st, Xh, Xm,
+                               norm32, npad, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d, cand_j, flags,
                                (int32_t)CAP);
         else
             hipLaunchKernelGGL(knn_filter<1>, dim3(ceil_div(r, TC), qtiles), dim3(256), 0, st, X32,
