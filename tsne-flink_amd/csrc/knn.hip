@@ -437,7 +437,7 @@ constexpr int GROW = 32;                         // bf16 per LDS row
 constexpr int GARR = FT * GROW * 2;              // one array of a stage: 16 KB
 constexpr int GSTAGE = 4 * GARR;                 // Qh, Qm, Ch, Cm: 64 KB
 constexpr int G_NQ = 2 * GSTAGE, G_TAU = G_NQ + FT * 4, G_QOFF = G_TAU + FT * 4, G_NC = G_QOFF + FT * 8;
-constexpr int G_LDS = G_NC + FTPB * FT * 4;      // 140 KB
+constexpr int G_THR = G_NC + FTPB * FT * 4, G_LDS = G_THR + FT * 4;   // 141 KB
 __device__ __forceinline__ int gslot(int row, int part) { return part ^ ((row >> 2) & 3); }
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
@@ -447,13 +447,14 @@ __global__ __launch_bounds__(1024) void knn_filter_glds(
     const unsigned short *__restrict__ Xh, const unsigned short *__restrict__ Xm, const float *__restrict__ norm32,
     int32_t dpad, int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale, const float *__restrict__ tau,
     int32_t *__restrict__ cnt, float *__restrict__ cand_d, int32_t *__restrict__ cand_j, int32_t *__restrict__ flags,
-    int32_t cap) {
+    int32_t cap, float nmax) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[G_LDS];
     float *nq_s = reinterpret_cast<float *>(lds + G_NQ);
+    float *thr_s = reinterpret_cast<float *>(lds + G_THR);
     float *tau_s = reinterpret_cast<float *>(lds + G_TAU);
     int64_t *qoff_s = reinterpret_cast<int64_t *>(lds + G_QOFF);
     float *nc_s = reinterpret_cast<float *>(lds + G_NC);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
     // super-tile raster (see knn_filter_bf)
     const int64_t nqt = (q1 - q0 + FT - 1) / FT;
@@ -466,15 +467,22 @@ __global__ __launch_bounds__(1024) void knn_filter_glds(
     const int64_t qb = q0 + qt * FT;
     const int64_t cfirst = c0 + cg * FTPB * FT;
     const int ntile = (int)min<int64_t>(FTPB, (c1 - cfirst + FT - 1) / FT);
+    const int qlim = (int)min<int64_t>(FT, q1 - qb), qi0 = (int)(qb - q0);
     if (tid < FT) {
         const int64_t q = qb + tid;
-        nq_s[tid] = norm32[q];
-        tau_s[tid] = q < q1 ? tau[q - q0] : 0.f;
+        const float nq = norm32[q], t = q < q1 ? tau[q - q0] : 0.f;
+        nq_s[tid] = nq;
+        tau_s[tid] = t;
         qoff_s[tid] = (q - q0) * (int64_t)cap;
+        // screening threshold of the epilogue: fma(-s, dot, |c|^2) <= thr
+        // holds whenever the exact test (|q|^2 + |c|^2) - s dot <= tau does.
+        // The two differ by the roundings of |q|^2 + |c|^2, s dot, their
+        // difference, the fma and tau - |q|^2: at most 4 u (|tau| + |q|^2 +
+        // max |c|^2) (|s dot| <= |q|^2 + |c|^2); 2^-19 is 8x that.
+        thr_s[tid] = tid < qlim ? (t - nq) + 1.9073486328125e-06f * (fabsf(t) + nq + nmax) : -__builtin_inff();
     }
     for (int i = tid; i < ntile * FT; i += 1024) nc_s[i] = norm32[cfirst + i];
     __syncthreads();   // nothing in flight yet
-    const int qlim = (int)min<int64_t>(FT, q1 - qb), qi0 = (int)(qb - q0);
     // this wave's DMA share of a stage: array ga, rows grb .. grb + 63 (4 x 16 rows)
     const int ga = wave >> 2, grb = (wave & 3) * 64;
     const unsigned short *gsrc = (ga & 1) ? Xm : Xh;
@@ -556,44 +564,64 @@ __global__ __launch_bounds__(1024) void knn_filter_glds(
         // every wave is done reading buffer g & 1 before stage g + 2 is copied into it
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-        // epilogue of candidate tile it
-        const int lh = lane >> 5, lr = lane & 31;
+        // epilogue of candidate tile it.  Screening: one fma and one compare
+        // per element against the row's thr_s (a superset of the exact
+        // test); only a wave with a screened element runs the exact test
+        // and the candidate append (rare: a few in 10^4 elements).
         const int64_t cb = cfirst + (int64_t)it * FT;
         const float *ncb = nc_s + it * FT;
         const int clim = (int)min<int64_t>(FT, c1 - cb);
         const int64_t dqc = qb - cb;
         const int dself = (dqc > -FT && dqc < FT) ? (int)dqc : (1 << 20);
-        // row / column bases made opaque here: otherwise the 64 (row, col)
-        // address and bound values of this unrolled epilogue are hoisted out
-        // of the stage loop (loop-invariant) and spilled
-        int rbase = wr * 64 + 4 * lh, cbase = wc * 64 + lr;
-        asm volatile("" : "+v"(rbase), "+v"(cbase));
+        // lane-derived row / column bases from an opaque lane id: otherwise
+        // they are hoisted out of the tile loop and spilled (and the spill
+        // reload's vmcnt(0) waits for the next tile's first stage)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const int lh = ln >> 5, lr = ln & 31;
+        const int rbase = wr * 64 + 4 * lh, cbase = wc * 64 + lr;
+        float cv[2];
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn) {
+            const int lc = cbase + nn * 32;
+            cv[nn] = lc < clim ? ncb[lc] : __builtin_inff();
+        }
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
 #pragma unroll
-            for (int nn = 0; nn < 2; ++nn) {
-                const int lc = cbase + nn * 32;
-                const float ncv = ncb[lc];
+            for (int rq = 0; rq < 4; ++rq) {
+                const float4 th4 = *reinterpret_cast<const float4 *>(thr_s + rbase + m * 32 + 8 * rq);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int lrow = rbase + m * 32 + (r & 3) + 8 * (r >> 2);
-                    const float dv = nq_s[lrow] + ncv - dot_scale * acc[m][nn][r];
-                    const bool ok = lrow < qlim && lc < clim && lc != lrow + dself && dv <= tau_s[lrow];
-                    const uint64_t msk = __ballot(ok);
-                    if (msk) {
-                        const uint32_t mine = lh ? (uint32_t)(msk >> 32) : (uint32_t)msk;
-                        const int leader = __ffs(mine) - 1;
-                        int base = 0;
-                        if (ok && lr == leader) base = atomicAdd(&cnt[qi0 + lrow], __popc(mine));
-                        base = __shfl(base, (lh << 5) + (leader < 0 ? 0 : leader), 64);
-                        if (ok) {
-                            const int slot = base + __popc(mine & ((1u << lr) - 1u));
-                            if (slot < cap) {
-                                const int64_t o = qoff_s[lrow] + slot;
-                                cand_d[o] = dv;
-                                cand_j[o] = (int32_t)(cb + lc);
-                            } else {
-                                flags[qi0 + lrow] = 1;
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int r = 4 * rq + r4;
+                    const float th = r4 == 0 ? th4.x : r4 == 1 ? th4.y : r4 == 2 ? th4.z : th4.w;
+#pragma unroll
+                    for (int nn = 0; nn < 2; ++nn) {
+                        const float a = acc[m][nn][r];
+                        if (__builtin_expect(__ballot(__builtin_fmaf(-dot_scale, a, cv[nn]) <= th) != 0, 0)) {
+                            // bases re-made opaque inside the branch: nothing
+                            // of this cold path is computed ahead of the test
+                            int rb = rbase, cbs = cbase;
+                            asm volatile("" : "+v"(rb), "+v"(cbs));
+                            const int lrow = rb + m * 32 + (r & 3) + 8 * (r >> 2);
+                            const int lc = cbs + nn * 32;
+                            const float dv = nq_s[lrow] + ncb[lc] - dot_scale * a;
+                            const bool ok = lrow < qlim && lc < clim && lc != lrow + dself && dv <= tau_s[lrow];
+                            const uint64_t msk = __ballot(ok);
+                            const uint32_t mine = lh ? (uint32_t)(msk >> 32) : (uint32_t)msk;
+                            const int leader = __ffs(mine) - 1;
+                            int base = 0;
+                            if (ok && lr == leader) base = atomicAdd(&cnt[qi0 + lrow], __popc(mine));
+                            base = __shfl(base, (lh << 5) + (leader < 0 ? 0 : leader), 64);
+                            if (ok) {
+                                const int slot = base + __popc(mine & ((1u << lr) - 1u));
+                                if (slot < cap) {
+                                    const int64_t o = qoff_s[lrow] + slot;
+                                    cand_d[o] = dv;
+                                    cand_j[o] = (int32_t)(cb + lc);
+                                } else {
+                                    flags[qi0 + lrow] = 1;
+                                }
                             }
                         }
                     }
@@ -895,7 +923,7 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
             hipLaunchKernelGGL(knn_filter_glds,
                                dim3(round_up(ceil_div(nq, FT), FSQ) * round_up(ceil_div(r, (int64_t)FT * FTPB), FSC)),
                                dim3(1024), 0, st, Xh, Xm, norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt,
-                               cand_d, cand_j, flags, (int32_t)CAP);
+                               cand_d, cand_j, flags, (int32_t)CAP, nmax);
         else if (use_bf)
             hipLaunchKernelGGL(knn_filter_bf,
                                dim3(round_up(ceil_div(nq, FT), FSQ) * round_up(ceil_div(r, (int64_t)FT * FTPB), FSC)),
