@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
 // coalesced dwordx4 load per lane, the next chunk prefetched into registers)
 // and read back as wave-uniform broadcasts.  Lanes whose bound holds are
 // counted for the next iteration's moment gate.
-__global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void tile_apply(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
                                                   const double *__restrict__ mom,
                                                   const TileTask *__restrict__ ttask,
                                                   const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1,
@@ -1402,10 +1402,11 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
                                                   int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
                                                   double2 *__restrict__ F, double *__restrict__ Z,
                                                   unsigned long long *__restrict__ visits, int qmajor, int pack,
-                                                  const int32_t *__restrict__ torder) {
+                                                  float lw_cost, const int32_t *__restrict__ torder) {
     __shared__ double2 tbuf[4][64];
     __shared__ uint64_t sbm[4][64];
     __shared__ int smark[4][64];
+    __shared__ int2 srng[4][64];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t blk = torder ? (int64_t)torder[blockIdx.x]
                       : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
@@ -1428,8 +1429,93 @@ __global__ __launch_bounds__(256) void tile_apply(const double2 *__restrict__ po
     unsigned long long wt_tasks = 0, wt_dense_pts = 0, wt_momchk = 0;   // wave-level diagnostics
     double2 *buf = tbuf[w];
     const TileTask *mytt = ttask + wid * TILE_CAP;
+    int masked_until = 0;   // pack 2: tiles before this one take the masked sweep
     for (int t = 0; t < nt;) {
         const TileTask tt = mytt[t];
+        if (pack == 2 && t >= masked_until && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
+            // Lane-wise window: the run of <= 64 consecutive small tiles
+            // starting at t.  Each lane walks only the points of ITS tiles
+            // (its bits of the 64 masks, transposed by 64 ballots), gathering
+            // them itself, so a sweep costs the busiest lane's point count
+            // instead of every tile point with most lanes masked off (the
+            // masks of small tiles hold ~1/4 of the lanes in the mid phase).
+            // Per lane the order is fixed (tile order, then point order).
+            const int ti = t + lane;
+            bool sm = false;
+            int a_i = 0, b_i = -1;
+            uint64_t m_i = 0;
+            if (ti < nt) {
+                const TileTask h = mytt[ti];
+                if (h.last - h.first + 1 < MOM_MIN_POINTS) { sm = true; a_i = h.first; b_i = h.last; m_i = h.mask; }
+            }
+            const uint64_t nsm = ~__ballot(sm);
+            const int wn = nsm ? __ffsll((long long)nsm) - 1 : 64;   // >= 1: tile t is small
+            if (lane >= wn) m_i = 0;
+            // 64 x 64 bit transpose (row i = tile t + i's lane mask): six
+            // butterfly stages swapping the off-diagonal blocks of halving size
+            uint64_t W = m_i;
+#pragma unroll
+            for (int st = 0; st < 6; ++st) {
+                const int j = 32 >> st;
+                const uint64_t lo = st == 0 ? 0x00000000FFFFFFFFull : st == 1 ? 0x0000FFFF0000FFFFull
+                                  : st == 2 ? 0x00FF00FF00FF00FFull : st == 3 ? 0x0F0F0F0F0F0F0F0Full
+                                  : st == 4 ? 0x3333333333333333ull : 0x5555555555555555ull;
+                const uint32_t ylo = __shfl_xor((uint32_t)W, j, 64), yhi = __shfl_xor((uint32_t)(W >> 32), j, 64);
+                const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+                W = (lane & j) ? ((W & ~lo) | ((y & ~lo) >> j)) : ((W & lo) | ((y & lo) << j));
+            }
+            // W bit i: tile t + i is one of mine.  Lane-wise costs the busiest
+            // lane's points, the masked 64-slot sweep every point: take the
+            // cheaper (lw_cost: lane-wise cost per point relative to a sweep
+            // slot, gathers and refills included), the sweep for the whole window.
+            const int cnt_i = b_i - a_i + 1;
+            __builtin_amdgcn_wave_barrier();
+            srng[w][lane] = make_int2(a_i, b_i);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            int cl = 0;
+            for (uint64_t wb = W; wb; wb &= wb - 1) {
+                const int2 r = srng[w][__ffsll((long long)wb) - 1];
+                cl += r.y - r.x + 1;
+            }
+            const int cmax = wave_max(cl), ctot = wave_sum(lane < wn ? cnt_i : 0);
+            if ((float)cmax * lw_cost >= (float)ctot) {
+                masked_until = t + wn;
+                goto masked;
+            }
+            double ux = 0.0, uy = 0.0, uz = 0.0;
+            int p = 0, last = -1, nmine = 0;
+            while (true) {
+                if (p > last && W) {
+                    const int i = __ffsll((long long)W) - 1;
+                    W &= W - 1;
+                    const int2 r = srng[w][i];
+                    p = r.x; last = r.y;
+                }
+                const bool on = p <= last;
+                if (__ballot(on) == 0) break;
+                if (on) {
+                    const bool two = p + 1 <= last;
+                    const double2 p0 = pos[p];
+                    const double2 p1 = pos[two ? p + 1 : p];
+                    pair_force(qx, qy, p0.x, p0.y, ux, uy, uz);
+                    if (two) pair_force(qx, qy, p1.x, p1.y, ux, uy, uz);
+                    p += 2;
+                    nmine += two ? 2 : 1;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            fx += ux; fy += uy; zs += uz;
+            ndense += (unsigned long long)nmine;
+            if (visits) {
+                wt_tasks += (unsigned long long)wn;
+                wt_dense_pts += (unsigned long long)wave_sum(lane < wn ? b_i - a_i + 1 : 0);
+            }
+            t += wn;
+            continue;
+        }
+    masked:
         if (pack && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
             // Packed round: the run of consecutive small tiles (no moments below
             // MOM_MIN_POINTS) whose points fit 64 slots is staged as one batch of
@@ -2038,8 +2124,11 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
     // dense tiles: query-major passes for sparse lane masks (TSNE_TILE_QMAJOR=0: lane-major only)
     static const int qmajor = [] { const char *e = getenv("TSNE_TILE_QMAJOR"); return e ? atoi(e) : 1; }();
-    // small tiles: packed 64-slot rounds (TSNE_TILE_PACK=0: one round per tile)
-    static const int pack = [] { const char *e = getenv("TSNE_TILE_PACK"); return e ? atoi(e) : 1; }();
+    // small tiles (TSNE_TILE_PACK): 2 per 64-tile window the cheaper of lane-wise walks and
+    // packed 64-slot masked sweeps (C3 snapshots: tile_apply -6 % at t = 250, -18 % at t = 500),
+    // 1 packed sweeps only, 0 one round per tile
+    static const int pack = [] { const char *e = getenv("TSNE_TILE_PACK"); return e ? atoi(e) : 2; }();
+    static const float lw_cost = [] { const char *e = getenv("TSNE_TILE_LW"); return e ? (float)atof(e) : 1.6f; }();
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the wave's pops and tile points
     const int mode = visits ? 2 : (bcost ? 1 : 0);
@@ -2068,7 +2157,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     hipLaunchKernelGGL(tile_apply, dim3(nblocks), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.ttask, t.ttask_n, s0, s1, qlist, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor,
-                       pack, torder);
+                       pack, lw_cost, torder);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();
