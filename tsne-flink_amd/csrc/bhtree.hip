@@ -431,6 +431,22 @@ __device__ __forceinline__ void leaf_force(double qx, double qy, double px, doub
     zs += r;
 }
 
+// Masked forms for the traversal's child loop: every lane evaluates, `take`
+// selects whether the term is added (a zero term leaves the sums bit-equal).
+// Branch-free, so the accumulators are updated in place -- the branchy forms
+// made the compiler copy fx, fy, zs at every merge of the divergent paths.
+__device__ __forceinline__ void leaf_force_m(bool take, double qx, double qy, double px, double py, double &fx,
+                                             double &fy, double &zs) {
+    take = take && !(px == qx && py == qy);
+    const double dx = qx - px, dy = qy - py;
+    const double D = __fma_rn(dx, dx, dy * dy);
+    const double r = recip_bh(1.0 + D);
+    const double sc = r * r;
+    fx = __fma_rn(take ? sc : 0.0, dx, fx);
+    fy = __fma_rn(take ? sc : 0.0, dy, fy);
+    zs += take ? r : 0.0;
+}
+
 // Pair term for dense tiles, without the equality test (see the caller):
 // r = 1/(1 + dx^2 + dy^2) with the 1 folded into the FMA chain.
 __device__ __forceinline__ void pair_force(double qx, double qy, double px, double py, double &fx,
@@ -1315,35 +1331,51 @@ __global__ __launch_bounds__(256) void bh_traverse(
             for (int c = 0; c < 4; ++c) {
                 if (c >= nch) break;
                 const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
-                if (kind == QK_LEAF) {
-                    if (act) { if (STATS) ++nvis; leaf_force(qx, qy, nd.ccx[c], nd.ccy[c], fx, fy, zs); }
-                } else if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
-                    if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
-                        if (STATS) ++nvis;
-                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                        cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
-                    }
-                } else if (kind == QK_TIE) {
-                    const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
-                    for (int p = tn.first; p <= tn.last; ++p) {
-                        const double2 pp = pos[p];
-                        if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
-                    }
-                } else {
-                    bool open = false;
-                    if (act) {
-                        if (STATS) ++nvis;
-                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                        const double D = __fma_rn(dx, dx, dy * dy);
-                        if (summarise(nd.ch[c], D, dx, dy, th_lo, th_hi, theta))
-                            cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
-                        else
-                            open = true;
-                    }
+                if (kind == QK_CELL || kind == QK_LEAF) {
+                    // A cell (summarise() and cell_force() in masked form) or a
+                    // leaf: ch = QCH_LEAF < 0 passes the test, ccnt = 1 makes
+                    // cell_force leaf_force exactly, and a leaf equal to the
+                    // query adds nothing (a cell at D = 0 is never summarised)
+                    if (STATS && act) ++nvis;
+                    const double px = nd.ccx[c], py = nd.ccy[c];
+                    const double dx = qx - px, dy = qy - py;
+                    const double D = __fma_rn(dx, dx, dy * dy);
+                    const double h = nd.ch[c];
+                    bool acc = h < th_lo * D;
+                    if (act && !acc && !(h > th_hi * D))
+                        acc = h / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                    const bool take = act && acc && !(px == qx && py == qy);
+                    const double Q = recip_bh(1.0 + D);
+                    const double mult = (double)nd.ccnt[c] * Q;
+                    const double sc = mult * Q;
+                    fx = __fma_rn(take ? sc : 0.0, dx, fx);
+                    fy = __fma_rn(take ? sc : 0.0, dy, fy);
+                    zs += take ? mult : 0.0;
+                    const bool open = act && !acc;
                     const uint64_t om = __ballot(open);
                     if (om) {
                         if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
                         ++sp;
+                    }
+                }
+            }
+            // duplicate kinds (rare), after the others: out of the main loop,
+            // whose accumulators then stay in place
+            if (__builtin_expect((nflags & (0xAA << QNCH_KIND)) != 0, 0)) {
+                for (int c = 0; c < nch; ++c) {
+                    const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
+                    if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                        if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
+                            if (STATS) ++nvis;
+                            const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                            cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
+                        }
+                    } else if (kind == QK_TIE) {
+                        const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
+                        for (int p = tn.first; p <= tn.last; ++p) {
+                            const double2 pp = pos[p];
+                            if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                        }
                     }
                 }
             }
