@@ -1082,7 +1082,8 @@ __global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict_
         if (dups && dv.vflag[i]) {   // node i's chain top C_1: one child, node i itself (cells C_2..C_k)
             const BHNode &nd = nodes[i];
             QRec v;
-            v.cx = dv.vcom[2 * i]; v.cy = dv.vcom[2 * i + 1]; v.rball = 0.0; v.hmin = nd.hmin;
+            v.cx = dv.vcom[2 * i]; v.cy = dv.vcom[2 * i + 1]; v.rball = 0.0;
+            v.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax);
             v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
             v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
             v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.ch[0] = nd.h; v.cref[0] = i; v.ccnt[0] = nd.cnt;
@@ -1102,7 +1103,9 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     const int32_t *tiecnt = dv.tiecnt, *notile = dv.notile;
     const BHNode &nd = nodes[i];
     if (nd.h < 0.0) return;                 // transparent or key tie: no record
-    r.cx = nd.cx; r.cy = nd.cy; r.rball = nd.rball; r.hmin = nd.hmin;
+    // the traversal's all-open thresholds, precomputed (see QRec)
+    r.cx = nd.cx; r.cy = nd.cy; r.rball = nd.rball * nd.rball * (1.0 - 1e-9);
+    r.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax);
     r.bx0 = nd.bx0; r.bx1 = nd.bx1; r.by0 = nd.by0; r.by1 = nd.by1;
     r.first = nd.first; r.last = nd.last; r.cnt = nd.cnt;
     // <= 3 transparent nodes per quad level: a 2-deep descent covers them
@@ -1216,7 +1219,6 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const long long t_start = COST ? clock64() : 0;
     int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next block orders
     const int root = meta[1];
-    const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
@@ -1291,13 +1293,13 @@ __global__ __launch_bounds__(256) void bh_traverse(
             if ((nflags & QNCH_TILE) && act) {
                 const double cdx = qx - nd.cx, cdy = qy - nd.cy;
                 const double dc = cdx * cdx + cdy * cdy;
-                tile = dc <= nd.rball * nd.rball * (1.0 - 1e-9);
+                tile = dc <= nd.rball;   // rball^2 (1 - 1e-9)
                 if (!tile) {
                     const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
                     const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
                     const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
                     const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-                    tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
+                    tile = dmax <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax)
                 }
             }
             const uint64_t tm = __ballot(tile);

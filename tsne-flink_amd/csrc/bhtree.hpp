@@ -47,7 +47,8 @@ constexpr int QNCH_KIND = 16;
 constexpr int QK_CELL = 0, QK_LEAF = 1, QK_TIE = 2, QK_MULTI = 3;
 struct __attribute__((aligned(16))) QRec {
     double cx, cy;              // centre of mass
-    double rball, hmin;         // all-open tests (see bottom_up)
+    double rball, hmin;         // all-open tests, precomputed (build_qrec): rball^2 (1 - 1e-9) and
+                                // max(hmin / theta (1 - 1e-12), near_dmax) (see bottom_up)
     double bx0, bx1, by0, by1;  // bounding box of the subtree's points
     int32_t first, last;        // leaf range in sorted order
     int32_t cnt, nch;           // cumSize, number of quad children | QNCH_TILE
