@@ -316,6 +316,11 @@ def main():
     attr_ms = float(np.mean(win_alone)) if win_alone else (float(np.mean(all_alone)) if all_alone else None)
     attr_src = ("t <= K (timed window)" if win_alone else "whole schedule (no loss iteration in the window)")
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
+    # the optimizer's tiled layout (attract_tiles) unless disabled or the rows
+    # are dense over a small embedding (the library's own rule, optimize.hip)
+    dense_small = nnz // max(n, 1) > 1024 and n * 16 <= (2 << 20)
+    tiles_on = os.environ.get("TSNE_ATTRACT_TILES", "1")[:1] != "0" and not dense_small
+    attr_kernel = "attract_tiles<LOSS=true>" if tiles_on else "attract_rows<64,4,LOSS=true>"
     knn_flops = 2.0 * (r1 - r0) * n * d
     knn_mode = "f32" if os.environ.get("TSNE_KNN_BF16", "1")[:1] == "0" else "bf16x3"
     upd_bytes = 128 * rows   # N*C*(5 reads + 3 writes)*8 B, C = 2
@@ -370,7 +375,7 @@ def main():
         "opt_setup_s": t_setup,
         "final_loss": losses.get(max(losses)) if losses else None,
         "losses_sampled": {str(t): losses[t] for t in sorted(losses) if t in (10, 20, 100, 200, 500, 1000)},
-        "roofline": {"kernel": "attract_rows<64,4,LOSS=true> (CSR attraction + KL terms, TsneHelpers.scala:269-306): "
+        "roofline": {"kernel": attr_kernel + " (CSR attraction + KL terms, TsneHelpers.scala:269-306): "
                                "mean HIP-event time of its standalone launches (loss iterations t%10==0, alone on "
                                "the context stream) in " + attr_src,
                      "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

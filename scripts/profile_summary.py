@@ -1,7 +1,7 @@
 """Summarise a scripts/gpu_check.sh run (gpurun_out/) into profiles/:
 
   <tag>_rocprof_kernel_stats.csv     rocprofv3 --stats of `bench.py --steps K --warmup W` (whole schedule)
-  <tag>_attract_dispatches.json      attract_rows<..., LOSS=true> dispatch durations from the kernel trace,
+  <tag>_attract_dispatches.json      attract_tiles / attract_rows (LOSS=true) dispatch durations from the kernel trace,
                                      mapped to iterations (the k-th standalone launch after the warmup's is
                                      t = 10 k), averaged over the timed window t <= K and the whole schedule
   r02_attract_traffic.json           FETCH_SIZE / WRITE_SIZE per standalone launch in the window
@@ -26,9 +26,19 @@ def rows(p):
         return list(csv.DictReader(fh))
 
 
+def is_loss_attraction(name):
+    """The standalone (LOSS=true) attraction kernel: attract_tiles<true, MET> (the
+    optimizer's tiled layout) or attract_rows<LPR, U, true, MET> (CSR rows)."""
+    return ("attract_tiles<true" in name) or ("attract_rows<" in name and ", true," in name)
+
+
+def kernel_label(name):
+    return "attract_tiles<LOSS=true>" if "attract_tiles<" in name else "attract_rows<64,4,LOSS=true>"
+
+
 def loss_dispatches(trace_rows):
     """Dispatches of the standalone (LOSS=true) attraction kernel, in dispatch order."""
-    sel = [r for r in trace_rows if "attract_rows<" in r["Kernel_Name"] and ", true," in r["Kernel_Name"]]
+    sel = [r for r in trace_rows if is_loss_attraction(r["Kernel_Name"])]
     return sorted(sel, key=lambda r: int(r["Dispatch_Id"]))
 
 
@@ -47,9 +57,10 @@ def main():
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in ld]
     its = [10 * (k + 1) for k in range(len(durs))]
     win = [d for t, d in zip(its, durs) if t <= K]
+    label = kernel_label(ld[0]["Kernel_Name"]) if ld else "attract_rows<64,4,LOSS=true>"
     summary = {
         "source": "rocprofv3 --kernel-trace --stats -- python bench.py --steps %d --warmup %d --no-cpu-baseline "
-                  "(scripts/gpu_check.sh); dispatches of attract_rows<64,4,true,0> after the warmup's" % (K, W),
+                  "(scripts/gpu_check.sh); dispatches of %s after the warmup's" % (K, W, label),
         "launches": len(durs),
         "per_launch_ms": dict(zip(map(str, its), durs)),
         "avg_ms_window": sum(win) / len(win) if win else None,
@@ -60,7 +71,7 @@ def main():
     # PMC: per standalone launch in the window (bench.py --no-rest: the window's launches only)
     def per_launch(kind, counter):
         rs = [r for r in rows(OUT / kind / "pmc_counter_collection.csv")
-              if ", true," in r["Kernel_Name"] and r["Counter_Name"] == counter]
+              if is_loss_attraction(r["Kernel_Name"]) and r["Counter_Name"] == counter]
         rs.sort(key=lambda r: int(r["Dispatch_Id"]))
         return [float(r["Counter_Value"]) * 1024.0 for r in rs[warm_loss:]]   # KiB -> bytes
     fetch = per_launch("pmc_fetch", "FETCH_SIZE")
@@ -86,7 +97,7 @@ def main():
     tf = PROF / "r02_attract_traffic.json"
     tj = json.loads(tf.read_text()) if tf.exists() else {}
     tj.update({
-        "kernel": "attract_rows<64,4,LOSS=true>",
+        "kernel": label,
         "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) -- python bench.py --steps K "
                   "--warmup W --no-rest --no-cpu-baseline --trace 0 (scripts/gpu_check.sh)",
         "unit": "bytes per launch",

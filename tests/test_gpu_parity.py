@@ -416,6 +416,41 @@ def test_device_optimizer_matches_host_path(ctx):
     assert ctx.dev_opt_losses() == lh
 
 
+@pytest.mark.parametrize("metric", ["sqeuclidean", "euclidean", "cosine"])
+def test_tiled_attraction_matches_oracle(ctx, metric):
+    """The optimizer's tiled attraction (attract_tiles: 512-row blocks x
+    3840-label column windows, per-row segmented sums across waves) on a P with
+    dense hub rows and columns -- rows spanning several waves and windows --
+    over 10 iterations at theta 0 (exact repulsion on both sides): the
+    embedding and the loss at t = 10 against the oracle."""
+    import scipy.sparse as sp
+    n = 6000
+    rp, col, val = random_problem(n, 30, seed=71)
+    A = sp.csr_matrix((val, col, rp), shape=(n, n))
+    rng = np.random.default_rng(72)
+    hubs = np.array([3, 2500, 5999])
+    B = sp.lil_matrix((n, n))
+    for h in hubs:
+        B[h, :] = rng.random(n) * 1e-7
+    B = B.tocsr()
+    B.setdiag(0.0)
+    P = (A + B + B.T).tocsr()
+    P.eliminate_zeros()
+    P.sort_indices()
+    P = P / P.sum()
+    rp2, col2, val2 = P.indptr.astype(np.int64), P.indices.astype(np.int32), P.data.astype(np.float64)
+    assert np.diff(rp2)[hubs].min() > 4000
+    Y0 = np.random.default_rng(73).normal(size=(n, 2)) * 5.0
+    prm = default_params(iterations=10, theta=0.0, metric=metric, learning_rate=200.0)
+    Yg, ug, gg = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lg = ctx.optimize(rp2, col2, val2, Yg, ug, gg, prm)
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lo = O.optimize(rp2, col2, val2, Yo, uo, go, metric=metric, learning_rate=200.0, iterations=10, theta=0.0,
+                    threads=8)
+    assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max()
+    assert abs(lg[10] - lo[10]) <= 1e-9 * abs(lo[10])
+
+
 def test_moment_path_engaged(ctx):
     """Tiny embedding (the first iterations): every query's whole tree is one
     near-exact subtree, evaluated from the root's moments (one moment task per

@@ -30,6 +30,22 @@
 
 namespace tsne {
 
+// one tile of the tiled attraction (attract_tiles): the entries of a row
+// block whose column lies in one window of labels, as 64-row slices
+struct ATile {
+    int32_t s0;    // first slice
+    int32_t ns;    // slices
+    int32_t cb;    // column window
+    int32_t rb;    // row block
+};
+struct ASlice {
+    int64_t base;    // first entry (step 0, lane 0)
+    int32_t width;   // steps: entries of the slice's first (longest) lane
+    int32_t wide;    // 1: one long row split over the 64 lanes (wave-reduced)
+    int32_t j0;      // first (sorted) segment
+    int32_t cnt;     // segments (rows): <= 64, or 1 for a wide slice
+};
+
 struct OptState {
     tsne_params p{};
     int C = 2;
@@ -93,6 +109,16 @@ struct OptState {
     // or on the side stream concurrently with the BH traversal
     std::vector<std::pair<int32_t, int32_t>> attract_iter;
     double *mpart = nullptr;  // centring mean: block partials of combine_update
+    // tiled attraction layout of the owned rows (attract_tiles), rebuilt with them
+    bool at_on = false;
+    int64_t at_nrb = 0, at_ncb = 0;
+    int at_cfg = 0;
+    ATile *at_tiles = nullptr;
+    int32_t *at_rbt = nullptr;
+    ASlice *at_slices = nullptr;
+    uint32_t *at_srow = nullptr;
+    uint16_t *at_pk = nullptr;
+    double *at_pv = nullptr;
     double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits[10] = {};
 };
@@ -140,7 +166,7 @@ __global__ void reduce_final(const double *__restrict__ part, int np, double *__
 // (TsneHelpers.scala:293), metric fixed at compile time; v_rcp_f64 + two
 // Newton steps.
 template <int MET>
-__device__ __forceinline__ double qterm_t(double ax, double ay, double bx, double by) {
+__device__ __forceinline__ double qterm_t(double ax, double ay, double bx, double by, double &x) {
     double m;
     if (MET == TSNE_METRIC_COSINE) {
         const double dt = __dadd_rn(__dmul_rn(ax, bx), __dmul_rn(ay, by));
@@ -152,11 +178,16 @@ __device__ __forceinline__ double qterm_t(double ax, double ay, double bx, doubl
         const double s2 = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
         m = MET == TSNE_METRIC_EUCLIDEAN ? sqrt(s2) : s2;
     }
-    const double x = 1.0 + m;
+    x = 1.0 + m;
     double r = __builtin_amdgcn_rcp(x);
     r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
     r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
     return r;
+}
+template <int MET>
+__device__ __forceinline__ double qterm_t(double ax, double ay, double bx, double by) {
+    double x;
+    return qterm_t<MET>(ax, ay, bx, by, x);
 }
 
 // Attraction over the CSR rows [r0, r1) (TsneHelpers.scala:269-306):
@@ -235,6 +266,314 @@ __global__ __launch_bounds__(256) void attract_rows(
         __syncthreads();
         if (threadIdx.x == 0) lpart[blockIdx.x] = (sl[0] + sl[1]) + (sl[2] + sl[3]);
     }
+}
+
+// ---- Tiled attraction (the optimizer's own rows of P, rebuilt with the labels)
+// attract_rows is bound by its Y_j gathers: 16 B from a random line of a
+// 1.6 MB blob of Y per entry, each an L1 miss served by the L2, at the CU's
+// outstanding-miss limit (~0.11 misses/cycle/CU) -- 0.17 of the HBM roofline.
+// Here the owned rows are cut into row blocks of RB rows and their entries
+// regrouped by column window of W labels.  A "tile" (row block, window) is
+// processed by one workgroup: it copies the window's Y into LDS (coalesced
+// 16-byte loads, from L2), then sums the tile's entries with Y_j from LDS.
+// Within a tile each row is one lane of a 64-row slice, the tile's rows sorted
+// by their entry count (descending), and a slice is stored in jagged-diagonal
+// order: step k holds the k-th entry of every lane whose row has more than k,
+// contiguously (those lanes are a prefix, as the counts descend) -- the
+// loads of a step are coalesced and no slot is padding.  Per entry only the
+// bytes of a CSR pair cross HBM: a 16-bit column offset within the window and
+// the value (10 B instead of 12).  A lane sums its row's entries of the tile
+// in the row's own order and adds the sum to the row's LDS accumulator; every
+// row has exactly one lane per tile, so nothing is shared and every sum runs
+// in one fixed order (bit-reproducible).
+template <int RB_, int W_, int NT_>
+struct ATCfg {
+    static constexpr int RB = RB_, W = W_, NT = NT_, WAVES = NT_ / 64;
+    static constexpr int ROWBITS = __builtin_ctz(RB_);
+    static_assert((RB_ & (RB_ - 1)) == 0 && RB_ <= 4096 && W_ <= 65536, "tile packing");
+};
+using ATCfg0 = ATCfg<2048, 5632, 1024>;   // 120 KB LDS
+using ATCfg1 = ATCfg<4096, 3840, 1024>;   // 124 KB
+using ATCfg2 = ATCfg<4096, 5632, 1024>;   // 152 KB
+using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
+constexpr int AT_U = 12;          // jagged steps whose loads are issued together
+constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
+
+// One workgroup per row block (owned rows [b0, b0 + RB) of [0, rows), label
+// r0 + local row); XCD-chunked block order.  attr / lpart as attract_rows.
+template <class CF, bool LOSS, int MET>
+__global__ __launch_bounds__(CF::NT) void attract_tiles(
+    const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
+    const uint32_t *__restrict__ srow, int64_t rows, int64_t r0, int64_t n, const uint16_t *__restrict__ pk,
+    const double *__restrict__ pv, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
+    int64_t xcd_chunk, double2 *__restrict__ attr, double *__restrict__ lpart) {
+    constexpr int RB = CF::RB, W = CF::W, NT = CF::NT, WAVES = CF::WAVES;
+    __shared__ double2 win[W];
+    __shared__ double2 acc[RB];
+    __shared__ double sl[WAVES];
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t b0 = rb * RB;
+    const int nr = (int)min((int64_t)RB, rows - b0);
+    const double2 *Y2 = reinterpret_cast<const double2 *>(Y);
+    const double2 *Yrow = Y2 + r0 + b0;
+    for (int i = tid; i < nr; i += NT) acc[i] = make_double2(0.0, 0.0);
+    const double Z = LOSS ? scal[0] : 1.0;
+    double lsum = 0.0;
+    constexpr int WL = (W + NT - 1) / NT;
+    const int t0 = rbt[rb], t1 = rbt[rb + 1];
+    for (int t = t0; t < t1; ++t) {
+        const ATile tl = tiles[t];
+        {   // the tile's window: all of a thread's loads in flight before its LDS stores
+            const int64_t base = (int64_t)tl.cb * W;
+            const int wn = (int)min((int64_t)W, n - base);
+            double2 yv[WL];
+#pragma unroll
+            for (int k = 0; k < WL; ++k) yv[k] = Y2[base + min(tid + k * NT, wn - 1)];
+#pragma unroll
+            for (int k = 0; k < WL; ++k) {
+                const int i = tid + k * NT;
+                if (i < wn) win[i] = yv[k];
+            }
+        }
+        __syncthreads();
+        const int s0 = tl.s0, send = tl.s0 + tl.ns;
+        // the wave's slices s0 + w, s0 + w + WAVES, ...; the next slice's record
+        // and lane word are fetched during the current one
+        int s = s0 + w;
+        ASlice sd{};
+        uint32_t rl = 0;
+        if (s < send) {
+            sd = slices[s];
+            rl = srow[(int64_t)s * 64 + lane];
+        }
+        while (s < send) {
+            const int len = (int)(rl & ((1u << AT_LENBITS) - 1)), lrow = (int)(rl >> AT_LENBITS);
+            double2 yi = make_double2(0.0, 0.0);
+            if (len > 0) yi = Yrow[lrow];
+            const int sn = s + WAVES;
+            ASlice sdn{};
+            uint32_t rln = 0;
+            double fx = 0.0, fy = 0.0;
+            int64_t off = sd.base;   // wave-uniform: the current step's first entry
+            for (int k0 = 0; k0 < sd.width; k0 += AT_U) {
+                uint32_t cu[AT_U];   // one register each: a packed 16-bit array would wait on every load
+                double vu[AT_U];
+#pragma unroll
+                for (int u = 0; u < AT_U; ++u) {
+                    const int k = k0 + u;
+                    cu[u] = 0;
+                    vu[u] = 0.0;
+                    if (k < len) { cu[u] = pk[off + lane]; vu[u] = pv[off + lane]; }
+                    off += __popcll(__ballot(len > k));   // the step's active lanes (a prefix)
+                }
+                if (k0 == 0 && sn < send) {
+                    sdn = slices[sn];
+                    rln = srow[(int64_t)sn * 64 + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < AT_U; ++u) {
+                    if (k0 + u < len) {
+                        const double2 yj = win[cu[u]];
+                        const double pij = __dmul_rn(vu[u], ex);
+                        double x1m;   // 1 + metric = 1 / q
+                        const double q = qterm_t<MET>(yi.x, yi.y, yj.x, yj.y, x1m);
+                        const double sc = __dmul_rn(pij, q);
+                        fx = __dadd_rn(fx, __dmul_rn(sc, __dsub_rn(yi.x, yj.x)));
+                        fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yi.y, yj.y)));
+                        // P ln(P / (q / Z)) = P ln(P Z (1 + metric)): no divisions
+                        // (0 ln 0 = NaN for an underflowed P, as the reference)
+                        if (LOSS) lsum += pij * log(pij * Z * x1m);
+                    }
+                }
+            }
+            if (sd.wide) {   // one row over the 64 lanes: a fixed-order tree
+                fx = wave_sum(fx);
+                fy = wave_sum(fy);
+                if (lane == 0) {
+                    const double2 o = acc[lrow];
+                    acc[lrow] = make_double2(__dadd_rn(o.x, fx), __dadd_rn(o.y, fy));
+                }
+            } else if (len > 0) {
+                const double2 o = acc[lrow];
+                acc[lrow] = make_double2(__dadd_rn(o.x, fx), __dadd_rn(o.y, fy));
+            }
+            s = sn;
+            sd = sdn;
+            rl = rln;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < nr; i += NT) attr[b0 + i] = acc[i];
+    if (LOSS) {
+        lsum = wave_sum(lsum);
+        if (lane == 0) sl[w] = lsum;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int k = 0; k < WAVES; ++k) s += sl[k];
+            lpart[blockIdx.x] = s;
+        }
+    }
+}
+
+// ---- tile layout build (at every relabel; see build_attract_tiles)
+// 1. key (row block * ncb + window) << rowbits | local row of every owned
+//    entry (wave per row), for a stable radix sort
+__global__ void at_keys(const int64_t *__restrict__ rpw, const int32_t *__restrict__ colw, int64_t rows, int64_t ncb,
+                        int rowbits, int64_t W, uint64_t *__restrict__ key, int32_t *__restrict__ idx) {
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const uint64_t hi = (uint64_t)((r >> rowbits) * ncb);
+    const uint64_t lr = (uint64_t)(r & ((1 << rowbits) - 1));
+    for (int64_t e = rpw[r] + lane_id(); e < rpw[r + 1]; e += 64) {
+        key[e] = ((hi + (uint64_t)(colw[e] / W)) << rowbits) | lr;
+        idx[e] = (int32_t)e;
+    }
+}
+
+// 2. sorted position p <- entry perm[p]: column offset in the window, value,
+//    and the start flag of each (tile, row) segment
+__global__ void at_gather(const uint64_t *__restrict__ ks, const int32_t *__restrict__ perm, int64_t m, int64_t ncb,
+                          int rowbits, int64_t W, const int32_t *__restrict__ colw, const double *__restrict__ valw,
+                          uint16_t *__restrict__ cs, double *__restrict__ vs, int32_t *__restrict__ flag) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= m) return;
+    const int64_t e = perm[p];
+    const uint64_t k = ks[p];
+    const int64_t cb = (int64_t)((k >> rowbits) % (uint64_t)ncb);
+    cs[p] = (uint16_t)(colw[e] - cb * W);
+    vs[p] = valw[e];
+    flag[p] = (p == 0 || ks[p - 1] != k) ? 1 : 0;
+}
+
+// 3. segments: start, key; then (next kernel) length and the sort key
+//    (tile << 20 | ~length) that orders a tile's rows by descending count
+__global__ void at_segs(const uint64_t *__restrict__ ks, const int32_t *__restrict__ flag,
+                        const int32_t *__restrict__ sid, int64_t m, int32_t *__restrict__ sstart,
+                        uint64_t *__restrict__ skey) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= m || !flag[p]) return;
+    sstart[sid[p]] = (int32_t)p;
+    skey[sid[p]] = ks[p];
+}
+__global__ void at_seglen(const int32_t *__restrict__ sstart, const uint64_t *__restrict__ skey, int32_t ns, int64_t m,
+                          int rowbits, int32_t *__restrict__ slen, uint64_t *__restrict__ okey,
+                          int32_t *__restrict__ oval) {
+    const int32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ns) return;
+    const int32_t len = (int32_t)((g + 1 < ns ? (int64_t)sstart[g + 1] : m) - sstart[g]);
+    slen[g] = len;
+    okey[g] = ((skey[g] >> rowbits) << AT_LENBITS) | (uint64_t)((1u << AT_LENBITS) - 1 - (uint32_t)len);
+    oval[g] = g;
+}
+
+// 4. over the sorted segments j: lengths in sorted order and tile-start flags
+__global__ void at_sorted(const uint64_t *__restrict__ okey, const int32_t *__restrict__ og,
+                          const int32_t *__restrict__ slen, int32_t ns, int64_t *__restrict__ lenj,
+                          int32_t *__restrict__ tflag) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns) return;
+    lenj[j] = slen[og[j]];
+    tflag[j] = (j == 0 || (okey[j - 1] >> AT_LENBITS) != (okey[j] >> AT_LENBITS)) ? 1 : 0;
+}
+// 5. tiles: first sorted segment, segment count -> slices (count / 64, scanned)
+__global__ void at_tilefirst(const uint64_t *__restrict__ okey, const int32_t *__restrict__ tflag,
+                             const int32_t *__restrict__ tix, int32_t ns, int64_t ncb, int32_t *__restrict__ tfirst,
+                             ATile *__restrict__ tiles) {
+    const int32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ns || !tflag[j]) return;
+    const uint64_t tile = okey[j] >> AT_LENBITS;
+    const int32_t t = tix[j];
+    tfirst[t] = j;
+    tiles[t].cb = (int32_t)(tile % (uint64_t)ncb);
+    tiles[t].rb = (int32_t)(tile / (uint64_t)ncb);
+}
+// rows with more than AT_WIDE entries in a tile get a slice of their own: the
+// row cut into 64 consecutive pieces, one per lane, summed by a wave
+// reduction -- a hub row would otherwise keep one wave busy while the
+// workgroup waits for it at the tile's barrier
+constexpr int AT_WIDE = 48;
+__global__ void at_tilecount(const int32_t *__restrict__ tfirst, const int64_t *__restrict__ lenj, int32_t nt,
+                             int32_t ns, int32_t *__restrict__ tns, int32_t *__restrict__ twide) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt) return;
+    const int32_t j0 = tfirst[t], cnt = (t + 1 < nt ? tfirst[t + 1] : ns) - j0;
+    int32_t nw = 0;
+    while (nw < cnt && lenj[j0 + nw] > AT_WIDE) ++nw;   // sorted by descending length
+    twide[t] = nw;
+    tns[t] = nw + (cnt - nw + 63) / 64;
+}
+// 6. slice records (one thread per tile writes its slices)
+__global__ void at_slices(const int32_t *__restrict__ tfirst, const int32_t *__restrict__ tns,
+                          const int32_t *__restrict__ twide, const int32_t *__restrict__ ts0,
+                          const int64_t *__restrict__ lenj, const int64_t *__restrict__ ebase, int32_t nt, int32_t ns,
+                          ATile *__restrict__ tiles, ASlice *__restrict__ slices) {
+    const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nt) return;
+    tiles[t].s0 = ts0[t];
+    tiles[t].ns = tns[t];
+    const int32_t j0 = tfirst[t], jend = t + 1 < nt ? tfirst[t + 1] : ns, nw = twide[t];
+    for (int32_t q = 0; q < tns[t]; ++q) {
+        ASlice sd;
+        if (q < nw) {
+            sd.j0 = j0 + q;
+            sd.cnt = 1;
+            sd.wide = 1;
+            sd.width = (int32_t)((lenj[sd.j0] + 63) / 64);
+        } else {
+            sd.j0 = j0 + nw + 64 * (q - nw);
+            sd.cnt = min(64, jend - sd.j0);
+            sd.wide = 0;
+            sd.width = (int32_t)lenj[sd.j0];
+        }
+        sd.base = ebase[sd.j0];
+        slices[ts0[t] + q] = sd;
+    }
+}
+// 7. one wave per slice: lane words and the jagged-diagonal scatter of the
+//    lanes' rows (step k: the k-th entry of each row longer than k)
+__global__ void at_fill(const ASlice *__restrict__ slices, int32_t nsl, const int32_t *__restrict__ og,
+                        const int32_t *__restrict__ sstart, const uint64_t *__restrict__ skey,
+                        const int64_t *__restrict__ lenj, int rowbits, const uint16_t *__restrict__ cs,
+                        const double *__restrict__ vs, uint32_t *__restrict__ srow, uint16_t *__restrict__ pk,
+                        double *__restrict__ pv) {
+    const int64_t s = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    if (s >= nsl) return;
+    const int lane = lane_id();
+    const ASlice sd = slices[s];
+    int len = 0, lrow = 0;
+    int64_t src = 0;
+    if (sd.wide) {   // piece `lane` of the row: entries [lane * width, ...)
+        const int32_t g = og[sd.j0];
+        const int64_t L = lenj[sd.j0];
+        len = (int)max((int64_t)0, min((int64_t)sd.width, L - (int64_t)lane * sd.width));
+        lrow = (int)(skey[g] & ((1u << rowbits) - 1));
+        src = sstart[g] + (int64_t)lane * sd.width;
+    } else if (lane < sd.cnt) {
+        const int32_t g = og[sd.j0 + lane];
+        len = (int)lenj[sd.j0 + lane];
+        lrow = (int)(skey[g] & ((1u << rowbits) - 1));
+        src = sstart[g];
+    }
+    srow[s * 64 + lane] = ((uint32_t)lrow << AT_LENBITS) | (uint32_t)len;
+    int64_t off = sd.base;
+    for (int k = 0; k < sd.width; ++k) {
+        if (k < len) {
+            pk[off + lane] = cs[src + k];
+            pv[off + lane] = vs[src + k];
+        }
+        off += __popcll(__ballot(k < len));
+    }
+}
+
+// 8. the row blocks' tile ranges: rbt[rb] = first tile of a row block >= rb
+__global__ void at_ranges(const ATile *__restrict__ tiles, int32_t nt, int64_t nrb, int32_t *__restrict__ rbt) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > nt) return;
+    const int64_t lo = t == 0 ? 0 : (int64_t)tiles[t - 1].rb + 1;
+    const int64_t hi = t < nt ? (int64_t)tiles[t].rb : nrb;
+    for (int64_t r = lo; r <= hi; ++r) rbt[r] = (int32_t)t;
 }
 
 // grad = attr - F / Z (TsneHelpers.scala:311-317); MODE 0 writes it, MODE 1
@@ -906,6 +1245,127 @@ static void gather_working_set(tsne_ctx *ctx, OptState *s) {
     comm_allgatherv(ctx, s->gains[c], off.data());
 }
 
+// TSNE_AT_CFG: tile configuration 0..3 (ATCfg0..3)
+static int at_cfg() {
+    static const int c = [] { const char *e = getenv("TSNE_AT_CFG"); return e ? std::max(0, std::min(3, atoi(e))) : 3; }();
+    return c;
+}
+
+// The tiled layout of the owned rows (attract_tiles): a stable radix sort of
+// the entries by (row block, column window, local row) -- within a row the
+// entries keep their order -- then per tile its rows sorted by entry count
+// (a second radix sort of the (tile, row) segments), 64-row slices, and the
+// jagged-diagonal scatter of the column offsets and values.
+// Skipped (attract_rows runs) for dense rows over a small embedding (C5: all
+// of Y sits in one L2), for >= 2^31 owned entries, or with TSNE_ATTRACT_TILES=0.
+static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
+    static const bool on = [] { const char *e = getenv("TSNE_ATTRACT_TILES"); return !(e && e[0] == '0'); }();
+    hipStream_t st = ctx->stream;
+    Workspace &ws = ctx->ws;
+    const int64_t rows = s->L1 - s->L0, n = s->n;
+    s->at_on = false;
+    if (!on || rows <= 0) return;
+    if (s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
+    int64_t m = 0;
+    TSNE_HIP(hipMemcpyAsync(&m, s->rpw + rows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    if (m <= 0 || m >= (int64_t)INT32_MAX) return;
+    const int cfg = at_cfg();
+    const int rowbits = cfg == 0 ? ATCfg0::ROWBITS : cfg == 1 ? ATCfg1::ROWBITS : cfg == 2 ? ATCfg2::ROWBITS : ATCfg3::ROWBITS;
+    const int64_t W = cfg == 0 ? ATCfg0::W : cfg == 1 ? ATCfg1::W : cfg == 2 ? ATCfg2::W : ATCfg3::W;
+    const int64_t nrb = ceil_div(rows, (int64_t)1 << rowbits), ncb = ceil_div(n, W);
+    int bits = rowbits;
+    for (uint64_t v = (uint64_t)(nrb * ncb - 1); v; v >>= 1) ++bits;
+    uint64_t *key = ws.get<uint64_t>("opt.at.key", m), *key2 = ws.get<uint64_t>("opt.at.key2", m);
+    int32_t *idx = ws.get<int32_t>("opt.at.idx", m), *idx2 = ws.get<int32_t>("opt.at.idx2", m);
+    auto scan_i32 = [&](const int32_t *in, int32_t *out, int64_t cnt) {
+        size_t b = 0;
+        TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b, in, out, (int)cnt, st));
+        TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(ws.get<uint8_t>("opt.at.stmp", b), b, in, out, (int)cnt, st));
+    };
+    auto total = [&](const int32_t *excl, const int32_t *in, int64_t cnt) {   // excl[cnt-1] + in[cnt-1]
+        int32_t h[2] = {0, 0};
+        TSNE_HIP(hipMemcpyAsync(h, excl + cnt - 1, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        TSNE_HIP(hipMemcpyAsync(h + 1, in + cnt - 1, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        TSNE_HIP(hipStreamSynchronize(st));
+        return h[0] + h[1];
+    };
+    // 1-2: entries sorted by (tile, local row), row order kept within a row
+    hipLaunchKernelGGL(at_keys, dim3(ceil_div(rows, 4)), dim3(256), 0, st, s->rpw, s->colw, rows, ncb, rowbits, W, key,
+                       idx);
+    size_t tb = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, idx, idx2, (int)m, 0, bits, st));
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(ws.get<uint8_t>("opt.at.tmp", tb), tb, key, key2, idx, idx2, (int)m, 0,
+                                                bits, st));
+    uint16_t *cs = ws.get<uint16_t>("opt.at.cs", m);
+    double *vs = ws.get<double>("opt.at.vs", m);
+    int32_t *flag = ws.get<int32_t>("opt.at.flag", m), *sid = ws.get<int32_t>("opt.at.sid", m);
+    hipLaunchKernelGGL(at_gather, dim3(ceil_div(m, 256)), dim3(256), 0, st, key2, idx2, m, ncb, rowbits, W, s->colw,
+                       s->valw, cs, vs, flag);
+    // 3: (tile, row) segments, sorted by tile and descending length
+    scan_i32(flag, sid, m);
+    const int32_t ns = total(sid, flag, m);
+    int32_t *sstart = ws.get<int32_t>("opt.at.sstart", ns), *slen = ws.get<int32_t>("opt.at.slen", ns);
+    uint64_t *skey = ws.get<uint64_t>("opt.at.skey", ns);
+    uint64_t *okey = ws.get<uint64_t>("opt.at.okey", ns), *okey2 = ws.get<uint64_t>("opt.at.okey2", ns);
+    int32_t *oval = ws.get<int32_t>("opt.at.oval", ns), *og = ws.get<int32_t>("opt.at.og", ns);
+    hipLaunchKernelGGL(at_segs, dim3(ceil_div(m, 256)), dim3(256), 0, st, key2, flag, sid, m, sstart, skey);
+    hipLaunchKernelGGL(at_seglen, dim3(ceil_div(ns, 256)), dim3(256), 0, st, sstart, skey, ns, m, rowbits, slen, okey,
+                       oval);
+    const int obits = bits - rowbits + AT_LENBITS;
+    tb = 0;
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, okey, okey2, oval, og, (int)ns, 0, obits, st));
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(ws.get<uint8_t>("opt.at.tmp", tb), tb, okey, okey2, oval, og, (int)ns,
+                                                0, obits, st));
+    // 4-5: tiles, their slices, slice bases (prefix of the sorted lengths)
+    int64_t *lenj = ws.get<int64_t>("opt.at.lenj", ns), *ebase = ws.get<int64_t>("opt.at.ebase", ns);
+    int32_t *tflag = ws.get<int32_t>("opt.at.tflag", ns), *tix = ws.get<int32_t>("opt.at.tix", ns);
+    hipLaunchKernelGGL(at_sorted, dim3(ceil_div(ns, 256)), dim3(256), 0, st, okey2, og, slen, ns, lenj, tflag);
+    {
+        size_t b = 0;
+        TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b, lenj, ebase, (int)ns, st));
+        TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(ws.get<uint8_t>("opt.at.stmp", b), b, lenj, ebase, (int)ns, st));
+    }
+    scan_i32(tflag, tix, ns);
+    const int32_t nt = total(tix, tflag, ns);
+    int32_t *tfirst = ws.get<int32_t>("opt.at.tfirst", nt), *tns = ws.get<int32_t>("opt.at.tns", nt);
+    int32_t *ts0 = ws.get<int32_t>("opt.at.ts0", nt), *twide = ws.get<int32_t>("opt.at.twide", nt);
+    s->at_tiles = ws.get<ATile>("opt.at.tiles", nt);
+    hipLaunchKernelGGL(at_tilefirst, dim3(ceil_div(ns, 256)), dim3(256), 0, st, okey2, tflag, tix, ns, ncb, tfirst,
+                       s->at_tiles);
+    hipLaunchKernelGGL(at_tilecount, dim3(ceil_div(nt, 256)), dim3(256), 0, st, tfirst, lenj, nt, ns, tns, twide);
+    scan_i32(tns, ts0, nt);
+    const int32_t nsl = total(ts0, tns, nt);
+    s->at_slices = ws.get<ASlice>("opt.at.slices", nsl);
+    hipLaunchKernelGGL(at_slices, dim3(ceil_div(nt, 256)), dim3(256), 0, st, tfirst, tns, twide, ts0, lenj, ebase, nt,
+                       ns, s->at_tiles, s->at_slices);
+    // 6-7: the jagged-diagonal entries and the lane words
+    s->at_srow = ws.get<uint32_t>("opt.at.srow", (size_t)nsl * 64);
+    s->at_pk = ws.get<uint16_t>("opt.at.pk", m);
+    s->at_pv = ws.get<double>("opt.at.pv", m);
+    hipLaunchKernelGGL(at_fill, dim3(ceil_div(nsl, 4)), dim3(256), 0, st, s->at_slices, nsl, og, sstart, skey, lenj,
+                       rowbits, cs, vs, s->at_srow, s->at_pk, s->at_pv);
+    s->at_rbt = ws.get<int32_t>("opt.at.rbt", nrb + 1);
+    hipLaunchKernelGGL(at_ranges, dim3(ceil_div(nt + 1, 256)), dim3(256), 0, st, s->at_tiles, nt, nrb, s->at_rbt);
+    TSNE_LAUNCH_CHECK();
+    static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;
+    if (dbg) {   // layout statistics: tiles, segments, slices, slice widths
+        std::vector<ASlice> hs(nsl);
+        TSNE_HIP(hipMemcpyAsync(hs.data(), s->at_slices, sizeof(ASlice) * nsl, hipMemcpyDeviceToHost, st));
+        TSNE_HIP(hipStreamSynchronize(st));
+        int64_t wsum = 0, wmax = 0;
+        for (const ASlice &x : hs) { wsum += x.width; wmax = std::max<int64_t>(wmax, x.width); }
+        fprintf(stderr, "[attract tiles] cfg=%d rows=%lld m=%lld nrb=%lld ncb=%lld tiles=%d segments=%d slices=%d "
+                "width avg=%.2f max=%lld entries/slice=%.1f\n", cfg, (long long)rows, (long long)m, (long long)nrb,
+                (long long)ncb, nt, ns, nsl, nsl ? (double)wsum / nsl : 0.0, (long long)wmax,
+                nsl ? (double)m / nsl : 0.0);
+    }
+    s->at_nrb = nrb;
+    s->at_ncb = ncb;
+    s->at_cfg = cfg;
+    s->at_on = true;
+}
+
 // this rank's rows of P in the current labels (2-D)
 static void build_own_rows(tsne_ctx *ctx, OptState *s) {
     hipStream_t st = ctx->stream;
@@ -918,6 +1378,7 @@ static void build_own_rows(tsne_ctx *ctx, OptState *s) {
         hipLaunchKernelGGL(own_rows, dim3(ceil_div(m, 4)), dim3(256), 0, st, orig, s->lab, s->rp0, s->col0, s->val0,
                            s->L0, s->L1, s->rpw, s->colw, s->valw);
     TSNE_LAUNCH_CHECK();
+    build_attract_tiles(ctx, s);
 }
 
 // world > 1: the sorted positions of this rank's labels, ascending
@@ -1255,6 +1716,40 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     relabel(ctx, s, s->tree.idx_sorted, cuts);
 }
 
+// The optimizer's attraction: attract_tiles over the tiled layout when it was
+// built, else attract_rows over the owned CSR rows.  Returns the blocks (loss
+// partials) written.
+template <class CF, bool LOSS, int MET>
+static void attract_tiles_launch_c(hipStream_t st, const OptState *s, const AttractArgs &a) {
+    const int64_t nb = s->at_nrb;
+    hipLaunchKernelGGL((attract_tiles<CF, LOSS, MET>), dim3(nb), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt,
+                       s->at_slices, s->at_srow, a.r1 - a.r0, a.r0, s->n, s->at_pk, s->at_pv, a.Y, a.scal, a.ex,
+                       nb / NUM_XCD, a.attr, a.lpart);
+}
+template <bool LOSS, int MET>
+static void attract_tiles_launch_m(hipStream_t st, const OptState *s, const AttractArgs &a) {
+    switch (s->at_cfg) {
+        case 0: attract_tiles_launch_c<ATCfg0, LOSS, MET>(st, s, a); break;
+        case 1: attract_tiles_launch_c<ATCfg1, LOSS, MET>(st, s, a); break;
+        case 3: attract_tiles_launch_c<ATCfg3, LOSS, MET>(st, s, a); break;
+        default: attract_tiles_launch_c<ATCfg2, LOSS, MET>(st, s, a); break;
+    }
+}
+template <bool LOSS>
+static void attract_tiles_launch_l(hipStream_t st, const OptState *s, const AttractArgs &a) {
+    switch (a.metric) {
+        case TSNE_METRIC_EUCLIDEAN: attract_tiles_launch_m<LOSS, TSNE_METRIC_EUCLIDEAN>(st, s, a); break;
+        case TSNE_METRIC_COSINE: attract_tiles_launch_m<LOSS, TSNE_METRIC_COSINE>(st, s, a); break;
+        default: attract_tiles_launch_m<LOSS, TSNE_METRIC_SQEUCLIDEAN>(st, s, a); break;
+    }
+}
+static int64_t attract_launch_opt(hipStream_t st, const OptState *s, const AttractArgs &a, bool loss) {
+    if (!s->at_on) return attract_launch(st, a, loss);
+    if (loss) attract_tiles_launch_l<true>(st, s, a);
+    else attract_tiles_launch_l<false>(st, s, a);
+    return s->at_nrb;
+}
+
 void opt_step(tsne_ctx *ctx, int32_t t) {
     OptState *s = ctx->opt;
     TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
@@ -1303,7 +1798,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     auto side_attract = [&] {
         if (ov_mode != 2) side_wait();
         ctx->timers.begin("opt.attract", s->side);
-        attract_launch(s->side, aa, false);
+        attract_launch_opt(s->side, s, aa, false);
         TSNE_LAUNCH_CHECK();
         ctx->timers.end("opt.attract", s->side);
         s->attract_iter.push_back({t, 0});
@@ -1340,7 +1835,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     } else {
         ctx->timers.begin("opt.attract", st);
-        blocks = attract_launch(st, aa, true);
+        blocks = attract_launch_opt(st, s, aa, true);
         TSNE_LAUNCH_CHECK();
         ctx->timers.end("opt.attract", st);
         s->attract_iter.push_back({t, 1});
