@@ -29,7 +29,7 @@ def rows(p):
 def is_loss_attraction(name):
     """The standalone (LOSS=true) attraction kernel: attract_tiles<true, MET> (the
     optimizer's tiled layout) or attract_rows<LPR, U, true, MET> (CSR rows)."""
-    return ("attract_tiles<true" in name) or ("attract_rows<" in name and ", true," in name)
+    return ("attract_tiles<" in name or "attract_rows<" in name) and ", true," in name
 
 
 def kernel_label(name):
@@ -57,6 +57,7 @@ def main():
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in ld]
     its = [10 * (k + 1) for k in range(len(durs))]
     win = [d for t, d in zip(its, durs) if t <= K]
+    # the window's launches (t <= K) name the kernel of the roofline
     label = kernel_label(ld[0]["Kernel_Name"]) if ld else "attract_rows<64,4,LOSS=true>"
     summary = {
         "source": "rocprofv3 --kernel-trace --stats -- python bench.py --steps %d --warmup %d --no-cpu-baseline "

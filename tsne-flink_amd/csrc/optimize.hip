@@ -113,6 +113,7 @@ struct OptState {
     bool at_on = false;
     int64_t at_nrb = 0, at_ncb = 0;
     int at_cfg = 0;
+    bool morton_labels = false;   // the labels follow the embedding's Morton order (a relabel happened)
     ATile *at_tiles = nullptr;
     int32_t *at_rbt = nullptr;
     ASlice *at_slices = nullptr;
@@ -188,6 +189,39 @@ template <int MET>
 __device__ __forceinline__ double qterm_t(double ax, double ay, double bx, double by) {
     double x;
     return qterm_t<MET>(ax, ay, bx, by, x);
+}
+
+// ln x in fp64 for the KL terms (the loss), ~4x fewer instructions than the
+// libm log: x = 2^e m with m in [1/sqrt2, sqrt2), ln m = 2 atanh(s),
+// s = (m - 1) / (m + 1) (|s| <= 0.1716, v_rcp_f64 + two Newton steps), the
+// odd series to s^21 (remainder < 3e-17 relative), e ln2 in two parts
+// (fdlibm's split).  Within a few ulp of log(); zero, negative, infinite
+// and NaN arguments take log() itself (0 ln 0 stays NaN).
+__device__ __forceinline__ double log_kl(double x) {
+    if (!(x >= 0x1p-1022 && x < INFINITY)) return log(x);
+    const long long b = __double_as_longlong(x);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    double m = __longlong_as_double((b & 0x000fffffffffffffll) | 0x3ff0000000000000ll);
+    if (m > 1.4142135623730951) { m *= 0.5; ++e; }
+    const double f = m - 1.0;   // exact
+    const double d = 2.0 + f;
+    double r = __builtin_amdgcn_rcp(d);
+    r = __fma_rn(r, __fma_rn(-d, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-d, r, 1.0), r);
+    const double s = f * r, s2 = s * s;
+    double p = 2.0 / 21.0;
+    p = __fma_rn(p, s2, 2.0 / 19.0);
+    p = __fma_rn(p, s2, 2.0 / 17.0);
+    p = __fma_rn(p, s2, 2.0 / 15.0);
+    p = __fma_rn(p, s2, 2.0 / 13.0);
+    p = __fma_rn(p, s2, 2.0 / 11.0);
+    p = __fma_rn(p, s2, 2.0 / 9.0);
+    p = __fma_rn(p, s2, 2.0 / 7.0);
+    p = __fma_rn(p, s2, 2.0 / 5.0);
+    p = __fma_rn(p, s2, 2.0 / 3.0);
+    const double lnm = __fma_rn(s * s2, p, 2.0 * s);
+    const double de = (double)e;
+    return __fma_rn(de, 6.93147180369123816490e-01, __fma_rn(de, 1.90821492927058770002e-10, lnm));
 }
 
 // Attraction over the CSR rows [r0, r1) (TsneHelpers.scala:269-306):
@@ -292,10 +326,14 @@ struct ATCfg {
     static constexpr int ROWBITS = __builtin_ctz(RB_);
     static_assert((RB_ & (RB_ - 1)) == 0 && RB_ <= 4096 && W_ <= 65536, "tile packing");
 };
-using ATCfg0 = ATCfg<2048, 5632, 1024>;   // 120 KB LDS
-using ATCfg1 = ATCfg<4096, 3840, 1024>;   // 124 KB
-using ATCfg2 = ATCfg<4096, 5632, 1024>;   // 152 KB
-using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
+// Measured at C3 (window loss launch / non-loss launch): 4096 x 5888 1.12 /
+// 0.77 ms, 4096 x 5632 1.45 / 0.79 (before the division-free loss), 2048 x
+// 3840 1.59 / 1.14, 1024 x 3840 (2 workgroups per CU) 2.28 / 1.13: fewer,
+// longer row segments per tile win over occupancy.
+using ATCfg0 = ATCfg<1024, 3840, 512>;    // 76 KB LDS: 2 workgroups per CU
+using ATCfg1 = ATCfg<2048, 2560, 512>;    // 72 KB: 2 workgroups per CU
+using ATCfg2 = ATCfg<2048, 3840, 1024>;   // 92 KB
+using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB (default)
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
 
@@ -383,7 +421,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
                         fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yi.y, yj.y)));
                         // P ln(P / (q / Z)) = P ln(P Z (1 + metric)): no divisions
                         // (0 ln 0 = NaN for an underflowed P, as the reference)
-                        if (LOSS) lsum += pij * log(pij * Z * x1m);
+                        if (LOSS) lsum += pij * log_kl(pij * Z * x1m);
                     }
                 }
             }
@@ -418,6 +456,8 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
 }
 
 // ---- tile layout build (at every relabel; see build_attract_tiles)
+// 1. key (row block * ncb + window) << rowbits | local row of every owned
+//    entry (wave per row), for a stable radix sort
 // 1. key (row block * ncb + window) << rowbits | local row of every owned
 //    entry (wave per row), for a stable radix sort
 __global__ void at_keys(const int64_t *__restrict__ rpw, const int32_t *__restrict__ colw, int64_t rows, int64_t ncb,
@@ -489,18 +529,20 @@ __global__ void at_tilefirst(const uint64_t *__restrict__ okey, const int32_t *_
     tiles[t].cb = (int32_t)(tile % (uint64_t)ncb);
     tiles[t].rb = (int32_t)(tile / (uint64_t)ncb);
 }
-// rows with more than AT_WIDE entries in a tile get a slice of their own: the
-// row cut into 64 consecutive pieces, one per lane, summed by a wave
+// A row with more than AT_WIDE_MIN entries in a tile gets a slice of its own:
+// the row cut into 64 consecutive pieces, one per lane, summed by a wave
 // reduction -- a hub row would otherwise keep one wave busy while the
-// workgroup waits for it at the tile's barrier
-constexpr int AT_WIDE = 48;
+// workgroup waits for it at the tile's barrier.  (Measured at C3: wide above
+// 48 entries 1.11 ms per loss launch; wide only above max(64, twice the
+// slice's 64th row) 1.31 ms -- balanced lanes beat fewer slices.)
+constexpr int AT_WIDE_MIN = 48;
 __global__ void at_tilecount(const int32_t *__restrict__ tfirst, const int64_t *__restrict__ lenj, int32_t nt,
                              int32_t ns, int32_t *__restrict__ tns, int32_t *__restrict__ twide) {
     const int32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nt) return;
     const int32_t j0 = tfirst[t], cnt = (t + 1 < nt ? tfirst[t + 1] : ns) - j0;
-    int32_t nw = 0;
-    while (nw < cnt && lenj[j0 + nw] > AT_WIDE) ++nw;   // sorted by descending length
+    int32_t nw = 0;   // segments sorted by descending length
+    while (nw < cnt && lenj[j0 + nw] > AT_WIDE_MIN) ++nw;
     twide[t] = nw;
     tns[t] = nw + (cnt - nw + 63) / 64;
 }
@@ -1264,7 +1306,11 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
     Workspace &ws = ctx->ws;
     const int64_t rows = s->L1 - s->L0, n = s->n;
     s->at_on = false;
-    if (!on || rows <= 0) return;
+    // Only while the labels are P's graph order: once they follow the
+    // embedding's Morton order, a row's Y_j are spatially local and
+    // attract_rows' gathers hit the L2 (C3 loss launches: attract_rows 1.58
+    // ms, attract_tiles 2.4 ms over t = 300..1000; in graph order 1.45 vs 1.11).
+    if (!on || rows <= 0 || s->morton_labels) return;
     if (s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
     int64_t m = 0;
     TSNE_HIP(hipMemcpyAsync(&m, s->rpw + rows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -1355,6 +1401,7 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
         TSNE_HIP(hipStreamSynchronize(st));
         int64_t wsum = 0, wmax = 0;
         for (const ASlice &x : hs) { wsum += x.width; wmax = std::max<int64_t>(wmax, x.width); }
+
         fprintf(stderr, "[attract tiles] cfg=%d rows=%lld m=%lld nrb=%lld ncb=%lld tiles=%d segments=%d slices=%d "
                 "width avg=%.2f max=%lld entries/slice=%.1f\n", cfg, (long long)rows, (long long)m, (long long)nrb,
                 (long long)ncb, nt, ns, nsl, nsl ? (double)wsum / nsl : 0.0, (long long)wmax,
@@ -1713,6 +1760,7 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
         TSNE_HIP(hipMemcpyAsync(cuts.data(), s->bounds, sizeof(int64_t) * (ctx->world + 1), hipMemcpyDeviceToHost, st));
         TSNE_HIP(hipStreamSynchronize(st));
     }
+    s->morton_labels = true;
     relabel(ctx, s, s->tree.idx_sorted, cuts);
 }
 
