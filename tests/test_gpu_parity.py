@@ -416,19 +416,14 @@ def test_device_optimizer_matches_host_path(ctx):
     assert ctx.dev_opt_losses() == lh
 
 
-@pytest.mark.parametrize("metric", ["sqeuclidean", "euclidean", "cosine"])
-def test_tiled_attraction_matches_oracle(ctx, metric):
-    """The optimizer's tiled attraction (attract_tiles: 512-row blocks x
-    3840-label column windows, per-row segmented sums across waves) on a P with
-    dense hub rows and columns -- rows spanning several waves and windows --
-    over 10 iterations at theta 0 (exact repulsion on both sides): the
-    embedding and the loss at t = 10 against the oracle."""
+def hub_problem(n=6000, seed=71):
+    """A kNN joint P plus three dense hub rows/columns (rows spanning several
+    waves, windows and wide slices of the tiled attraction)."""
     import scipy.sparse as sp
-    n = 6000
-    rp, col, val = random_problem(n, 30, seed=71)
+    rp, col, val = random_problem(n, 30, seed=seed)
     A = sp.csr_matrix((val, col, rp), shape=(n, n))
-    rng = np.random.default_rng(72)
-    hubs = np.array([3, 2500, 5999])
+    rng = np.random.default_rng(seed + 1)
+    hubs = np.array([3, n // 2 - 500, n - 1])
     B = sp.lil_matrix((n, n))
     for h in hubs:
         B[h, :] = rng.random(n) * 1e-7
@@ -438,8 +433,19 @@ def test_tiled_attraction_matches_oracle(ctx, metric):
     P.eliminate_zeros()
     P.sort_indices()
     P = P / P.sum()
-    rp2, col2, val2 = P.indptr.astype(np.int64), P.indices.astype(np.int32), P.data.astype(np.float64)
-    assert np.diff(rp2)[hubs].min() > 4000
+    assert np.diff(P.indptr)[hubs].min() > 4000
+    return P.indptr.astype(np.int64), P.indices.astype(np.int32), P.data.astype(np.float64)
+
+
+@pytest.mark.parametrize("metric", ["sqeuclidean", "euclidean", "cosine"])
+def test_tiled_attraction_matches_oracle(ctx, metric):
+    """The optimizer's tiled attraction (attract_tiles: row blocks x 5888-label
+    column windows, rows as lanes of jagged-diagonal slices, hub rows split
+    over a wave) on a P with dense hub rows and columns, over 10 iterations at
+    theta 0 (exact repulsion on both sides): the embedding and the loss at
+    t = 10 against the oracle."""
+    n = 6000
+    rp2, col2, val2 = hub_problem(n)
     Y0 = np.random.default_rng(73).normal(size=(n, 2)) * 5.0
     prm = default_params(iterations=10, theta=0.0, metric=metric, learning_rate=200.0)
     Yg, ug, gg = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
@@ -449,6 +455,45 @@ def test_tiled_attraction_matches_oracle(ctx, metric):
                     threads=8)
     assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max()
     assert abs(lg[10] - lo[10]) <= 1e-9 * abs(lo[10])
+
+
+_TILE_CFG_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import tsne_amd as T
+from tsne_amd.api import default_params
+from test_gpu_parity import hub_problem
+rp, col, val = hub_problem(12000)
+Y = np.random.default_rng(74).normal(size=(12000, 2)) * 5.0
+u, g = np.zeros_like(Y), np.ones_like(Y)
+with T.Context(0) as c:
+    l = c.optimize(rp, col, val, Y, u, g, default_params(iterations=10, theta=0.0, learning_rate=200.0))
+np.save(sys.argv[3], np.concatenate([Y.ravel(), [l[10]]]))
+"""
+
+
+def test_tiled_attraction_every_config(tmp_path):
+    """Each row-block configuration of attract_tiles (512 ... 4096 rows; a run
+    picks one by its owned rows, TSNE_AT_CFG forces it) and attract_rows
+    (TSNE_ATTRACT_TILES=0), in child processes, against the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = 12000
+    rp, col, val = hub_problem(n)
+    Yo = np.random.default_rng(74).normal(size=(n, 2)) * 5.0
+    uo, go = np.zeros_like(Yo), np.ones_like(Yo)
+    lo = O.optimize(rp, col, val, Yo, uo, go, learning_rate=200.0, iterations=10, theta=0.0, threads=8)
+    for env in ({"TSNE_AT_CFG": "0"}, {"TSNE_AT_CFG": "1"}, {"TSNE_AT_CFG": "2"}, {"TSNE_AT_CFG": "3"},
+                {"TSNE_ATTRACT_TILES": "0"}):
+        out = tmp_path / ("r_%s.npy" % "_".join(env.values()))
+        subprocess.run([sys.executable, "-c", _TILE_CFG_CHILD, os.path.join(root, "tsne-flink_amd"),
+                        os.path.join(root, "tests"), str(out)], env=dict(os.environ, **env), check=True, timeout=120)
+        r = np.load(out)
+        Yg, lg = r[:-1].reshape(n, 2), r[-1]
+        assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max(), env
+        assert abs(lg - lo[10]) <= 1e-9 * abs(lo[10]), env
 
 
 def test_moment_path_engaged(ctx):

@@ -330,10 +330,13 @@ struct ATCfg {
 // 0.77 ms, 4096 x 5632 1.45 / 0.79 (before the division-free loss), 2048 x
 // 3840 1.59 / 1.14, 1024 x 3840 (2 workgroups per CU) 2.28 / 1.13: fewer,
 // longer row segments per tile win over occupancy.
-using ATCfg0 = ATCfg<1024, 3840, 512>;    // 76 KB LDS: 2 workgroups per CU
-using ATCfg1 = ATCfg<2048, 2560, 512>;    // 72 KB: 2 workgroups per CU
-using ATCfg2 = ATCfg<2048, 3840, 1024>;   // 92 KB
-using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB (default)
+// The row block shrinks with the owned rows (a rank of a multi-GPU run) so
+// that the grid still covers the CUs: the largest of 4096 / 2048 / 1024 / 512
+// rows giving at least one workgroup per CU.
+using ATCfg0 = ATCfg<512, 5888, 1024>;    // 102 KB LDS
+using ATCfg1 = ATCfg<1024, 5888, 1024>;   // 110 KB
+using ATCfg2 = ATCfg<2048, 5888, 1024>;   // 126 KB
+using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
 
@@ -1287,10 +1290,13 @@ static void gather_working_set(tsne_ctx *ctx, OptState *s) {
     comm_allgatherv(ctx, s->gains[c], off.data());
 }
 
-// TSNE_AT_CFG: tile configuration 0..3 (ATCfg0..3)
-static int at_cfg() {
-    static const int c = [] { const char *e = getenv("TSNE_AT_CFG"); return e ? std::max(0, std::min(3, atoi(e))) : 3; }();
-    return c;
+// Tile configuration for `rows` owned rows (TSNE_AT_CFG=0..3 forces one)
+static int at_cfg(tsne_ctx *ctx, int64_t rows) {
+    static const int forced = [] { const char *e = getenv("TSNE_AT_CFG"); return e ? std::max(0, std::min(3, atoi(e))) : -1; }();
+    if (forced >= 0) return forced;
+    for (int c = 3; c > 0; --c)
+        if (ceil_div(rows, (int64_t)512 << c) >= ctx->cu_count - ctx->cu_count / 16) return c;
+    return 0;
 }
 
 // The tiled layout of the owned rows (attract_tiles): a stable radix sort of
@@ -1316,7 +1322,7 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
     TSNE_HIP(hipMemcpyAsync(&m, s->rpw + rows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     TSNE_HIP(hipStreamSynchronize(st));
     if (m <= 0 || m >= (int64_t)INT32_MAX) return;
-    const int cfg = at_cfg();
+    const int cfg = at_cfg(ctx, rows);
     const int rowbits = cfg == 0 ? ATCfg0::ROWBITS : cfg == 1 ? ATCfg1::ROWBITS : cfg == 2 ? ATCfg2::ROWBITS : ATCfg3::ROWBITS;
     const int64_t W = cfg == 0 ? ATCfg0::W : cfg == 1 ? ATCfg1::W : cfg == 2 ? ATCfg2::W : ATCfg3::W;
     const int64_t nrb = ceil_div(rows, (int64_t)1 << rowbits), ncb = ceil_div(n, W);
