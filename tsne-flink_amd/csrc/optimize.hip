@@ -1797,8 +1797,13 @@ static void attract_tiles_launch_l(hipStream_t st, const OptState *s, const Attr
         default: attract_tiles_launch_m<LOSS, TSNE_METRIC_SQEUCLIDEAN>(st, s, a); break;
     }
 }
+// attract_tiles only while the tree build takes the root-tile path: beside
+// the BH traversal of the later phases its 156 KB of LDS per CU keeps the
+// traversal's workgroups off those CUs (t = 180..300 at C3: 5.4 ms per
+// concurrent launch vs 3.1 for attract_rows), and there the attraction is
+// hidden behind the traversal anyway.
 static int64_t attract_launch_opt(hipStream_t st, const OptState *s, const AttractArgs &a, bool loss) {
-    if (!s->at_on) return attract_launch(st, a, loss);
+    if (!s->at_on || !s->tree.root_tile) return attract_launch(st, a, loss);
     if (loss) attract_tiles_launch_l<true>(st, s, a);
     else attract_tiles_launch_l<false>(st, s, a);
     return s->at_nrb;
