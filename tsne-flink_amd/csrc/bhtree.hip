@@ -1226,6 +1226,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
+    unsigned long long wfull = 0, wpart = 0;                                   // STATS only
     int sp = 0;
     int ntt = 0;
     TileTask *mytt = ttask + wid * TILE_CAP;
@@ -1355,6 +1356,12 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     zs += take ? mult : 0.0;
                     const bool open = act && !acc;
                     const uint64_t om = __ballot(open);
+                    if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
+                        const uint64_t am = __ballot(act), tk = __ballot(take);
+                        if (am && tk == am) {
+                            if (am == __ballot(valid)) ++wfull; else ++wpart;
+                        }
+                    }
                     if (om) {
                         if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
                         ++sp;
@@ -1414,6 +1421,8 @@ __global__ __launch_bounds__(256) void bh_traverse(
             atomicMax(visits + 7, wpops + wtile / 16);   // heaviest wave (pops + tile points/16)
             atomicMax(visits + 8, wpops);
             atomicMax(visits + 9, wtile);
+            atomicAdd(visits + 13, wfull);
+            atomicAdd(visits + 14, wpart);
         }
     }
 }

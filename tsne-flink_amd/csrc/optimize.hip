@@ -1675,8 +1675,9 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
     for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
     static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
     if (dbg)
-        fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu\n", t,
-                v[10], v[11], v[12], v[1], v[2]);
+        fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu "
+                "pops=%llu child_slots=%llu all_take_full=%llu all_take_partial=%llu\n", t,
+                v[10], v[11], v[12], v[1], v[2], v[3], v[6], v[13], v[14]);
 }
 
 // One iteration of the 3-D (octree) optimizer: labels are the original
