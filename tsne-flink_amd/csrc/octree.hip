@@ -395,11 +395,214 @@ __device__ __forceinline__ bool summarise3(double h, double dx, double dy, doubl
     return h / D < theta;
 }
 
+// ---- Subtree moments in 3-D (the 2-D moment path of bhtree.hip, restated
+// for the octree).  For a node with box centre c and a query q: v = q - c,
+// A = |v|^2, B = 1 / (1 + A), and per point P = p - c, s = |P|^2,
+// delta = D - A = s - 2 v.P.  Then
+//   1 / (1 + D) = B sum_k (-B delta)^k,
+//   z = B sum_k (-B)^k T_k,            T_k = sum_p delta^k,
+//   F = B^2 sum_k (k + 1) (-B)^k (v T_k - U_k),   U_k = sum_p P delta^k,
+// and T_k, U_k are polynomials in v whose coefficients are the moments
+// M(a; b) = sum_p s^a P^b (a + |b| <= MOM3_ORDER + 1).  Truncated at
+// k <= MOM3_ORDER; with rho = B (R^2 + 2 |v| R) >= |B delta| (R: the box's
+// half-diagonal) the remainder is below (K + 2) rho^(K+1) / (1 - rho)^2
+// relative, taken only when that is <= MOM3_TOL (fp64 rounding level).  A
+// subtree evaluated this way is one the traversal sums exactly (an all-open or
+// near-exact tile), so the result equals that exact leaf sum to 1e-14.
+constexpr int MOM3_ORDER = 3;
+constexpr int MOM3_K = 70;          // (a, bx, by, bz) with a + bx + by + bz <= 4
+constexpr int MOM3_MIN = 64;        // nodes of >= 64 points carry moments
+constexpr int MOM3_CHUNK = 1024;    // points per moment item
+constexpr double MOM3_TOL = 1e-14;
+constexpr int MOM3_GROUP = 10;      // moments accumulated per pass over an item's points
+constexpr int MOM3_TASKS = 32;      // moment tiles recorded per query; more -> dense tiles
+
+struct M3Tab {
+    int8_t a[MOM3_K], bx[MOM3_K], by[MOM3_K], bz[MOM3_K];
+    int8_t idx[5][5][5][5];
+};
+__host__ __device__ constexpr M3Tab make_m3tab() {
+    M3Tab t{};
+    int k = 0;
+    for (int a = 0; a <= 4; ++a)
+        for (int j = 0; j <= 4 - a; ++j)
+            for (int bx = j; bx >= 0; --bx)
+                for (int by = j - bx; by >= 0; --by) {
+                    const int bz = j - bx - by;
+                    t.a[k] = (int8_t)a; t.bx[k] = (int8_t)bx; t.by[k] = (int8_t)by; t.bz[k] = (int8_t)bz;
+                    t.idx[a][bx][by][bz] = (int8_t)k;
+                    ++k;
+                }
+    return t;
+}
+__constant__ M3Tab kM3 = make_m3tab();
+static_assert(make_m3tab().a[MOM3_K - 1] == 4, "70 moments");
+
+__device__ __forceinline__ bool mom3_node(const OctNode &nd) { return nd.cnt >= MOM3_MIN && nd.delta < 63; }
+
+// items: node i (an internal node, i < m - 1) gets ceil(cnt / CHUNK) of them
+__global__ void oct_mom_count(const OctNode *__restrict__ nodes, int64_t n, const int32_t *__restrict__ meta,
+                              const int32_t *__restrict__ mom_flag, int32_t *__restrict__ mcnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t c = 0;
+    if (mom_flag[0] && i < (int64_t)meta[0] - 1 && mom3_node(nodes[i])) c = (nodes[i].cnt + MOM3_CHUNK - 1) / MOM3_CHUNK;
+    mcnt[i] = c;
+}
+__global__ void oct_mom_fill(const int32_t *__restrict__ mcnt, const int32_t *__restrict__ moff, int64_t n,
+                             int64_t cap, int32_t *__restrict__ item_node) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < mcnt[i]; ++c)
+        if (moff[i] + c < cap) item_node[moff[i] + c] = (int32_t)i;
+}
+__device__ __forceinline__ void box3(const OctNode &nd, double &cx, double &cy, double &cz, double &R) {
+    cx = 0.5 * (nd.bx0 + nd.bx1);
+    cy = 0.5 * (nd.by0 + nd.by1);
+    cz = 0.5 * (nd.bz0 + nd.bz1);
+    const double ex = 0.5 * (nd.bx1 - nd.bx0), ey = 0.5 * (nd.by1 - nd.by0), ez = 0.5 * (nd.bz1 - nd.bz0);
+    R = sqrt(ex * ex + ey * ey + ez * ez) * (1.0 + 1e-12);
+}
+__host__ __device__ constexpr double factd3(int k) { return k <= 1 ? 1.0 : k * factd3(k - 1); }
+__device__ __forceinline__ double ipow(double x, int e) {
+    double r = 1.0;
+    for (int k = 0; k < e; ++k) r *= x;
+    return r;
+}
+// One wave per item: lanes over the item's points, MOM3_GROUP moments per
+// pass (registers), a fixed-order wave reduction per moment.
+__global__ __launch_bounds__(256) void oct_mom_items(const double4 *__restrict__ pos, const OctNode *__restrict__ nodes,
+                                                     const int32_t *__restrict__ mcnt, const int32_t *__restrict__ moff,
+                                                     int64_t n, const int32_t *__restrict__ item_node, int64_t cap,
+                                                     double *__restrict__ part) {
+    const int64_t total = min((int64_t)moff[n - 1] + mcnt[n - 1], cap);
+    const int lane = lane_id();
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < total; it += nw) {
+        const int node = __builtin_amdgcn_readfirstlane(item_node[it]);
+        const OctNode &nd = nodes[node];
+        double cx, cy, cz, R;
+        box3(nd, cx, cy, cz, R);
+        const int c = (int)(it - moff[node]);
+        const int p0 = nd.first + c * MOM3_CHUNK, p1 = min(nd.last + 1, p0 + MOM3_CHUNK);
+        for (int g0 = 0; g0 < MOM3_K; g0 += MOM3_GROUP) {
+            double acc[MOM3_GROUP];
+#pragma unroll
+            for (int g = 0; g < MOM3_GROUP; ++g) acc[g] = 0.0;
+            for (int p = p0 + lane; p < p1; p += 64) {
+                const double4 q = pos[p];
+                const double ux = q.x - cx, uy = q.y - cy, uz = q.z - cz;
+                const double s = ux * ux + uy * uy + uz * uz;
+#pragma unroll
+                for (int g = 0; g < MOM3_GROUP; ++g) {
+                    const int k = g0 + g;
+                    if (k < MOM3_K)
+                        acc[g] = __fma_rn(ipow(s, kM3.a[k]) * ipow(ux, kM3.bx[k]) * ipow(uy, kM3.by[k]),
+                                          ipow(uz, kM3.bz[k]), acc[g]);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < MOM3_GROUP; ++g) {
+                const double v = wave_sum(acc[g]);
+                if (lane == 0 && g0 + g < MOM3_K) part[it * MOM3_K + g0 + g] = v;
+            }
+        }
+    }
+}
+// node moments: its items' partials summed in item order (thread per (node, moment))
+__global__ void oct_mom_reduce(const int32_t *__restrict__ mcnt, const int32_t *__restrict__ moff, int64_t n,
+                               int64_t cap, const double *__restrict__ part, double *__restrict__ mom) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = e / MOM3_K;
+    const int k = (int)(e - i * MOM3_K);
+    if (i >= n || mcnt[i] == 0 || moff[i] + mcnt[i] > cap) return;
+    double s = 0.0;
+    for (int c = 0; c < mcnt[i]; ++c) s += part[(moff[i] + c) * MOM3_K + k];
+    mom[i * MOM3_K + k] = s;
+}
+// the moments exist this iteration if the previous traversal had demand for
+// them (lanes whose tile could use them: >= n / 64), or at the first build
+__global__ void oct_mom_gate(int32_t *mom_flag) {
+    mom_flag[0] = mom_flag[1] >= mom_flag[2];
+    mom_flag[1] = 0;
+}
+
+__device__ __forceinline__ bool mom3_ok(double vx, double vy, double vz, double R) {
+    const double A = vx * vx + vy * vy + vz * vz;
+    const double rho = (R * R + 2.0 * sqrt(A) * R) / (1.0 + A) * (1.0 + 1e-12);
+    if (!(rho < 0.25)) return false;
+    double rp = rho;
+#pragma unroll
+    for (int k = 0; k < MOM3_ORDER; ++k) rp *= rho;
+    return (MOM3_ORDER + 2) * rp <= MOM3_TOL * (1.0 - rho) * (1.0 - rho);
+}
+// z += sum 1/(1+D), F += sum (q - p)/(1+D)^2 over the node's points from its
+// moments mu (wave-uniform: scalar loads), the query itself included (D = 0:
+// 1 to z, 0 to F -- taken off by the caller like the dense tile)
+__device__ __forceinline__ void mom3_eval(const double *__restrict__ mu, double vx, double vy, double vz, double &fx,
+                                          double &fy, double &fz, double &zs) {
+    const double A = vx * vx + vy * vy + vz * vz;
+    const double B = rcp2(1.0 + A);
+    double px[4], py[4], pz[4];
+    px[0] = py[0] = pz[0] = 1.0;
+#pragma unroll
+    for (int e = 1; e < 4; ++e) { px[e] = px[e - 1] * vx; py[e] = py[e - 1] * vy; pz[e] = pz[e - 1] * vz; }
+    double T[MOM3_ORDER + 1], Ux[MOM3_ORDER + 1], Uy[MOM3_ORDER + 1], Uz[MOM3_ORDER + 1];
+#pragma unroll
+    for (int k = 0; k <= MOM3_ORDER; ++k) {
+        double t = 0.0, ux = 0.0, uy = 0.0, uz = 0.0;
+        double ckj = 1.0, m2 = 1.0;   // C(k, j), (-2)^j
+#pragma unroll
+        for (int j = 0; j <= k; ++j) {
+            // sum over |b| = j of multinom(j; b) v^b M(k - j; b) (and b + e_x, e_y, e_z)
+            double st = 0.0, sx = 0.0, sy = 0.0, sz = 0.0;
+#pragma unroll
+            for (int bx = j; bx >= 0; --bx)
+#pragma unroll
+                for (int by = j - bx; by >= 0; --by) {
+                    const int bz = j - bx - by;
+                    const double mult = factd3(j) / (factd3(bx) * factd3(by) * factd3(bz));   // multinomial
+                    const double w = mult * px[bx] * py[by] * pz[bz];
+                    const int a = k - j;
+                    st = __fma_rn(w, mu[kM3.idx[a][bx][by][bz]], st);
+                    sx = __fma_rn(w, mu[kM3.idx[a][bx + 1][by][bz]], sx);
+                    sy = __fma_rn(w, mu[kM3.idx[a][bx][by + 1][bz]], sy);
+                    sz = __fma_rn(w, mu[kM3.idx[a][bx][by][bz + 1]], sz);
+                }
+            const double c = ckj * m2;
+            t = __fma_rn(c, st, t);
+            ux = __fma_rn(c, sx, ux);
+            uy = __fma_rn(c, sy, uy);
+            uz = __fma_rn(c, sz, uz);
+            ckj = ckj * (double)(k - j) / (double)(j + 1);
+            m2 *= -2.0;
+        }
+        T[k] = t; Ux[k] = ux; Uy[k] = uy; Uz[k] = uz;
+    }
+    double z = 0.0, gx = 0.0, gy = 0.0, gz = 0.0, bk = 1.0;   // bk = (-B)^k
+#pragma unroll
+    for (int k = 0; k <= MOM3_ORDER; ++k) {
+        z = __fma_rn(bk, T[k], z);
+        const double c = (double)(k + 1) * bk;
+        gx = __fma_rn(c, vx * T[k] - Ux[k], gx);
+        gy = __fma_rn(c, vy * T[k] - Uy[k], gy);
+        gz = __fma_rn(c, vz * T[k] - Uz[k], gz);
+        bk *= -B;
+    }
+    const double B2 = B * B;
+    zs += B * z;
+    fx += B2 * gx;
+    fy += B2 * gy;
+    fz += B2 * gz;
+}
+
 __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ pos, const int32_t *__restrict__ dupc,
                                                     const OctNode *__restrict__ nodes,
                                                     const int32_t *__restrict__ meta, double theta, double near_dmax,
                                                     int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
-                                                    double *__restrict__ F, double *__restrict__ Z) {
+                                                    int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
+                                                    int32_t *__restrict__ mtask_n, double *__restrict__ F,
+                                                    double *__restrict__ Z) {
     __shared__ int32_t sref[4][STACK3];
     __shared__ uint64_t smask[4][STACK3];
     __shared__ double4 tbuf[4][64];
@@ -419,6 +622,9 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
     double fx = 0.0, fy = 0.0, fz = 0.0, zs = 0.0;
     double4 *buf = tbuf[w];
     int sp = 0;
+    const bool mom_on = mom_flag[0] != 0;
+    int nwant = 0;   // tiles whose moments this lane could take (the next build's gate)
+    int ntask = 0;
     if (root == ~0) {
         if (valid) { const double4 p = pos[0]; leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs); }
     } else if (root >= 0) {
@@ -465,7 +671,24 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
                 tile = dmax <= nd.hmin * inv_theta * (1.0 - 1e-12) || dmax <= near_dmax;
             }
         }
-        if (__ballot(tile)) {
+        // a tile from the node's moments when the truncation bound holds: a
+        // task of this query's list (oct_mom_apply evaluates it afterwards)
+        bool usem = false;
+        if (tile && mom3_node(nd)) {
+            double cx, cy, cz, R;
+            box3(nd, cx, cy, cz, R);
+            if (mom3_ok(qx - cx, qy - cy, qz - cz, R)) {
+                ++nwant;
+                if (mom_on && ntask < MOM3_TASKS) {
+                    usem = true;
+                    mtask[s * MOM3_TASKS + ntask++] = ref;
+                    zs -= (s >= nd.first && s <= nd.last) ? (double)ndup : 0.0;
+                }
+            }
+        }
+        if (usem) act = false;
+        const bool dense = tile && !usem;
+        if (__ballot(dense)) {
             // points staged through LDS 64 at a time, read back as broadcasts; the
             // query's exact duplicates (itself included) add 1 each to z: taken off
             const int a = nd.first, b = nd.last;
@@ -477,7 +700,7 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_s_waitcnt(0);
                 __builtin_amdgcn_wave_barrier();
-                if (tile) {
+                if (dense) {
                     for (int j = 0; j < cn; ++j) {
                         const double4 pp = buf[j];
                         const double dx = qx - pp.x, dy = qy - pp.y, dz = qz - pp.z;
@@ -491,7 +714,7 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
                 }
             }
             __builtin_amdgcn_wave_barrier();
-            if (tile) {
+            if (dense) {
                 fx += ux; fy += uy; fz += uz;
                 zs += uq - ((s >= a && s <= b) ? (double)ndup : 0.0);
                 act = false;
@@ -544,7 +767,38 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
         F[3 * s + 1] = fy;
         F[3 * s + 2] = fz;
         Z[s] = zs;
+        mtask_n[s] = ntask;
     }
+    // demand for the next build's moments (only until the gate's threshold:
+    // one memory-side atomic per wave on one word would serialise n / 64 of them)
+    const int ww = wave_sum(nwant);
+    if (lane == 0 && ww && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
+        atomicAdd(&mom_flag[1], ww);
+}
+
+// Each query's moment tasks (in traversal order), added to its F and z.
+__global__ __launch_bounds__(256) void oct_mom_apply(const double4 *__restrict__ pos, const OctNode *__restrict__ nodes,
+                                                     const double *__restrict__ mom, const int32_t *__restrict__ mtask,
+                                                     const int32_t *__restrict__ mtask_n, int64_t g0, int64_t g1,
+                                                     const int32_t *__restrict__ qlist, double *__restrict__ F,
+                                                     double *__restrict__ Z) {
+    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= g1) return;
+    const int64_t s = qlist ? (int64_t)qlist[k] : k;
+    const int nt = mtask_n[s];
+    if (nt == 0) return;
+    const double4 q = pos[s];
+    double fx = 0.0, fy = 0.0, fz = 0.0, zs = 0.0;
+    for (int i = 0; i < nt; ++i) {
+        const int node = mtask[s * MOM3_TASKS + i];
+        double cx, cy, cz, R;
+        box3(nodes[node], cx, cy, cz, R);
+        mom3_eval(mom + (int64_t)node * MOM3_K, q.x - cx, q.y - cy, q.z - cz, fx, fy, fz, zs);
+    }
+    F[3 * s] += fx;
+    F[3 * s + 1] += fy;
+    F[3 * s + 2] += fz;
+    Z[s] += zs;
 }
 
 }  // namespace
@@ -573,6 +827,26 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
                                                64, ctx->stream));
     t.sort_tmp_bytes = tb;
     t.sort_tmp = ws.get<uint8_t>("oct.sort_tmp", tb);
+    t.mom = ws.get<double>("oct.mom", (size_t)MOM3_K * n);
+    t.mcnt = ws.get<int32_t>("oct.mcnt", n);
+    t.moff = ws.get<int32_t>("oct.moff", n);
+    t.item_cap = n / 8 + 64;
+    t.item_node = ws.get<int32_t>("oct.item_node", t.item_cap);
+    t.mom_part = ws.get<double>("oct.mom_part", (size_t)MOM3_K * t.item_cap);
+    t.mom_flag = ws.get<int32_t>("oct.mom_flag", 4);
+    t.mtask = ws.get<int32_t>("oct.mtask", (size_t)MOM3_TASKS * n);
+    t.mtask_n = ws.get<int32_t>("oct.mtask_n", n);
+    size_t mb = 0;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, mb, t.mcnt, t.moff, (int)n, ctx->stream));
+    t.mscan_tmp_bytes = mb;
+    t.mscan_tmp = ws.get<uint8_t>("oct.mscan_tmp", mb);
+    // the first build computes moments (demand := threshold); threshold n / 64
+    // lanes; TSNE_OCT_MOMENTS=0 turns the path off
+    static const bool on = [] { const char *e = getenv("TSNE_OCT_MOMENTS"); return !(e && e[0] == '0'); }();
+    const int32_t thr = (int32_t)std::max<int64_t>(1, n / 64);
+    const int32_t f[4] = {0, on ? thr : 0, on ? thr : INT32_MAX, 0};
+    TSNE_HIP(hipMemcpyAsync(t.mom_flag, f, sizeof(f), hipMemcpyHostToDevice, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
@@ -594,6 +868,17 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(bottom_up3<512>, dim3(ceil_div(n, 512)), dim3(512), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root3, dim3(1), dim3(1), 0, st, t.meta);
+    // subtree moments (when the last traversal wanted them)
+    hipLaunchKernelGGL(oct_mom_gate, dim3(1), dim3(1), 0, st, t.mom_flag);
+    hipLaunchKernelGGL(oct_mom_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_flag, t.mcnt);
+    size_t mb = t.mscan_tmp_bytes;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.mscan_tmp, mb, t.mcnt, t.moff, (int)n, st));
+    hipLaunchKernelGGL(oct_mom_fill, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.mcnt, t.moff, n, t.item_cap,
+                       t.item_node);
+    hipLaunchKernelGGL(oct_mom_items, dim3(std::max<int64_t>(1, std::min<int64_t>(4096, ceil_div(t.item_cap, 4)))),
+                       dim3(256), 0, st, t.pos, t.nodes, t.mcnt, t.moff, n, t.item_node, t.item_cap, t.mom_part);
+    hipLaunchKernelGGL(oct_mom_reduce, dim3(ceil_div(n * MOM3_K, 256)), dim3(256), 0, st, t.mcnt, t.moff, n, t.item_cap,
+                       t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
 }
 
@@ -612,7 +897,9 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
     if (s1 <= s0) return;
     const int64_t waves = ceil_div(s1 - s0, 64);
     hipLaunchKernelGGL(oct_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, dF, dz);
+                       t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz);
+    hipLaunchKernelGGL(oct_mom_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
+                       t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

@@ -40,6 +40,14 @@ struct OctTree {
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     int bbox_blocks = 0;
+    // subtree moments (70 per node of >= MOM3_MIN points, about its box
+    // centre), built in chunks; gated by the previous traversal's demand
+    double *mom = nullptr, *mom_part = nullptr;
+    int32_t *mcnt = nullptr, *moff = nullptr, *item_node = nullptr, *mom_flag = nullptr;
+    int32_t *mtask = nullptr, *mtask_n = nullptr;   // per query: nodes evaluated from their moments
+    void *mscan_tmp = nullptr;
+    size_t mscan_tmp_bytes = 0;
+    int64_t item_cap = 0;
 };
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n);
