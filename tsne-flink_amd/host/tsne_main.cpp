@@ -136,10 +136,17 @@ int main(int argc, char **argv) {
         double t2 = now();
         std::vector<Triple> pw = h.pairwiseAffinities(knn, perplexity);
         std::vector<Triple> joint = h.jointDistribution(pw);
-        std::vector<int32_t> ids;
-        for (const auto &e : joint) ids.push_back(e.i);
-        std::sort(ids.begin(), ids.end());
-        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        std::vector<int32_t> ids;   // the rows of P (jointDistribution emits them grouped, ascending)
+        bool ascending = true;
+        for (const auto &e : joint) {
+            if (!ids.empty() && e.i == ids.back()) continue;
+            if (!ids.empty() && e.i < ids.back()) ascending = false;
+            ids.push_back(e.i);
+        }
+        if (!ascending) {
+            std::sort(ids.begin(), ids.end());
+            ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        }
         std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %zu)\n", now() - t2, joint.size());
         WorkingSet ws = h.initWorkingSet(ids, (int32_t)nComponents, randomState);
         std::map<int32_t, double> loss;
