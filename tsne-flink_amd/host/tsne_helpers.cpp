@@ -80,100 +80,109 @@ Csr toCsr(const std::vector<Triple> &t, const std::vector<int32_t> *idsIn) {
     return c;
 }
 
-std::vector<Triple> TsneHelpers::kNearestNeighbors(const Vectors &input, int32_t k, int32_t metric) {
-    if (input.size() < 2) return {};
-    const int64_t n = (int64_t)input.size();
-    const int32_t d = (int32_t)input[0].second.size();
-    std::vector<size_t> order(input.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return input[a].first < input[b].first; });
-    std::vector<double> X((size_t)n * d);
-    std::vector<int32_t> ids(n);
-    for (int64_t r = 0; r < n; ++r) {
-        const auto &v = input[order[r]];
-        if ((int32_t)v.second.size() != d) throw std::invalid_argument("vectors of different lengths");
-        ids[r] = v.first;
-        std::memcpy(&X[(size_t)r * d], v.second.data(), sizeof(double) * d);
-    }
-    const int64_t kk = std::min<int64_t>(k, n - 1);
-    std::vector<int32_t> idx((size_t)(n * kk));
-    std::vector<double> dist((size_t)(n * kk));
-    check(tsne_knn(ctx_, X.data(), n, d, metric, k, 0, n, idx.data(), dist.data()));
+std::vector<Triple> fromCsr(const Csr &c) {
     std::vector<Triple> out;
-    out.reserve(idx.size());
-    for (int64_t r = 0; r < n; ++r)
-        for (int64_t t = 0; t < kk; ++t)
-            out.push_back({ids[r], ids[idx[(size_t)(r * kk + t)]], dist[(size_t)(r * kk + t)]});
+    out.reserve(c.val.size());
+    for (size_t i = 0; i + 1 < c.row_ptr.size(); ++i)
+        for (int64_t e = c.row_ptr[i]; e < c.row_ptr[i + 1]; ++e) out.push_back({c.ids[i], c.ids[c.col[e]], c.val[e]});
     return out;
 }
 
-// projectKnn (TsneHelpers.scala:93-160): the iterations-1 shift vectors are
-// uniform [0,1)^dimension draws (DenseVector.rand, unseeded in the reference)
-// from a 64-bit Mersenne twister seeded with randomState.
-std::vector<Triple> TsneHelpers::projectKnn(const Vectors &input, int32_t k, int32_t metric, int32_t iterations,
-                                            int64_t randomState) {
-    if (input.size() < 2) return {};
-    const int64_t n = (int64_t)input.size();
-    const int32_t d = (int32_t)input[0].second.size();
-    std::vector<size_t> order(input.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+// The input's dense rows sorted by id (the kNN row order), as one n x d array.
+static void denseInput(const Vectors &input, std::vector<int32_t> &ids, std::vector<double> &X, int32_t &d) {
+    const size_t n = input.size();
+    d = (int32_t)input[0].second.size();
+    std::vector<size_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = i;
     std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return input[a].first < input[b].first; });
-    std::vector<double> X((size_t)n * d);
-    std::vector<int32_t> ids(n);
-    for (int64_t r = 0; r < n; ++r) {
+    X.resize(n * (size_t)d);
+    ids.resize(n);
+    for (size_t r = 0; r < n; ++r) {
         const auto &v = input[order[r]];
         if ((int32_t)v.second.size() != d) throw std::invalid_argument("vectors of different lengths");
         ids[r] = v.first;
-        std::memcpy(&X[(size_t)r * d], v.second.data(), sizeof(double) * d);
+        std::memcpy(&X[r * (size_t)d], v.second.data(), sizeof(double) * d);
     }
-    std::mt19937_64 rng((uint64_t)randomState);
-    std::vector<double> shifts((size_t)std::max(iterations - 1, 0) * d);
-    for (double &v : shifts) v = (double)(rng() >> 11) * 0x1.0p-53;
+}
+
+// kNearestNeighbors (TsneHelpers.scala:41-59, also partitionKnn :61-91: the
+// same exact result) or projectKnn (:93-160: the iterations-1 shift vectors
+// are uniform [0,1)^dimension draws -- DenseVector.rand, unseeded in the
+// reference -- from a 64-bit Mersenne twister seeded with randomState).
+Csr TsneHelpers::kNearestNeighborsCsr(const Vectors &input, int32_t k, int32_t metric, const std::string &method,
+                                      int32_t iterations, int64_t randomState) {
+    Csr c;
+    if (input.size() < 2) {
+        c.row_ptr.assign(1, 0);
+        return c;
+    }
+    std::vector<double> X;
+    int32_t d = 0;
+    denseInput(input, c.ids, X, d);
+    const int64_t n = (int64_t)c.ids.size();
     const int64_t kk = std::min<int64_t>(k, n - 1);
-    std::vector<int32_t> idx((size_t)(n * kk));
-    std::vector<double> dist((size_t)(n * kk));
-    check(tsne_project_knn(ctx_, X.data(), n, d, metric, k, iterations, shifts.empty() ? nullptr : shifts.data(),
-                           idx.data(), dist.data()));
-    std::vector<Triple> out;
-    out.reserve(idx.size());
-    for (int64_t r = 0; r < n; ++r)
-        for (int64_t t = 0; t < kk; ++t)
-            out.push_back({ids[r], ids[idx[(size_t)(r * kk + t)]], dist[(size_t)(r * kk + t)]});
-    return out;
+    c.col.resize((size_t)(n * kk));
+    c.val.resize((size_t)(n * kk));
+    if (method == "project") {
+        std::mt19937_64 rng((uint64_t)randomState);
+        std::vector<double> shifts((size_t)std::max(iterations - 1, 0) * d);
+        for (double &v : shifts) v = (double)(rng() >> 11) * 0x1.0p-53;
+        check(tsne_project_knn(ctx_, X.data(), n, d, metric, k, iterations, shifts.empty() ? nullptr : shifts.data(),
+                               c.col.data(), c.val.data()));
+    } else {
+        check(tsne_knn(ctx_, X.data(), n, d, metric, k, 0, n, c.col.data(), c.val.data()));
+    }
+    c.row_ptr.resize((size_t)n + 1);
+    for (int64_t r = 0; r <= n; ++r) c.row_ptr[(size_t)r] = r * kk;
+    return c;
+}
+
+std::vector<Triple> TsneHelpers::kNearestNeighbors(const Vectors &input, int32_t k, int32_t metric) {
+    return fromCsr(kNearestNeighborsCsr(input, k, metric));
+}
+
+std::vector<Triple> TsneHelpers::projectKnn(const Vectors &input, int32_t k, int32_t metric, int32_t iterations,
+                                            int64_t randomState) {
+    return fromCsr(kNearestNeighborsCsr(input, k, metric, "project", iterations, randomState));
 }
 
 std::vector<Triple> TsneHelpers::partitionKnn(const Vectors &input, int32_t k, int32_t metric, int32_t) {
     return kNearestNeighbors(input, k, metric);
 }
 
+Csr TsneHelpers::pairwiseAffinitiesCsr(const Csr &knn, double perplexity) {
+    Csr c;
+    c.ids = knn.ids;
+    c.row_ptr = knn.row_ptr;
+    c.col = knn.col;
+    c.val.resize(knn.val.size());
+    check(tsne_pairwise_affinities(ctx_, knn.row_ptr.data(), knn.val.data(), (int64_t)knn.ids.size(), perplexity,
+                                   c.val.data()));
+    return c;
+}
+
 std::vector<Triple> TsneHelpers::pairwiseAffinities(const std::vector<Triple> &knn, double perplexity) {
-    Csr c = toCsr(knn);
-    std::vector<double> p(c.val.size());
-    check(tsne_pairwise_affinities(ctx_, c.row_ptr.data(), c.val.data(), (int64_t)c.ids.size(), perplexity,
-                                   p.data()));
-    std::vector<Triple> out;
-    out.reserve(p.size());
-    for (size_t i = 0; i + 1 < c.row_ptr.size(); ++i)
-        for (int64_t e = c.row_ptr[i]; e < c.row_ptr[i + 1]; ++e)
-            out.push_back({c.ids[i], c.ids[c.col[e]], p[e]});
-    return out;
+    return fromCsr(pairwiseAffinitiesCsr(toCsr(knn), perplexity));
+}
+
+Csr TsneHelpers::jointDistributionCsr(const Csr &aff) {
+    const int64_t n = (int64_t)aff.ids.size();
+    const int64_t cap = 2 * (int64_t)aff.val.size() + 1;
+    Csr c;
+    c.ids = aff.ids;
+    c.row_ptr.resize((size_t)n + 1);
+    c.col.resize((size_t)cap);
+    c.val.resize((size_t)cap);
+    int64_t nnz = 0;
+    check(tsne_joint_distribution(ctx_, aff.row_ptr.data(), aff.col.data(), aff.val.data(), n, cap,
+                                  c.row_ptr.data(), c.col.data(), c.val.data(), &nnz));
+    c.col.resize((size_t)nnz);
+    c.val.resize((size_t)nnz);
+    return c;
 }
 
 std::vector<Triple> TsneHelpers::jointDistribution(const std::vector<Triple> &aff) {
-    Csr c = toCsr(aff);
-    const int64_t n = (int64_t)c.ids.size();
-    const int64_t cap = 2 * (int64_t)c.val.size() + 1;
-    std::vector<int64_t> orp(n + 1);
-    std::vector<int32_t> oc(cap);
-    std::vector<double> ov(cap);
-    int64_t nnz = 0;
-    check(tsne_joint_distribution(ctx_, c.row_ptr.data(), c.col.data(), c.val.data(), n, cap, orp.data(),
-                                  oc.data(), ov.data(), &nnz));
-    std::vector<Triple> out;
-    out.reserve(nnz);
-    for (int64_t i = 0; i < n; ++i)
-        for (int64_t e = orp[i]; e < orp[i + 1]; ++e) out.push_back({c.ids[i], c.ids[oc[e]], ov[e]});
-    return out;
+    return fromCsr(jointDistributionCsr(toCsr(aff)));
 }
 
 WorkingSet TsneHelpers::initWorkingSet(const std::vector<int32_t> &ids, int32_t nComponents,
@@ -215,10 +224,10 @@ void TsneHelpers::centerEmbedding(WorkingSet &ws) {
     check(tsne_center_embedding(ctx_, (int64_t)ws.ids.size(), ws.n_components, ws.y.data()));
 }
 
-void TsneHelpers::optimize(const std::vector<Triple> &P, WorkingSet &ws, double learningRate, int32_t iterations,
-                           int32_t metric, double earlyExaggeration, double initialMomentum, double finalMomentum,
-                           double theta, std::map<int32_t, double> *loss) {
-    Csr c = toCsr(P, &ws.ids);
+void TsneHelpers::optimizeCsr(const Csr &c, WorkingSet &ws, double learningRate, int32_t iterations, int32_t metric,
+                              double earlyExaggeration, double initialMomentum, double finalMomentum, double theta,
+                              std::map<int32_t, double> *loss) {
+    if (c.ids != ws.ids) throw std::invalid_argument("P's rows are not the working set's ids");
     tsne_params p;
     tsne_params_default(&p);
     p.n_components = ws.n_components;
@@ -237,6 +246,13 @@ void TsneHelpers::optimize(const std::vector<Triple> &P, WorkingSet &ws, double 
                         ws.y.data(), ws.upd.data(), ws.gains.data(), keys.data(), vals.data(), cap, &nl));
     if (loss)
         for (int32_t k = 0; k < std::min(nl, cap); ++k) (*loss)[keys[k]] += vals[k];
+}
+
+void TsneHelpers::optimize(const std::vector<Triple> &P, WorkingSet &ws, double learningRate, int32_t iterations,
+                           int32_t metric, double earlyExaggeration, double initialMomentum, double finalMomentum,
+                           double theta, std::map<int32_t, double> *loss) {
+    optimizeCsr(toCsr(P, &ws.ids), ws, learningRate, iterations, metric, earlyExaggeration, initialMomentum,
+                finalMomentum, theta, loss);
 }
 
 // java.lang.Double.toString: shortest round-trip digits; plain notation for

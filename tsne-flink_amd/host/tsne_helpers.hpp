@@ -35,6 +35,14 @@ struct WorkingSet {
     std::vector<double> y, upd, gains;  // ids.size() x n_components, row-major
 };
 
+// CSR of triples over a dense id map (ids sorted ascending).
+struct Csr {
+    std::vector<int32_t> ids;        // dense index -> original id
+    std::vector<int64_t> row_ptr;
+    std::vector<int32_t> col;        // dense indices
+    std::vector<double> val;
+};
+
 // Tsne.getMetric (Tsne.scala:161-168): the name validated, the id returned.
 int32_t getMetric(const std::string &name);
 
@@ -73,6 +81,17 @@ class TsneHelpers {
                   double initialMomentum, double finalMomentum, double theta,
                   std::map<int32_t, double> *loss);
 
+    // The same operators on CSR (rows = the sorted ids, columns dense row
+    // indices): the CLI's path, without materialising 10^8 triples per stage.
+    // knnMethod: "bruteforce" / "partition" (exact) or "project".
+    Csr kNearestNeighborsCsr(const Vectors &input, int32_t k, int32_t metric, const std::string &method = "bruteforce",
+                             int32_t iterations = 3, int64_t randomState = 0);
+    Csr pairwiseAffinitiesCsr(const Csr &knn, double perplexity);
+    Csr jointDistributionCsr(const Csr &affinities);
+    void optimizeCsr(const Csr &P, WorkingSet &ws, double learningRate, int32_t iterations, int32_t metric,
+                     double earlyExaggeration, double initialMomentum, double finalMomentum, double theta,
+                     std::map<int32_t, double> *loss);
+
     tsne_ctx *ctx() { return ctx_; }
 
   private:
@@ -82,14 +101,9 @@ class TsneHelpers {
 // Throws std::invalid_argument for TSNE_ERR_ARG, std::runtime_error otherwise.
 void check(int status);
 
-// CSR of triples over a dense id map (ids sorted ascending).
-struct Csr {
-    std::vector<int32_t> ids;        // dense index -> original id
-    std::vector<int64_t> row_ptr;
-    std::vector<int32_t> col;        // dense indices
-    std::vector<double> val;
-};
 Csr toCsr(const std::vector<Triple> &t, const std::vector<int32_t> *ids = nullptr);
+// CSR -> triples (ids restored), row by row
+std::vector<Triple> fromCsr(const Csr &c);
 
 // java.lang.Double.toString formatting and java.util.HashMap<Integer,Double>.toString
 std::string javaDouble(double v);

@@ -119,40 +119,40 @@ int main(int argc, char **argv) {
         const int32_t metric = getMetric(metricName);  // IllegalArgumentException before any work
         TsneHelpers h(device);
         double t0 = now();
-        std::vector<Triple> knn;
+        // P as CSR over the sorted point ids; the kNN methods keep that form
+        // from the GPU's output on (no 10^8-element triple vectors)
+        Csr knn;
         if (inputDistanceMatrix) {
-            knn = readDistanceMatrix(inputPath);
+            knn = toCsr(readDistanceMatrix(inputPath));
         } else {
             Vectors input = readInput(inputPath, inputDimension);
             double t1 = now();
             std::fprintf(stderr, "[tsne_hip] read %zu points in %.3f s\n", input.size(), t1 - t0);
-            if (knnMethod == "bruteforce") knn = h.kNearestNeighbors(input, (int32_t)neighbors, metric);
-            else if (knnMethod == "partition") knn = h.partitionKnn(input, (int32_t)neighbors, metric, 1);
-            else if (knnMethod == "project")
-                knn = h.projectKnn(input, (int32_t)neighbors, metric, (int32_t)knnIterations, randomState);
-            else throw std::invalid_argument("Knn method '" + metricName + "' not defined");  // Tsne.scala:78
+            if (knnMethod != "bruteforce" && knnMethod != "partition" && knnMethod != "project")
+                throw std::invalid_argument("Knn method '" + metricName + "' not defined");  // Tsne.scala:78
+            knn = h.kNearestNeighborsCsr(input, (int32_t)neighbors, metric, knnMethod, (int32_t)knnIterations,
+                                         randomState);
             std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", now() - t1);
         }
         double t2 = now();
-        std::vector<Triple> pw = h.pairwiseAffinities(knn, perplexity);
-        std::vector<Triple> joint = h.jointDistribution(pw);
-        std::vector<int32_t> ids;   // the rows of P (jointDistribution emits them grouped, ascending)
-        bool ascending = true;
-        for (const auto &e : joint) {
-            if (!ids.empty() && e.i == ids.back()) continue;
-            if (!ids.empty() && e.i < ids.back()) ascending = false;
-            ids.push_back(e.i);
+        Csr P = h.jointDistributionCsr(h.pairwiseAffinitiesCsr(knn, perplexity));
+        {   // the working set's rows are P's non-empty rows (points without an entry drop out)
+            bool all = true;
+            for (size_t i = 0; i + 1 < P.row_ptr.size(); ++i) all = all && P.row_ptr[i + 1] > P.row_ptr[i];
+            if (!all) {
+                const std::vector<Triple> t = fromCsr(P);
+                std::vector<int32_t> ids;
+                for (const auto &e : t)
+                    if (ids.empty() || e.i != ids.back()) ids.push_back(e.i);
+                P = toCsr(t, &ids);
+            }
         }
-        if (!ascending) {
-            std::sort(ids.begin(), ids.end());
-            ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-        }
-        std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %zu)\n", now() - t2, joint.size());
-        WorkingSet ws = h.initWorkingSet(ids, (int32_t)nComponents, randomState);
+        std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %zu)\n", now() - t2, P.val.size());
+        WorkingSet ws = h.initWorkingSet(P.ids, (int32_t)nComponents, randomState);
         std::map<int32_t, double> loss;
         double t3 = now();
-        h.optimize(joint, ws, learningRate, (int32_t)iterations, metric, earlyExaggeration, initialMomentum,
-                   finalMomentum, theta, &loss);
+        h.optimizeCsr(P, ws, learningRate, (int32_t)iterations, metric, earlyExaggeration, initialMomentum,
+                      finalMomentum, theta, &loss);
         std::fprintf(stderr, "[tsne_hip] %ld iterations in %.3f s\n", iterations, now() - t3);
 
         {   // result.map(x => (x._1, x._2(0), x._2(1))).writeAsCsv (Tsne.scala:86);
