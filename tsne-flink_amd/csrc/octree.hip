@@ -416,6 +416,7 @@ constexpr int MOM3_CHUNK = 1024;    // points per moment item
 constexpr double MOM3_TOL = 1e-14;
 constexpr int MOM3_GROUP = 10;      // moments accumulated per pass over an item's points
 constexpr int MOM3_TASKS = 32;      // moment tiles recorded per query; more -> dense tiles
+constexpr int DENSE3_MAX = 2048;    // larger tiles only by moments (else traversed)
 
 struct M3Tab {
     int8_t a[MOM3_K], bx[MOM3_K], by[MOM3_K], bz[MOM3_K];
@@ -687,6 +688,10 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
             }
         }
         if (usem) act = false;
+        // a large tile the moments cannot take is declined: the lane keeps
+        // traversing it (the reference's own path), and its sub-tiles are
+        // taken further down -- by moments, or densely once small
+        if (tile && !usem && nd.cnt > DENSE3_MAX) tile = false;
         const bool dense = tile && !usem;
         if (__ballot(dense)) {
             // points staged through LDS 64 at a time, read back as broadcasts; the
