@@ -597,13 +597,14 @@ __device__ __forceinline__ void mom3_eval(const double *__restrict__ mu, double 
     fz += B2 * gz;
 }
 
+template <bool DBG>
 __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ pos, const int32_t *__restrict__ dupc,
                                                     const OctNode *__restrict__ nodes,
                                                     const int32_t *__restrict__ meta, double theta, double near_dmax,
                                                     int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
                                                     int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
                                                     int32_t *__restrict__ mtask_n, double *__restrict__ F,
-                                                    double *__restrict__ Z) {
+                                                    double *__restrict__ Z, unsigned long long *__restrict__ dbg) {
     __shared__ int32_t sref[4][STACK3];
     __shared__ uint64_t smask[4][STACK3];
     __shared__ double4 tbuf[4][64];
@@ -626,6 +627,7 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
     const bool mom_on = mom_flag[0] != 0;
     int nwant = 0;   // tiles whose moments this lane could take (the next build's gate)
     int ntask = 0;
+    unsigned long long d_pops = 0, d_childs = 0, d_dense = 0, d_declined = 0;   // TSNE_DEBUG_OCT counters
     if (root == ~0) {
         if (valid) { const double4 p = pos[0]; leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs); }
     } else if (root >= 0) {
@@ -691,8 +693,12 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
         // a large tile the moments cannot take is declined: the lane keeps
         // traversing it (the reference's own path), and its sub-tiles are
         // taken further down -- by moments, or densely once small
-        if (tile && !usem && nd.cnt > DENSE3_MAX) tile = false;
+        if (tile && !usem && nd.cnt > DENSE3_MAX) { tile = false; if (DBG) ++d_declined; }
         const bool dense = tile && !usem;
+        if (DBG) {
+            ++d_pops;
+            if (dense) d_dense += (unsigned long long)(nd.last - nd.first + 1);
+        }
         if (__ballot(dense)) {
             // points staged through LDS 64 at a time, read back as broadcasts; the
             // query's exact duplicates (itself included) add 1 each to z: taken off
@@ -727,6 +733,7 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
         }
         if (__ballot(act) == 0) continue;
         const int32_t chs[2] = {nd.left, nd.right};
+        if (DBG && act) d_childs += 2;
         // push order: right first, so the left (lower keys: earlier children) pops first
         int32_t push_ref[2];
         uint64_t push_mask[2] = {0ull, 0ull};
@@ -776,6 +783,17 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
     }
     // demand for the next build's moments (only until the gate's threshold:
     // one memory-side atomic per wave on one word would serialise n / 64 of them)
+    if (DBG) {   // [0] wave pops, [1] lane child evaluations, [2] lane dense tile points, [3] lane declined tiles, [4] moment tasks
+        const unsigned long long a = wave_sum(d_childs), b = wave_sum(d_dense), c = wave_sum(d_declined),
+                                 e = wave_sum((unsigned long long)ntask);
+        if (lane == 0) {
+            atomicAdd(dbg, d_pops);
+            atomicAdd(dbg + 1, a);
+            atomicAdd(dbg + 2, b);
+            atomicAdd(dbg + 3, c);
+            atomicAdd(dbg + 4, e);
+        }
+    }
     const int ww = wave_sum(nwant);
     if (lane == 0 && ww && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
         atomicAdd(&mom_flag[1], ww);
@@ -900,11 +918,31 @@ static double oct_near_dmax(double theta) {
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF, double *dz,
                    const int32_t *qlist) {
     if (s1 <= s0) return;
+    static const bool debug = getenv("TSNE_DEBUG_OCT") != nullptr;   // traversal counters on stderr (synchronises)
+    unsigned long long *dbg = nullptr;
+    if (debug) {
+        dbg = ctx->ws.get<unsigned long long>("oct.dbg", 8);
+        TSNE_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    }
     const int64_t waves = ceil_div(s1 - s0, 64);
-    hipLaunchKernelGGL(oct_traverse, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz);
+    if (debug)
+        hipLaunchKernelGGL(oct_traverse<true>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                           t.nodes, t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                           dF, dz, dbg);
+    else
+        hipLaunchKernelGGL(oct_traverse<false>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                           t.nodes, t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                           dF, dz, dbg);
     hipLaunchKernelGGL(oct_mom_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
+    if (debug) {
+        unsigned long long h[8];
+        TSNE_HIP(hipMemcpy(h, dbg, sizeof(h), hipMemcpyDeviceToHost));
+        const double q = (double)(s1 - s0);
+        fprintf(stderr, "[oct] queries=%lld pops/wave=%.1f child_evals/query=%.1f dense_pts/query=%.1f "
+                "declined/query=%.2f moment_tasks/query=%.2f\n", (long long)(s1 - s0), h[0] / (q / 64.0), h[1] / q,
+                h[2] / q, h[3] / q, h[4] / q);
+    }
     TSNE_LAUNCH_CHECK();
 }
 
