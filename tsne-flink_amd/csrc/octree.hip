@@ -415,7 +415,7 @@ constexpr int MOM3_MIN = 64;        // nodes of >= 64 points carry moments
 constexpr int MOM3_CHUNK = 1024;    // points per moment item
 constexpr double MOM3_TOL = 1e-14;
 constexpr int MOM3_GROUP = 10;      // moments accumulated per pass over an item's points
-constexpr int MOM3_TASKS = 32;      // moment tiles recorded per query; more -> dense tiles
+constexpr int MOM3_TASKS = 512;     // moment tiles recorded per query; more -> dense tiles
 constexpr int DENSE3_MAX = 2048;    // larger tiles only by moments (else traversed)
 
 struct M3Tab {
