@@ -1,10 +1,11 @@
 """Summarise a scripts/gpu_check.sh run (gpurun_out/) into profiles/:
 
   <tag>_rocprof_kernel_stats.csv     rocprofv3 --stats of `bench.py --steps K --warmup W` (whole schedule)
-  <tag>_attract_dispatches.json      attract_tiles / attract_rows (LOSS=true) dispatch durations from the kernel trace,
-                                     mapped to iterations (the k-th standalone launch after the warmup's is
-                                     t = 10 k), averaged over the timed window t <= K and the whole schedule
-  r02_attract_traffic.json           FETCH_SIZE / WRITE_SIZE per standalone launch in the window
+  <tag>_attract_dispatches.json      attract_tiles / attract_rows dispatch durations from the kernel trace: the
+                                     non-loss launches (roofline kernel; the k-th after the warmup's is the k-th
+                                     t with t % 10 != 0) and the loss launches (t = 10 k), averaged over the
+                                     timed window t <= K and the whole schedule
+  r02_attract_traffic.json           FETCH_SIZE / WRITE_SIZE per non-loss launch in the window
                                      (separate PMC passes of `bench.py --no-rest`), corrected by the
                                      calibration run (scripts/pmc_calib.hip)
 
@@ -27,18 +28,26 @@ def rows(p):
 
 
 def is_loss_attraction(name):
-    """The standalone (LOSS=true) attraction kernel: attract_tiles<true, MET> (the
+    """The loss (LOSS=true) attraction kernel: attract_tiles<true, MET> (the
     optimizer's tiled layout) or attract_rows<LPR, U, true, MET> (CSR rows)."""
     return ("attract_tiles<" in name or "attract_rows<" in name) and ", true," in name
 
 
+def is_plain_attraction(name):
+    """The non-loss attraction kernel (the roofline kernel): attract_tiles<false, MET>
+    or attract_rows<LPR, U, false, MET>."""
+    return ("attract_tiles<" in name or "attract_rows<" in name) and ", false," in name
+
+
 def kernel_label(name):
-    return "attract_tiles<LOSS=true>" if "attract_tiles<" in name else "attract_rows<64,4,LOSS=true>"
+    loss = ", true," in name
+    base = "attract_tiles<LOSS=%s>" if "attract_tiles<" in name else "attract_rows<64,4,LOSS=%s>"
+    return base % ("true" if loss else "false")
 
 
-def loss_dispatches(trace_rows):
-    """Dispatches of the standalone (LOSS=true) attraction kernel, in dispatch order."""
-    sel = [r for r in trace_rows if is_loss_attraction(r["Kernel_Name"])]
+def dispatches(trace_rows, pred):
+    """Dispatches of the selected attraction kernel, in dispatch order."""
+    sel = [r for r in trace_rows if pred(r["Kernel_Name"])]
     return sorted(sel, key=lambda r: int(r["Dispatch_Id"]))
 
 
@@ -50,31 +59,41 @@ def main():
     a = ap.parse_args()
     K, W = a.steps, a.warmup
     warm_loss = W // 10          # loss iterations inside the warmup (t = 10, 20, ... <= W)
+    warm_plain = W - warm_loss   # non-loss iterations inside the warmup
 
     shutil.copy(OUT / "prof" / "prof_kernel_stats.csv", PROF / f"{a.tag}_rocprof_kernel_stats.csv")
     tr = rows(OUT / "prof" / "prof_kernel_trace.csv")
-    ld = loss_dispatches(tr)[warm_loss:]
-    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in ld]
-    its = [10 * (k + 1) for k in range(len(durs))]
-    win = [d for t, d in zip(its, durs) if t <= K]
-    # the window's launches (t <= K) name the kernel of the roofline
-    label = kernel_label(ld[0]["Kernel_Name"]) if ld else "attract_rows<64,4,LOSS=true>"
+    dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+    # the roofline kernel: non-loss launches, iteration t = the k-th t with t % 10 != 0
+    pd = dispatches(tr, is_plain_attraction)[warm_plain:]
+    pits = [t for t in range(1, 100000) if t % 10][:len(pd)]
+    pdur = [dur(r) for r in pd]
+    pwin = [d for t, d in zip(pits, pdur) if t <= K]
+    ld = dispatches(tr, is_loss_attraction)[warm_loss:]
+    ldur = [dur(r) for r in ld]
+    lits = [10 * (k + 1) for k in range(len(ldur))]
+    lwin = [d for t, d in zip(lits, ldur) if t <= K]
+    label = kernel_label(pd[0]["Kernel_Name"]) if pd else "attract_rows<64,4,LOSS=false>"
     summary = {
         "source": "rocprofv3 --kernel-trace --stats -- python bench.py --steps %d --warmup %d --no-cpu-baseline "
                   "(scripts/gpu_check.sh); dispatches of %s after the warmup's" % (K, W, label),
-        "launches": len(durs),
-        "per_launch_ms": dict(zip(map(str, its), durs)),
-        "avg_ms_window": sum(win) / len(win) if win else None,
-        "avg_ms_whole_schedule": sum(durs) / len(durs) if durs else None,
+        "launches": len(pdur),
+        "avg_ms_window": sum(pwin) / len(pwin) if pwin else None,
+        "avg_ms_whole_schedule": sum(pdur) / len(pdur) if pdur else None,
+        "per_launch_ms_window": dict(zip(map(str, pits), pwin)),
+        "loss_launches": {"kernel": kernel_label(ld[0]["Kernel_Name"]) if ld else None,
+                          "avg_ms_window": sum(lwin) / len(lwin) if lwin else None,
+                          "avg_ms_whole_schedule": sum(ldur) / len(ldur) if ldur else None,
+                          "per_launch_ms": dict(zip(map(str, lits), ldur))},
     }
     (PROF / f"{a.tag}_attract_dispatches.json").write_text(json.dumps(summary, indent=1) + "\n")
 
-    # PMC: per standalone launch in the window (bench.py --no-rest: the window's launches only)
+    # PMC: per non-loss launch in the window (bench.py --no-rest: the window's launches only)
     def per_launch(kind, counter):
         rs = [r for r in rows(OUT / kind / "pmc_counter_collection.csv")
-              if is_loss_attraction(r["Kernel_Name"]) and r["Counter_Name"] == counter]
+              if is_plain_attraction(r["Kernel_Name"]) and r["Counter_Name"] == counter]
         rs.sort(key=lambda r: int(r["Dispatch_Id"]))
-        return [float(r["Counter_Value"]) * 1024.0 for r in rs[warm_loss:]]   # KiB -> bytes
+        return [float(r["Counter_Value"]) * 1024.0 for r in rs[warm_plain:]]   # KiB -> bytes
     fetch = per_launch("pmc_fetch", "FETCH_SIZE")
     write = per_launch("pmc_write", "WRITE_SIZE")
     # calibration: FETCH_SIZE of known-byte streams and gathers
@@ -111,7 +130,7 @@ def main():
     tj.setdefault("per_window", {})[f"steps{K}"] = {
         "fetch_bytes_raw": fetch, "write_bytes": write,
         "traffic_bytes": (corr * sum(fetch) / len(fetch) + sum(write) / len(write)) if fetch and write else None,
-        "note": f"window t=1..{K} (standalone launches t=10..{10 * len(fetch)}), FETCH_SIZE x2 (calibrated) + WRITE_SIZE",
+        "note": f"window t=1..{K} ({len(fetch)} non-loss launches), FETCH_SIZE x2 (calibrated) + WRITE_SIZE",
     }
     tf.write_text(json.dumps(tj, indent=1) + "\n")
     print(json.dumps(summary, indent=1))

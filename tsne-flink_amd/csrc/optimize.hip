@@ -149,6 +149,30 @@ __global__ void reduce_partial(const double *__restrict__ v, int64_t n, int stri
     if (threadIdx.x == 0) part[blockIdx.x] = (sw[0] + sw[1]) + (sw[2] + sw[3]);
 }
 
+// Sum of v[0 .. *np) into NPART block partials (reduce_partial with a device count).
+__global__ void reduce_partial_devn(const double *__restrict__ v, const int64_t *__restrict__ np,
+                                    double *__restrict__ part) {
+    __shared__ double sw[4];
+    const int64_t n = *np;
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        s += v[i];
+    s = wave_sum(s);
+    if (lane_id() == 0) sw[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = (sw[0] + sw[1]) + (sw[2] + sw[3]);
+}
+
+// Z-free KL terms: the kernels summed P ln(P (1 + metric)); the loss adds
+// ln(Z) sum p (p = ex P over this rank's owned entries, sum P in scal[6])
+// once Z is known.
+__global__ void loss_add_lnz(double *scal, double ex) {
+    if (threadIdx.x == 0) scal[1] += log(scal[0]) * (scal[6] * ex);
+}
+__global__ void set_unit(double *x) {
+    if (threadIdx.x == 0) *x = 1.0;
+}
+
 __global__ void reduce_final(const double *__restrict__ part, int np, double *__restrict__ out,
                              double scale_div) {
     __shared__ double sw[4];
@@ -1431,6 +1455,11 @@ static void build_own_rows(tsne_ctx *ctx, OptState *s) {
         hipLaunchKernelGGL(own_rows, dim3(ceil_div(m, 4)), dim3(256), 0, st, orig, s->lab, s->rp0, s->col0, s->val0,
                            s->L0, s->L1, s->rpw, s->colw, s->valw);
     TSNE_LAUNCH_CHECK();
+    // sum of the owned P entries (scal[6]) and Z = 1 (scal[7]) for the Z-free
+    // loss terms of an attraction launched before this iteration's Z
+    hipLaunchKernelGGL(reduce_partial_devn, dim3(NPART), dim3(256), 0, st, s->valw, s->rpw + m, s->part2);
+    hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 6, 0.0);
+    hipLaunchKernelGGL(set_unit, dim3(1), dim3(64), 0, st, s->scal + 7);
     build_attract_tiles(ctx, s);
 }
 
@@ -1638,10 +1667,12 @@ static void reduce_Z(tsne_ctx *ctx, OptState *s, const double *z) {
 }
 
 // loss of this iteration (all ranks' partial sums) into its slot
-static void record_loss(tsne_ctx *ctx, OptState *s, int32_t t, int64_t blocks) {
+static void record_loss(tsne_ctx *ctx, OptState *s, int32_t t, int64_t blocks, bool zfree = false,
+                        double ex = 1.0) {
     hipStream_t st = ctx->stream;
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
+    if (zfree) hipLaunchKernelGGL(loss_add_lnz, dim3(1), dim3(64), 0, st, s->scal, ex);
     if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
     const int slot = t / 10 - 1;
     if (slot >= 0 && slot < s->loss_slots) {
@@ -1836,14 +1867,19 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     }
     // attraction over this rank's rows (row pointer local to L0)
     AttractArgs aa{s->rpw - s->L0, s->colw, s->valw, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr, s->part};
-    // 0. attraction sums on the side stream (not in loss iterations: the KL
-    // terms need Z), concurrent with the BH traversal -- or, while the last
+    // 0. attraction sums on the side stream, concurrent with the BH
+    // traversal (in loss iterations with Z-free KL terms, P ln(P (1 + metric)):
+    // ln(Z) sum P is added once Z is known; TSNE_LOSS_ALONE=1 instead runs the
+    // loss launch after Z on the context stream) -- or, while the last
     // build took the root-tile path, already with the tree build, on 3 blocks
     // per CU (as fast as 8: miss-bound) so that the build's short kernels
     // keep the other slots.  A full build is not overlapped: its latency-bound
     // kernels stretch under the attraction (morton_keys 15 -> 800 us; whole
     // schedule 8.53 -> 8.97 s).  TSNE_OVERLAP=tree / after / bh forces a mode.
-    const bool overlap = !want_loss;
+    static const bool loss_alone = [] { const char *e = getenv("TSNE_LOSS_ALONE"); return e && e[0] == '1'; }();
+    const bool overlap = !want_loss || !loss_alone;
+    if (want_loss && overlap) aa.scal = s->scal + 7;   // Z = 1 in the kernel
+    int64_t blocks = 0;
     static const int ov_env = [] {
         const char *e = getenv("TSNE_OVERLAP");
         const std::string v = e ? e : "";
@@ -1858,10 +1894,10 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     auto side_attract = [&] {
         if (ov_mode != 2) side_wait();
         ctx->timers.begin("opt.attract", s->side);
-        attract_launch_opt(s->side, s, aa, false);
+        blocks = attract_launch_opt(s->side, s, aa, want_loss != 0);
         TSNE_LAUNCH_CHECK();
         ctx->timers.end("opt.attract", s->side);
-        s->attract_iter.push_back({t, 0});
+        s->attract_iter.push_back({t, want_loss ? 2 : 0});
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
     if (overlap && ov_mode == 0) side_attract();
@@ -1889,8 +1925,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
     reduce_Z(ctx, s, s->z);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
-    // 4. attraction (loss iterations: here, after Z) + update for owned rows
-    int64_t blocks = 0;
+    // 4. attraction (TSNE_LOSS_ALONE loss iterations: here, after Z) + update for owned rows
     if (overlap) {
         TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     } else {
@@ -1908,7 +1943,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int c = s->cur;
     combine_launch<1>(st, s->L0, s->L1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
                       s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
-    if (want_loss) record_loss(ctx, s, t, blocks);
+    if (want_loss) record_loss(ctx, s, t, blocks, overlap, ex);
     // 5. exchange (all-gather of the owned slices) + 6. centre
     if (fused_mean) {
         hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256), (double)n,
