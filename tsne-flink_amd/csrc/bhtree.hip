@@ -1217,6 +1217,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
     if (__ballot(valid) == 0) return;
     const long long t_start = COST ? clock64() : 0;
+    const unsigned long long w_start = STATS ? wall_clock64() : 0;
     int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next block orders
     const int root = meta[1];
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
@@ -1423,6 +1424,11 @@ __global__ __launch_bounds__(256) void bh_traverse(
             atomicMax(visits + 9, wtile);
             atomicAdd(visits + 13, wfull);
             atomicAdd(visits + 14, wpart);
+            const unsigned long long w_end = wall_clock64();   // [15] longest wave, [16] ~first start,
+            atomicMax(visits + 15, w_end - w_start);            // [17] last end, [18] sum of wave times
+            atomicMax(visits + 16, ~0ull - w_start);
+            atomicMax(visits + 17, w_end);
+            atomicAdd(visits + 18, w_end - w_start);
         }
     }
 }

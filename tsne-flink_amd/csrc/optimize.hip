@@ -1599,7 +1599,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 16);
+    s->visits = ws.get<unsigned long long>("opt.visits", 20);
     if (world > 1) {
         const int64_t nb = ceil_div(n, 256);
         s->qlist = ws.get<int32_t>("opt.qlist", n);
@@ -1701,7 +1701,7 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
         return;
     }
-    unsigned long long v[16] = {};
+    unsigned long long v[20] = {};
     TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
     for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
     static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
@@ -1709,6 +1709,10 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu "
                 "pops=%llu child_slots=%llu all_take_full=%llu all_take_partial=%llu\n", t,
                 v[10], v[11], v[12], v[1], v[2], v[3], v[6], v[13], v[14]);
+    if (dbg && v[17] > 0)   // traversal wave times (100 MHz wall clock): span of the grid vs its waves
+        fprintf(stderr, "[waves] t=%d span_us=%.1f max_wave_us=%.1f mean_wave_us=%.2f\n", t,
+                (double)(v[17] - (~0ull - v[16])) * 0.01, (double)v[15] * 0.01,
+                (double)v[18] * 0.01 / (double)std::max<int64_t>(1, ceil_div(s->L1 - s->L0, 64)));
 }
 
 // One iteration of the 3-D (octree) optimizer: labels are the original
@@ -1862,7 +1866,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int world = ctx->world;
     double *Y = s->Y[s->cur];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 16 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 20 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // attraction over this rank's rows (row pointer local to L0)
