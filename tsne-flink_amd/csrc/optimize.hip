@@ -1780,6 +1780,13 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     // row gathers all of Y, which sits in one XCD's L2 (n * 16 B <= 2 MiB)
     // whatever the labels, so a relabel (a copy of the whole P) buys nothing
     if (ctx->world == 1 && s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
+    // TSNE_RELABEL: 0 never, 1 by the locality score, 2 always; unset: by the
+    // score, except on one rank with the tiled layout, which keeps P's graph
+    // order (attract_tiles reads Y in label windows; a Morton relabel hands
+    // the attraction back to attract_rows: whole C3 schedule 7.23 -> 7.01 s
+    // without relabels, A/B on one box)
+    static const int mode = [] { const char *e = getenv("TSNE_RELABEL"); return e ? atoi(e) : -1; }();
+    if (mode == 0 || (mode == -1 && ctx->world == 1 && s->at_on)) return;
     // a fixed sample of rows, ~1 << 22 entries at most (dense rows: fewer rows)
     const int64_t avg = std::max<int64_t>(1, s->nnz / std::max<int64_t>(1, n));
     const int64_t nsamp = std::max<int64_t>(1, std::min<int64_t>({n, 1 << 16, (1 << 22) / avg}));
@@ -1792,8 +1799,7 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     TSNE_HIP(hipMemcpyAsync(sc, s->lscore, sizeof(sc), hipMemcpyDeviceToHost, st));
     TSNE_HIP(hipStreamSynchronize(st));
     ++s->relabel_checks;
-    static const int mode = [] { const char *e = getenv("TSNE_RELABEL"); return e ? atoi(e) : 1; }();   // 0 never, 2 always
-    const bool go = mode == 2 || (mode == 1 && sc[1] > sc[0]);
+    const bool go = mode == 2 || sc[1] > sc[0];
     if (!go) return;
     std::vector<int64_t> cuts = s->own;
     if (ctx->world > 1) {
@@ -1839,7 +1845,10 @@ static void attract_tiles_launch_l(hipStream_t st, const OptState *s, const Attr
 // concurrent launch vs 3.1 for attract_rows), and there the attraction is
 // hidden behind the traversal anyway.
 static int64_t attract_launch_opt(hipStream_t st, const OptState *s, const AttractArgs &a, bool loss) {
-    if (!s->at_on || !s->tree.root_tile) return attract_launch(st, a, loss);
+    // tiles in every phase while the labels are P's graph order
+    // (TSNE_AT_PHASE=root: only while the tree takes the root-tile path)
+    static const bool at_root = [] { const char *e = getenv("TSNE_AT_PHASE"); return e && std::string(e) == "root"; }();
+    if (!s->at_on || (!s->tree.root_tile && at_root)) return attract_launch(st, a, loss);
     if (loss) attract_tiles_launch_l<true>(st, s, a);
     else attract_tiles_launch_l<false>(st, s, a);
     return s->at_nrb;
