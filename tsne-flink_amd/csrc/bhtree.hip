@@ -1472,6 +1472,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     double qx = 0.0, qy = 0.0;
     if (valid) { const double2 q = pos[s]; qx = q.x; qy = q.y; }
     const bool mom_on = mom_flag[0] != 0;
+    const unsigned long long w_start = visits ? wall_clock64() : 0;
     double fx = 0.0, fy = 0.0, zs = 0.0;
     int nwant = 0, ntask = 0;
     unsigned long long ndense = 0;
@@ -1723,6 +1724,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             atomicAdd(visits + 12, wt_momchk);
             atomicAdd(visits + 1, tm);
             atomicAdd(visits + 2, td);
+            const unsigned long long w_end = wall_clock64();   // [19] longest wave, [20] ~first start,
+            atomicMax(visits + 19, w_end - w_start);            // [21] last end, [22] sum of wave times
+            atomicMax(visits + 20, ~0ull - w_start);
+            atomicMax(visits + 21, w_end);
+            atomicAdd(visits + 22, w_end - w_start);
         }
     }
 }

@@ -1599,7 +1599,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 20);
+    s->visits = ws.get<unsigned long long>("opt.visits", 24);
     if (world > 1) {
         const int64_t nb = ceil_div(n, 256);
         s->qlist = ws.get<int32_t>("opt.qlist", n);
@@ -1701,7 +1701,7 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
         return;
     }
-    unsigned long long v[20] = {};
+    unsigned long long v[24] = {};
     TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
     for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
     static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
@@ -1713,6 +1713,9 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         fprintf(stderr, "[waves] t=%d span_us=%.1f max_wave_us=%.1f mean_wave_us=%.2f\n", t,
                 (double)(v[17] - (~0ull - v[16])) * 0.01, (double)v[15] * 0.01,
                 (double)v[18] * 0.01 / (double)std::max<int64_t>(1, ceil_div(s->L1 - s->L0, 64)));
+    if (dbg && v[21] > 0)   // tile_apply waves (only waves with tiles report)
+        fprintf(stderr, "[twaves] t=%d span_us=%.1f max_wave_us=%.1f\n", t,
+                (double)(v[21] - (~0ull - v[20])) * 0.01, (double)v[19] * 0.01);
 }
 
 // One iteration of the 3-D (octree) optimizer: labels are the original
@@ -1875,7 +1878,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int world = ctx->world;
     double *Y = s->Y[s->cur];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 20 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 24 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // attraction over this rank's rows (row pointer local to L0)
