@@ -1000,29 +1000,104 @@ __device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, do
 // Moment tasks of each query (query slots [g0, g1): sorted positions, or
 // qlist[slot] when a rank computes a list of them), in traversal order, added
 // to the traversal's F and z.
+// Tile chunks (TSNE_TILE_CHUNK=0: off): a traversal wave whose tile cost
+// (points + 16 per task) exceeds 2x the mean (and 4096) has its tile list cut
+// into C contiguous index ranges, each a tile_apply wave of its own.  Chunk
+// slots write partial sums (Fp, Zp) and moment lists per slot lane;
+// chunk_combine adds them to F, Z in chunk order: deterministic.
+struct ChunkView {
+    const int32_t *slot_w = nullptr, *slot_c = nullptr, *nslots = nullptr;
+    double2 *Fp = nullptr;
+    double *Zp = nullptr;
+};
+constexpr int CHUNK_MAX = 32;
+constexpr int CHUNK_MIN = 4096;
+__global__ void chunk_total(const int32_t *__restrict__ tcost, int64_t waves, unsigned long long *__restrict__ total) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long c = w < waves ? (unsigned long long)max(tcost[w], 0) : 0ull;
+    const unsigned long long ws = wave_sum(c);
+    if (lane_id() == 0 && ws) atomicAdd(total, ws);
+}
+__global__ void chunk_parts(const int32_t *__restrict__ tcost, const unsigned long long *__restrict__ total,
+                            int64_t waves, int32_t *__restrict__ Cw) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w > waves) return;
+    if (w == waves) { Cw[w] = 0; return; }
+    const long long target = max((long long)CHUNK_MIN, (long long)(2 * (*total) / (unsigned long long)max<int64_t>(waves, 1)));
+    Cw[w] = 1 + (int32_t)min((long long)(CHUNK_MAX - 1), (long long)max(tcost[w], 0) / target);
+}
+__global__ void chunk_fill(const int32_t *__restrict__ Cw, const int32_t *__restrict__ slot0,
+                           const int32_t *__restrict__ tcost, int64_t waves, int32_t *__restrict__ slot_w,
+                           int32_t *__restrict__ slot_c, int32_t *__restrict__ scost, int64_t slots_max,
+                           int32_t *__restrict__ nslots) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w == waves) *nslots = slot0[waves];
+    if (w < waves) {
+        const int C = Cw[w];
+        for (int j = 0; j < C; ++j) {
+            slot_w[slot0[w] + j] = (int32_t)w;
+            slot_c[slot0[w] + j] = j | (C << 16);
+            scost[slot0[w] + j] = tcost[w] / C;
+        }
+    }
+    // slots past the plan: no work, lowest cost
+    for (int64_t k = slot0[waves] + w; w <= waves && k < slots_max; k += waves + 1) scost[k] = 0;
+}
+// F, Z of each query += its chunks' partial sums, in chunk order
+__global__ void chunk_combine(const double2 *__restrict__ Fp, const double *__restrict__ Zp,
+                              const int32_t *__restrict__ Cw, const int32_t *__restrict__ slot0, int64_t g0, int64_t g1,
+                              const int32_t *__restrict__ qlist, double2 *__restrict__ F, double *__restrict__ Z) {
+    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= g1) return;
+    const int64_t w = (k - g0) >> 6, lane = (k - g0) & 63;
+    const int64_t s = qlist ? (int64_t)qlist[k] : k;
+    const int64_t b = (int64_t)slot0[w] * 64 + lane;
+    double fx = 0.0, fy = 0.0, z = 0.0;
+    for (int j = 0; j < Cw[w]; ++j) {
+        const double2 g = Fp[b + 64 * j];
+        fx += g.x; fy += g.y;
+        z += Zp[b + 64 * j];
+    }
+    if (fx != 0.0 || fy != 0.0 || z != 0.0) {
+        const double2 f = F[s];
+        F[s] = make_double2(f.x + fx, f.y + fy);
+        Z[s] = Z[s] + z;
+    }
+}
+
 __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ pos,
                                                     const BHNode *__restrict__ nodes,
                                                     const double *__restrict__ mom,
                                                     const int32_t *__restrict__ mtask,
                                                     const int32_t *__restrict__ mtask_n, int64_t g0,
                                                     int64_t g1, const int32_t *__restrict__ qlist,
-                                                    double2 *__restrict__ F, double *__restrict__ Z) {
-    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                    double2 *__restrict__ F, double *__restrict__ Z,
+                                                    ChunkView cv) {
+    // entry = query slot, or (tile chunks) chunk slot lane with partial sums Fp / Zp
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t k = g0 + i;
+    if (cv.slot_w) {
+        if ((i >> 6) >= *cv.nslots) return;
+        k = g0 + (int64_t)cv.slot_w[i >> 6] * 64 + (i & 63);
+    }
     if (k >= g1) return;
     const int64_t s = qlist ? (int64_t)qlist[k] : k;
-    const int nt = mtask_n[s];
+    const int64_t e = cv.slot_w ? i : s;
+    const int nt = mtask_n[e];
     if (nt == 0) return;
     const double2 q = pos[s];
     double fx = 0.0, fy = 0.0, zs = 0.0;
-    for (int k = 0; k < nt; ++k) {
-        const int node = mtask[s * MOM_TASKS + k];
+    for (int t = 0; t < nt; ++t) {
+        const int node = mtask[e * MOM_TASKS + t];
         double cx, cy, R;
         box_centre(nodes[node], cx, cy, R);
         moment_eval(mom + (int64_t)node * MOM_K, q.x - cx, q.y - cy, fx, fy, zs);
     }
-    const double2 f = F[s];
-    F[s] = make_double2(f.x + fx, f.y + fy);
-    Z[s] = Z[s] + zs;
+    double2 *Fo = cv.slot_w ? cv.Fp : F;
+    double *Zo = cv.slot_w ? cv.Zp : Z;
+    const double2 f = Fo[e];
+    Fo[e] = make_double2(f.x + fx, f.y + fy);
+    Zo[e] = Zo[e] + zs;
 }
 
 // fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
@@ -1451,7 +1526,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                                                   int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
                                                   double2 *__restrict__ F, double *__restrict__ Z,
                                                   unsigned long long *__restrict__ visits, int qmajor, int pack,
-                                                  float lw_cost, const int32_t *__restrict__ torder) {
+                                                  float lw_cost, const int32_t *__restrict__ torder, ChunkView cv) {
     __shared__ double2 tbuf[4][64];
     __shared__ uint64_t sbm[4][64];
     __shared__ int smark[4][64];
@@ -1460,13 +1535,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     const int64_t blk = torder ? (int64_t)torder[blockIdx.x]
                       : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
-    if (g0 + wid * 64 >= g1) return;
-    const int64_t kq = g0 + wid * 64 + lane;
+    int64_t qw = wid;   // chunks: slot wid = chunk c of C of traversal wave qw's tile list
+    int ch = 0, C = 1;
+    if (cv.slot_w) {
+        if (wid >= *cv.nslots) return;
+        qw = cv.slot_w[wid];
+        const int32_t v = cv.slot_c[wid];
+        ch = v & 0xffff;
+        C = v >> 16;
+    }
+    if (g0 + qw * 64 >= g1) return;
+    const int64_t kq = g0 + qw * 64 + lane;
     const bool valid = kq < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
-    const int nt = ttask_n[wid];
-    if (nt == 0) {
-        if (valid) mtask_n[s] = 0;
+    const int64_t e = cv.slot_w ? wid * 64 + lane : s;   // moment list / partial-sum entry
+    const int ntw = ttask_n[qw];
+    const int tb = (int)((int64_t)ntw * ch / C), nt = (int)((int64_t)ntw * (ch + 1) / C);
+    if (nt == tb) {
+        if (valid) {
+            mtask_n[e] = 0;
+            if (cv.slot_w) { cv.Fp[e] = make_double2(0.0, 0.0); cv.Zp[e] = 0.0; }
+        }
         return;
     }
     double qx = 0.0, qy = 0.0;
@@ -1478,9 +1567,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     unsigned long long ndense = 0;
     unsigned long long wt_tasks = 0, wt_dense_pts = 0, wt_momchk = 0;   // wave-level diagnostics
     double2 *buf = tbuf[w];
-    const TileTask *mytt = ttask + wid * TILE_CAP;
-    int masked_until = 0;   // pack 2: tiles before this one take the masked sweep
-    for (int t = 0; t < nt;) {
+    const TileTask *mytt = ttask + qw * TILE_CAP;
+    int masked_until = tb;   // pack 2: tiles before this one take the masked sweep
+    for (int t = tb; t < nt;) {
         const TileTask tt = mytt[t];
         if (pack == 2 && t >= masked_until && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
             // Lane-wise window: the run of <= 64 consecutive small tiles
@@ -1637,7 +1726,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 ++nwant;
                 if (mom_on) {
                     usem = true;
-                    mtask[s * MOM_TASKS + ntask++] = ref;
+                    mtask[e * MOM_TASKS + ntask++] = ref;
                 }
             }
         }
@@ -1702,7 +1791,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             if (dense) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)(b - a + 1); }
         }
     }
-    if (valid) {
+    if (valid && cv.slot_w) {
+        mtask_n[e] = ntask;
+        cv.Fp[e] = make_double2(fx, fy);
+        cv.Zp[e] = zs;
+    } else if (valid) {
         mtask_n[s] = ntask;
         if (fx != 0.0 || fy != 0.0 || zs != 0.0) {
             const double2 f = F[s];
@@ -1974,9 +2067,11 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     const int32_t flag_init[3] = {1, INT32_MAX, (int32_t)std::min<int64_t>(INT32_MAX, (n >> 6) + 1)};   // first build: moments on
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
-    t.mtask = ws.get<int32_t>("bh.mtask", (size_t)n * MOM_TASKS);
-    t.mtask_n = ws.get<int32_t>("bh.mtask_n", n);
-    t.tile_waves = ceil_div(n, 64) + 4;
+    // tile_apply slots: traversal waves + at most half as many extra chunks (+ margin)
+    const int64_t qwaves = ceil_div(n, 64) + 4;
+    t.tile_waves = qwaves + qwaves / 2 + 64;
+    t.mtask = ws.get<int32_t>("bh.mtask", (size_t)std::max<int64_t>(n, t.tile_waves * 64) * MOM_TASKS);
+    t.mtask_n = ws.get<int32_t>("bh.mtask_n", std::max<int64_t>(n, t.tile_waves * 64));
     t.ttask = ws.get<TileTask>("bh.ttask", (size_t)t.tile_waves * TILE_CAP);
     t.ttask_n = ws.get<int32_t>("bh.ttask_n", t.tile_waves);
     size_t sb = 0;
@@ -2012,6 +2107,19 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.osort_tmp_bytes = ob;
     t.osort_tmp = ws.get<uint8_t>("bh.osort_tmp", ob);
     t.have_cost = false;
+    t.ch_C = ws.get<int32_t>("bh.ch_C", qwaves + 1);
+    t.ch_slot0 = ws.get<int32_t>("bh.ch_slot0", qwaves + 1);
+    t.ch_slot_w = ws.get<int32_t>("bh.ch_slot_w", t.tile_waves);
+    t.ch_slot_c = ws.get<int32_t>("bh.ch_slot_c", t.tile_waves);
+    t.ch_scost = ws.get<int32_t>("bh.ch_scost", t.tile_waves);
+    t.ch_nslots = ws.get<int32_t>("bh.ch_nslots", 1);
+    t.ch_total = ws.get<unsigned long long>("bh.ch_total", 1);
+    t.ch_Fp = ws.get<double2>("bh.ch_Fp", (size_t)t.tile_waves * 64);
+    t.ch_Zp = ws.get<double>("bh.ch_Zp", (size_t)t.tile_waves * 64);
+    size_t cb = 0;
+    TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cb, t.ch_C, t.ch_slot0, (int)(qwaves + 1), ctx->stream));
+    t.ch_scan_bytes = cb;
+    t.ch_scan_tmp = ws.get<uint8_t>("bh.ch_scan_tmp", cb);
 }
 
 // Cost-balanced query slices for the next iteration: one 1024-thread block
@@ -2206,15 +2314,39 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                        t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd,
                        (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost);
     t.have_cost = true;
+    // tile chunks of heavy waves (ChunkView; TSNE_TILE_CHUNK=0: one tile_apply wave per traversal wave)
+    static const bool chunk_on = [] { const char *e = getenv("TSNE_TILE_CHUNK"); return !(e && e[0] == '0'); }();
+    ChunkView cv;
+    int64_t tslots = waves;
+    const int32_t *tcost = t.tcost;
+    if (chunk_on) {
+        hipStream_t st = ctx->stream;
+        const int64_t wb = ceil_div(waves + 1, 256);
+        tslots = std::min<int64_t>(t.tile_waves, waves + waves / 2 + 64);
+        TSNE_HIP(hipMemsetAsync(t.ch_total, 0, sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(chunk_total, dim3(wb), dim3(256), 0, st, t.tcost, waves, t.ch_total);
+        hipLaunchKernelGGL(chunk_parts, dim3(wb), dim3(256), 0, st, t.tcost, t.ch_total, waves, t.ch_C);
+        size_t tb = t.ch_scan_bytes;
+        TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.ch_scan_tmp, tb, t.ch_C, t.ch_slot0, (int)(waves + 1), st));
+        hipLaunchKernelGGL(chunk_fill, dim3(wb), dim3(256), 0, st, t.ch_C, t.ch_slot0, t.tcost, waves, t.ch_slot_w,
+                           t.ch_slot_c, t.ch_scost, tslots, t.ch_nslots);
+        cv.slot_w = t.ch_slot_w; cv.slot_c = t.ch_slot_c; cv.nslots = t.ch_nslots;
+        cv.Fp = t.ch_Fp; cv.Zp = t.ch_Zp;
+        tcost = t.ch_scost;
+    }
+    const int64_t tblocks = ceil_div(tslots, 4);
     if (lpt_bits & 2) {
-        block_order(ctx, t, t.tcost, waves, nblocks, t.torder);
+        block_order(ctx, t, tcost, tslots, tblocks, t.torder);
         torder = t.torder;
     }
-    hipLaunchKernelGGL(tile_apply, dim3(nblocks), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
+    hipLaunchKernelGGL(tile_apply, dim3(tblocks), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.ttask, t.ttask_n, s0, s1, qlist, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor,
-                       pack, lw_cost, torder);
-    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
+                       pack, lw_cost, torder, cv);
+    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(cv.slot_w ? tslots * 64 : s1 - s0, 256)), dim3(256), 0,
+                       ctx->stream, t.pos, t.nodes, t.mom, t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
+    if (cv.slot_w)
+        hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.ch_Fp, t.ch_Zp,
+                           t.ch_C, t.ch_slot0, s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

@@ -125,6 +125,16 @@ struct BHTree {
     void *osort_tmp = nullptr;
     size_t osort_tmp_bytes = 0;
     bool have_cost = false;
+    // tile chunks (bhtree.hip ChunkView): chunks per traversal wave, first
+    // chunk slot (waves + 1), slot -> wave and chunk | C << 16, slot costs,
+    // slot count; partial sums per chunk slot lane
+    int32_t *ch_C = nullptr, *ch_slot0 = nullptr, *ch_slot_w = nullptr, *ch_slot_c = nullptr;
+    int32_t *ch_scost = nullptr, *ch_nslots = nullptr;
+    unsigned long long *ch_total = nullptr;
+    double2 *ch_Fp = nullptr;
+    double *ch_Zp = nullptr;
+    void *ch_scan_tmp = nullptr;
+    size_t ch_scan_bytes = 0;
 };
 
 // Allocate (from ctx->ws) for n points.
