@@ -54,16 +54,18 @@ def parse():
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: 1M x 128 GMM (the metric's workload); c5: 50,000-point precomputed distance matrix "
                          "(--inputDistanceMatrix: affinities + joint + optimizer, no kNN)")
-    ap.add_argument("--steps", type=int, default=20, help="timed iterations t=1..K (0 = the whole schedule T)")
-    ap.add_argument("--warmup", type=int, default=5, help="untimed, profiled iterations on a restored snapshot")
-    ap.add_argument("--no-rest", action="store_true", help="stop after the timed window (skip t = K+1..T)")
+    ap.add_argument("--steps", type=int, default=20,
+                    help="the timed schedule t=1..T as K steps of T/K iterations (0 = one step per iteration)")
+    ap.add_argument("--warmup", type=int, default=5,
+                    help="untimed warmup: the first W steps of the schedule on a restored snapshot")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=90)
     ap.add_argument("--perplexity", type=float, default=30.0)
     ap.add_argument("--theta", type=float, default=0.5)
     ap.add_argument("--iterations", type=int, default=1000, help="schedule length T")
-    ap.add_argument("--trace", type=int, default=50, help="profile every N-th timed iteration (0 = off)")
+    ap.add_argument("--trace", type=int, default=50,
+                    help="trace pass after the timed region: profile t=1..5 and every N-th iteration (0 = no pass)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
     ap.add_argument("--cpu-knn-sample", type=int, default=32, help="queries in the CPU baseline kNN sample")
@@ -102,8 +104,7 @@ def trace_entry(ctx, t, rows, Y, n):
     per_wave = max(1, rows / 64)
     return {"t": t, "tree_ms": ms_t[0], "bh_ms": ms_t[1], "exchange_ms": ms_t[2],
             "attract_ms": ms_t[3], "update_ms": ms_t[4],
-            "bh_interactions": vis_t[0],
-            "bh_interactions_per_s": vis_t[0] / (ms_t[1] * 1e-3) if ms_t[1] > 0 else None,
+            "pops": vis_t[3], "child_evals": vis_t[5], "dense_pairs": vis_t[2], "moment_evals": vis_t[1],
             "visits_per_point": vis_t[0] / max(1, rows),
             "moment_evals_per_point": vis_t[1] / max(1, rows),
             "dense_pairs_per_point": vis_t[2] / max(1, rows),
@@ -247,81 +248,85 @@ def main():
     sync_barrier(world)
     t_setup = max_over_ranks(time.perf_counter() - t0, world)
 
-    # ------------------------ warmup on a snapshot: profiled (t = 1..W of the window)
-    window_profile = []
-    snap_at = sorted({1, max(1, a.iterations // 10), max(1, a.iterations // 5), max(1, 2 * a.iterations // 5),
-                      a.iterations})
-    snaps = {}
-    want_snaps = rank == 0 and world == 1 and not a.no_cpu_baseline
-    for t in range(1, min(a.warmup, a.iterations) + 1):
-        ctx.dev_opt_profile(1)
+    # ---------- warmup on a snapshot: the first W steps of the schedule, untimed;
+    # inside it the pre-expansion window t = 1..20 is timed on its own (window_it_s)
+    chunks = [(a.iterations * (k - 1) // steps + 1, a.iterations * k // steps) for k in range(1, steps + 1)]
+    w_end = chunks[min(a.warmup, steps) - 1][1] if a.warmup > 0 else 0
+    win = min(20, a.iterations)
+    t_win = None
+    for t in range(1, w_end + 1):
+        if t == 1:
+            sync_barrier(world)
+            t0 = time.perf_counter()
         ctx.dev_opt_step(t)
-        window_profile.append(trace_entry(ctx, t, r1 - r0, Y, n))
-        if want_snaps and t in snap_at:
-            snaps[t] = Y[:n].cpu().numpy().copy()
+        if t == win:
+            sync_barrier(world)
+            t_win = max_over_ranks(time.perf_counter() - t0, world)
     torch.cuda.synchronize()
     Y.copy_(snap[0]); upd.copy_(snap[1]); gains.copy_(snap[2])
-    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)   # fresh loss slots and kernel logs
+    ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)   # fresh loss slots, kernel logs, labels
 
-    # ------------------------------------------- timed window: t = 1..K, nothing traced
+    # ------------- timed region: the whole schedule t = 1..T as K steps of T/K iterations
     sync_barrier(world)
     t0 = time.perf_counter()
-    for t in range(1, steps + 1):
-        ctx.dev_opt_step(t)
+    t_progress = t0
+    for (c0, c1) in chunks:
+        for t in range(c0, c1 + 1):
+            ctx.dev_opt_step(t)
+        if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
+            t_progress = time.perf_counter()
+            print(f"[bench] t={c1}/{a.iterations} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)
     sync_barrier(world)
-    t_window = max_over_ranks(time.perf_counter() - t0, world)
+    t_loop = max_over_ranks(time.perf_counter() - t0, world)
+    t0 = time.perf_counter()
+    losses = ctx.dev_opt_losses()
+    Y_final = Y[:n].cpu().numpy() if rank == 0 else None   # noqa: F841 (the D2H of the result, timed)
+    t_out = time.perf_counter() - t0
+    alog = ctx.dev_opt_attract_log()
+    upd_ms = ctx.stage_ms("opt.update")
 
-    # --------------------------- rest of the schedule: t = K+1..T, profiled every --trace
-    timeline = []
-    t_rest = 0.0
-    if not a.no_rest and steps < a.iterations:
-        sync_barrier(world)
-        t0 = time.perf_counter()
-        t_progress = t0
-        for t in range(steps + 1, a.iterations + 1):
-            traced = a.trace and t % a.trace == 0
+    # ------- trace pass (untimed): the same schedule again from the same state,
+    # profiled every --trace iterations (per-stage times, BH work counters),
+    # plus the CPU baseline's trajectory snapshots and --dump-y
+    window_profile, timeline, snaps = [], [], {}
+    snap_at = sorted({1, max(1, a.iterations // 10), max(1, a.iterations // 5), max(1, 2 * a.iterations // 5),
+                      a.iterations})
+    want_snaps = rank == 0 and world == 1 and not a.no_cpu_baseline
+    dumps = {int(v) for v in a.dump_y.split(",")} if a.dump_y else set()
+    if a.trace > 0 or want_snaps or dumps:
+        Y.copy_(snap[0]); upd.copy_(snap[1]); gains.copy_(snap[2])
+        ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)
+        for t in range(1, a.iterations + 1):
+            traced = a.trace > 0 and (t <= 5 or t % a.trace == 0)
             if traced:
                 ctx.dev_opt_profile(1)
             ctx.dev_opt_step(t)
             if traced:
-                timeline.append(trace_entry(ctx, t, r1 - r0, Y, n))
+                (window_profile if t <= 5 else timeline).append(trace_entry(ctx, t, r1 - r0, Y, n))
             if want_snaps and t in snap_at:
                 torch.cuda.synchronize()
                 snaps[t] = Y[:n].cpu().numpy().copy()
-            if rank == 0 and a.dump_y and t in {int(v) for v in a.dump_y.split(",")}:
+            if rank == 0 and t in dumps:
                 os.makedirs(a.dump_dir, exist_ok=True)
                 np.save(os.path.join(a.dump_dir, f"Y_t{t}.npy"), Y[:n].cpu().numpy())
-            if rank == 0 and time.perf_counter() - t_progress > 20.0:   # keep long runs visibly alive
-                t_progress = time.perf_counter()
-                print(f"[bench] t={t}/{a.iterations} elapsed {t_progress - t0:.1f}s", file=sys.stderr, flush=True)
-        sync_barrier(world)
-        t_rest = max_over_ranks(time.perf_counter() - t0, world)
-    done = a.iterations if (not a.no_rest) else steps
-    t0 = time.perf_counter()
-    losses = ctx.dev_opt_losses()
-    Y_final = Y[:n].cpu().numpy() if rank == 0 else None
-    t_out = time.perf_counter() - t0
+        torch.cuda.synchronize()
 
-    value = steps / t_window
-    # ---- roofline of the HBM-bound gradient kernel attract_rows (stage [3])
+    value = a.iterations / t_loop
+    # ---- roofline of the HBM-bound gradient kernel (the attraction, stage [3])
     # bytes per launch = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr
     #   + rows*(16 own Y + 16 attr out) + n*16 (gathered Y_j, counted once)
     rows = r1 - r0
     attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 32 + n * 16
-    alog = ctx.dev_opt_attract_log()
-    # log flags: 0 = non-loss launch (side stream, beside the tree build / BH),
-    # 1 = loss launch alone on the context stream (TSNE_LOSS_ALONE=1),
-    # 2 = loss launch on the side stream (Z-free KL terms)
-    win_conc = [ms for (t, sa, ms) in alog if sa == 0 and t <= steps]
-    all_conc = [ms for (t, sa, ms) in alog if sa == 0]
-    win_loss = [ms for (t, sa, ms) in alog if sa and t <= steps]
-    all_loss = [ms for (t, sa, ms) in alog if sa]
-    upd_ms = ctx.stage_ms("opt.update")
-    # the roofline kernel: the attraction launch of the non-loss iterations,
-    # the window's dominant kernel (K - K/10 of its K launches)
-    attr_ms = float(np.mean(win_conc)) if win_conc else (float(np.mean(all_conc)) if all_conc else None)
-    attr_src = ("t <= K (timed window)" if win_conc else "whole schedule (no non-loss iteration in the window)")
+    # log flags: 0 = non-loss launch on the side stream (beside the tree build / BH),
+    # 1 = launch alone on the context stream, 2 = loss launch on the side stream
+    # (Z-free KL terms), 3 = non-loss launch alone on the context stream
+    nonloss = [ms for (t, sa, ms) in alog if sa in (0, 3)]
+    loss_l = [ms for (t, sa, ms) in alog if sa in (1, 2)]
+    win_nl = [ms for (t, sa, ms) in alog if sa in (0, 3) and t <= win]
+    attr_ms = float(np.mean(nonloss)) if nonloss else None
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
+    placement = {0: "side stream beside the tree build / BH", 3: "context stream, alone"}
+    kinds = sorted({sa for (_, sa, _) in alog if sa in (0, 3)})
     # the optimizer's tiled layout (attract_tiles) unless disabled or the rows
     # are dense over a small embedding (the library's own rule, optimize.hip)
     dense_small = nnz // max(n, 1) > 1024 and n * 16 <= (2 << 20)
@@ -330,11 +335,20 @@ def main():
     knn_flops = 2.0 * (r1 - r0) * n * d
     knn_mode = "f32" if os.environ.get("TSNE_KNN_BF16", "1")[:1] == "0" else "bf16x3"
     upd_bytes = 128 * rows   # N*C*(5 reads + 3 writes)*8 B, C = 2
-    upd_win = upd_ms[:steps]
-    upd_avg = float(np.mean(upd_win)) if upd_win else None
-    bh_int = [e["bh_interactions"] for e in window_profile + timeline]
-    bh_ms = [e["bh_ms"] for e in window_profile + timeline]
-    t_loop_full = t_window + t_rest
+    upd_avg = float(np.mean(upd_ms)) if upd_ms else None
+    prof = window_profile + timeline
+    bh_ms_sum = sum(e["bh_ms"] for e in prof)
+
+    def bh_rate(key):
+        return sum(e[key] for e in prof) / (bh_ms_sum * 1e-3) if bh_ms_sum > 0 else None
+
+    workload = (f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, theta {a.theta}" if a.config == "c3"
+                else f"C5: {n}-point precomputed distance matrix ({n}x{n - 1} entries), perplexity {a.perplexity}, "
+                     f"theta {a.theta}")
+    workload += (f"; timed region = the reference's whole schedule t=1..{a.iterations} (TsneHelpers.scala:396-430) "
+                 f"as {steps} steps of {a.iterations // steps} iterations, value = T / loop seconds; the "
+                 f"pre-expansion window t=1..{win} (root-tile phase) is reported apart as window_it_s")
+    e2e = t_knn + t_aff + t_setup + t_loop + t_out
 
     out = {
         "metric": METRIC,
@@ -343,7 +357,7 @@ def main():
         "n_gpus": world,
         "steps": steps,
         "warmup": a.warmup,
-        "ms_per_step": 1e3 * t_window / steps,
+        "ms_per_step": 1e3 * t_loop / steps,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -352,18 +366,17 @@ def main():
                  if a.config == "c3" else
                  "full sqeuclidean distance matrix (diagonal excluded) of a synthetic 10-blob 64-D Gaussian "
                  "mixture (seed 4), seeded Y0 ~ N(0, 1e-4^2)"),
-        "config": {"workload": (f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, "
-                                f"theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}")
-                   if a.config == "c3" else
-                   (f"C5: {n}-point precomputed distance matrix ({n}x{n - 1} entries), perplexity "
-                    f"{a.perplexity}, theta {a.theta}, schedule T={a.iterations}, timed t=1..{steps}"),
-                   "n": n, "dim": d, "k": k, "theta": a.theta, "parallelism": f"rows{world}",
-                   "nnz_P": int(nnz)},
-        "window": f"t=1..{steps} of T={a.iterations}",
-        "full_schedule_it_s": (done / t_loop_full) if done == a.iterations else None,
-        "loop_full_s": t_loop_full if done == a.iterations else None,
-        "end_to_end_s": t_knn + t_aff + t_setup + t_loop_full + t_out,
-        "end_to_end_note": "kNN + affinities + joint + optimizer setup + every iteration run + D2H of Y and losses; "
+        "config": {"workload": workload, "n": n, "dim": d, "k": k, "theta": a.theta, "iterations": a.iterations,
+                   "parallelism": f"rows{world}", "nnz_P": int(nnz),
+                   "loop_full_s": t_loop, "full_schedule_it_s": value, "end_to_end_s": e2e,
+                   "window_it_s": (win / t_win) if t_win else None},
+        "loop_full_s": t_loop,
+        "full_schedule_it_s": value,
+        "window_it_s": (win / t_win) if t_win else None,
+        "window_note": f"t=1..{win}, timed inside the warmup from the same initial state: the root-tile phase, "
+                       "where the step is the attraction kernel's time; not the metric's workload",
+        "end_to_end_s": e2e,
+        "end_to_end_note": "kNN + affinities + joint + optimizer setup + the whole schedule + D2H of Y and losses; "
                            "input already in HBM (synthetic), CSV/loss-file formatting not included",
         "knn_s": t_knn,
         "knn_pts_per_s": n / t_knn if t_knn > 0 else None,
@@ -381,46 +394,51 @@ def main():
         "opt_setup_s": t_setup,
         "final_loss": losses.get(max(losses)) if losses else None,
         "losses_sampled": {str(t): losses[t] for t in sorted(losses) if t in (10, 20, 100, 200, 500, 1000)},
-        "roofline": {"kernel": attr_kernel + " (CSR attraction, TsneHelpers.scala:269-306): mean HIP-event time "
-                               "of its launches (every non-loss iteration, on the side stream it runs on, sharing "
-                               "the GPU with the tree build / BH) in " + attr_src,
+        "roofline": {"kernel": attr_kernel + " (CSR attraction, TsneHelpers.scala:269-306): mean HIP-event time of "
+                               "its non-loss launches over the timed region (the whole schedule), on the stream "
+                               "each ran on (" + "; ".join(placement[k_] for k_ in kinds) + ")",
                      "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
-                     "bytes_per_launch": attr_bytes, "avg_ms": attr_ms,
-                     "launches": len(win_conc) if win_conc else len(all_conc),
-                     "avg_ms_whole_schedule": float(np.mean(all_conc)) if all_conc else None,
+                     "bytes_per_launch": attr_bytes, "avg_ms": attr_ms, "launches": len(nonloss),
+                     "avg_ms_window": float(np.mean(win_nl)) if win_nl else None,
                      "loss_launch": {"kernel": attr_kernel.replace("LOSS=false", "LOSS=true") + " + KL terms",
-                                     "placement": "context stream after Z" if any(sa == 1 for (_, sa, _) in alog)
-                                     else "side stream (Z-free terms)",
-                                     "avg_ms_window": float(np.mean(win_loss)) if win_loss else None,
-                                     "avg_ms_whole_schedule": float(np.mean(all_loss)) if all_loss else None}},
+                                     "avg_ms": float(np.mean(loss_l)) if loss_l else None,
+                                     "launches": len(loss_l)}},
         "update_centre": {"kernels": "combine_update<1> (+ centring mean partials) + mean2_final + center_scatter",
                           "avg_ms": upd_avg, "bytes_per_iteration": upd_bytes,
                           "achieved_GBs": upd_bytes / (upd_avg * 1e-3) / 1e9 if upd_avg else None,
                           "frac": upd_bytes / (upd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if upd_avg else None},
-        "bh_interactions_per_s": (sum(bh_int) / (sum(bh_ms) * 1e-3)) if sum(bh_ms) > 0 else None,
-        "bh_interactions_note": "reference-equivalent node evaluations (device counter) / BH kernel time, over the "
-                                "profiled iterations (warmup t=1..W and every --trace-th of the rest)",
+        "bh": {"note": "Barnes-Hut repulsion (QuadTree.scala:123-152): fp64 VALU / latency bound, no HBM roofline "
+                       "(SURVEY 8d); executed work per second of BH kernel time over the traced iterations of the "
+                       "trace pass (t=1..5 and every --trace-th)",
+               "kernel_ms_traced": bh_ms_sum,
+               "pops_per_s": bh_rate("pops"), "lane_child_evals_per_s": bh_rate("child_evals"),
+               "dense_pair_terms_per_s": bh_rate("dense_pairs"), "moment_evals_per_s": bh_rate("moment_evals")},
         "window_profile": window_profile,
         "timeline": timeline,
     }
-    # HBM bytes per non-loss attraction launch in the same window, from
-    # committed PMC passes of this command (profiles/r02_attract_traffic.json)
-    tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02_attract_traffic.json")
-    if os.path.exists(tf) and n == 1_000_000 and d == 128 and world == 1:
-        with open(tf) as fh:
-            tj = json.load(fh)
-        key = f"steps{steps}"
-        if key in tj.get("per_window", {}):
-            out["roofline"]["traffic"] = tj["per_window"][key]["traffic_bytes"]
-            out["roofline"]["traffic_source"] = tj["source"] + "; " + tj["per_window"][key]["note"]
+    # HBM bytes per non-loss attraction launch over the same command's timed
+    # region, from committed PMC passes (profiles/r03_attract_traffic.json);
+    # BH VALU utilisation from committed PMC passes (profiles/r03_bh_valu.json)
+    here = os.path.dirname(os.path.abspath(__file__))
+    if n == 1_000_000 and d == 128 and world == 1 and a.config == "c3":
+        tf = os.path.join(here, "profiles", "r03_attract_traffic.json")
+        if os.path.exists(tf):
+            with open(tf) as fh:
+                tj = json.load(fh)
+            out["roofline"]["traffic"] = tj.get("traffic_bytes_per_launch")
+            out["roofline"]["traffic_source"] = tj.get("source")
+        pmc = os.path.join(here, "profiles", "r03_bh_valu.json")
+        if os.path.exists(pmc):
+            with open(pmc) as fh:
+                out["bh"]["valu_pmc"] = json.load(fh)
     if a.config == "c5":
         out["metric"] = "t-SNE iterations/sec at the 50k precomputed-distance-matrix config (C5); affinities+joint s"
         for key in ("knn_s", "knn_pts_per_s", "knn_filter_ms", "knn_mfma_tflops", "knn_mfma_frac_of_peak",
                     "knn_mfma_frac_whole_knn"):
             out.pop(key, None)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(snaps, a, n, steps, X_host, (orp, oc, ov))
+        out["cpu_baseline"] = cpu_baseline(snaps, a, n, X_host, (orp, oc, ov))
     if rank == 0 and a.locality:
         locality_report(Y[:n], orp, oc, n)
     if rank == 0:
@@ -458,7 +476,7 @@ def cpu_threads():
     return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
 
 
-def cpu_baseline(snaps, a, n, steps, X_host, P_dev):
+def cpu_baseline(snaps, a, n, X_host, P_dev):
     """The oracle (C fp64 restatement of the reference, OpenMP) timed on a
     bounded sample of the same run.  Optimizer: at embedding snapshots taken
     from the GPU trajectory (t in snaps), the reference quadtree build of all n
@@ -498,13 +516,13 @@ def cpu_baseline(snaps, a, n, steps, X_host, P_dev):
     def total(t_end):
         return sum(per_t[min(ts, key=lambda s: abs(s - it))] for it in range(1, t_end + 1))
 
-    out = {"value": steps / total(steps), "unit": "iterations/s", "cores": threads, "kind": "port",
-           "full_schedule_it_s": a.iterations / total(a.iterations),
+    out = {"value": a.iterations / total(a.iterations), "unit": "iterations/s", "cores": threads, "kind": "port",
+           "window_it_s": min(20, a.iterations) / total(min(20, a.iterations)),
            "per_iteration_s_at": {str(t): per_t[t] for t in ts},
            "sample": f"oracle (C fp64 reference restatement, OpenMP {threads} threads): at GPU-trajectory "
                      f"snapshots t={ts}, reference quadtree build of all {n} points + BH repulsion of {q} "
                      f"random queries extrapolated to {n}, + attraction/loss/update of {nr} rows (1 thread) "
-                     f"extrapolated; piecewise-constant over t=1..{steps} (value) and t=1..{a.iterations}"}
+                     f"extrapolated; piecewise-constant over t=1..{a.iterations} (value)"}
     if X_host is not None:
         qk = min(a.cpu_knn_sample, n)
         t0 = time.perf_counter()

@@ -15,8 +15,10 @@
  *     thread-local message.  No C++ exception crosses this boundary.
  *   - tsne_* functions take HOST buffers (caller-owned); tsne_dev_* take
  *     DEVICE buffers on the context's device and enqueue on its stream.
- * Numerics are fp64 everywhere except the kNN candidate filter, which runs on
- * fp32 MFMA with a rigorous error bound and an exact fp64 re-rank.
+ * Numerics are fp64 everywhere except the kNN candidate filter: a bf16x3
+ * split-precision MFMA pass (each fp32 coordinate as two bf16 parts, three
+ * bf16 products per term, fp32 accumulation) with a rigorous error bound,
+ * followed by an exact fp64 re-rank of the survivors.
  */
 #ifndef TSNE_HIP_H
 #define TSNE_HIP_H
@@ -94,8 +96,11 @@ int tsne_ctx_create(int32_t device, tsne_ctx **out);
  * single GPU, for testing).  On the returned handle tsne_knn splits the query
  * rows and tsne_optimize shards the rows of P and the BH queries over the
  * ranks, one host thread per rank, results written to the caller's buffers
- * once; every other host-buffer operator, and the tsne_dev_* calls, run on
- * the first device.  Destroy with tsne_ctx_destroy. */
+ * once; every other host-buffer operator, and the single-device tsne_dev_*
+ * calls (kNN, affinities, joint, repulsion), run on the first device.  The
+ * device-resident optimizer (tsne_dev_opt_*) holds one rank's state and
+ * returns TSNE_ERR_UNSUPPORTED on a handle of ndev > 1: use tsne_optimize
+ * there, or one context per rank.  Destroy with tsne_ctx_destroy. */
 int tsne_ctx_create_multi(const int32_t *devices, int32_t ndev, tsne_ctx **out);
 int tsne_ctx_destroy(tsne_ctx *ctx);
 /* Enqueue on a caller-owned hipStream_t (e.g. torch's current stream). NULL = own stream. */
@@ -247,11 +252,16 @@ int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t);
 int tsne_dev_opt_sync(tsne_ctx *ctx);
 int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap,
                         int32_t *n_loss);
+/* The Z normaliser (sum of the BH sumQ over all points, TsneHelpers.scala:266)
+ * of the last tsne_dev_opt_step: the value its gradient and loss used.
+ * Synchronises the context stream. */
+int tsne_dev_opt_last_z(tsne_ctx *ctx, double *z_out);
 /* Per-stage timing of the last step (HIP events on the ctx stream), in ms:
- * [0] tree build, [1] BH repulsion kernel, [2] (F, z) exchange + Z reduce,
- * [3] attraction kernel (attract_rows, timed on the stream it runs on: outside
- * loss iterations a second stream concurrent with [0]-[2]), [4] wait for it,
- * combine + update, loss, embedding exchange, centring.
+ * [0] tree build, [1] BH repulsion (traversal + tile and moment kernels),
+ * [2] Z reduce (+ its all-reduce with several ranks), [3] attraction kernel
+ * (attract_tiles / attract_rows, timed on the stream it runs on -- a side
+ * stream when it overlaps [0]-[2]), [4] wait for it, combine + update, loss,
+ * embedding exchange, centring.
  * Also BH work counters of the last step (counters_out5, may be NULL):
  * [0] reference-equivalent node evaluations (lane visits; a leaf tile of m
  * points counts m), [1] subtree-moment evaluations, [2] dense pair terms,
@@ -262,11 +272,12 @@ int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, in
  * enable: 1 on, 0 off, -1 leave unchanged. */
 int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out10);
 /* Kernel time of every attraction launch since tsne_dev_opt_setup (HIP
- * events on the stream it ran on): its iteration t, standalone = 1 when it
- * ran alone on the context stream (loss iterations, t % 10 == 0), 0 when on
- * the side stream concurrently with the BH traversal; ms.  Synchronises on
- * the recorded events; *count = number of launches (entries beyond cap are
- * not written). */
+ * events on the stream it ran on): its iteration t, a placement code
+ * (0 non-loss launch on the side stream, concurrent with the tree build / BH
+ * traversal; 1 loss launch alone on the context stream after Z; 2 loss launch
+ * on the side stream with Z-free KL terms; 3 non-loss launch alone on the
+ * context stream), ms.  Synchronises on the recorded events; *count = number
+ * of launches kept (the last 16384; entries beyond cap are not written). */
 int tsne_dev_opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap,
                              int32_t *count);
 /* Stage timers of the context (HIP events around the stage's kernels, on

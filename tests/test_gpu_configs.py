@@ -137,25 +137,88 @@ def pipeline(ctx, Xd, k, metric, perplexity):
     return host, (orp, oc[:nnz], ov[:nnz])
 
 
-def run_schedule(ctx, Pd, n, c, params, snaps, seed=0, stop=None):
+def run_schedule(ctx, Pd, n, c, params, snaps, seed=0, stop=None, steps=(), Y0=None):
     """The device optimizer over the real schedule; host copies of Y after the
-    iterations in `snaps`."""
+    iterations in `snaps`, and for every t in `steps` the optimizer's whole
+    state (Y, upd, gains; original order, via tsne_dev_opt_sync) before and
+    after its own step t."""
     dev = Pd[0].device
     Yh, uh, gh = ctx.initWorkingSet(n, c, seed=seed)
+    if Y0 is not None:
+        Yh = Y0.copy()
     Y = torch.from_numpy(Yh).to(dev)
     u = torch.from_numpy(uh).to(dev)
     g = torch.from_numpy(gh).to(dev)
     ctx.dev_opt_setup(params, *Pd, n, Y, u, g)
-    out = {}
+
+    def state():
+        ctx.dev_opt_sync()
+        ctx.synchronize()
+        return tuple(x.cpu().numpy().copy() for x in (Y, u, g))
+
+    out, st = {}, {}
     for t in range(1, (stop or params.iterations) + 1):
+        before = state() if t in steps else None
         ctx.dev_opt_step(t)
+        if t in steps:
+            st[t] = (before, state(), ctx.dev_opt_last_z())
         if t in snaps:
             ctx.synchronize()
             out[t] = Y.cpu().numpy().copy()
-    return out, ctx.dev_opt_losses()
+    return out, ctx.dev_opt_losses(), st
 
 
-def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, grad_rows, q0, stop=None):
+def momentum(t, T_):
+    return 0.5 if t <= min(T_, 20) else 0.8
+
+
+def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, loss_gpu=None, lr=1000.0):
+    """The optimizer's OWN iteration t (attract_tiles / attract_rows, the
+    Z-free loss terms, combine_update, centring -- tsne_dev_opt_step) against
+    the oracle from the same state: TsneHelpers.scala:269-317 (gradient),
+    :341-369 (updateEmbedding), :320-329 (centerEmbedding).
+      * the step's gradient of rows [r0, r0+nr), recovered exactly from its
+        momentum update u' = mom u - lr gain' grad, within 1e-4 x max|grad|
+        (north_star) of the oracle's attraction + BH repulsion with the same Z;
+      * the gains (the reference's sign rule; a sign may differ only where
+        |grad| is inside the tolerance);
+      * the new Y: Y' + mean = the oracle's uncentred update, i.e. the offset
+        is one vector over the rows, and Y' is centred;
+      * the loss of iteration t (t % 10 == 0) against the oracle's KL over
+        every row of P with the same Z, at 1e-9.
+    Z is the step's own BH normaliser (tsne_dev_opt_last_z); it must equal the
+    sum of the per-point z of the same state (tsne_repulsion, whose sampled
+    rows are checked against the oracle) to BH_NEAR_TOL."""
+    Y0, u0, g0 = before
+    Y1, u1, g1 = after
+    n = Y0.shape[0]
+    ex, mom = exaggeration(t, T_), momentum(t, T_)
+    _, z = ctx.repulsion(Y0, theta)
+    assert abs(z.sum() - Z) <= NEAR_TOL * Z, (t, "Z", Z, z.sum())
+    Q = np.ascontiguousarray(Y0[r0:r0 + nr])
+    rep_o, z_o = (O.repulsion_queries if c == 2 else O.repulsion3_queries)(Y0, theta, Q, threads=THREADS)
+    assert np.abs(z[r0:r0 + nr] - z_o).max() <= NEAR_TOL * z_o.max(), (t, "per-point z")
+    rep = np.zeros((n, c))
+    rep[r0:r0 + nr] = rep_o
+    attr = O.attraction_rows if c == 2 else O.attraction3_rows
+    g_o, _ = attr(*P, Y0, rep, Z, r0, r0 + nr, metric=metric, exaggeration=ex)
+    rows = slice(r0, r0 + nr)
+    tol = 1e-4 * np.abs(g_o).max()
+    grad = (mom * u0[rows] - u1[rows]) / (lr * g1[rows])
+    assert np.abs(grad - g_o).max() <= tol, (t, np.abs(grad - g_o).max(), tol)
+    Yn, un, gn = (np.ascontiguousarray(x[rows]) for x in (Y0, u0, g0))
+    O.update(np.ascontiguousarray(g_o), Yn, un, gn, 0.01, mom, lr)
+    assert ((gn == g1[rows]) | (np.abs(g_o) <= tol)).all(), (t, "gains")
+    off = Yn - Y1[rows]
+    spread = np.abs(off - off.mean(0)).max()
+    assert spread <= 2.0 * lr * g1[rows].max() * tol + 1e-12 * np.abs(Yn).max(), (t, spread)
+    assert np.abs(Y1.mean(0)).max() <= 1e-9 * np.abs(Y1).max(), (t, "centred")
+    if loss_gpu is not None:
+        _, l_o = attr(*P, Y0, np.zeros((n, c)), Z, 0, n, metric=metric, exaggeration=ex, want_loss=True)
+        assert abs(loss_gpu - l_o) <= 1e-9 * abs(l_o), (t, loss_gpu, l_o)
+
+
+def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, grad_rows, q0, stop=None, steps=()):
     n = Xd.shape[0]
     host, Pd = pipeline(ctx, Xd, k, metric, perplexity)
     check_knn_rows(X_host, host["idx"], host["dist"], k, metric, q0)
@@ -164,11 +227,14 @@ def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, gra
     check_joint_rows(host["idx"], host["p"], *host["P"], rows[:16])
     del host["idx"], host["dist"], host["p"]
     params = default_params(iterations=T_, theta=theta, metric=metric, n_components=c)
-    Ys, losses = run_schedule(ctx, Pd, n, c, params, set(snaps), stop=stop)
+    Ys, losses, st = run_schedule(ctx, Pd, n, c, params, set(snaps), stop=stop, steps=set(steps))
     for t, nr in snaps.items():
         r0 = grad_rows
         check_gradient_snapshot(ctx, host["P"], Ys[t], theta, exaggeration(t + 1, T_), metric, r0, nr, c=c,
                                 loss=(t == max(snaps)))
+    for t in sorted(steps):   # the optimizer's own step at config size
+        check_opt_step(ctx, host["P"], *st[t], t, T_, theta, metric, grad_rows + 64, 64, c=c,
+                       loss_gpu=losses.get(t))
     return losses
 
 
@@ -231,7 +297,8 @@ def test_c2_mnist_shaped_full_size(ctx):
     X = CF.c2()
     Xd = torch.from_numpy(X).cuda()
     losses = full_config(ctx, Xd, X, 90, "sqeuclidean", 30.0, 0.5, 1000, 2,
-                         snaps={1: 32, 100: 64, 300: 64, 1000: 64}, grad_rows=40_000, q0=12_345)
+                         snaps={1: 32, 100: 64, 300: 64, 1000: 64}, grad_rows=40_000, q0=12_345,
+                         steps=(300, 1000))
     assert sorted(losses) == list(range(10, 1001, 10))
     assert all(np.isfinite(v) for v in losses.values())
 
@@ -241,7 +308,8 @@ def test_c3_gmm_1m_full_size(ctx):
     Xd = CF.c3_torch()
     X = Xd.cpu().numpy()
     losses = full_config(ctx, Xd, X, 90, "sqeuclidean", 30.0, 0.5, 1000, 2,
-                         snaps={1: 16, 200: 64, 400: 64, 1000: 64}, grad_rows=654_321, q0=123_456)
+                         snaps={1: 16, 200: 64, 400: 64, 1000: 64}, grad_rows=654_321, q0=123_456,
+                         steps=(1, 200, 400, 1000))
     assert sorted(losses) == list(range(10, 1001, 10))
     assert all(np.isfinite(v) for v in losses.values())
 
@@ -250,8 +318,8 @@ def test_c3_gmm_1m_full_size(ctx):
 def test_c4_sparse_cosine_3d_full_size(ctx):
     X = CF.c4()
     Xd = torch.from_numpy(X).cuda()
-    full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 3: 16}, grad_rows=250_000,
-                q0=77_777, stop=3)
+    full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 150: 32}, grad_rows=250_000,
+                q0=77_777, stop=300, steps=(1, 120, 150, 300))
 
 
 # ------------------------------------------------------------------- C5
@@ -327,3 +395,72 @@ def test_c5_distance_matrix_5k_matches_oracle(ctx):
     _, _, kg = ctx.gradient(*S, Y.cpu().numpy(), 0.5, want_loss=True)
     _, _, ko = ctx.gradient(*S, Yo, 0.5, want_loss=True)
     assert abs(kg - ko) <= 0.01 * abs(ko), (kg, ko)
+
+
+def test_c5_distance_matrix_50k_full_size(ctx):
+    """C5 at its stated size (BASELINE configs[4]): the full 50,000 x 49,999
+    sqeuclidean matrix of a 64-D GMM (2.5e9 entries, built on the device like
+    bench.py --config c5) through affinities, joint and the device optimizer.
+    Sampled affinity rows at 1e-12 and joint rows (pattern exact, values
+    1e-13 relative) against the oracle / a restatement of jointDistribution;
+    the optimizer's own step at t = 1 and t = 60 (check_opt_step: gradient
+    rows at 1e-4 x max|grad|, gains, centred update); the loss keys with the
+    reference's NaN (0 ln 0 of underflowed affinities, TsneHelpers.scala:300)."""
+    n, d, T_ = 50_000, 64, 60
+    m = n - 1
+    dev = torch.device("cuda", 0)
+    Xd = torch.from_numpy(CF.c5_points(n, d, 4)).to(dev)
+    sq = (Xd * Xd).sum(1)
+    dist = torch.empty((n, m), dtype=torch.float64, device=dev)
+    col = torch.empty((n, m), dtype=torch.int32, device=dev)
+    ar = torch.arange(n, device=dev, dtype=torch.int32)
+    for b0 in range(0, n, 1024):
+        b1 = min(n, b0 + 1024)
+        D = (sq[b0:b1, None] + sq[None, :] - 2.0 * (Xd[b0:b1] @ Xd.T)).clamp_(min=0.0)
+        keep = torch.ones((b1 - b0, n), dtype=torch.bool, device=dev)
+        keep[torch.arange(b1 - b0, device=dev), torch.arange(b0, b1, device=dev)] = False
+        dist[b0:b1] = D[keep].view(b1 - b0, m)
+        col[b0:b1] = ar.expand(b1 - b0, n)[keep].view(b1 - b0, m)
+        del D, keep
+    rp = torch.arange(0, n * m + 1, m, dtype=torch.int64, device=dev)
+    p = torch.empty_like(dist)
+    ctx.dev_affinities(rp, dist, n, 30.0, p)
+    ctx.synchronize()
+    sample = [0, 1, 12_345, 31_337, n - 1]
+    for i in sample:   # workgroup-per-row beta search over 49,999 entries
+        po, _ = O.affinities(np.array([0, m], dtype=np.int64), dist[i].cpu().numpy(), 30.0)
+        assert np.abs(p[i].cpu().numpy() - po).max() <= 1e-12, i
+    del dist
+    cap = n * m
+    orp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    oc = torch.empty(cap, dtype=torch.int32, device=dev)
+    ov = torch.empty(cap, dtype=torch.float64, device=dev)
+    nnz = ctx.dev_joint(rp, col, p, n, cap, orp, oc, ov)
+    assert nnz == n * m
+    tot = 2.0 * p.sum().item()
+    jrows = torch.arange(n, device=dev)
+    for i in sample[:3]:   # P_ij = (p_j|i + p_i|j) / sum J over the union (all mutual here)
+        others = jrows[jrows != i]
+        pos = torch.where(others > i, torch.full_like(others, i), torch.full_like(others, i - 1))
+        want = ((p[i] + p[others, pos]) / tot).cpu().numpy()
+        a, b = int(orp[i].item()), int(orp[i + 1].item())
+        assert np.array_equal(oc[a:b].cpu().numpy(), others.cpu().numpy().astype(np.int32)), i
+        got = ov[a:b].cpu().numpy()
+        assert np.all(np.abs(got - want) <= 1e-13 * want), i
+    underflow = bool((ov == 0).any().item())
+    del col, p
+    torch.cuda.empty_cache()
+    Pd = (orp, oc, ov)
+    params = default_params(iterations=T_, theta=0.5)
+    r0, nr = 20_000, 32
+    _, losses, st = run_schedule(ctx, Pd, n, 2, params, set(), seed=4, steps={1, 60})
+    # the sampled rows of P on the host (the oracle's attraction reads rows [r0, r0 + nr) only)
+    a, b = int(orp[r0].item()), int(orp[r0 + nr].item())
+    rps = np.clip(orp.cpu().numpy() - a, 0, b - a)
+    Ps = (rps, oc[a:b].cpu().numpy(), ov[a:b].cpu().numpy())
+    for t in (1, 60):
+        check_opt_step(ctx, Ps, *st[t], t, T_, 0.5, "sqeuclidean", r0, nr)
+    assert sorted(losses) == list(range(10, T_ + 1, 10))
+    assert all(np.isnan(losses[t]) == underflow for t in losses)
+    del Pd, orp, oc, ov
+    torch.cuda.empty_cache()

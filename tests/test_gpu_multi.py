@@ -115,6 +115,30 @@ def test_multi_rejects_mixed_devices():
     assert e.value.status == -1
 
 
+def test_multi_handle_refuses_device_optimizer():
+    """tsne_dev_opt_* hold one rank's state: on a handle of two loopback ranks
+    they fail with TSNE_ERR_UNSUPPORTED instead of rank 0 waiting forever in
+    a collective for a rank that never calls in (tsne_optimize is the
+    multi-rank form)."""
+    n = 256
+    rng = np.random.default_rng(3)
+    rp = np.arange(0, n * 4 + 1, 4, dtype=np.int64)
+    dev = torch.device("cuda", 0)
+    Pd = (torch.from_numpy(rp).to(dev), torch.from_numpy(rng.integers(0, n, n * 4).astype(np.int32)).to(dev),
+          torch.full((n * 4,), 1.0 / (n * 4), dtype=torch.float64, device=dev))
+    Y = torch.from_numpy(rng.normal(size=(n, 2)) * 1e-4).to(dev)
+    m = T.Context.multi([0, 0])
+    try:
+        with pytest.raises(T.TsneError) as e:
+            m.dev_opt_setup(default_params(iterations=10), *Pd, n, Y, torch.zeros_like(Y), torch.ones_like(Y))
+        assert e.value.status == -4
+        with pytest.raises(T.TsneError) as e:
+            m.dev_opt_step(1)
+        assert e.value.status == -4
+    finally:
+        m.close()
+
+
 # ------------------------------------------ caller-supplied collectives (gloo)
 def _free_port():
     s = socket.socket()

@@ -1023,16 +1023,28 @@ __global__ void chunk_parts(const int32_t *__restrict__ tcost, const unsigned lo
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w > waves) return;
     if (w == waves) { Cw[w] = 0; return; }
-    const long long target = max((long long)CHUNK_MIN, (long long)(2 * (*total) / (unsigned long long)max<int64_t>(waves, 1)));
+    // ceil(2 total / waves): the extra chunks sum to <= total / target <= waves / 2,
+    // inside the slot capacity (waves + waves / 2 + 64, bh_alloc)
+    const unsigned long long W = (unsigned long long)max<int64_t>(waves, 1);
+    const long long target = max((long long)CHUNK_MIN, (long long)((2 * (*total) + W - 1) / W));
     Cw[w] = 1 + (int32_t)min((long long)(CHUNK_MAX - 1), (long long)max(tcost[w], 0) / target);
 }
-__global__ void chunk_fill(const int32_t *__restrict__ Cw, const int32_t *__restrict__ slot0,
+__global__ void chunk_fill(int32_t *__restrict__ Cw, int32_t *__restrict__ slot0,
                            const int32_t *__restrict__ tcost, int64_t waves, int32_t *__restrict__ slot_w,
                            int32_t *__restrict__ slot_c, int32_t *__restrict__ scost, int64_t slots_max,
                            int32_t *__restrict__ nslots) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w == waves) *nslots = slot0[waves];
-    if (w < waves) {
+    // the plan fits by construction (chunk_parts); should it not, every wave
+    // falls back to one slot (C = 1) rather than a chunk being dropped
+    const bool fits = slot0[waves] <= slots_max;
+    if (w == waves) *nslots = fits ? slot0[waves] : (int32_t)waves;
+    if (w < waves && !fits) {
+        Cw[w] = 1;
+        slot0[w] = (int32_t)w;
+        slot_w[w] = (int32_t)w;
+        slot_c[w] = 1 << 16;
+        scost[w] = tcost[w];
+    } else if (w < waves) {
         const int C = Cw[w];
         for (int j = 0; j < C; ++j) {
             slot_w[slot0[w] + j] = (int32_t)w;
@@ -1041,7 +1053,7 @@ __global__ void chunk_fill(const int32_t *__restrict__ Cw, const int32_t *__rest
         }
     }
     // slots past the plan: no work, lowest cost
-    for (int64_t k = slot0[waves] + w; w <= waves && k < slots_max; k += waves + 1) scost[k] = 0;
+    for (int64_t k = (fits ? slot0[waves] : waves) + w; w <= waves && k < slots_max; k += waves + 1) scost[k] = 0;
 }
 // F, Z of each query += its chunks' partial sums, in chunk order
 __global__ void chunk_combine(const double2 *__restrict__ Fp, const double *__restrict__ Zp,

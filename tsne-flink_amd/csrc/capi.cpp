@@ -43,6 +43,17 @@ static void check_ctx(tsne_ctx *ctx) {
 // Single-device operators on a group handle run on its first rank.
 static tsne_ctx *primary(tsne_ctx *ctx) { return ctx->group.empty() ? ctx : ctx->group[0]; }
 
+// The device-resident optimizer (tsne_dev_opt_*) is one rank's state: on a
+// tsne_ctx_create_multi handle of several ranks its first context is rank 0 of
+// a world > 1 communicator, whose collectives would wait for ranks that never
+// call in.  Such handles run the optimizer through tsne_optimize (every rank
+// on its own thread); the device form is refused.
+static tsne_ctx *opt_ctx(tsne_ctx *ctx) {
+    if (ctx->group.size() > 1)
+        fail(TSNE_ERR_UNSUPPORTED, "tsne_dev_opt_* on a multi-rank handle: use tsne_optimize, or one context per rank");
+    return primary(ctx);
+}
+
 // Run fn(rank context, rank) on every rank of a group, one host thread each
 // (device made current per thread); the first failure is rethrown here after
 // the other ranks were released (loopback barrier abort) and joined.
@@ -57,7 +68,9 @@ template <class Fn> static void run_group(tsne_ctx *g, Fn &&fn) {
                 fn(g->group[r], r);
             } catch (...) {
                 err[r] = std::current_exception();
-                comm_abort(g->group[r]);
+                // release every rank: a loopback barrier, or the peers' RCCL
+                // collectives still waiting for this rank (ncclCommAbort)
+                for (tsne_ctx *c : g->group) comm_abort(c);
             }
         });
     for (auto &t : th) t.join();
@@ -358,7 +371,7 @@ int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *
                        double *d_upd, double *d_gains) {
     return guard([&] {
         check_ctx(ctx);
-        ctx = primary(ctx);
+        ctx = opt_ctx(ctx);
         DeviceGuard g(ctx->device);
         opt_setup(ctx, params, d_row_ptr, d_col, d_P, n, d_Y, d_upd, d_gains);
     });
@@ -367,7 +380,7 @@ int tsne_dev_opt_setup(tsne_ctx *ctx, const tsne_params *params, const int64_t *
 int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t) {
     return guard([&] {
         check_ctx(ctx);
-        ctx = primary(ctx);
+        ctx = opt_ctx(ctx);
         DeviceGuard g(ctx->device);
         opt_step(ctx, t);
     });
@@ -376,7 +389,7 @@ int tsne_dev_opt_step(tsne_ctx *ctx, int32_t t) {
 int tsne_dev_opt_losses(tsne_ctx *ctx, int32_t *loss_keys, double *loss_vals, int32_t cap, int32_t *n_loss) {
     return guard([&] {
         check_ctx(ctx);
-        ctx = primary(ctx);
+        ctx = opt_ctx(ctx);
         DeviceGuard g(ctx->device);
         int32_t k = opt_losses(ctx, loss_keys, loss_vals, cap);
         if (n_loss) *n_loss = k;
@@ -399,17 +412,27 @@ int tsne_dev_opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone,
                              int32_t *count) {
     return guard([&] {
         check_ctx(ctx);
-        ctx = primary(ctx);
+        ctx = opt_ctx(ctx);
         DeviceGuard g(ctx->device);
         int32_t k = opt_attract_log(ctx, iters, standalone, ms, cap);
         if (count) *count = k;
     });
 }
 
+int tsne_dev_opt_last_z(tsne_ctx *ctx, double *z_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        ctx = opt_ctx(ctx);
+        DeviceGuard g(ctx->device);
+        TSNE_REQUIRE(z_out != nullptr, "z_out is NULL");
+        *z_out = opt_last_z(ctx);
+    });
+}
+
 int tsne_dev_opt_profile(tsne_ctx *ctx, int32_t enable, double *ms_out5, int64_t *counters_out10) {
     return guard([&] {
         check_ctx(ctx);
-        ctx = primary(ctx);
+        ctx = opt_ctx(ctx);
         DeviceGuard g(ctx->device);
         opt_profile(ctx, enable, ms_out5, counters_out10);
     });
@@ -711,7 +734,7 @@ int tsne_optimize(tsne_ctx *ctx, const tsne_params *params, const int64_t *row_p
 int tsne_dev_opt_sync(tsne_ctx *ctx) {
     return guard([&] {
         check_ctx(ctx);
-        ctx = primary(ctx);
+        ctx = opt_ctx(ctx);
         DeviceGuard g(ctx->device);
         opt_sync(ctx);
     });

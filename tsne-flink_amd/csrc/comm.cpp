@@ -17,6 +17,7 @@
 // costs and an all-gather of the momentum / gains slices.
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 
@@ -31,6 +32,9 @@ struct Comm {
     virtual void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) = 0;
     // in place: rank r's bytes [off[r], off[r+1]) of buf are copied to every rank
     virtual void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) = 0;
+    // a rank failed: make every pending and later collective of this rank
+    // fail (TSNE_ERR_COMM) instead of waiting for it; callable from another thread
+    virtual void abort() {}
 };
 
 namespace {
@@ -41,17 +45,31 @@ void nccl_check(ncclResult_t r, const char *what) {
 
 struct RcclComm : Comm {
     ncclComm_t comm = nullptr;
+    std::atomic<bool> aborted{false};
     ~RcclComm() override {
-        if (comm) (void)ncclCommDestroy(comm);
+        if (comm && !aborted.load()) (void)ncclCommDestroy(comm);
+    }
+    // ncclCommAbort stops this rank's in-flight collective kernels and frees
+    // the communicator: a peer blocked in a collective with it then fails
+    // instead of hanging (run_group aborts every rank of a group once one
+    // rank has thrown).  Later calls report TSNE_ERR_COMM.
+    void abort() override {
+        if (comm && !aborted.exchange(true)) (void)ncclCommAbort(comm);
+    }
+    void live() {
+        if (aborted.load()) fail(TSNE_ERR_COMM, "RCCL communicator aborted (another rank failed)");
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override {
+        live();
         nccl_check(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, ctx->stream), "ncclAllReduce");
     }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override {
+        live();
         nccl_check(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm, ctx->stream), "ncclAllReduce");
     }
     // ragged all-gather: one in-place broadcast per root, fused into one group
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
+        live();
         uint8_t *b = static_cast<uint8_t *>(buf);
         nccl_check(ncclGroupStart(), "ncclGroupStart");
         for (int r = 0; r < ctx->world; ++r) {
@@ -117,6 +135,7 @@ struct LoopComm : Comm {
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override { allreduce(ctx, buf, count); }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override { allreduce(ctx, buf, count); }
+    void abort() override { g->abort(); }
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
         publish(ctx, buf);
         uint8_t *b = static_cast<uint8_t *>(buf);
@@ -233,9 +252,10 @@ void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback) {
     }
 }
 
-// A rank of a loopback group failed: release the others from the barrier.
+// A rank failed: its collectives (and, for a loopback group, every rank's
+// barrier) fail from now on instead of waiting.
 void comm_abort(tsne_ctx *ctx) {
-    if (auto *lc = dynamic_cast<LoopComm *>(ctx->comm)) lc->g->abort();
+    if (ctx->comm) ctx->comm->abort();
 }
 
 void comm_destroy(tsne_ctx *ctx) {

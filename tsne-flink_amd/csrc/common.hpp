@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -84,9 +85,12 @@ struct Workspace {
 
 // Named kernel-stage timers: HIP event pairs recorded on the stream the
 // stage's kernels run on, read (and synchronised) only when asked for, so a
-// timed loop never waits on them.  Events are pooled and reused.
+// timed loop never waits on them.  Events are pooled and reused; a stage keeps
+// its last CAP intervals (older pairs are recycled), so a long device loop
+// holds a bounded number of events.
 struct StageTimers {
-    std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> rec;
+    static constexpr size_t CAP = 1 << 14;
+    std::map<std::string, std::deque<std::pair<hipEvent_t, hipEvent_t>>> rec;
     std::vector<hipEvent_t> pool;
     hipEvent_t take() {
         if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
@@ -100,30 +104,45 @@ struct StageTimers {
         for (auto &p : it->second) { pool.push_back(p.first); pool.push_back(p.second); }
         it->second.clear();
     }
-    // begin(): returns the index of the new interval; end() closes the last one.
-    size_t begin(const std::string &name, hipStream_t st) {
+    // begin(): opens a new interval (recycling the oldest beyond CAP); end() closes it.
+    void begin(const std::string &name, hipStream_t st) {
         auto &v = rec[name];
+        if (v.size() >= CAP) {   // the oldest interval's events are complete or reusable: re-recorded below
+            pool.push_back(v.front().first);
+            pool.push_back(v.front().second);
+            v.pop_front();
+        }
         v.push_back({take(), take()});
         if (hipEventRecord(v.back().first, st) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventRecord failed");
-        return v.size() - 1;
     }
     void end(const std::string &name, hipStream_t st) {
         auto &v = rec[name];
         if (v.empty()) fail(TSNE_ERR_HIP, "stage timer " + name + " not started");
         if (hipEventRecord(v.back().second, st) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventRecord failed");
     }
-    // elapsed ms of every interval of `name` (synchronises on their events)
+    static double elapsed(const std::pair<hipEvent_t, hipEvent_t> &p) {
+        if (hipEventSynchronize(p.second) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventSynchronize failed");
+        float f = 0.f;
+        if (hipEventElapsedTime(&f, p.first, p.second) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventElapsedTime failed");
+        return f;
+    }
+    // elapsed ms of every kept interval of `name` (synchronises on their events)
     std::vector<double> ms(const std::string &name) {
         std::vector<double> out;
         auto it = rec.find(name);
         if (it == rec.end()) return out;
-        for (auto &p : it->second) {
-            if (hipEventSynchronize(p.second) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventSynchronize failed");
-            float f = 0.f;
-            if (hipEventElapsedTime(&f, p.first, p.second) != hipSuccess) fail(TSNE_ERR_HIP, "hipEventElapsedTime failed");
-            out.push_back(f);
-        }
+        for (auto &p : it->second) out.push_back(elapsed(p));
         return out;
+    }
+    // elapsed ms of the last interval only (0 if none)
+    double last_ms(const std::string &name) {
+        auto it = rec.find(name);
+        if (it == rec.end() || it->second.empty()) return 0.0;
+        return elapsed(it->second.back());
+    }
+    size_t count(const std::string &name) const {
+        auto it = rec.find(name);
+        return it == rec.end() ? 0 : it->second.size();
     }
     void clear() {
         for (auto &kv : rec)
@@ -209,6 +228,7 @@ void opt_step(tsne_ctx *ctx, int32_t t);
 void opt_sync(tsne_ctx *ctx);
 int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap);
 void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits);
+double opt_last_z(tsne_ctx *ctx);
 int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap);
 void opt_destroy(tsne_ctx *ctx);
 

@@ -107,7 +107,12 @@ struct OptState {
     // per launch of the attraction kernel (ctx->timers "opt.attract"): its
     // iteration and whether it ran alone on the main stream (loss iterations)
     // or on the side stream concurrently with the BH traversal
-    std::vector<std::pair<int32_t, int32_t>> attract_iter;
+    // (kept in step with the stage timer: its last StageTimers::CAP launches)
+    std::deque<std::pair<int32_t, int32_t>> attract_iter;
+    void log_attract(int32_t t, int32_t kind) {
+        attract_iter.push_back({t, kind});
+        while (attract_iter.size() > StageTimers::CAP) attract_iter.pop_front();
+    }
     double *mpart = nullptr;  // centring mean: block partials of combine_update
     // tiled attraction layout of the owned rows (attract_tiles), rebuilt with them
     bool at_on = false;
@@ -1696,7 +1701,7 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         if (k != 3) TSNE_HIP(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
         s->last_ms[k] = ms;
     }
-    s->last_ms[3] = ctx->timers.ms("opt.attract").back();
+    s->last_ms[3] = ctx->timers.last_ms("opt.attract");
     if (s->C == 3) {
         for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
         return;
@@ -1749,7 +1754,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     const int64_t blocks = attract3_launch(st, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex,
                                            s->attr3, s->part, want_loss);
     ctx->timers.end("opt.attract", st);
-    s->attract_iter.push_back({t, 1});
+    s->log_attract(t, 1);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     ctx->timers.begin("opt.update", st);
     if (s->L1 > s->L0)
@@ -1893,15 +1898,16 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // kernels stretch under the attraction (morton_keys 15 -> 800 us; whole
     // schedule 8.53 -> 8.97 s).  TSNE_OVERLAP=tree / after / bh forces a mode.
     static const bool loss_alone = [] { const char *e = getenv("TSNE_LOSS_ALONE"); return e && e[0] == '1'; }();
-    const bool overlap = !want_loss || !loss_alone;
-    if (want_loss && overlap) aa.scal = s->scal + 7;   // Z = 1 in the kernel
-    int64_t blocks = 0;
     static const int ov_env = [] {
         const char *e = getenv("TSNE_OVERLAP");
         const std::string v = e ? e : "";
-        return v == "tree" ? 0 : v == "after" ? 1 : v == "bh" ? 2 : -1;
+        return v == "tree" ? 0 : v == "after" ? 1 : v == "bh" ? 2 : v == "none" ? 3 : -1;
     }();
     const int ov_mode = ov_env >= 0 ? ov_env : s->tree.root_tile ? 0 : 1;
+    // serial: the attraction on the context stream after Z, alone on the GPU
+    const bool overlap = ov_mode != 3 && (!want_loss || !loss_alone);
+    if (want_loss && overlap) aa.scal = s->scal + 7;   // Z = 1 in the kernel
+    int64_t blocks = 0;
     if (overlap && ov_mode == 0 && s->tree.root_tile) aa.bpc = 3;
     auto side_wait = [&] {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
@@ -1913,7 +1919,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         blocks = attract_launch_opt(s->side, s, aa, want_loss != 0);
         TSNE_LAUNCH_CHECK();
         ctx->timers.end("opt.attract", s->side);
-        s->attract_iter.push_back({t, want_loss ? 2 : 0});
+        s->log_attract(t, want_loss ? 2 : 0);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
     if (overlap && ov_mode == 0) side_attract();
@@ -1946,10 +1952,10 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     } else {
         ctx->timers.begin("opt.attract", st);
-        blocks = attract_launch_opt(st, s, aa, true);
+        blocks = attract_launch_opt(st, s, aa, want_loss != 0);
         TSNE_LAUNCH_CHECK();
         ctx->timers.end("opt.attract", st);
-        s->attract_iter.push_back({t, 1});
+        s->log_attract(t, want_loss ? 1 : 3);
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     // update + centre: combine_update (with the mean's block partials when one
@@ -2026,6 +2032,15 @@ int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, doub
         if (ms) ms[e] = v[e];
     }
     return k;
+}
+
+double opt_last_z(tsne_ctx *ctx) {
+    OptState *s = ctx->opt;
+    TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    double z = 0.0;
+    TSNE_HIP(hipMemcpyAsync(&z, s->scal, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    return z;
 }
 
 void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits) {

@@ -76,6 +76,7 @@ SIGNATURES = {
     "tsne_dev_opt_sync": (C.c_int, [P]),
     "tsne_dev_opt_losses": (C.c_int, [P, P, P, I32, PI32]),
     "tsne_dev_opt_profile": (C.c_int, [P, I32, P, P]),
+    "tsne_dev_opt_last_z": (C.c_int, [P, PD]),
     "tsne_dev_opt_attract_log": (C.c_int, [P, P, P, P, I32, PI32]),
     "tsne_ctx_stage_ms": (C.c_int, [P, C.c_char_p, P, I32, PI32]),
 }

@@ -288,6 +288,12 @@ class Context:
     def dev_opt_sync(self):
         check(lib().tsne_dev_opt_sync(self._h))
 
+    def dev_opt_last_z(self):
+        """Z of the last tsne_dev_opt_step (the normaliser its gradient and loss used)."""
+        z = C.c_double()
+        check(lib().tsne_dev_opt_last_z(self._h, C.byref(z)))
+        return z.value
+
     def dev_opt_losses(self, cap=1024):
         keys = np.zeros(cap, dtype=np.int32)
         vals = np.zeros(cap)
