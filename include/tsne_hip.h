@@ -72,6 +72,15 @@ const char *tsne_last_error(void);
 void tsne_params_default(tsne_params *p);
 /* Tsne.getMetric (Tsne.scala:161-168): unknown name -> TSNE_ERR_ARG. */
 int tsne_metric_from_name(const char *name, int32_t *metric_out);
+/* Host-side CSR from COO triples, for callers that receive a DataSet's
+ * triples one at a time (the JNI operator bodies stream a Flink iterator into
+ * off-heap arrays: TsneHelpers.scala:162-196's groupBy(0) without JVM arrays,
+ * so nothing is bounded by 2^31 elements).  row[e] in [0, n); rows come out
+ * in index order, each row's entries in input order (a stable counting sort,
+ * the reference's group order).  row_ptr_out: n + 1; col_out / val_out: nnz
+ * (val / val_out may be NULL).  No context, no device. */
+int tsne_coo_to_csr(const int32_t *row, const int32_t *col, const double *val, int64_t nnz, int64_t n,
+                    int64_t *row_ptr_out, int32_t *col_out, double *val_out);
 /* Row shard [r0, r1) of rank `rank` out of `world` (contiguous, balanced). */
 int tsne_shard_rows(int64_t n, int32_t world, int32_t rank, int64_t *r0, int64_t *r1);
 /* Cost-balanced cuts of the Morton-sorted BH queries (the rule the multi-GPU

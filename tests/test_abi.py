@@ -83,3 +83,45 @@ def test_create_multi_argument_errors():
         assert rc == -1 and b"distinct" in L.tsne_last_error()
     rc = L.tsne_ctx_create_multi(None, 0, C.byref(h))
     assert rc == -1
+
+
+def coo_to_csr(row, col, val, n):
+    import ctypes as C
+    import numpy as np
+    row = np.ascontiguousarray(row, dtype=np.int32)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    val = None if val is None else np.ascontiguousarray(val, dtype=np.float64)
+    rp = np.zeros(n + 1, dtype=np.int64)
+    oc = np.zeros(max(1, len(col)), dtype=np.int32)
+    ov = None if val is None else np.zeros(max(1, len(val)))
+    p = lambda a: None if a is None else a.ctypes.data_as(C.c_void_p)
+    rc = T.lib().tsne_coo_to_csr(p(row), p(col), p(val), len(row), n, p(rp), p(oc), p(ov))
+    return rc, rp, oc[:len(col)], (None if ov is None else ov[:len(col)])
+
+
+def test_coo_to_csr_groups_rows_stably():
+    """tsne_coo_to_csr: the JNI bodies' groupBy(0) (TsneHelpers.scala:162-196)
+    -- rows in index order, each row's entries in input order, empty rows kept."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    n, nnz = 300, 5000
+    row = rng.integers(0, n, nnz)
+    row[row % 7 == 3] = 11            # a heavy row; some rows stay empty
+    col = rng.integers(0, 10 ** 6, nnz)
+    val = rng.random(nnz)
+    rc, rp, oc, ov = coo_to_csr(row, col, val, n)
+    assert rc == 0
+    order = np.argsort(row, kind="stable")
+    assert np.array_equal(rp, np.concatenate([[0], np.cumsum(np.bincount(row, minlength=n))]))
+    assert np.array_equal(oc, col[order]) and np.array_equal(ov, val[order])
+    rc, rp2, oc2, _ = coo_to_csr(row, col, None, n)
+    assert rc == 0 and np.array_equal(rp2, rp) and np.array_equal(oc2, oc)
+    rc, rp3, _, _ = coo_to_csr([], [], [], 4)
+    assert rc == 0 and list(rp3) == [0, 0, 0, 0, 0]
+
+
+def test_coo_to_csr_rejects_bad_rows():
+    rc, _, _, _ = coo_to_csr([0, 5], [1, 2], [1.0, 2.0], 5)
+    assert rc == -1 and b"out of [0, n)" in T.lib().tsne_last_error()
+    rc, _, _, _ = coo_to_csr([0, -1], [1, 2], [1.0, 2.0], 5)
+    assert rc == -1

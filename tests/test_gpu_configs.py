@@ -430,7 +430,12 @@ def test_c5_distance_matrix_50k_full_size(ctx):
     for i in sample:   # workgroup-per-row beta search over 49,999 entries
         po, _ = O.affinities(np.array([0, m], dtype=np.int64), dist[i].cpu().numpy(), 30.0)
         assert np.abs(p[i].cpu().numpy() - po).max() <= 1e-12, i
-    del dist
+    # the host-buffer entry point (what the JNI bodies call) with all 2.5e9
+    # entries: 64-bit counts and offsets end to end, the same values
+    ph = ctx.pairwiseAffinities(rp.cpu().numpy(), dist.cpu().numpy().ravel(), 30.0)
+    assert ph.size == n * m > 2 ** 31
+    assert np.array_equal(ph, p.cpu().numpy().ravel())
+    del ph, dist
     cap = n * m
     orp = torch.empty(n + 1, dtype=torch.int64, device=dev)
     oc = torch.empty(cap, dtype=torch.int32, device=dev)

@@ -1,0 +1,119 @@
+"""Dynamic splitting of heavy BH traversal waves (bhtree.hip "Dynamic
+splitting"): a wave over its pop budget hands its remaining stack to task
+passes; the tasks' partial sums are combined in spill order.  The result is
+the same reference sum over the same cells (QuadTree.scala:123-152), only
+re-associated, so it must equal the unsplit traversal to rounding and the
+oracle to BH_NEAR_TOL -- with every region full (the finish pass over saved
+stacks) as well.  TSNE_BH_BUDGET_FIXED forces the budget of a traversal."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle_ctypes as O
+import tsne_amd as T
+from tsne_amd.api import default_params
+
+pytestmark = pytest.mark.gpu
+NEAR_TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = T.Context(0)
+    yield c
+    c.close()
+
+
+class budget:
+    """TSNE_BH_BUDGET_FIXED for the calls inside the block (read per traversal)."""
+
+    def __init__(self, pops):
+        self.pops = pops
+
+    def __enter__(self):
+        if self.pops is not None:
+            os.environ["TSNE_BH_BUDGET_FIXED"] = str(self.pops)
+
+    def __exit__(self, *a):
+        os.environ.pop("TSNE_BH_BUDGET_FIXED", None)
+
+
+def clustered(n, seed):
+    """A mid-schedule-like embedding: 20 blobs of extent ~1 over a ~30-wide
+    field, a quarter of each blob in a dense core (the heavy waves)."""
+    rng = np.random.default_rng(seed)
+    centres = rng.uniform(-15, 15, size=(20, 2))
+    lab = rng.integers(0, 20, n)
+    sd = np.where(rng.random(n) < 0.25, 0.02, 0.5)[:, None]
+    return centres[lab] + rng.normal(size=(n, 2)) * sd
+
+
+@pytest.mark.parametrize("pops", [1, 48, 600])
+def test_spilled_repulsion_equals_unsplit(ctx, pops):
+    """Budgets from 'every wave spills at once, regions overflow into the
+    finish pass' to 'only the heavy waves spill'."""
+    n = 40_000
+    Y = clustered(n, 5)
+    F0, z0 = ctx.repulsion(Y, 0.5)            # fresh tree state: no budget, no spill
+    with budget(pops):
+        F1, z1 = ctx.repulsion(Y, 0.5)
+    assert np.all(np.abs(z1 - z0) <= 1e-12 * z0)
+    assert np.abs(F1 - F0).max() <= 1e-12 * np.abs(F0).max()
+    with budget(pops):                         # deterministic: the same spill, the same sums
+        F2, z2 = ctx.repulsion(Y, 0.5)
+    assert np.array_equal(F1, F2) and np.array_equal(z1, z2)
+    q = np.arange(0, n, 97)
+    rep, zi = O.repulsion_queries(Y, 0.5, np.ascontiguousarray(Y[q]), threads=8)
+    assert np.abs(z1[q] - zi).max() <= NEAR_TOL * zi.max()
+    assert np.abs(F1[q] - rep).max() <= NEAR_TOL * np.abs(rep).max()
+
+
+def test_spilled_repulsion_with_duplicates(ctx):
+    """Exact duplicates (the reference's multiplicities, virtual chain tops)
+    inside spilled subtrees."""
+    n = 20_000
+    Y = clustered(n, 9)
+    Y[[5, 900, 17_000]] = Y[5]
+    Y[100:140] = Y[100]
+    F0, z0 = ctx.repulsion(Y, 0.25)
+    with budget(16):
+        F1, z1 = ctx.repulsion(Y, 0.25)
+    assert np.all(np.abs(z1 - z0) <= 1e-12 * z0)
+    assert np.abs(F1 - F0).max() <= 1e-12 * np.abs(F0).max()
+    rep, zi = O.repulsion(Y, 0.25, threads=8)
+    assert np.abs(z1 - zi).max() <= NEAR_TOL * zi.max()
+    assert np.abs(F1 - rep).max() <= NEAR_TOL * np.abs(rep).max()
+
+
+def test_optimizer_with_spills_deterministic(ctx):
+    """The device optimizer with a tiny forced budget (spills every
+    iteration): run twice -> bit-identical; against the default budget rule ->
+    the same trajectory to re-association level."""
+    from test_gpu_parity import random_problem
+    n = 4000
+    rp, col, val = random_problem(n, 30, seed=23)
+    Y0 = np.random.default_rng(4).normal(size=(n, 2)) * 1e-4
+    p = default_params(iterations=120, theta=0.5)
+    dev = torch.device("cuda", 0)
+    Pd = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (rp, col, val))
+
+    def run(pops):
+        Y = torch.from_numpy(Y0.copy()).to(dev)
+        u, g = torch.zeros_like(Y), torch.ones_like(Y)
+        ctx.dev_opt_setup(p, *Pd, n, Y, u, g)
+        with budget(pops):
+            for t in range(1, p.iterations + 1):
+                ctx.dev_opt_step(t)
+        ctx.synchronize()
+        return Y.cpu().numpy(), ctx.dev_opt_losses()
+
+    Ya, la = run(8)
+    Yb, lb = run(8)
+    assert np.array_equal(Ya, Yb) and la == lb
+    Yc, lc = run(None)
+    assert sorted(la) == sorted(lc)
+    assert np.abs(Ya - Yc).max() <= 1e-8 * np.abs(Yc).max()
+    for t in lc:
+        assert abs(la[t] - lc[t]) <= 1e-9 * abs(lc[t]), t

@@ -1275,248 +1275,539 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
 // dense_apply sums the tiles afterwards.  This keeps the traversal at <= 64
 // VGPRs (8 waves per SIMD to hide the record fetches) instead of ~100.
 
+// ---- Dynamic splitting of heavy traversal waves (spill tasks).
+// A wave's BH work is the depth-first walk of its shared stack.  In dense
+// clusters a few waves carry many times the mean work and set the grid's
+// span (the longest wave is the span from t ~ 350 on).  A wave
+// whose cost (pops + tile points / 64) reaches the iteration's budget
+// (TSNE_BH_BUDGET x the previous traversal's mean wave cost) hands its whole
+// remaining stack to the next pass as tasks: contiguous runs of stack entries
+// of about gfac x budget points each (<= TASK_ENT entries); a task is the same
+// 64 queries over those subtrees.  Task passes run on a fixed grid; a task
+// over budget spills again into the next region (the last pass never
+// spills).  Each task writes its 64 lanes' partial (F, z).  The combine adds
+// every task's children (its spill, in stack-entry order) bottom-up by
+// region, then a wave's children into F, Z: the summation order is fixed by
+// the spill structure, not by which wave ran what (deterministic).  Subtree
+// sums are additive, so the result is the reference's sum over the same
+// cells; only its association changes.  Tasks sum their all-open / near-exact
+// tiles densely inline (the exact leaf sum, as tile_apply's dense path).
+
+// Hand the stack [0, sp) of one wave to region r as tasks (wave-uniform);
+// false, and nothing handed over, when the region is full.
+__device__ bool spill_stack(const SpillView &sv, int r, int lane, int sp, const int32_t *sref_w,
+                            const uint64_t *smask_w, uint64_t *sbm_w, const QRec *__restrict__ qrec, int32_t wid,
+                            int32_t gpts, int32_t &c0, int32_t &nc) {
+    static_assert(STACK % 64 == 0, "spill rounds");
+    const int nr = (sp + 63) >> 6;
+    const double inv = 1.0 / (double)gpts;
+    int32_t carry_incl = 0, carry_g = -1, ng = 0;
+#pragma unroll 1
+    for (int q = 0; q < nr; ++q) {   // group boundaries, 64 entries a round (lane masks in LDS)
+        const int i = q * 64 + lane;
+        const bool in = i < sp;
+        const int32_t c = in ? qrec[sref_w[i]].cnt : 0;
+        int32_t incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        incl += carry_incl;
+        const int32_t g = (int32_t)((double)(incl - c) * inv);   // group of the exclusive prefix
+        int32_t gp = __shfl_up(g, 1, 64);
+        if (lane == 0) gp = carry_g;
+        const uint64_t bm = __ballot(in && (i == 0 || g != gp || i % TASK_ENT == 0));
+        if (lane == 0) sbm_w[q] = bm;
+        ng += (int)__popcll(bm);
+        carry_incl = __shfl(incl, 63, 64);
+        carry_g = __shfl(g, 63, 64);
+    }
+    int32_t tb = 0, eb = 0;
+    if (lane == 0) {
+        tb = atomicAdd(&sv.cnt[2 * r], ng);
+        eb = atomicAdd(&sv.cnt[2 * r + 1], sp);
+    }
+    tb = __shfl(tb, 0, 64);
+    eb = __shfl(eb, 0, 64);
+    BHTask *T = sv.task + (int64_t)(r - 1) * sv.task_cap;
+    if ((int64_t)tb + ng > sv.task_cap || (int64_t)eb + sp > sv.ent_cap) {
+        // region full: the slots reserved inside it stay empty tasks (ne = 0),
+        // which no combine reads; the wave keeps its stack
+        for (int j = lane; j < ng; j += 64)
+            if ((int64_t)tb + j < sv.task_cap) {
+                BHTask e{};
+                e.wid = wid;
+                T[tb + j] = e;
+            }
+        return false;
+    }
+    int32_t *ER = sv.tent_ref + (int64_t)(r - 1) * sv.ent_cap;
+    uint64_t *EM = sv.tent_mask + (int64_t)(r - 1) * sv.ent_cap;
+    for (int i = lane; i < sp; i += 64) {
+        ER[eb + i] = sref_w[i];
+        EM[eb + i] = smask_w[i];
+    }
+    int before = 0;
+#pragma unroll 1
+    for (int q = 0; q < nr; ++q) {   // one task per group: its first entry and length
+        const uint64_t bm = __builtin_amdgcn_readfirstlane(sbm_w[q] & 0xffffffffull) |
+                            ((uint64_t)__builtin_amdgcn_readfirstlane(sbm_w[q] >> 32) << 32);
+        const int i = q * 64 + lane;
+        if ((bm >> lane) & 1ull) {
+            const int gi = before + (int)__popcll(bm & lanemask_lt());
+            const uint64_t above = lane < 63 ? (bm >> (lane + 1)) : 0ull;
+            int nxt = sp;
+            if (above) {
+                nxt = i + __ffsll((long long)above);
+            } else {
+                for (int q2 = q + 1; q2 < nr; ++q2) {
+                    const uint64_t b2 = sbm_w[q2];
+                    if (b2) { nxt = q2 * 64 + __ffsll((long long)b2) - 1; break; }
+                }
+            }
+            BHTask e{};
+            e.wid = wid;
+            e.e0 = eb + i;
+            e.ne = nxt - i;
+            T[tb + gi] = e;
+        }
+        before += (int)__popcll(bm);
+    }
+    c0 = tb;
+    nc = ng;
+    return true;
+}
+
 // Traversal kernel (see the comment above).  STATS: per-wave work counters
 // (profiling, and the bucket costs of the multi-GPU balancing); the
-// production instantiation carries none.
-template <int KPOP, int MODE>   // MODE 0 plain, 1 wave times for bcost only, 2 all counters
+// production instantiation carries none.  TASK = false: one wave per 64
+// query slots (pass 0), spilling into region 1 when sv.task is set; TASK =
+// true: the tasks of `region`, grid-stride over a fixed grid, spilling into
+// region + 1 (none from the last region), tiles summed inline.
+template <int KPOP, int MODE, bool TASK>   // MODE 0 plain, 1 wave times for bcost only, 2 all counters
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
     int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, int32_t virt, double2 *__restrict__ F,
     double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost,
-    const int32_t *__restrict__ border, int32_t *__restrict__ wcost, int32_t *__restrict__ tcost) {
+    const int32_t *__restrict__ border, int32_t *__restrict__ wcost, int32_t *__restrict__ tcost, SpillView sv,
+    int region) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
     __shared__ QRec srec[4][KPOP];
     __shared__ int32_t bref[4][KPOP];
     __shared__ uint64_t bmask[4][KPOP];
+    __shared__ double2 tbuf[4][TASK ? 64 : 1];
+    __shared__ uint64_t sbm[4][STACK / 64];   // spill: group boundary masks
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int64_t blk = border ? (int64_t)border[blockIdx.x]
-                      : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
-    const int64_t wid = blk * 4 + w;   // wave slot: query slots g0 + 64 wid .. + 63, tile list wid
-    // query slot k -> sorted position s (the identity, or this rank's list of
-    // its own queries in sorted order: the waves stay Morton-coherent)
-    const int64_t k = g0 + wid * 64 + lane;
-    const bool valid = k < g1;
-    const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
-    if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
-    if (__ballot(valid) == 0) return;
-    const long long t_start = COST ? clock64() : 0;
-    const unsigned long long w_start = STATS ? wall_clock64() : 0;
-    int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next block orders
-    const int root = meta[1];
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
-    double qx = 0.0, qy = 0.0;
-    if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
-    const double qmag = fabs(qx) + fabs(qy);
-    const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
-    double fx = 0.0, fy = 0.0, zs = 0.0;
-    unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
-    unsigned long long wfull = 0, wpart = 0;                                   // STATS only
-    int sp = 0;
-    int ntt = 0;
-    TileTask *mytt = ttask + wid * TILE_CAP;
-    // ---- the root: a single point, a key-tie group, or a cell tested like any child
-    if (root == ~0) {
-        if (valid) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
-    } else if (root >= 0) {
-        const BHNode &rt = nodes[root];
-        if (rt.delta >= 62) {
-            for (int p = rt.first; p <= rt.last; ++p) {
-                const double2 pp = pos[p];
-                if (valid) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+    // the pop budget of this traversal and the spill group size (points)
+    // region SPILL_PASSES + 1 (TASK): the finish pass over saved stacks (sv.ovf), without budget
+    const bool finish = TASK && region > SPILL_PASSES;
+    const bool can_spill = sv.task != nullptr && (!TASK || region < SPILL_PASSES);
+    const int32_t budget0 = can_spill ? sv.budget[0] : INT32_MAX;
+    const int32_t gpts = (int32_t)min((int64_t)INT32_MAX, max((int64_t)1, (int64_t)budget0 * sv.gfac));
+    const int64_t nsrc_w = sv.nwaves;   // saved-stack sources: waves [0, nwaves), then tasks by global id
+    const int64_t ntask = !TASK ? 1 : finish ? (int64_t)sv.cnt[0] : min((int64_t)sv.cnt[2 * region], (int64_t)sv.task_cap);
+    const int64_t gstride = TASK ? (int64_t)gridDim.x * 4 : 1;
+    for (int64_t ti = TASK ? (int64_t)blockIdx.x * 4 + w : 0; ti < ntask; ti += gstride) {
+        BHTask tk{};
+        int64_t wid, src = 0;
+        if constexpr (TASK) {
+            if (finish) {   // a saved stack: entries from its save area
+                const int2 o = sv.ovf[ti];
+                src = o.x;
+                tk.ne = o.y;
+                tk.wid = src < nsrc_w ? (int32_t)src : sv.task[src - nsrc_w].wid;
+            } else {
+                tk = sv.task[(int64_t)(region - 1) * sv.task_cap + ti];
+                if (tk.ne == 0) continue;   // an empty slot of a full region (uniform)
             }
+            wid = tk.wid;
         } else {
-            // the root cell; with duplicates whose copies the reference root
-            // counts differently from the cells below it: its virtual record
-            // (h = W, every copy), opened into the real root node
-            double rh = rt.h, rcx = rt.cx, rcy = rt.cy;
-            int32_t rcnt = rt.cnt, rpush = root;
-            if (meta[3]) {
-                const QRec &vq = qrec[virt + root];
-                rh = ldexp(rt.h, rt.delta >> 1);
-                rcx = vq.cx; rcy = vq.cy; rcnt = vq.cnt; rpush = virt + root;
-            }
-            bool open = false;
-            if (valid) {
-                if (STATS) ++nvis;
-                const double dx = qx - rcx, dy = qy - rcy;
-                const double D = __fma_rn(dx, dx, dy * dy);
-                if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rcnt, fx, fy, zs);
-                else open = true;
-            }
-            const uint64_t om = __ballot(open);
-            if (om) {
-                if (lane == 0) { sref[w][0] = rpush; smask[w][0] = om; }
-                sp = 1;
-            }
+            const int64_t blk = border ? (int64_t)border[blockIdx.x]
+                              : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk)
+                                              : (int64_t)blockIdx.x;
+            wid = blk * 4 + w;   // wave slot: query slots g0 + 64 wid .. + 63, tile list wid
         }
-    }
-    // Pop up to KPOP cells at a time: their records are fetched with one
-    // round of coalesced 16-byte vector loads into LDS (the pops' memory
-    // latencies overlap), then processed one by one from LDS broadcasts.
-    while (sp > 0) {
-        const int k = sp > STACK / 2 ? 1 : (sp < KPOP ? sp : KPOP);
-        sp -= k;
-        if (lane < k) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
-        for (int e = lane; e < QREC_V4 * k; e += 64) {
-            const int rr = e / QREC_V4, part = e - rr * QREC_V4;
-            const int rf = sref[w][sp + rr];
-            reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
+        // query slot k -> sorted position s (the identity, or this rank's list of
+        // its own queries in sorted order: the waves stay Morton-coherent)
+        const int64_t k = g0 + wid * 64 + lane;
+        const bool valid = k < g1;
+        const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
+        if constexpr (!TASK) {
+            if (lane == 0) {
+                ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0;
+                if (sv.wspill) sv.wspill[wid] = make_int2(0, 0);
+            }
+            if (__ballot(valid) == 0) return;
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
-        __builtin_amdgcn_wave_barrier();
-        npops += k;
-        for (int r = 0; r < k; ++r) {
-            if (STATS) ++wpops;
-            const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
-            const uint64_t msk = bmask[w][r];
-            bool act = (msk >> lane) & 1ull;
-            const QRec &nd = srec[w][r];
-            // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
-            bool tile = false;
-            const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
-            if ((nflags & QNCH_TILE) && act) {
-                const double cdx = qx - nd.cx, cdy = qy - nd.cy;
-                const double dc = cdx * cdx + cdy * cdy;
-                tile = dc <= nd.rball;   // rball^2 (1 - 1e-9)
-                if (!tile) {
-                    const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-                    const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
-                    const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-                    const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-                    tile = dmax <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax)
-                }
-            }
-            const uint64_t tm = __ballot(tile);
-            if (tm) {
-                // The wave records (subtree, lanes) for tile_apply, or, when its
-                // list is full, the lanes keep traversing (the reference's path).
-                // The range holds whole equal-key runs, so either all of the
-                // query's exact duplicates (itself included) are in it or none
-                // is; they add exactly 1 each to z in the leaf sum: taken off here.
-                if (ntt < TILE_CAP) {
-                    const int a = nd.first, b = nd.last;
-                    if (lane == 0) {
-                        TileTask tt; tt.ref = ref; tt.first = a; tt.last = b; tt.pad = nd.cnt; tt.mask = tm;
-                        mytt[ntt] = tt;
+        const long long t_start = COST ? clock64() : 0;
+        const unsigned long long w_start = STATS ? wall_clock64() : 0;
+        int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next block orders
+        int32_t budget = budget0;
+        double qx = 0.0, qy = 0.0;
+        if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
+        const double qmag = fabs(qx) + fabs(qy);
+        const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
+        double fx = 0.0, fy = 0.0, zs = 0.0;
+        unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
+        unsigned long long wfull = 0, wpart = 0;                                   // STATS only
+        int sp = 0;
+        int ntt = 0;
+        TileTask *mytt = TASK ? nullptr : ttask + wid * TILE_CAP;
+        if constexpr (TASK) {   // the task's stack entries, in their original stack order
+            const int32_t *er = finish ? sv.save_ref + src * STACK : sv.tent_ref + (int64_t)(region - 1) * sv.ent_cap + tk.e0;
+            const uint64_t *em = finish ? sv.save_mask + src * STACK : sv.tent_mask + (int64_t)(region - 1) * sv.ent_cap + tk.e0;
+            for (int i = lane; i < tk.ne; i += 64) { sref[w][i] = er[i]; smask[w][i] = em[i]; }
+            sp = tk.ne;
+        } else {
+            // ---- the root: a single point, a key-tie group, or a cell tested like any child
+            const int root = meta[1];
+            if (root == ~0) {
+                if (valid) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
+            } else if (root >= 0) {
+                const BHNode &rt = nodes[root];
+                if (rt.delta >= 62) {
+                    for (int p = rt.first; p <= rt.last; ++p) {
+                        const double2 pp = pos[p];
+                        if (valid) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
                     }
-                    ++ntt;
-                    ntilepts += b - a + 1;
-                    if (STATS) wtile += (unsigned long long)(b - a + 1);
-                    if (tile) {
-                        if (STATS) nvis += (unsigned long long)(b - a + 1);
-                        if (s >= a && s <= b) zs -= (double)ndup;
+                } else {
+                    // the root cell; with duplicates whose copies the reference root
+                    // counts differently from the cells below it: its virtual record
+                    // (h = W, every copy), opened into the real root node
+                    double rh = rt.h, rcx = rt.cx, rcy = rt.cy;
+                    int32_t rcnt = rt.cnt, rpush = root;
+                    if (meta[3]) {
+                        const QRec &vq = qrec[virt + root];
+                        rh = ldexp(rt.h, rt.delta >> 1);
+                        rcx = vq.cx; rcy = vq.cy; rcnt = vq.cnt; rpush = virt + root;
                     }
-                    act = act && !tile;
-                }
-            }
-            if (__ballot(act) == 0) continue;
-            // the opened cell's quad children, from its record
-            const int nch = nflags & 0xff;
-            if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                if (c >= nch) break;
-                const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
-                if (kind == QK_CELL || kind == QK_LEAF) {
-                    // A cell (summarise() and cell_force() in masked form) or a
-                    // leaf: ch = QCH_LEAF < 0 passes the test, ccnt = 1 makes
-                    // cell_force leaf_force exactly, and a leaf equal to the
-                    // query adds nothing (a cell at D = 0 is never summarised)
-                    if (STATS && act) ++nvis;
-                    const double px = nd.ccx[c], py = nd.ccy[c];
-                    const double dx = qx - px, dy = qy - py;
-                    const double D = __fma_rn(dx, dx, dy * dy);
-                    const double h = nd.ch[c];
-                    bool acc = h < th_lo * D;
-                    if (act && !acc && !(h > th_hi * D))
-                        acc = h / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
-                    const bool take = act && acc && !(px == qx && py == qy);
-                    const double Q = recip_bh(1.0 + D);
-                    const double mult = (double)nd.ccnt[c] * Q;
-                    const double sc = mult * Q;
-                    fx = __fma_rn(take ? sc : 0.0, dx, fx);
-                    fy = __fma_rn(take ? sc : 0.0, dy, fy);
-                    zs += take ? mult : 0.0;
-                    const bool open = act && !acc;
+                    bool open = false;
+                    if (valid) {
+                        if (STATS) ++nvis;
+                        const double dx = qx - rcx, dy = qy - rcy;
+                        const double D = __fma_rn(dx, dx, dy * dy);
+                        if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rcnt, fx, fy, zs);
+                        else open = true;
+                    }
                     const uint64_t om = __ballot(open);
-                    if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
-                        const uint64_t am = __ballot(act), tk = __ballot(take);
-                        if (am && tk == am) {
-                            if (am == __ballot(valid)) ++wfull; else ++wpart;
-                        }
-                    }
                     if (om) {
-                        if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
-                        ++sp;
+                        if (lane == 0) { sref[w][0] = rpush; smask[w][0] = om; }
+                        sp = 1;
                     }
                 }
             }
-            // duplicate kinds (rare), after the others: out of the main loop,
-            // whose accumulators then stay in place
-            if (__builtin_expect((nflags & (0xAA << QNCH_KIND)) != 0, 0)) {
-                for (int c = 0; c < nch; ++c) {
-                    const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
-                    if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
-                        if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
-                            if (STATS) ++nvis;
-                            const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                            cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
+        }
+        // Pop up to KPOP cells at a time: their records are fetched with one
+        // round of coalesced 16-byte vector loads into LDS (the pops' memory
+        // latencies overlap), then processed one by one from LDS broadcasts.
+        while (sp > 0) {
+            if (sp >= 2 && npops + (ntilepts >> 6) >= budget) break;   // over budget: spilled at the end
+            const int k = sp > STACK / 2 ? 1 : (sp < KPOP ? sp : KPOP);
+            sp -= k;
+            if (lane < k) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
+            for (int e = lane; e < QREC_V4 * k; e += 64) {
+                const int rr = e / QREC_V4, part = e - rr * QREC_V4;
+                const int rf = sref[w][sp + rr];
+                reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
+            __builtin_amdgcn_wave_barrier();
+            npops += k;
+            for (int r = 0; r < k; ++r) {
+                if (STATS) ++wpops;
+                const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
+                const uint64_t msk = bmask[w][r];
+                bool act = (msk >> lane) & 1ull;
+                const QRec &nd = srec[w][r];
+                // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
+                bool tile = false;
+                const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
+                if ((nflags & QNCH_TILE) && act) {
+                    const double cdx = qx - nd.cx, cdy = qy - nd.cy;
+                    const double dc = cdx * cdx + cdy * cdy;
+                    tile = dc <= nd.rball;   // rball^2 (1 - 1e-9)
+                    if (!tile) {
+                        const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+                        const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                        const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                        const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
+                        tile = dmax <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax)
+                    }
+                }
+                const uint64_t tm = __ballot(tile);
+                if (tm) {
+                    const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
+                    if constexpr (TASK) {
+                        // the tile's exact leaf sum, densely, by the tile lanes (points
+                        // staged through LDS 64 at a time); the range holds whole
+                        // equal-key runs: the query's duplicates (itself included) add
+                        // exactly 1 each to z and are taken off
+                        double ux = 0.0, uy = 0.0, uz = 0.0;
+                        for (int c0 = a; c0 <= b; c0 += 64) {
+                            const int cn = min(64, b - c0 + 1);
+                            __builtin_amdgcn_wave_barrier();
+                            tbuf[w][lane] = lane < cn ? pos[c0 + lane] : make_double2(0.0, 0.0);
+                            __builtin_amdgcn_wave_barrier();
+                            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes landed
+                            __builtin_amdgcn_wave_barrier();
+                            for (int j = 0; j < cn; ++j) {
+                                const double2 pp = tbuf[w][j];
+                                pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                            }
                         }
-                    } else if (kind == QK_TIE) {
-                        const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
-                        for (int p = tn.first; p <= tn.last; ++p) {
-                            const double2 pp = pos[p];
-                            if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                        __builtin_amdgcn_wave_barrier();
+                        if (tile) {
+                            fx += ux; fy += uy; zs += uz;
+                            if (s >= a && s <= b) zs -= (double)ndup;
+                            if (STATS) nvis += (unsigned long long)(b - a + 1);
+                        }
+                        ntilepts += b - a + 1;
+                        if (STATS) wtile += (unsigned long long)(b - a + 1);
+                        act = act && !tile;
+                    } else if (ntt < TILE_CAP) {
+                        // The wave records (subtree, lanes) for tile_apply, or, when its
+                        // list is full, the lanes keep traversing (the reference's path).
+                        // The range holds whole equal-key runs, so either all of the
+                        // query's exact duplicates (itself included) are in it or none
+                        // is; they add exactly 1 each to z in the leaf sum: taken off here.
+                        if (lane == 0) {
+                            TileTask tt; tt.ref = ref; tt.first = a; tt.last = b; tt.pad = nd.cnt; tt.mask = tm;
+                            mytt[ntt] = tt;
+                        }
+                        ++ntt;
+                        ntilepts += b - a + 1;
+                        if (STATS) wtile += (unsigned long long)(b - a + 1);
+                        if (tile) {
+                            if (STATS) nvis += (unsigned long long)(b - a + 1);
+                            if (s >= a && s <= b) zs -= (double)ndup;
+                        }
+                        act = act && !tile;
+                    }
+                }
+                if (__ballot(act) == 0) continue;
+                // the opened cell's quad children, from its record
+                const int nch = nflags & 0xff;
+                if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    if (c >= nch) break;
+                    const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
+                    if (kind == QK_CELL || kind == QK_LEAF) {
+                        // A cell (summarise() and cell_force() in masked form) or a
+                        // leaf: ch = QCH_LEAF < 0 passes the test, ccnt = 1 makes
+                        // cell_force leaf_force exactly, and a leaf equal to the
+                        // query adds nothing (a cell at D = 0 is never summarised)
+                        if (STATS && act) ++nvis;
+                        const double px = nd.ccx[c], py = nd.ccy[c];
+                        const double dx = qx - px, dy = qy - py;
+                        const double D = __fma_rn(dx, dx, dy * dy);
+                        const double h = nd.ch[c];
+                        bool acc = h < th_lo * D;
+                        if (act && !acc && !(h > th_hi * D))
+                            acc = h / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                        const bool take = act && acc && !(px == qx && py == qy);
+                        const double Q = recip_bh(1.0 + D);
+                        const double mult = (double)nd.ccnt[c] * Q;
+                        const double sc = mult * Q;
+                        fx = __fma_rn(take ? sc : 0.0, dx, fx);
+                        fy = __fma_rn(take ? sc : 0.0, dy, fy);
+                        zs += take ? mult : 0.0;
+                        const bool open = act && !acc;
+                        const uint64_t om = __ballot(open);
+                        if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
+                            const uint64_t am = __ballot(act), tk2 = __ballot(take);
+                            if (am && tk2 == am) {
+                                if (am == __ballot(valid)) ++wfull; else ++wpart;
+                            }
+                        }
+                        if (om) {
+                            if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
+                            ++sp;
+                        }
+                    }
+                }
+                // duplicate kinds (rare), after the others: out of the main loop,
+                // whose accumulators then stay in place
+                if (__builtin_expect((nflags & (0xAA << QNCH_KIND)) != 0, 0)) {
+                    for (int c = 0; c < nch; ++c) {
+                        const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
+                        if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                            if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
+                                if (STATS) ++nvis;
+                                const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                                cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
+                            }
+                        } else if (kind == QK_TIE) {
+                            const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
+                            for (int p = tn.first; p <= tn.last; ++p) {
+                                const double2 pp = pos[p];
+                                if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                            }
                         }
                     }
                 }
             }
         }
-    }
-    if (valid) {
-        F[s] = make_double2(fx, fy);
-        Z[s] = zs;
-    }
-    if (lane == 0) {
-        ttask_n[wid] = ntt;
-        wcost[wid] = npops + (ntilepts >> 6);
-        tcost[wid] = ntilepts + 16 * ntt;
-    }
-    if (COST && bcost) {   // cost of this wave into its first query's 256-query bucket
-        // MODE 1: the wave's own run time (shader clock / 64; the slices only
-        // move work between ranks, every query's sums are unchanged);
-        // MODE 2: cell pops + tile points / 48
-        const unsigned long long c =
-            MODE == 1 ? ((unsigned long long)(clock64() - t_start) >> 6) + 1 : wpops + wtile / 48 + 4;
-        const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
-        if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
-    }
-    if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
-                             // [4] wave-level tile points, [5] lane child evaluations, [6] wave
-                             // child slots, [7..9] heaviest wave ([1], [2]: tile_apply)
-        const unsigned long long tv = wave_sum(nvis), te = wave_sum(nevals);
-        if (lane == 0) {
-            atomicAdd(visits, tv);
-            atomicAdd(visits + 3, wpops);
-            atomicAdd(visits + 4, wtile);
-            atomicAdd(visits + 5, te);
-            atomicAdd(visits + 6, wslots);
-            atomicMax(visits + 7, wpops + wtile / 16);   // heaviest wave (pops + tile points/16)
-            atomicMax(visits + 8, wpops);
-            atomicMax(visits + 9, wtile);
-            atomicAdd(visits + 13, wfull);
-            atomicAdd(visits + 14, wpart);
-            const unsigned long long w_end = wall_clock64();   // [15] longest wave, [16] ~first start,
-            atomicMax(visits + 15, w_end - w_start);            // [17] last end, [18] sum of wave times
-            atomicMax(visits + 16, ~0ull - w_start);
-            atomicMax(visits + 17, w_end);
-            atomicAdd(visits + 18, w_end - w_start);
+        if constexpr (TASK) {   // the task's partial sums; its cost onto the origin wave (next budget)
+            if (finish && src < nsrc_w) {   // a saved wave stack: into the wave's own sums
+                if (valid) {
+                    const double2 f = F[s];
+                    F[s] = make_double2(f.x + fx, f.y + fy);
+                    Z[s] = Z[s] + zs;
+                }
+            } else if (finish) {            // a saved task stack: into that task's partial
+                const int64_t gid = src - nsrc_w;
+                const double2 f = sv.tF[gid * 64 + lane];
+                sv.tF[gid * 64 + lane] = make_double2(f.x + fx, f.y + fy);
+                sv.tZ[gid * 64 + lane] += zs;
+            } else {
+                const int64_t gid = (int64_t)(region - 1) * sv.task_cap + ti;
+                sv.tF[gid * 64 + lane] = make_double2(fx, fy);
+                sv.tZ[gid * 64 + lane] = zs;
+            }
+            if (lane == 0) atomicAdd(&wcost[wid], npops + (ntilepts >> 6));
+        } else {
+            if (valid) {
+                F[s] = make_double2(fx, fy);
+                Z[s] = zs;
+            }
+            if (lane == 0) {
+                ttask_n[wid] = ntt;
+                wcost[wid] = npops + (ntilepts >> 6);
+                tcost[wid] = ntilepts + 16 * ntt;
+            }
         }
+        if (COST && bcost) {   // cost of this wave (or task) into its first query's 256-query bucket
+            // MODE 1: the wave's own run time (shader clock / 64; the slices only
+            // move work between ranks, every query's sums are unchanged);
+            // MODE 2: cell pops + tile points / 48
+            const unsigned long long c =
+                MODE == 1 ? ((unsigned long long)(clock64() - t_start) >> 6) + 1 : wpops + wtile / 48 + 4;
+            const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
+            if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
+        }
+        if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
+                                 // [4] wave-level tile points, [5] lane child evaluations, [6] wave
+                                 // child slots, [7..9] heaviest wave or task ([1], [2]: tile_apply),
+                                 // [23] spill tasks run
+            const unsigned long long tv = wave_sum(nvis), te = wave_sum(nevals);
+            if (lane == 0) {
+                atomicAdd(visits, tv);
+                atomicAdd(visits + 3, wpops);
+                atomicAdd(visits + 4, wtile);
+                atomicAdd(visits + 5, te);
+                atomicAdd(visits + 6, wslots);
+                atomicMax(visits + 7, wpops + wtile / 16);   // heaviest wave (pops + tile points/16)
+                atomicMax(visits + 8, wpops);
+                atomicMax(visits + 9, wtile);
+                atomicAdd(visits + 13, wfull);
+                atomicAdd(visits + 14, wpart);
+                if (TASK) atomicAdd(visits + 23, 1ull);
+                const unsigned long long w_end = wall_clock64();   // [15] longest wave, [16] ~first start,
+                atomicMax(visits + 15, w_end - w_start);            // [17] last end, [18] sum of wave times
+                atomicMax(visits + 16, ~0ull - w_start);
+                atomicMax(visits + 17, w_end);
+                atomicAdd(visits + 18, w_end - w_start);
+            }
+        }
+        if (sp > 0) {   // stopped over budget: hand the remaining stack to the next region
+            int32_t c0 = 0, nc = 0;
+            if (spill_stack(sv, TASK ? region + 1 : 1, lane, sp, sref[w], smask[w], sbm[w], qrec, (int32_t)wid, gpts,
+                            c0, nc)) {
+                if (lane == 0) {
+                    if constexpr (TASK) {
+                        BHTask &me = sv.task[(int64_t)(region - 1) * sv.task_cap + ti];
+                        me.c0 = c0;
+                        me.nc = nc;
+                    } else {
+                        sv.wspill[wid] = make_int2(c0, nc);
+                    }
+                }
+            } else {   // the region is full: save the stack for the finish pass (never full)
+                const int64_t src = TASK ? nsrc_w + (int64_t)(region - 1) * sv.task_cap + ti : wid;
+                for (int i = lane; i < sp; i += 64) {
+                    sv.save_ref[src * STACK + i] = sref[w][i];
+                    sv.save_mask[src * STACK + i] = smask[w][i];
+                }
+                if (lane == 0) sv.ovf[atomicAdd(&sv.cnt[0], 1)] = make_int2((int32_t)src, sp);
+            }
+        }
+    }
+}
+
+// A task's sum = its own partial + its children's sums in spill order (region
+// `region`; its children in region + 1 are final already: bottom-up launches).
+__global__ void task_combine(SpillView sv, int region) {
+    const int64_t ntask = min((int64_t)sv.cnt[2 * region], (int64_t)sv.task_cap);
+    const BHTask *T = sv.task + (int64_t)(region - 1) * sv.task_cap;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ntask * 64;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t ti = e >> 6, lane = e & 63;
+        const BHTask tk = T[ti];
+        if (tk.ne == 0 || tk.nc == 0) continue;
+        const int64_t gid = (int64_t)(region - 1) * sv.task_cap + ti;
+        double2 f = sv.tF[gid * 64 + lane];
+        double z = sv.tZ[gid * 64 + lane];
+        for (int j = 0; j < tk.nc; ++j) {
+            const int64_t cg = (int64_t)region * sv.task_cap + tk.c0 + j;
+            const double2 g = sv.tF[cg * 64 + lane];
+            f.x += g.x;
+            f.y += g.y;
+            z += sv.tZ[cg * 64 + lane];
+        }
+        sv.tF[gid * 64 + lane] = f;
+        sv.tZ[gid * 64 + lane] = z;
+    }
+}
+
+// F, Z of each query += its wave's spilled tasks' sums, in spill order.
+__global__ void wave_spill_combine(SpillView sv, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
+                                   double2 *__restrict__ F, double *__restrict__ Z) {
+    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= g1) return;
+    const int64_t wid = (k - g0) >> 6, lane = (k - g0) & 63;
+    const int2 sp = sv.wspill[wid];
+    if (sp.y == 0) return;
+    const int64_t s = qlist ? (int64_t)qlist[k] : k;
+    double fx = 0.0, fy = 0.0, z = 0.0;
+    for (int j = 0; j < sp.y; ++j) {
+        const int64_t cg = (int64_t)sp.x + j;   // region 1
+        const double2 g = sv.tF[cg * 64 + lane];
+        fx += g.x;
+        fy += g.y;
+        z += sv.tZ[cg * 64 + lane];
+    }
+    const double2 f = F[s];
+    F[s] = make_double2(f.x + fx, f.y + fy);
+    Z[s] = Z[s] + z;
+}
+
+__global__ void set_i32(int32_t *p, int32_t v) {
+    if (threadIdx.x == 0) *p = v;
+}
+
+// The next traversal's pop budget: fac x the mean wave cost of this one (its
+// spilled tasks' costs included), at least bmin.
+__global__ __launch_bounds__(1024) void spill_budget(const int32_t *__restrict__ wcost, int64_t waves,
+                                                     int32_t *__restrict__ budget, double fac, int32_t bmin) {
+    __shared__ long long part[16];
+    long long s = 0;
+    for (int64_t w = threadIdx.x; w < waves; w += blockDim.x) s += max(wcost[w], 0);
+    s = wave_sum(s);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k];
+        const double b = fac * (double)t / (double)max<int64_t>(waves, 1);
+        budget[0] = (int32_t)min(2e9, max((double)bmin, b));
     }
 }
 
@@ -2132,6 +2423,26 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cb, t.ch_C, t.ch_slot0, (int)(qwaves + 1), ctx->stream));
     t.ch_scan_bytes = cb;
     t.ch_scan_tmp = ws.get<uint8_t>("bh.ch_scan_tmp", cb);
+    // spill tasks: per region up to n / 16 tasks (>= 4096) and 4 entries per task
+    SpillView &sv = t.spill;
+    sv.task_cap = (int32_t)std::max<int64_t>(4096, std::min<int64_t>(1 << 22, ceil_div(n, 16)));
+    sv.ent_cap = 4 * sv.task_cap;
+    sv.task = ws.get<BHTask>("bh.sp_task", (size_t)SPILL_PASSES * sv.task_cap);
+    sv.tent_ref = ws.get<int32_t>("bh.sp_eref", (size_t)SPILL_PASSES * sv.ent_cap);
+    sv.tent_mask = ws.get<uint64_t>("bh.sp_emask", (size_t)SPILL_PASSES * sv.ent_cap);
+    sv.cnt = ws.get<int32_t>("bh.sp_cnt", 2 * (SPILL_PASSES + 1));
+    sv.wspill = ws.get<int2>("bh.sp_wave", t.tile_waves);
+    sv.tF = ws.get<double2>("bh.sp_F", (size_t)SPILL_PASSES * sv.task_cap * 64);
+    sv.tZ = ws.get<double>("bh.sp_Z", (size_t)SPILL_PASSES * sv.task_cap * 64);
+    sv.budget = ws.get<int32_t>("bh.sp_budget", 2);
+    sv.nwaves = t.tile_waves;
+    const int64_t nsrc = t.tile_waves + (int64_t)SPILL_PASSES * sv.task_cap;
+    sv.save_ref = ws.get<int32_t>("bh.sp_sref", (size_t)nsrc * STACK);
+    sv.save_mask = ws.get<uint64_t>("bh.sp_smask", (size_t)nsrc * STACK);
+    sv.ovf = ws.get<int2>("bh.sp_ovf", (size_t)nsrc);
+    const int32_t no_budget[2] = {INT32_MAX, 0};   // the first traversal: no spill (no wave costs yet)
+    TSNE_HIP(hipMemcpyAsync(sv.budget, no_budget, sizeof(no_budget), hipMemcpyHostToDevice, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 // Cost-balanced query slices for the next iteration: one 1024-thread block
@@ -2200,7 +2511,16 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     TSNE_HIP(hipMemsetAsync(t.dflag, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(bbox_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
     hipLaunchKernelGGL(bbox_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta, t.bb);
-    if (root_tile_ok) {   // one small read-back decides the path (the host must know which kernels to launch)
+    if (root_tile_ok) {   // small read-backs decide the path (the host must know which kernels to launch)
+        // the box conditions first (dflag still 0): once the embedding has
+        // outgrown the root tile, the duplicate rounds (~90 us at 1M) are skipped
+        hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, bh_near_dmax(theta),
+                           t.status);
+        TSNE_HIP(hipMemcpyAsync(t.status_h, t.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        TSNE_HIP(hipStreamSynchronize(st));
+        if (!t.status_h[0]) root_tile_ok = false;
+    }
+    if (root_tile_ok) {
         const auto Y2 = reinterpret_cast<const double2 *>(dY);
         for (int r = 0; r < DUP_ROUNDS; ++r) {
             hipLaunchKernelGGL(dup_store, dim3(ceil_div(n, 256)), dim3(256), 0, st, Y2, n, t.dup_tab, t.dup_mask,
@@ -2307,8 +2627,25 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the wave's pops and tile points
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    auto kern = kp >= 8 ? (mode == 2 ? bh_traverse<8, 2> : mode == 1 ? bh_traverse<8, 1> : bh_traverse<8, 0>)
-                        : (mode == 2 ? bh_traverse<4, 2> : mode == 1 ? bh_traverse<4, 1> : bh_traverse<4, 0>);
+    auto kern = kp >= 8 ? (mode == 2 ? bh_traverse<8, 2, false> : mode == 1 ? bh_traverse<8, 1, false> : bh_traverse<8, 0, false>)
+                        : (mode == 2 ? bh_traverse<4, 2, false> : mode == 1 ? bh_traverse<4, 1, false> : bh_traverse<4, 0, false>);
+    auto tkern = mode == 2 ? bh_traverse<4, 2, true> : mode == 1 ? bh_traverse<4, 1, true> : bh_traverse<4, 0, true>;
+    // dynamic splitting of heavy waves (TSNE_BH_SPILL=0: off); budget = TSNE_BH_BUDGET
+    // (default 2) x the previous traversal's mean wave cost, spill groups of
+    // TSNE_BH_GROUP (default 2) x budget points
+    static const bool spill_on = [] { const char *e = getenv("TSNE_BH_SPILL"); return !(e && e[0] == '0'); }();
+    static const double bfac = [] { const char *e = getenv("TSNE_BH_BUDGET"); return e ? atof(e) : 2.0; }();
+    static const int gfac = [] { const char *e = getenv("TSNE_BH_GROUP"); return e ? std::max(1, atoi(e)) : 2; }();
+    static const int32_t bmin = [] { const char *e = getenv("TSNE_BH_BUDGET_MIN"); return e ? std::max(1, atoi(e)) : 256; }();
+    SpillView sv;
+    if (spill_on) {
+        sv = t.spill;
+        sv.gfac = gfac;
+        TSNE_HIP(hipMemsetAsync(sv.cnt, 0, sizeof(int32_t) * 2 * (SPILL_PASSES + 1), ctx->stream));
+        // TSNE_BH_BUDGET_FIXED=N (read per call; tests): this traversal's budget is N pops
+        if (const char *e = getenv("TSNE_BH_BUDGET_FIXED"))
+            hipLaunchKernelGGL(set_i32, dim3(1), dim3(64), 0, ctx->stream, sv.budget, std::max(1, atoi(e)));
+    }
     // longest-first block orders, TSNE_BH_ORDER bits: 1 traversal (by the
     // previous traversal's wave costs), 2 tile_apply (by this traversal's
     // tile points); default 2 -- the traversal keeps launch order, whose
@@ -2324,7 +2661,15 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
                        t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd,
-                       (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost);
+                       (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost, sv, 0);
+    if (spill_on) {   // task passes over regions 1..P (fixed grid: one wave per SIMD slot of every CU)
+        const int tgrid = ctx->cu_count * 8;
+        // regions 1..P, then the finish pass (region P + 1) over stacks saved when a region was full
+        for (int r = 1; r <= SPILL_PASSES + 1; ++r)
+            hipLaunchKernelGGL(tkern, dim3(tgrid), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.qrec, t.ttask,
+                               t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd, (int32_t)t.n, dF,
+                               dz, visits, bcost, border, t.wcost, t.tcost, sv, r);
+    }
     t.have_cost = true;
     // tile chunks of heavy waves (ChunkView; TSNE_TILE_CHUNK=0: one tile_apply wave per traversal wave)
     static const bool chunk_on = [] { const char *e = getenv("TSNE_TILE_CHUNK"); return !(e && e[0] == '0'); }();
@@ -2359,6 +2704,14 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     if (cv.slot_w)
         hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.ch_Fp, t.ch_Zp,
                            t.ch_C, t.ch_slot0, s0, s1, qlist, dF, dz);
+    if (spill_on) {   // spilled tasks' sums, bottom-up, then into F, Z; the next budget
+        const int cgrid = ctx->cu_count * 4;
+        for (int r = SPILL_PASSES - 1; r >= 1; --r)
+            hipLaunchKernelGGL(task_combine, dim3(cgrid), dim3(256), 0, ctx->stream, sv, r);
+        hipLaunchKernelGGL(wave_spill_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, sv, s0, s1,
+                           qlist, dF, dz);
+        hipLaunchKernelGGL(spill_budget, dim3(1), dim3(1024), 0, ctx->stream, t.wcost, waves, sv.budget, bfac, bmin);
+    }
     TSNE_LAUNCH_CHECK();
 }
 

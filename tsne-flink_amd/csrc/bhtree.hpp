@@ -12,6 +12,34 @@ struct TileTask {
     uint64_t mask;
 };
 
+// Spill tasks of the traversal (bhtree.hip "Dynamic splitting"): a task is
+// the 64 queries of wave `wid` over a contiguous run of stack entries of its
+// region; its own spill (children in the next region) is [c0, c0 + nc).
+constexpr int SPILL_PASSES = 4;   // task regions 1..SPILL_PASSES after the query-wave pass
+constexpr int TASK_ENT = 16;      // stack entries per task at most
+struct BHTask {
+    int32_t wid;
+    int32_t e0, ne;
+    int32_t c0, nc;
+    int32_t pad[3];
+};
+struct SpillView {
+    BHTask *task = nullptr;          // region r (1..SPILL_PASSES) at (r - 1) * task_cap
+    int32_t *tent_ref = nullptr;     // stack entries, region r at (r - 1) * ent_cap
+    uint64_t *tent_mask = nullptr;
+    int32_t *cnt = nullptr;          // [2 r]: tasks, [2 r + 1]: entries allocated in region r
+    int2 *wspill = nullptr;          // per query wave: its spill (children in region 1)
+    double2 *tF = nullptr;           // per task (global id (r - 1) * task_cap + i) x 64 lanes
+    double *tZ = nullptr;
+    int32_t *budget = nullptr;       // [0] the traversal's pop budget
+    int32_t *save_ref = nullptr;     // saved stacks (a spill that found its region full), STACK per source:
+    uint64_t *save_mask = nullptr;   //   waves [0, nwaves), then tasks by global id
+    int2 *ovf = nullptr;             // (source, depth) of every saved stack; cnt[0] of them
+    int64_t nwaves = 0;
+    int32_t task_cap = 0, ent_cap = 0;
+    int32_t gfac = 2;                // spill group size: gfac x budget points
+};
+
 // Internal node of the binary radix tree over sorted Morton keys.  A node
 // whose common prefix ends inside a quad level is "transparent" (h == 0:
 // always opened); otherwise it IS the reference quadtree cell of half width
@@ -135,6 +163,8 @@ struct BHTree {
     double *ch_Zp = nullptr;
     void *ch_scan_tmp = nullptr;
     size_t ch_scan_bytes = 0;
+    // spill tasks of heavy traversal waves (SpillView)
+    SpillView spill;
 };
 
 // Allocate (from ctx->ws) for n points.

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <exception>
 #include <new>
+#include <algorithm>
 #include <thread>
 
 #include "bhtree.hpp"
@@ -131,6 +132,28 @@ int tsne_metric_from_name(const char *name, int32_t *metric_out) {
         else if (m == "cosine") v = TSNE_METRIC_COSINE;
         else fail(TSNE_ERR_ARG, "Metric '" + m + "' not defined");  // Tsne.scala:166
         if (metric_out) *metric_out = v;
+    });
+}
+
+int tsne_coo_to_csr(const int32_t *row, const int32_t *col, const double *val, int64_t nnz, int64_t n,
+                    int64_t *row_ptr_out, int32_t *col_out, double *val_out) {
+    return guard([&] {
+        TSNE_REQUIRE(nnz >= 0 && n >= 0 && row_ptr_out != nullptr, "bad arguments");
+        TSNE_REQUIRE(nnz == 0 || (row && col && col_out), "NULL buffer");
+        TSNE_REQUIRE((val == nullptr) == (val_out == nullptr), "val and val_out go together");
+        std::fill(row_ptr_out, row_ptr_out + n + 1, (int64_t)0);
+        for (int64_t e = 0; e < nnz; ++e) {
+            const int32_t r = row[e];
+            if (r < 0 || r >= n) fail(TSNE_ERR_ARG, "row index " + std::to_string(r) + " out of [0, n)");
+            ++row_ptr_out[r + 1];
+        }
+        for (int64_t r = 0; r < n; ++r) row_ptr_out[r + 1] += row_ptr_out[r];
+        std::vector<int64_t> next(row_ptr_out, row_ptr_out + n);   // stable: input order within a row
+        for (int64_t e = 0; e < nnz; ++e) {
+            const int64_t o = next[row[e]]++;
+            col_out[o] = col[e];
+            if (val_out) val_out[o] = val[e];
+        }
     });
 }
 

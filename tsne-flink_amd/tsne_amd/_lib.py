@@ -43,6 +43,7 @@ SIGNATURES = {
     "tsne_params_default": (None, [C.POINTER(Params)]),
     "tsne_metric_from_name": (C.c_int, [C.c_char_p, PI32]),
     "tsne_shard_rows": (C.c_int, [I64, I32, I32, PI64, PI64]),
+    "tsne_coo_to_csr": (C.c_int, [P, P, P, I64, I64, P, P, P]),
     "tsne_balance_cuts": (C.c_int, [P, I64, I64, I32, I32, P]),
     "tsne_dev_balance_cuts": (C.c_int, [P, P, I64, I32, P]),
     "tsne_ctx_create": (C.c_int, [I32, C.POINTER(P)]),
