@@ -15,6 +15,16 @@
 /* ------------------------------------------------------------------ metrics */
 
 /* breeze squaredDistance: sequential sum of (a_i - b_i)^2 in index order. */
+/* Neumaier-compensated running sum for the KL loss: a sequential sum over
+ * ~1e8 terms drifts by up to n*eps relative (1e-8 at C3's size), more than
+ * the 1e-9 the loss is checked at; the reference's reduce order is Flink's
+ * anyway (TsneHelpers.scala:297-299), so the exact sum is the oracle. */
+static void kahan_add(double *s, double *c, double x) {
+    const double t = *s + x;
+    *c += fabs(*s) >= fabs(x) ? (*s - t) + x : (x - t) + *s;
+    *s = t;
+}
+
 static double sqdist(const double *a, const double *b, int32_t d) {
     double s = 0.0;
     for (int32_t i = 0; i < d; ++i) {
@@ -377,7 +387,7 @@ int oracle_gradient(const int64_t *row_ptr, const int32_t *col, const double *va
     free(t.v);
     double Z = 0.0;                                  /* sumQ reduce (TsneHelpers.scala:266) */
     for (int64_t i = 0; i < n; ++i) Z = Z + zi[i];
-    double loss = 0.0;
+    double loss = 0.0, loss_c = 0.0;
     for (int64_t i = 0; i < n; ++i) {
         double gx = 0.0, gy = 0.0;
         const double *yi = Y + 2 * i;
@@ -388,14 +398,14 @@ int oracle_gradient(const int64_t *row_ptr, const int32_t *col, const double *va
             double s = pij * qij;
             gx = gx + s * (yi[0] - yj[0]);
             gy = gy + s * (yi[1] - yj[1]);
-            if (loss_out) loss += pij * log(pij / (qij / Z));
+            if (loss_out) kahan_add(&loss, &loss_c, pij * log(pij / (qij / Z)));
         }
         if (attr_out) { attr_out[2 * i] = gx; attr_out[2 * i + 1] = gy; }
         grad[2 * i] = gx - rep[2 * i] / Z;           /* attrForce - repForce / sumQ */
         grad[2 * i + 1] = gy - rep[2 * i + 1] / Z;
     }
     if (sumq_out) *sumq_out = Z;
-    if (loss_out) *loss_out = loss;
+    if (loss_out) *loss_out = loss + loss_c;
     if (rep_out) memcpy(rep_out, rep, sizeof(double) * 2 * (size_t)n);
     if (zi_out) memcpy(zi_out, zi, sizeof(double) * (size_t)n);
     free(rep); free(zi);
@@ -486,7 +496,7 @@ int oracle_attraction_rows(const int64_t *row_ptr, const int32_t *col, const dou
                            const double *Y, int metric, double exaggeration, const double *rep,
                            double Z, int64_t r0, int64_t r1, double *grad, double *loss) {
     if (!row_ptr || !Y || r0 < 0 || r1 > n || r0 > r1) return -1;
-    double l = 0.0;
+    double l = 0.0, l_c = 0.0;
     for (int64_t i = r0; i < r1; ++i) {
         double gx = 0.0, gy = 0.0;
         const double *yi = Y + 2 * i;
@@ -497,12 +507,12 @@ int oracle_attraction_rows(const int64_t *row_ptr, const int32_t *col, const dou
             double s = pij * qij;
             gx = gx + s * (yi[0] - yj[0]);
             gy = gy + s * (yi[1] - yj[1]);
-            if (loss) l += pij * log(pij / (qij / Z));
+            if (loss) kahan_add(&l, &l_c, pij * log(pij / (qij / Z)));
         }
         grad[2 * (i - r0)] = gx - rep[2 * i] / Z;
         grad[2 * (i - r0) + 1] = gy - rep[2 * i + 1] / Z;
     }
-    if (loss) *loss = l;
+    if (loss) *loss = l + l_c;
     return 0;
 }
 
@@ -649,7 +659,7 @@ int oracle_gradient3(const int64_t *row_ptr, const int32_t *col, const double *v
     free(t.v);
     double Z = 0.0;
     for (int64_t i = 0; i < n; ++i) Z = Z + zi[i];
-    double loss = 0.0;
+    double loss = 0.0, loss_c = 0.0;
     for (int64_t i = 0; i < n; ++i) {
         double g[3] = {0, 0, 0};
         const double *yi = Y + 3 * i;
@@ -659,12 +669,12 @@ int oracle_gradient3(const int64_t *row_ptr, const int32_t *col, const double *v
             double qij = 1.0 / (1.0 + oracle_metric(yi, yj, 3, metric));
             double s = pij * qij;
             for (int k = 0; k < 3; ++k) g[k] = g[k] + s * (yi[k] - yj[k]);
-            if (loss_out) loss += pij * log(pij / (qij / Z));
+            if (loss_out) kahan_add(&loss, &loss_c, pij * log(pij / (qij / Z)));
         }
         for (int k = 0; k < 3; ++k) grad[3 * i + k] = g[k] - rep[3 * i + k] / Z;
     }
     if (sumq_out) *sumq_out = Z;
-    if (loss_out) *loss_out = loss;
+    if (loss_out) *loss_out = loss + loss_c;
     if (rep_out) memcpy(rep_out, rep, sizeof(double) * 3 * (size_t)n);
     if (zi_out) memcpy(zi_out, zi, sizeof(double) * (size_t)n);
     free(rep); free(zi);
@@ -716,7 +726,7 @@ int oracle_attraction3_rows(const int64_t *row_ptr, const int32_t *col, const do
                             const double *Y, int metric, double exaggeration, const double *rep,
                             double Z, int64_t r0, int64_t r1, double *grad, double *loss) {
     if (!row_ptr || !Y || r0 < 0 || r1 > n || r0 > r1) return -1;
-    double l = 0.0;
+    double l = 0.0, l_c = 0.0;
     for (int64_t i = r0; i < r1; ++i) {
         double g[3] = {0, 0, 0};
         const double *yi = Y + 3 * i;
@@ -726,11 +736,11 @@ int oracle_attraction3_rows(const int64_t *row_ptr, const int32_t *col, const do
             double qij = 1.0 / (1.0 + oracle_metric(yi, yj, 3, metric));
             double s = pij * qij;
             for (int k = 0; k < 3; ++k) g[k] = g[k] + s * (yi[k] - yj[k]);
-            if (loss) l += pij * log(pij / (qij / Z));
+            if (loss) kahan_add(&l, &l_c, pij * log(pij / (qij / Z)));
         }
         for (int k = 0; k < 3; ++k) grad[3 * (i - r0) + k] = g[k] - rep[3 * i + k] / Z;
     }
-    if (loss) *loss = l;
+    if (loss) *loss = l + l_c;
     return 0;
 }
 

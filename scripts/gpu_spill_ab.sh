@@ -10,6 +10,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_spill.py -m gpu -x -v -p no
 B="python bench.py --no-cpu-baseline"
 timeout -k 10 300 $B > gpurun_out/spill_on.json 2> gpurun_out/spill_on.err || exit $?
 TSNE_BH_SPILL=0 timeout -k 10 300 $B --trace 0 > gpurun_out/spill_off.json 2> gpurun_out/spill_off.err || exit $?
+TSNE_OVERLAP=none timeout -k 10 300 $B > gpurun_out/spill_on_serial.json 2> gpurun_out/spill_on_serial.err || exit $?
 if [ "${RUN_SUITE:-1}" = 1 ]; then
   timeout -k 10 1200 python -u -m pytest tests -m gpu --maxfail=3 -v -p no:cacheprovider --timeout 600 \
     --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit $?

@@ -27,6 +27,7 @@ identities -- and end to end where the whole problem is small (C1):
       KL loss over all rows at 1e-9 (the oracle's attraction + loss with the
       same Z).
 """
+import math
 import re
 import subprocess
 from pathlib import Path
@@ -215,7 +216,21 @@ def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, 
     assert np.abs(Y1.mean(0)).max() <= 1e-9 * np.abs(Y1).max(), (t, "centred")
     if loss_gpu is not None:
         _, l_o = attr(*P, Y0, np.zeros((n, c)), Z, 0, n, metric=metric, exaggeration=ex, want_loss=True)
-        assert abs(loss_gpu - l_o) <= 1e-9 * abs(l_o), (t, loss_gpu, l_o)
+        if not abs(loss_gpu - l_o) <= 1e-9 * abs(l_o):   # diagnostics: the attract_rows loss, the sum of P
+            _, Zg, l_rows = ctx.gradient(*P, Y0, theta, metric, exaggeration=ex, want_loss=True)
+            info = dict(t=t, loss_opt=loss_gpu, loss_oracle=l_o, loss_attract_rows=l_rows, Zopt=Z,
+                        Zrep=z.sum(), Zgrad=Zg, sumP=float(P[2].sum()))
+            if metric == "sqeuclidean" and c == 2:   # an independent numpy restatement, exact sum
+                rp, cl, pv = P
+                rows = np.repeat(np.arange(n), np.diff(rp))
+                d = Y0[rows] - Y0[cl]
+                q = 1.0 / (1.0 + (d * d).sum(1))
+                pij = pv * ex
+                terms = pij * np.log(pij / (q / Z))
+                info.update(loss_numpy=math.fsum(terms), self_pairs=int((rows == cl).sum()),
+                            nonpos=int((pv <= 0).sum()), nonfinite=int((~np.isfinite(terms)).sum()),
+                            max_term=float(np.abs(terms).max()), nnz=len(pv))
+            assert False, repr(info)
 
 
 def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, grad_rows, q0, stop=None, steps=()):

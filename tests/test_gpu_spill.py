@@ -27,17 +27,20 @@ def ctx():
 
 
 class budget:
-    """TSNE_BH_BUDGET_FIXED for the calls inside the block (read per traversal)."""
+    """Spill on (TSNE_BH_SPILL=1, off by default) with TSNE_BH_BUDGET_FIXED for
+    the calls inside the block (both read per traversal)."""
 
     def __init__(self, pops):
         self.pops = pops
 
     def __enter__(self):
+        os.environ["TSNE_BH_SPILL"] = "1"
         if self.pops is not None:
             os.environ["TSNE_BH_BUDGET_FIXED"] = str(self.pops)
 
     def __exit__(self, *a):
         os.environ.pop("TSNE_BH_BUDGET_FIXED", None)
+        os.environ.pop("TSNE_BH_SPILL", None)
 
 
 def clustered(n, seed):
@@ -112,7 +115,7 @@ def test_optimizer_with_spills_deterministic(ctx):
     Ya, la = run(8)
     Yb, lb = run(8)
     assert np.array_equal(Ya, Yb) and la == lb
-    Yc, lc = run(None)
+    Yc, lc = run(None)   # spill on, the default budget rule
     assert sorted(la) == sorted(lc)
     assert np.abs(Ya - Yc).max() <= 1e-8 * np.abs(Yc).max()
     for t in lc:

@@ -1351,8 +1351,9 @@ __device__ bool spill_stack(const SpillView &sv, int r, int lane, int sp, const 
     int before = 0;
 #pragma unroll 1
     for (int q = 0; q < nr; ++q) {   // one task per group: its first entry and length
-        const uint64_t bm = __builtin_amdgcn_readfirstlane(sbm_w[q] & 0xffffffffull) |
-                            ((uint64_t)__builtin_amdgcn_readfirstlane(sbm_w[q] >> 32) << 32);
+        const uint64_t v = sbm_w[q];   // wave-uniform: its two halves to scalar registers (zero-extended)
+        const uint64_t bm = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
         const int i = q * 64 + lane;
         if ((bm >> lane) & 1ull) {
             const int gi = before + (int)__popcll(bm & lanemask_lt());
@@ -2630,10 +2631,11 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     auto kern = kp >= 8 ? (mode == 2 ? bh_traverse<8, 2, false> : mode == 1 ? bh_traverse<8, 1, false> : bh_traverse<8, 0, false>)
                         : (mode == 2 ? bh_traverse<4, 2, false> : mode == 1 ? bh_traverse<4, 1, false> : bh_traverse<4, 0, false>);
     auto tkern = mode == 2 ? bh_traverse<4, 2, true> : mode == 1 ? bh_traverse<4, 1, true> : bh_traverse<4, 0, true>;
-    // dynamic splitting of heavy waves (TSNE_BH_SPILL=0: off); budget = TSNE_BH_BUDGET
-    // (default 2) x the previous traversal's mean wave cost, spill groups of
-    // TSNE_BH_GROUP (default 2) x budget points
-    static const bool spill_on = [] { const char *e = getenv("TSNE_BH_SPILL"); return !(e && e[0] == '0'); }();
+    // dynamic splitting of heavy waves (TSNE_BH_SPILL=1: on; off by default --
+    // measured without gain over the C3 schedule); budget =
+    // TSNE_BH_BUDGET (default 2) x the previous traversal's mean wave cost,
+    // spill groups of TSNE_BH_GROUP (default 2) x budget points
+    const bool spill_on = [] { const char *e = getenv("TSNE_BH_SPILL"); return e && e[0] == '1'; }();   // per call
     static const double bfac = [] { const char *e = getenv("TSNE_BH_BUDGET"); return e ? atof(e) : 2.0; }();
     static const int gfac = [] { const char *e = getenv("TSNE_BH_GROUP"); return e ? std::max(1, atoi(e)) : 2; }();
     static const int32_t bmin = [] { const char *e = getenv("TSNE_BH_BUDGET_MIN"); return e ? std::max(1, atoi(e)) : 256; }();

@@ -142,6 +142,18 @@ class Context:
 
     def set_stream(self, stream_ptr):
         check(lib().tsne_ctx_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+        self._stream_ptr = int(stream_ptr or 0)
+
+    def _fence(self, t):
+        """The dev_* operators read torch tensors on the context's stream: unless
+        that is torch's current stream (set_stream), wait for torch's current
+        stream first, so inputs torch just produced are complete (the context's
+        own stream is non-blocking; the null stream cannot be shared).  Outputs
+        are ready after synchronize()."""
+        import torch
+        s = torch.cuda.current_stream(t.device)
+        if not getattr(self, "_stream_ptr", 0) or s.cuda_stream != self._stream_ptr:
+            s.synchronize()
 
     def synchronize(self):
         check(lib().tsne_ctx_synchronize(self._h))
@@ -222,6 +234,7 @@ class Context:
         return F, z
 
     def dev_repulsion(self, dY, theta, dF, dz):
+        self._fence(dY)
         n, c = dY.shape
         check(lib().tsne_dev_repulsion(self._h, _ptr(dY), n, c, theta, _ptr(dF), _ptr(dz)))
 
@@ -266,19 +279,23 @@ class Context:
 
     # ---- device operators (torch CUDA tensors)
     def dev_knn(self, dX, k, metric, q0, q1, d_idx, d_dist):
+        self._fence(dX)
         n, d = dX.shape
         check(lib().tsne_dev_knn(self._h, _ptr(dX), n, d, METRICS[metric], k, q0, q1, _ptr(d_idx), _ptr(d_dist)))
 
     def dev_affinities(self, d_row_ptr, d_dist, nrows, perplexity, d_p):
+        self._fence(d_dist)
         check(lib().tsne_dev_pairwise_affinities(self._h, _ptr(d_row_ptr), _ptr(d_dist), nrows, perplexity, _ptr(d_p)))
 
     def dev_joint(self, d_row_ptr, d_col, d_p, n, cap, d_orp, d_oc, d_ov):
+        self._fence(d_p)
         nnz = C.c_int64()
         check(lib().tsne_dev_joint_distribution(self._h, _ptr(d_row_ptr), _ptr(d_col), _ptr(d_p), n, cap,
                                                 _ptr(d_orp), _ptr(d_oc), _ptr(d_ov), C.byref(nnz)))
         return nnz.value
 
     def dev_opt_setup(self, params, d_row_ptr, d_col, d_P, n, dY, dupd, dgains):
+        self._fence(dY)
         check(lib().tsne_dev_opt_setup(self._h, C.byref(params), _ptr(d_row_ptr), _ptr(d_col), _ptr(d_P), n,
                                        _ptr(dY), _ptr(dupd), _ptr(dgains)))
 
@@ -304,6 +321,7 @@ class Context:
 
     def dev_balance_cuts(self, bcost, n, world, bounds):
         """tsne_dev_balance_cuts on device tensors (uint64/int64 bucket costs, int64 bounds[world+1])."""
+        self._fence(bcost)
         check(lib().tsne_dev_balance_cuts(self._h, _ptr(bcost), n, world, _ptr(bounds)))
 
     def dev_opt_attract_log(self):
