@@ -1174,7 +1174,10 @@ __global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict_
             v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
             v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
             v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.ch[0] = nd.h; v.cref[0] = i; v.ccnt[0] = nd.cnt;
-            for (int k = 1; k < 4; ++k) { v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.ch[k] = QCH_LEAF; v.cref[k] = 0; v.ccnt[k] = 0; }
+            v.ca[0] = nd.h * inv_theta * (1.0 + QACC_MARGIN);
+            for (int k = 1; k < 4; ++k) {
+                v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.ch[k] = QCH_LEAF; v.ca[k] = 0.0; v.cref[k] = 0; v.ccnt[k] = 0;
+            }
             qrec[dv.virt + i] = v;
         }
     }
@@ -1202,7 +1205,7 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     auto put = [&](int32_t c) {
         if (c < 0) {
             const double2 p = pos[~c];
-            r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ch[nc] = QCH_LEAF; r.cref[nc] = c; r.ccnt[nc] = 1;
+            r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ch[nc] = QCH_LEAF; r.ca[nc] = 0.0; r.cref[nc] = c; r.ccnt[nc] = 1;
         } else {
             const BHNode &cn = nodes[c];
             r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; r.ch[nc] = cn.delta >= 62 ? QCH_TIE : cn.h;
@@ -1214,6 +1217,7 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
                 r.ccx[nc] = dv.vcom[2 * c]; r.ccy[nc] = dv.vcom[2 * c + 1]; r.ch[nc] = 0.5 * nd.h;
                 r.cref[nc] = dv.virt + c; r.ccnt[nc] = dv.vcntf[c];
             }
+            r.ca[nc] = r.ch[nc] > 0.0 ? r.ch[nc] * inv_theta * (1.0 + QACC_MARGIN) : 0.0;
         }
         ++nc;
     };
@@ -1230,7 +1234,9 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
         }
     }
     (void)ncand;
-    for (int k = nc; k < 4; ++k) { r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ch[k] = QCH_LEAF; r.cref[k] = 0; r.ccnt[k] = 0; }
+    for (int k = nc; k < 4; ++k) {
+        r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ch[k] = QCH_LEAF; r.ca[k] = 0.0; r.cref[k] = 0; r.ccnt[k] = 0;
+    }
     // QNCH_TILE: some query could pass an all-open test here.  The box test's
     // max corner distance is at least the squared half-diagonal, so if that
     // exceeds both hmin / theta and near_dmax (and rball = 0) no query can.
@@ -1601,36 +1607,45 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     if (c >= nch) break;
                     const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
                     if (kind == QK_CELL || kind == QK_LEAF) {
-                        // A cell (summarise() and cell_force() in masked form) or a
-                        // leaf: ch = QCH_LEAF < 0 passes the test, ccnt = 1 makes
-                        // cell_force leaf_force exactly, and a leaf equal to the
-                        // query adds nothing (a cell at D = 0 is never summarised)
+                        // A leaf (cumSize 1, com = the point) always interacts, zero if
+                        // it is the query's own point (x - y == 0 iff x == y).  A cell is
+                        // summarised when ch / D < theta (QACC_BAND: two compares against
+                        // the record's bound, the exact quotient only inside the band;
+                        // at D = 0 never).  wm = the term's multiplicity where taken, else
+                        // 0: a zero term leaves the sums bit-equal.  Only wm is computed
+                        // per kind (uniform branch), so the accumulators stay in place.
                         if (STATS && act) ++nvis;
-                        const double px = nd.ccx[c], py = nd.ccy[c];
-                        const double dx = qx - px, dy = qy - py;
+                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
                         const double D = __fma_rn(dx, dx, dy * dy);
-                        const double h = nd.ch[c];
-                        bool acc = h < th_lo * D;
-                        if (act && !acc && !(h > th_hi * D))
-                            acc = h / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
-                        const bool take = act && acc && !(px == qx && py == qy);
+                        bool take;
+                        double wm;
+                        if (kind == QK_LEAF) {
+                            take = act && !(dx == 0.0 && dy == 0.0);
+                            wm = take ? 1.0 : 0.0;
+                        } else {
+                            const double A = nd.ca[c];
+                            bool acc = D > A;
+                            if (act && !acc && !(D < A * QACC_BAND))
+                                acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                            take = act && acc;
+                            wm = (double)(take ? nd.ccnt[c] : 0);
+                            const uint64_t om = __ballot(act && !acc);
+                            if (om) {
+                                if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
+                                ++sp;
+                            }
+                        }
                         const double Q = recip_bh(1.0 + D);
-                        const double mult = (double)nd.ccnt[c] * Q;
+                        const double mult = wm * Q;
                         const double sc = mult * Q;
-                        fx = __fma_rn(take ? sc : 0.0, dx, fx);
-                        fy = __fma_rn(take ? sc : 0.0, dy, fy);
-                        zs += take ? mult : 0.0;
-                        const bool open = act && !acc;
-                        const uint64_t om = __ballot(open);
+                        fx = __fma_rn(sc, dx, fx);
+                        fy = __fma_rn(sc, dy, fy);
+                        zs += mult;
                         if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
                             const uint64_t am = __ballot(act), tk2 = __ballot(take);
                             if (am && tk2 == am) {
                                 if (am == __ballot(valid)) ++wfull; else ++wpart;
                             }
-                        }
-                        if (om) {
-                            if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
-                            ++sp;
                         }
                     }
                 }

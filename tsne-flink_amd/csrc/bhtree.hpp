@@ -81,8 +81,14 @@ struct __attribute__((aligned(16))) QRec {
     int32_t first, last;        // leaf range in sorted order
     int32_t cnt, nch;           // cumSize, number of quad children | QNCH_TILE
     double ccx[4], ccy[4], ch[4];
+    double ca[4];               // cells: the sure-accept bound on D, ch / theta (1 + 2.5e-14) (see QACC_BAND)
     int32_t cref[4], ccnt[4];
 };
+// A cell child is summarised for sure when D > ca, opened for sure when
+// D < ca * QACC_BAND (= ch / theta (1 - 2.5e-14)); in between, the exact
+// IEEE quotient ch / D < theta decides (the reference's test, QuadTree.scala:134).
+constexpr double QACC_MARGIN = 2.5e-14;
+constexpr double QACC_BAND = (1.0 - QACC_MARGIN) / (1.0 + QACC_MARGIN);
 
 struct BHTree {
     int64_t n = 0;           // points (queries)
