@@ -118,6 +118,11 @@ struct BHTree {
     double *agg = nullptr;      // per-node bottom-up aggregates (AGG doubles)
     int32_t *parent_leaf = nullptr, *parent_node = nullptr;
     int32_t *arrive = nullptr;
+    // two-phase bottom-up (bottom_up_intra / bottom_up_top): frontier-subtree
+    // start marks (= gen of the build that set them), phase-2 arrival list
+    int32_t *fstart = nullptr, *top_list = nullptr, *top_cnt = nullptr;
+    int32_t gen = 0;
+    int rt_skip = 0;            // builds left before the root-tile test is tried again
     int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref, [2] = moment nodes
     // subtree moments (see bhtree.hip "Subtree moments"): per internal node
     // MOM_K scaled moments about its bounding-box centre, for nodes of
