@@ -501,7 +501,7 @@ __device__ __forceinline__ void bu_leaf(const double2 *__restrict__ pos, int s, 
 // them) and appends the parent to the arrival list of phase 2, as does a leaf
 // whose parent lies outside.  Nothing waits on another workgroup, so a
 // workgroup's run is its own short climb.
-__global__ __launch_bounds__(1024) void bottom_up_intra(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
+__global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
                                                         const double *__restrict__ Wp, double inv_theta, BHNode *nodes,
                                                         double *__restrict__ agg, const int32_t *__restrict__ parent_leaf,
                                                         const int32_t *__restrict__ parent_node,
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(1024) void bottom_up_intra(const double2 *__restric
     if (t < 2) sS[t] = INT32_MAX;
     __syncthreads();
     // a frontier subtree starts within any BU_FRONT + 1 consecutive leaves
-    for (int j = t; j < 2 * (BU_FRONT + 1); j += 1024) {
+    for (int j = t; j < 2 * (BU_FRONT + 1); j += BU_NB) {
         const int side = j / (BU_FRONT + 1);
         const int p = (b + side) * BU_NB + (j - side * (BU_FRONT + 1));
         if (p < m && fstart[p] == gen) atomicMin(&sS[side], p);
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(1024) void bottom_up_intra(const double2 *__restric
     __syncthreads();
     const int S0 = b == 0 ? 0 : min(sS[0], m);
     const int S1 = (b + 1) * BU_NB >= m ? m : min(sS[1], m);
-    for (int j = t; j < S1 - S0; j += 1024) {
+    for (int j = t; j < S1 - S0; j += BU_NB) {
         const int q = S0 + j;
         larr[j] = 0;
         if (q < m - 1) {
@@ -544,7 +544,7 @@ __global__ __launch_bounds__(1024) void bottom_up_intra(const double2 *__restric
     __syncthreads();
     const double W = *Wp;
     auto in_blk = [&](int q) { return q >= S0 && q < S1 && lfirst[q - S0] >= S0 && llast[q - S0] < S1; };
-    for (int s = S0 + t; s < S1; s += 1024) {
+    for (int s = S0 + t; s < S1; s += BU_NB) {
         int p = parent_leaf[s];
         if (p < 0) continue;
         if (!in_blk(p)) {   // a leaf hanging off a node above the frontier
@@ -1239,6 +1239,8 @@ struct ChunkView {
     double *Zp = nullptr;
 };
 constexpr int CHUNK_MAX = 32;
+constexpr int LW_CHUNK = 256;   // tile_apply pack 3: small tiles per lane-wise chunk
+constexpr int LW_D = 6;         // ... point loads in flight per lane
 constexpr int CHUNK_MIN = 4096;
 __global__ void chunk_total(const int32_t *__restrict__ tcost, int64_t waves, unsigned long long *__restrict__ total) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1712,6 +1714,25 @@ __device__ bool spill_stack(const SpillView &sv, int r, int lane, int sp, const 
     return true;
 }
 
+// The next 64-query group of a persistent traversal wave: group g (blocks with
+// blockIdx % 8 == g, which the dispatcher places on one XCD) takes the g-th
+// eighth of the waves in Morton order, so each XCD's L2 serves a contiguous
+// part of the tree; an exhausted eighth moves on to the next ones.  -1 when
+// every group is done.  (Which wave runs which group does not change any
+// result: a group's sums and tile list are its own.)
+__device__ __forceinline__ int64_t bh_dequeue(int32_t *qhead, int64_t nw, int grp) {
+    for (int k = 0; k < 8; ++k) {
+        const int g = (grp + k) & 7;
+        const int64_t lo = nw * g / 8, len = nw * (g + 1) / 8 - lo;
+        if (__hip_atomic_load(&qhead[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= len) continue;
+        int32_t v = 0;
+        if (lane_id() == 0) v = atomicAdd(&qhead[g], 1);
+        v = __shfl(v, 0, 64);
+        if (v < len) return lo + v;
+    }
+    return -1;
+}
+
 // Traversal kernel (see the comment above).  STATS: per-wave work counters
 // (profiling, and the bucket costs of the multi-GPU balancing); the
 // production instantiation carries none.  TASK = false: one wave per 64
@@ -1726,7 +1747,7 @@ __global__ __launch_bounds__(256) void bh_traverse(
     int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, int32_t virt, double2 *__restrict__ F,
     double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost,
     const int32_t *__restrict__ border, int32_t *__restrict__ wcost, int32_t *__restrict__ tcost, SpillView sv,
-    int region) {
+    int region, int32_t *__restrict__ qhead, const int32_t *__restrict__ cost_lab) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     __shared__ int32_t sref[4][STACK];
     __shared__ uint64_t smask[4][STACK];
@@ -1744,7 +1765,11 @@ __global__ __launch_bounds__(256) void bh_traverse(
     const int32_t budget0 = can_spill ? sv.budget[0] : INT32_MAX;
     const int32_t gpts = (int32_t)min((int64_t)INT32_MAX, max((int64_t)1, (int64_t)budget0 * sv.gfac));
     const int64_t nsrc_w = sv.nwaves;   // saved-stack sources: waves [0, nwaves), then tasks by global id
-    const int64_t ntask = !TASK ? 1 : finish ? (int64_t)sv.cnt[0] : min((int64_t)sv.cnt[2 * region], (int64_t)sv.task_cap);
+    // persistent query waves (qhead, !TASK): the grid is what fits on the chip
+    // and each wave dequeues 64-query groups (bh_dequeue) until none is left
+    const int64_t nqw = (g1 - g0 + 63) / 64;
+    const int64_t ntask = !TASK ? (qhead ? INT64_MAX : 1)
+                        : finish ? (int64_t)sv.cnt[0] : min((int64_t)sv.cnt[2 * region], (int64_t)sv.task_cap);
     const int64_t gstride = TASK ? (int64_t)gridDim.x * 4 : 1;
     for (int64_t ti = TASK ? (int64_t)blockIdx.x * 4 + w : 0; ti < ntask; ti += gstride) {
         BHTask tk{};
@@ -1760,6 +1785,9 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 if (tk.ne == 0) continue;   // an empty slot of a full region (uniform)
             }
             wid = tk.wid;
+        } else if (qhead) {
+            wid = bh_dequeue(qhead, nqw, (int)(blockIdx.x & 7));
+            if (wid < 0) break;
         } else {
             const int64_t blk = border ? (int64_t)border[blockIdx.x]
                               : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk)
@@ -1776,7 +1804,10 @@ __global__ __launch_bounds__(256) void bh_traverse(
                 ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0;
                 if (sv.wspill) sv.wspill[wid] = make_int2(0, 0);
             }
-            if (__ballot(valid) == 0) return;
+            if (__ballot(valid) == 0) {
+                if (qhead) continue;
+                return;
+            }
         }
         const long long t_start = COST ? clock64() : 0;
         const unsigned long long w_start = STATS ? wall_clock64() : 0;
@@ -2032,8 +2063,12 @@ __global__ __launch_bounds__(256) void bh_traverse(
             // MODE 2: cell pops + tile points / 48
             const unsigned long long c =
                 MODE == 1 ? ((unsigned long long)(clock64() - t_start) >> 6) + 1 : wpops + wtile / 48 + 4;
-            const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
-            if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
+            if (cost_lab) {   // by label: an equal share into each query's label bucket
+                if (valid) atomicAdd(&bcost[cost_lab[s] >> 8], (c + 63) >> 6);
+            } else {
+                const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
+                if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
+            }
         }
         if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
                                  // [4] wave-level tile points, [5] lane child evaluations, [6] wave
@@ -2176,6 +2211,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     __shared__ uint64_t sbm[4][64];
     __shared__ int smark[4][64];
     __shared__ int2 srng[4][64];
+    __shared__ int2 crng[4][LW_CHUNK];          // pack 3: the chunk's small-tile ranges
+    __shared__ uint64_t cmask[4][LW_CHUNK / 64][64];   // pack 3: per window, each lane's tiles (transposed masks)
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t blk = torder ? (int64_t)torder[blockIdx.x]
                       : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
@@ -2211,11 +2248,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     int nwant = 0, ntask = 0;
     unsigned long long ndense = 0;
     unsigned long long wt_tasks = 0, wt_dense_pts = 0, wt_momchk = 0;   // wave-level diagnostics
+    // per dense path (lane-wise, packed sweep, query-major, staged sweep): wave
+    // steps (pair slots the wave issues) and this lane's useful pairs
+    unsigned long long ps_steps[4] = {0, 0, 0, 0}, ps_pairs[4] = {0, 0, 0, 0};
     double2 *buf = tbuf[w];
     const TileTask *mytt = ttask + qw * TILE_CAP;
     int masked_until = tb;   // pack 2: tiles before this one take the masked sweep
     for (int t = tb; t < nt;) {
         const TileTask tt = mytt[t];
+        if (pack == 3 && tt.last - tt.first + 1 < MOM_MIN_POINTS) {   // small tiles: the lane-wise pass below
+            ++t;
+            continue;
+        }
         if (pack == 2 && t >= masked_until && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
             // Lane-wise window: the run of <= 64 consecutive small tiles
             // starting at t.  Each lane walks only the points of ITS tiles
@@ -2279,6 +2323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 }
                 const bool on = p <= last;
                 if (__ballot(on) == 0) break;
+                if (visits) ps_steps[0] += 2;
                 if (on) {
                     const bool two = p + 1 <= last;
                     const double2 p0 = pos[p];
@@ -2293,6 +2338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             fx += ux; fy += uy; zs += uz;
             ndense += (unsigned long long)nmine;
             if (visits) {
+                ps_pairs[0] += (unsigned long long)nmine;
                 wt_tasks += (unsigned long long)wn;
                 wt_dense_pts += (unsigned long long)wave_sum(lane < wn ? b_i - a_i + 1 : 0);
             }
@@ -2355,7 +2401,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             __builtin_amdgcn_wave_barrier();
             fx += ux; fy += uy; zs += uz;
             ndense += (unsigned long long)nmine;
-            if (visits) { wt_tasks += (unsigned long long)mtake; wt_dense_pts += (unsigned long long)total; }
+            if (visits) {
+                wt_tasks += (unsigned long long)mtake; wt_dense_pts += (unsigned long long)total;
+                ps_steps[1] += (unsigned long long)total; ps_pairs[1] += (unsigned long long)nmine;
+            }
             t += mtake;
             continue;
         }
@@ -2406,6 +2455,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 }
                 ux = wave_sum(ux); uy = wave_sum(uy); uz = wave_sum(uz);
                 if (lane == j) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)cnt_t; }
+                if (visits) {
+                    ps_steps[2] += (unsigned long long)((cnt_t + 63) / 64 + 6);
+                    if (lane == j) ps_pairs[2] += (unsigned long long)cnt_t;
+                }
             }
         } else if (dm) {
             double2 nxt = make_double2(0.0, 0.0);
@@ -2434,7 +2487,105 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             }
             __builtin_amdgcn_wave_barrier();
             if (dense) { fx += ux; fy += uy; zs += uz; ndense += (unsigned long long)(b - a + 1); }
+            if (visits) {
+                ps_steps[3] += (unsigned long long)(b - a + 1);
+                if (dense) ps_pairs[3] += (unsigned long long)(b - a + 1);
+            }
         }
+    }
+    if (pack == 3) {
+        // Small tiles (< MOM_MIN_POINTS points, always dense), lane-wise: in
+        // chunks of LW_CHUNK tiles each lane walks the points of ITS tiles (its
+        // bits of the masks, transposed 64 tiles at a time) in tile order, so a
+        // chunk costs its busiest lane's points and the lanes' imbalance
+        // averages over the whole chunk.  The walk keeps LW_D point loads in
+        // flight (a rotating register pipeline), so the gathers' latency hides
+        // behind the pair terms; the order per lane is fixed (tile, then point).
+        double ux = 0.0, uy = 0.0, uz = 0.0;
+        int nmine = 0;
+        for (int c0 = tb; c0 < nt; c0 += LW_CHUNK) {
+            const int c1 = min(nt, c0 + LW_CHUNK);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+            for (int k = 0; k < LW_CHUNK / 64; ++k) {
+                const int ti = c0 + k * 64 + lane;
+                uint64_t m_i = 0;
+                int2 r = make_int2(0, -1);
+                if (ti < c1) {
+                    const TileTask h = mytt[ti];
+                    if (h.last - h.first + 1 < MOM_MIN_POINTS) { m_i = h.mask; r = make_int2(h.first, h.last); }
+                }
+                crng[w][k * 64 + lane] = r;
+                uint64_t W = m_i;   // 64 x 64 bit transpose, as the pack-2 windows
+#pragma unroll
+                for (int st = 0; st < 6; ++st) {
+                    const int j = 32 >> st;
+                    const uint64_t lo = st == 0 ? 0x00000000FFFFFFFFull : st == 1 ? 0x0000FFFF0000FFFFull
+                                      : st == 2 ? 0x00FF00FF00FF00FFull : st == 3 ? 0x0F0F0F0F0F0F0F0Full
+                                      : st == 4 ? 0x3333333333333333ull : 0x5555555555555555ull;
+                    const uint32_t ylo = __shfl_xor((uint32_t)W, j, 64), yhi = __shfl_xor((uint32_t)(W >> 32), j, 64);
+                    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+                    W = (lane & j) ? ((W & ~lo) | ((y & ~lo) >> j)) : ((W & lo) | ((y & lo) << j));
+                }
+                cmask[w][k][lane] = W;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const int nwin = (c1 - c0 + 63) / 64;
+            int kw = 0, p = 0, last = -1;
+            uint64_t Wc = cmask[w][0][lane];
+            // the range after the current one, fetched ahead (np > nlast: none left)
+            auto fetch_next = [&](int &np, int &nl) {
+                while (Wc == 0 && kw + 1 < nwin) Wc = cmask[w][++kw][lane];
+                if (Wc == 0) { np = 1; nl = 0; return; }
+                const int i = __ffsll((long long)Wc) - 1;
+                Wc &= Wc - 1;
+                const int2 r = crng[w][kw * 64 + i];
+                np = r.x;
+                nl = r.y;
+            };
+            int np, nl;
+            fetch_next(np, nl);
+            // the next point of this lane's walk, -1 at its end
+            auto advance = [&]() -> int {
+                if (p < last) return ++p;
+                if (np > nl) return -1;
+                p = np;
+                last = nl;
+                fetch_next(np, nl);
+                return p;
+            };
+            double2 v[LW_D];
+            bool o[LW_D];
+            int c = advance();
+#pragma unroll
+            for (int k = 0; k < LW_D; ++k) {
+                o[k] = c >= 0;
+                v[k] = make_double2(0.0, 0.0);
+                if (o[k]) { v[k] = pos[c]; c = advance(); }
+            }
+            while (true) {
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < LW_D; ++k) any = any || o[k];
+                if (__ballot(any) == 0) break;
+                if (visits) ps_steps[0] += LW_D;
+#pragma unroll
+                for (int k = 0; k < LW_D; ++k) {
+                    if (o[k]) {
+                        pair_force(qx, qy, v[k].x, v[k].y, ux, uy, uz);
+                        ++nmine;
+                    }
+                    o[k] = c >= 0;
+                    if (o[k]) { v[k] = pos[c]; c = advance(); }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        fx += ux; fy += uy; zs += uz;
+        ndense += (unsigned long long)nmine;
+        if (visits) ps_pairs[0] += (unsigned long long)nmine;
     }
     if (valid && cv.slot_w) {
         mtask_n[e] = ntask;
@@ -2456,7 +2607,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     if (visits) {   // [1] moment evaluations, [2] dense pair terms; [10..12] diagnostics:
                     // tile tasks, wave-level dense points, tasks with a moment check
         const unsigned long long tm = wave_sum((unsigned long long)ntask), td = wave_sum(ndense);
+        unsigned long long pp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pp[k] = wave_sum(ps_pairs[k]);
         if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {   // [24 + 2k] wave steps, [25 + 2k] lane pairs of dense path k
+                atomicAdd(visits + 24 + 2 * k, ps_steps[k]);
+                atomicAdd(visits + 25 + 2 * k, pp[k]);
+            }
             atomicAdd(visits + 10, wt_tasks);
             atomicAdd(visits + 11, wt_dense_pts);
             atomicAdd(visits + 12, wt_momchk);
@@ -2724,6 +2883,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
     t.rt_skip = 0;
     t.top_list = ws.get<int32_t>("bh.top_list", 2 * (size_t)n);
     t.top_cnt = ws.get<int32_t>("bh.top_cnt", 1);
+    t.qhead = ws.get<int32_t>("bh.qhead", 8);
     t.meta = ws.get<int32_t>("bh.meta", 4);
     t.mom = ws.get<double>("bh.mom", (size_t)n * MOM_K);
     t.mom_cnt = ws.get<int32_t>("bh.mom_cnt", n + 1);
@@ -2952,7 +3112,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
         hipLaunchKernelGGL(bottom_up<1024>, dim3(ceil_div(n, 1024)), dim3(1024), 0, st, t.pos, t.meta, t.W, inv_theta,
                            t.nodes, t.agg, t.parent_leaf, t.parent_node, t.arrive);
     } else {
-        hipLaunchKernelGGL(bottom_up_intra, dim3(ceil_div(n, BU_NB)), dim3(1024), 0, st, t.pos, t.meta, t.W, inv_theta,
+        hipLaunchKernelGGL(bottom_up_intra, dim3(ceil_div(n, BU_NB)), dim3(BU_NB), 0, st, t.pos, t.meta, t.W, inv_theta,
                            t.nodes, t.agg, t.parent_leaf, t.parent_node, t.fstart, t.gen, t.top_list, t.top_cnt);
         hipLaunchKernelGGL(bottom_up_top, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.meta, t.W,
                            inv_theta, t.nodes, t.agg, t.parent_node, t.arrive, t.top_list, t.top_cnt);
@@ -2988,7 +3148,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
 
 void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist,
-                  unsigned long long *bcost) {
+                  unsigned long long *bcost, bool cost_by_label) {
     if (s1 <= s0) return;
     if (t.root_tile) {
         if (visits)
@@ -3048,16 +3208,26 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         block_order(ctx, t, t.wcost, waves, nblocks, t.border);
         border = t.border;
     }
-    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
+    // persistent query waves (TSNE_BH_PERSIST=1; default: one block per 4 query waves):
+    // cu_count x 8 blocks (the traversal's occupancy: 20 KB of LDS and 58
+    // VGPRs per 4-wave block) dequeue 64-query groups, per XCD group in
+    // Morton order (bh_dequeue)
+    static const bool persist = [] { const char *e = getenv("TSNE_BH_PERSIST"); return e && e[0] == '1'; }();
+    const bool pq = persist && !border;
+    if (pq) TSNE_HIP(hipMemsetAsync(t.qhead, 0, 8 * sizeof(int32_t), ctx->stream));
+    const int64_t tgrid0 = pq ? std::min<int64_t>(nblocks, (int64_t)ctx->cu_count * 8) : nblocks;
+    hipLaunchKernelGGL(kern, dim3(tgrid0), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
                        t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd,
-                       (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost, sv, 0);
+                       (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost, sv, 0, pq ? t.qhead : nullptr,
+                       cost_by_label ? t.idx_sorted : nullptr);
     if (spill_on) {   // task passes over regions 1..P (fixed grid: one wave per SIMD slot of every CU)
         const int tgrid = ctx->cu_count * 8;
         // regions 1..P, then the finish pass (region P + 1) over stacks saved when a region was full
         for (int r = 1; r <= SPILL_PASSES + 1; ++r)
             hipLaunchKernelGGL(tkern, dim3(tgrid), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.qrec, t.ttask,
                                t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd, (int32_t)t.n, dF,
-                               dz, visits, bcost, border, t.wcost, t.tcost, sv, r);
+                               dz, visits, bcost, border, t.wcost, t.tcost, sv, r, nullptr,
+                               cost_by_label ? t.idx_sorted : nullptr);
     }
     t.have_cost = true;
     // tile chunks of heavy waves (ChunkView; TSNE_TILE_CHUNK=0: one tile_apply wave per traversal wave)

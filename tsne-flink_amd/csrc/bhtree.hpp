@@ -123,6 +123,7 @@ struct BHTree {
     int32_t *fstart = nullptr, *top_list = nullptr, *top_cnt = nullptr;
     int32_t gen = 0;
     int rt_skip = 0;            // builds left before the root-tile test is tried again
+    int32_t *qhead = nullptr;   // persistent traversal: per XCD group, query waves handed out
     int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref, [2] = moment nodes
     // subtree moments (see bhtree.hip "Subtree moments"): per internal node
     // MOM_K scaled moments about its bounding-box centre, for nodes of
@@ -192,10 +193,11 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
 // (device, ascending sorted positions: one rank's own queries) the positions
 // qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted
 // position; visits (nullable) += node evaluations; bcost (nullable)
-// accumulates each wave's cost into the 256-position bucket of its first query.
+// accumulates each wave's cost into the 256-position bucket of its first query
+// (cost_by_label: an equal share into each query's 256-label bucket).
 void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist = nullptr,
-                  unsigned long long *bcost = nullptr);
+                  unsigned long long *bcost = nullptr, bool cost_by_label = false);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).
 void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int world, int64_t *bounds);
 

@@ -1604,7 +1604,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 24);
+    s->visits = ws.get<unsigned long long>("opt.visits", 32);
     if (world > 1) {
         const int64_t nb = ceil_div(n, 256);
         s->qlist = ws.get<int32_t>("opt.qlist", n);
@@ -1706,7 +1706,7 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
         return;
     }
-    unsigned long long v[24] = {};
+    unsigned long long v[32] = {};
     TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
     for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
     static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
@@ -1718,6 +1718,9 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         fprintf(stderr, "[waves] t=%d span_us=%.1f max_wave_us=%.1f mean_wave_us=%.2f\n", t,
                 (double)(v[17] - (~0ull - v[16])) * 0.01, (double)v[15] * 0.01,
                 (double)v[18] * 0.01 / (double)std::max<int64_t>(1, ceil_div(s->L1 - s->L0, 64)));
+    if (dbg)   // tile_apply dense paths: wave steps / useful lane pairs
+        fprintf(stderr, "[tpaths] t=%d lanewise %llu/%llu packed %llu/%llu qmajor %llu/%llu staged %llu/%llu\n", t,
+                v[24], v[25], v[26], v[27], v[28], v[29], v[30], v[31]);
     if (dbg && v[21] > 0)   // tile_apply waves (only waves with tiles report)
         fprintf(stderr, "[twaves] t=%d span_us=%.1f max_wave_us=%.1f\n", t,
                 (double)(v[21] - (~0ull - v[20])) * 0.01, (double)v[19] * 0.01);
@@ -1775,6 +1778,40 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     if (s->profile) finish_profile(ctx, s, t);
 }
 
+// Several ranks with the tiled layout keep P's graph order (TSNE_RELABEL
+// unset): the ownership is re-cut in that order instead of a Morton relabel,
+// which would hand the attraction back to attract_rows (C3 standalone: 2.35 vs
+// 0.77 ms).  Each query's traversal cost goes to its label's 256-label bucket
+// (an equal share of its wave's time); the all-reduced buckets give cuts of
+// equal cost, applied (owned rows and their tiles rebuilt) when a cut moves
+// by more than 1/16 of a rank's share.
+static bool recut_mode(tsne_ctx *ctx, OptState *s) {
+    static const int mode = [] { const char *e = getenv("TSNE_RELABEL"); return e ? atoi(e) : -1; }();
+    static const bool on = [] { const char *e = getenv("TSNE_RECUT"); return e && e[0] == '1'; }();
+    return on && mode == -1 && ctx->world > 1 && s->at_on && !s->morton_labels;
+}
+static void recut(tsne_ctx *ctx, OptState *s, const std::vector<int64_t> &cuts) {
+    gather_working_set(ctx, s);   // full upd / gains under the old cuts
+    s->own = cuts;
+    s->L0 = cuts[ctx->rank];
+    s->L1 = cuts[ctx->rank + 1];
+    build_own_rows(ctx, s);
+    ++s->relabels;
+}
+static void maybe_recut(tsne_ctx *ctx, OptState *s) {
+    hipStream_t st = ctx->stream;
+    const int64_t n = s->n;
+    ++s->relabel_checks;
+    std::vector<int64_t> cuts(ctx->world + 1);
+    comm_allreduce_sum_u64(ctx, s->bcost, (size_t)ceil_div(n, 256));
+    bh_balance(ctx, s->bcost, n, ctx->world, s->bounds);
+    TSNE_HIP(hipMemcpyAsync(cuts.data(), s->bounds, sizeof(int64_t) * (ctx->world + 1), hipMemcpyDeviceToHost, st));
+    TSNE_HIP(hipStreamSynchronize(st));
+    int64_t moved = 0;
+    for (int r = 1; r < ctx->world; ++r) moved = std::max<int64_t>(moved, std::llabs(cuts[r] - s->own[r]));
+    if (moved * 16 * ctx->world > n) recut(ctx, s, cuts);   // identical decision on every rank
+}
+
 // Relabel check (every RELABEL_EVERY iterations, 2-D): renumber the labels
 // into this iteration's Morton order when that order keeps more of P's edges
 // within a window of labels than the current one (identical decision on
@@ -1784,6 +1821,10 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
 static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     hipStream_t st = ctx->stream;
     const int64_t n = s->n;
+    if (recut_mode(ctx, s)) {   // several ranks on the tiled layout: re-cut the graph order by cost
+        maybe_recut(ctx, s);
+        return;
+    }
     // dense rows over a small embedding (the distance-matrix mode, C5): every
     // row gathers all of Y, which sits in one XCD's L2 (n * 16 B <= 2 MiB)
     // whatever the labels, so a relabel (a copy of the whole P) buys nothing
@@ -1883,7 +1924,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int world = ctx->world;
     double *Y = s->Y[s->cur];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 24 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, 32 * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // attraction over this rank's rows (row pointer local to L0)
@@ -1938,7 +1979,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (world > 1) {
         build_qlist(ctx, s, s->tree.idx_sorted);
         bh_repulsion(ctx, s->tree, p.theta, 0, s->L1 - s->L0, s->F, s->z, s->profile ? s->visits : nullptr, s->qlist,
-                     bcost);
+                     bcost, recut_mode(ctx, s));
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
