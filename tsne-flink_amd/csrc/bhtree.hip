@@ -2214,6 +2214,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     __shared__ int2 crng[4][LW_CHUNK];          // pack 3: the chunk's small-tile ranges
     __shared__ uint64_t cmask[4][LW_CHUNK / 64][64];   // pack 3: per window, each lane's tiles (transposed masks)
     const int lane = lane_id(), w = threadIdx.x >> 6;
+    const bool pklw = (pack & 4) == 0;   // packed rounds walked lane-wise (pack | 4: the masked sweep)
+    pack &= 3;
     const int64_t blk = torder ? (int64_t)torder[blockIdx.x]
                       : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
@@ -2391,19 +2393,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             __builtin_amdgcn_wave_barrier();
             double ux = 0.0, uy = 0.0, uz = 0.0;
             int nmine = 0;
-            for (int j = 0; j < total; ++j) {
-                const double2 pp = buf[j];
-                if ((sbm[w][j] >> lane) & 1ull) {
-                    pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
-                    ++nmine;
+            if (pklw) {
+                // lane-wise over the staged slots: each lane walks only ITS slots
+                // (the round's 64 slot masks transposed), two at a time, so the
+                // round costs its busiest lane's slots instead of all of them;
+                // a lane's order is still slot order (the same sums as the sweep)
+                uint64_t M = lane < total ? mk : 0ull;
+#pragma unroll
+                for (int st2 = 0; st2 < 6; ++st2) {
+                    const int j = 32 >> st2;
+                    const uint64_t lo = st2 == 0 ? 0x00000000FFFFFFFFull : st2 == 1 ? 0x0000FFFF0000FFFFull
+                                      : st2 == 2 ? 0x00FF00FF00FF00FFull : st2 == 3 ? 0x0F0F0F0F0F0F0F0Full
+                                      : st2 == 4 ? 0x3333333333333333ull : 0x5555555555555555ull;
+                    const uint32_t ylo = __shfl_xor((uint32_t)M, j, 64), yhi = __shfl_xor((uint32_t)(M >> 32), j, 64);
+                    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+                    M = (lane & j) ? ((M & ~lo) | ((y & ~lo) >> j)) : ((M & lo) | ((y & lo) << j));
                 }
+                while (__ballot(M != 0ull)) {
+                    if (M) {
+                        const int j0 = __ffsll((long long)M) - 1;
+                        M &= M - 1;
+                        const int j1 = M ? __ffsll((long long)M) - 1 : -1;
+                        if (M) M &= M - 1;
+                        const double2 p0 = buf[j0];
+                        const double2 p1 = buf[j1 < 0 ? j0 : j1];
+                        pair_force(qx, qy, p0.x, p0.y, ux, uy, uz);
+                        if (j1 >= 0) pair_force(qx, qy, p1.x, p1.y, ux, uy, uz);
+                        if (visits) nmine += j1 >= 0 ? 2 : 1;
+                    }
+                    if (visits) ps_steps[1] += 2;
+                }
+            } else {
+                for (int j = 0; j < total; ++j) {
+                    const double2 pp = buf[j];
+                    if ((sbm[w][j] >> lane) & 1ull) {
+                        pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                        ++nmine;
+                    }
+                }
+                if (visits) ps_steps[1] += (unsigned long long)total;
             }
             __builtin_amdgcn_wave_barrier();
             fx += ux; fy += uy; zs += uz;
             ndense += (unsigned long long)nmine;
             if (visits) {
                 wt_tasks += (unsigned long long)mtake; wt_dense_pts += (unsigned long long)total;
-                ps_steps[1] += (unsigned long long)total; ps_pairs[1] += (unsigned long long)nmine;
+                ps_pairs[1] += (unsigned long long)nmine;
             }
             t += mtake;
             continue;

@@ -97,6 +97,15 @@ def lib():
         path = lib_path()
         if not path.exists():
             raise TsneError(-2, f"{path} not built (run `make -C {PKG_ROOT}`); no CPU fallback exists")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64
+        # (same soname as /opt/rocm's).  Loaded first, it is the one this
+        # library binds to; if this library initialised /opt/rocm's runtime
+        # first, torch's own would later find no GPU ("No HIP GPUs are
+        # available", measured on the GPU box).  So torch, when present, goes first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(path))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
