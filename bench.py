@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-knn-sample", type=int, default=32, help="queries in the CPU baseline kNN sample")
     ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as <dump-dir>/Y_t<t>.npy")
     ap.add_argument("--dump-dir", default="gpurun_out")
+    ap.add_argument("--y0-perturb", type=float, default=0.0,
+                    help="relative N(0, eps^2) perturbation of Y0 (measures the chaotic spread of the final KL)")
+    ap.add_argument("--y0-perturb-seed", type=int, default=1)
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
@@ -239,6 +242,8 @@ def main():
     upd = torch.zeros_like(Y)
     gains = torch.ones_like(Y)
     Yh, _, _ = ctx.initWorkingSet(n, 2, seed=0)
+    if a.y0_perturb:
+        Yh = Yh * (1.0 + a.y0_perturb * np.random.default_rng(a.y0_perturb_seed).normal(size=Yh.shape))
     Y[:n].copy_(torch.from_numpy(Yh))
     snap = (Y.clone(), upd.clone(), gains.clone())
     params = default_params(iterations=a.iterations, theta=a.theta)
