@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--y0-perturb", type=float, default=0.0,
                     help="relative N(0, eps^2) perturbation of Y0 (measures the chaotic spread of the final KL)")
     ap.add_argument("--y0-perturb-seed", type=int, default=1)
+    ap.add_argument("--y0-seed", type=int, default=0, help="initWorkingSet seed (the reference is unseeded)")
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
@@ -241,7 +242,7 @@ def main():
     Y = torch.zeros((n, 2), dtype=torch.float64, device=dev)
     upd = torch.zeros_like(Y)
     gains = torch.ones_like(Y)
-    Yh, _, _ = ctx.initWorkingSet(n, 2, seed=0)
+    Yh, _, _ = ctx.initWorkingSet(n, 2, seed=a.y0_seed)
     if a.y0_perturb:
         Yh = Yh * (1.0 + a.y0_perturb * np.random.default_rng(a.y0_perturb_seed).normal(size=Yh.shape))
     Y[:n].copy_(torch.from_numpy(Yh))

@@ -47,7 +47,7 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 CLI = ROOT / "tsne-flink_amd" / "tsne_hip"
 THREADS = 16
-NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "1e-5"))   # BH_NEAR_TOL (bhtree.hip)
+NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "5e-6"))   # BH_NEAR_TOL (bhtree.hip)
 
 
 @pytest.fixture(scope="module")

@@ -160,7 +160,7 @@ def test_gradient_golden(ctx):
     assert abs(Z - G["denseSumQ"]) <= 1e-9
 
 
-NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "1e-5"))   # BH_NEAR_TOL (bhtree.hip): per-cell relative bound of the near-exact tiles
+NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "5e-6"))   # BH_NEAR_TOL (bhtree.hip): per-cell relative bound of the near-exact tiles
 
 
 def random_problem(n, k, seed):
@@ -358,7 +358,9 @@ def test_optimize_loss_matches_oracle(ctx):
         runs.append(O.optimize(rp, col, val, Yo, uo, go, iterations=200, theta=0.5))
     lo = runs[0]
     assert sorted(lg) == sorted(lo) == list(range(10, 201, 10))
-    early = (10, 20, 30, 40, 50) if NEAR_TOL < 5e-6 else (10, 20, 30)
+    # a looser near-exact bound moves the early trajectory sooner (chaotic
+    # growth of any per-iteration difference): at 1e-5 the 1% window is t <= 30
+    early = (10, 20, 30, 40, 50) if NEAR_TOL <= 5e-6 else (10, 20, 30)
     for t in early:
         assert abs(lg[t] - lo[t]) <= 0.01 * abs(lo[t]), t
     final = np.array([r[200] for r in runs])

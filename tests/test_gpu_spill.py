@@ -16,7 +16,7 @@ import tsne_amd as T
 from tsne_amd.api import default_params
 
 pytestmark = pytest.mark.gpu
-NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "1e-5"))   # BH_NEAR_TOL (bhtree.hip)
+NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "5e-6"))   # BH_NEAR_TOL (bhtree.hip)
 
 
 @pytest.fixture(scope="module")

@@ -62,9 +62,12 @@ constexpr int MOM_CHUNK = 2048;
 constexpr double MOM_TOL = 1e-12;
 __device__ double g_mom_tol = MOM_TOL;   // TSNE_MOM_TOL (experiments): the bound moment_ok applies
 constexpr int MOM_TASKS = 128;  // moment evaluations recorded per query; more -> dense tiles
-constexpr double BH_NEAR_TOL = 1e-5;    // near-exact subtree test (bh_traverse): 10x below the
-                                        // north-star 1e-4 gradient tolerance (C3 schedule at 1e-6:
-                                        // 7.05 s, 5e-6: 5.92, 1e-5: 5.35, one box)
+constexpr double BH_NEAR_TOL = 1e-6;    // near-exact subtree test (bh_traverse): 100x below
+                                        // the north-star 1e-4 gradient tolerance -- single
+                                        // gradients and the optimizer's early-exaggeration phase
+constexpr double BH_NEAR_TOL_LATE = 5e-6;   // ... the optimizer after early exaggeration (20x
+                                        // below; DESIGN.md 3a: the early phase amplifies any
+                                        // per-iteration difference fastest)
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
 __host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }
 __host__ __device__ constexpr double fact(int k) { return k <= 1 ? 1.0 : k * fact(k - 1); }
@@ -3060,18 +3063,27 @@ void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int w
     TSNE_LAUNCH_CHECK();
 }
 
-// Largest D for which 48 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL (see bh_traverse).
-double bh_near_dmax(double theta) {
+// The near-exact tolerances (TSNE_BH_NEAR_TOL_EARLY / TSNE_BH_NEAR_TOL: experiment
+// overrides of BH_NEAR_TOL / BH_NEAR_TOL_LATE; 0 disables the test)
+double bh_near_tol(bool late) {
+    static const double early = [] { const char *e = getenv("TSNE_BH_NEAR_TOL_EARLY"); return e ? atof(e) : BH_NEAR_TOL; }();
+    static const double lt = [] { const char *e = getenv("TSNE_BH_NEAR_TOL"); return e ? atof(e) : BH_NEAR_TOL_LATE; }();
+    return late ? lt : early;
+}
+
+// Largest D for which 48 theta^2 D^2 (1 + 8 D) <= tol (see bh_traverse).
+double bh_near_dmax(double theta, double tol) {
     if (!(theta > 0.0)) return __builtin_inf();   // theta = 0: the reference opens every cell
-    // TSNE_BH_NEAR_TOL: experiment override of the tolerance (0 disables the test)
-    static const double tol = [] { const char *e = getenv("TSNE_BH_NEAR_TOL"); return e ? atof(e) : BH_NEAR_TOL; }();
     if (!(tol > 0.0)) return -1.0;
     double d = std::sqrt(tol / (48.0 * theta * theta));
     while (48.0 * theta * theta * d * d * (1.0 + 8.0 * d) > tol) d *= 0.99;
     return d;
 }
 
-void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap, bool root_tile_ok) {
+void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap, bool root_tile_ok,
+              double near_tol) {
+    if (near_tol < 0.0) near_tol = bh_near_tol(false);
+    t.near_dmax = bh_near_dmax(theta, near_tol);
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
     t.rowmap = rowmap;
@@ -3092,7 +3104,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     if (root_tile_ok) {   // small read-backs decide the path (the host must know which kernels to launch)
         // the box conditions first (dflag still 0): once the embedding has
         // outgrown the root tile, the duplicate rounds (~90 us at 1M) are skipped
-        hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, bh_near_dmax(theta),
+        hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, t.near_dmax,
                            t.status);
         TSNE_HIP(hipMemcpyAsync(t.status_h, t.status, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         TSNE_HIP(hipStreamSynchronize(st));
@@ -3110,7 +3122,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
             hipLaunchKernelGGL(dup_probe, dim3(ceil_div(n, 256)), dim3(256), 0, st, Y2, n, t.dup_tab, t.dup_mask,
                                t.dup_open, r, t.dflag);
         }
-        hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, bh_near_dmax(theta),
+        hipLaunchKernelGGL(root_tile_check, dim3(1), dim3(1), 0, st, t.dflag, t.bb, t.W, n, theta, t.near_dmax,
                            t.status);
         TSNE_HIP(hipMemcpyAsync(t.status_h, t.status, sizeof(int32_t), hipMemcpyDeviceToHost, st));
         TSNE_HIP(hipStreamSynchronize(st));
@@ -3170,7 +3182,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
                        t.vflag, t.vcnt, t.vsum, t.vcntf, t.vcom, t.nodes);
     const DupView dv{t.tiecnt, t.notile, t.vflag, t.vcntf, t.vcom, (int32_t)n};
     hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, QREC_BLK)), dim3(QREC_BLK), 0, st, t.nodes, t.pos, t.meta, inv_theta,
-                       bh_near_dmax(theta), t.dflag, dv, t.qrec);
+                       t.near_dmax, t.dflag, dv, t.qrec);
     // subtree moments for the all-open fast path
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 1024)), dim3(1024), 0, st, t.nodes, n, t.meta, t.mom_flag,
                        t.mom_cnt, t.mom_list, t.meta, t.mom_off, t.mom_item);
@@ -3201,7 +3213,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         TSNE_LAUNCH_CHECK();
         return;
     }
-    const double near_dmax = bh_near_dmax(theta);
+    const double near_dmax = t.near_dmax;
     // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD block order (TSNE_BH_XCD = run
     // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
     static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();

@@ -123,6 +123,7 @@ struct BHTree {
     int32_t *fstart = nullptr, *top_list = nullptr, *top_cnt = nullptr;
     int32_t gen = 0;
     int rt_skip = 0;            // builds left before the root-tile test is tried again
+    double near_dmax = 0.0;     // this build's near-exact radius (squared distance), bh_near_dmax
     int32_t *qhead = nullptr;   // persistent traversal: per XCD group, query waves handed out
     int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref, [2] = moment nodes
     // subtree moments (see bhtree.hip "Subtree moments"): per internal node
@@ -187,8 +188,11 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
 // With root_tile_ok, the build stops after the sort when every query's whole
 // tree is one near-exact subtree evaluated from the root's moments (the
 // small-embedding phase, see bh_root_tile): t.root_tile tells which.
+// near_tol: the near-exact tolerance of this build and the traversals on it
+// (< 0: bh_near_tol(false), the strict one).
 void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap = nullptr,
-              bool root_tile_ok = false);
+              bool root_tile_ok = false, double near_tol = -1.0);
+double bh_near_tol(bool late);
 // Repulsion for the query slots [s0, s1): sorted positions, or with qlist
 // (device, ascending sorted positions: one rank's own queries) the positions
 // qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted

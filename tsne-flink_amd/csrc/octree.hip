@@ -29,7 +29,9 @@ namespace {
 constexpr int LEVELS3 = 21;                 // 63 key bits
 constexpr uint64_t OUT_KEY3 = 1ull << 63;   // outside the root cell: sorts last
 constexpr int STACK3 = 256;                 // single pops, <= 2 pushes each: depth-bounded
-constexpr double BH_NEAR_TOL3 = 1e-7;
+constexpr double BH_NEAR_TOL3 = 1e-7;        // single gradients and the early-exaggeration phase
+constexpr double BH_NEAR_TOL3_LATE = 5e-6;   // the optimizer after early exaggeration, as 2-D's
+                                             // BH_NEAR_TOL_LATE (C4 loop 29.7 -> 19.5 s, losses to 6 digits)
 constexpr int AGG3 = 12;                    // sx, sy, sz, x0, x1, y0, y1, z0, z1, hmin, cnt, rball
 
 __global__ void bbox3_partial(const double *__restrict__ Y, int64_t n, double *__restrict__ part) {
@@ -413,7 +415,8 @@ constexpr int MOM3_ORDER = 3;
 constexpr int MOM3_K = 70;          // (a, bx, by, bz) with a + bx + by + bz <= 4
 constexpr int MOM3_MIN = 64;        // nodes of >= 64 points carry moments
 constexpr int MOM3_CHUNK = 1024;    // points per moment item
-constexpr double MOM3_TOL = 1e-14;
+constexpr double MOM3_TOL = 1e-12;   // round 3 (1e-14 before): >= 1e5 below the near-exact tolerances
+__device__ double g_mom3_tol = MOM3_TOL;   // TSNE_MOM3_TOL (experiments): the bound oct moment_ok applies
 constexpr int MOM3_GROUP = 10;      // moments accumulated per pass over an item's points
 constexpr int MOM3_TASKS = 512;     // moment tiles recorded per query; more -> dense tiles
 constexpr int DENSE3_MAX = 2048;    // larger tiles only by moments (else traversed)
@@ -535,7 +538,7 @@ __device__ __forceinline__ bool mom3_ok(double vx, double vy, double vz, double 
     double rp = rho;
 #pragma unroll
     for (int k = 0; k < MOM3_ORDER; ++k) rp *= rho;
-    return (MOM3_ORDER + 2) * rp <= MOM3_TOL * (1.0 - rho) * (1.0 - rho);
+    return (MOM3_ORDER + 2) * rp <= g_mom3_tol * (1.0 - rho) * (1.0 - rho);
 }
 // z += sum 1/(1+D), F += sum (q - p)/(1+D)^2 over the node's points from its
 // moments mu (wave-uniform: scalar loads), the query itself included (D = 0:
@@ -827,6 +830,10 @@ __global__ __launch_bounds__(256) void oct_mom_apply(const double4 *__restrict__
 }  // namespace
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
+    if (const char *e = getenv("TSNE_MOM3_TOL")) {
+        const double v = atof(e);
+        TSNE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mom3_tol), &v, sizeof(double)));
+    }
     Workspace &ws = ctx->ws;
     t.n = n;
     t.keys = ws.get<uint64_t>("oct.keys", n);
@@ -908,15 +915,20 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
 // Largest D with 72 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL3: the 2-D bound
 // (bhtree.hip bh_near_dmax) scaled by 12/8 for the larger 3-D cell diagonal
 // (second-order remainder (2 + 8D) r^2 / 2 with r^2 <= 12 h^2 instead of 8 h^2).
-static double oct_near_dmax(double theta) {
+static double oct_near_dmax(double theta, bool late) {
     if (!(theta > 0.0)) return __builtin_inf();
-    double d = std::sqrt(BH_NEAR_TOL3 / (72.0 * theta * theta));
-    while (72.0 * theta * theta * d * d * (1.0 + 8.0 * d) > BH_NEAR_TOL3) d *= 0.99;
+    // TSNE_BH_NEAR_TOL3 / TSNE_BH_NEAR_TOL3_EARLY: experiment overrides of the late / early tolerance
+    static const double tl = [] { const char *e = getenv("TSNE_BH_NEAR_TOL3"); return e ? atof(e) : BH_NEAR_TOL3_LATE; }();
+    static const double te = [] { const char *e = getenv("TSNE_BH_NEAR_TOL3_EARLY"); return e ? atof(e) : BH_NEAR_TOL3; }();
+    const double tol = late ? tl : te;
+    if (!(tol > 0.0)) return -1.0;
+    double d = std::sqrt(tol / (72.0 * theta * theta));
+    while (72.0 * theta * theta * d * d * (1.0 + 8.0 * d) > tol) d *= 0.99;
     return d;
 }
 
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF, double *dz,
-                   const int32_t *qlist) {
+                   const int32_t *qlist, bool late) {
     if (s1 <= s0) return;
     static const bool debug = getenv("TSNE_DEBUG_OCT") != nullptr;   // traversal counters on stderr (synchronises)
     unsigned long long *dbg = nullptr;
@@ -927,11 +939,11 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
     const int64_t waves = ceil_div(s1 - s0, 64);
     if (debug)
         hipLaunchKernelGGL(oct_traverse<true>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                           t.nodes, t.meta, theta, oct_near_dmax(theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
                            dF, dz, dbg);
     else
         hipLaunchKernelGGL(oct_traverse<false>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, oct_near_dmax(theta), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                           t.nodes, t.meta, theta, oct_near_dmax(theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
                            dF, dz, dbg);
     hipLaunchKernelGGL(oct_mom_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);

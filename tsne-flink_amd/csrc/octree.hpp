@@ -55,8 +55,9 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n);
 void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta);
 // Repulsion for the query slots [s0, s1) (sorted positions, or qlist[slot]:
 // a rank's own queries, ascending): F (n x 3, sorted order) and z written
-// at the sorted position.
+// at the sorted position.  late: the optimizer after early exaggeration
+// (the looser near-exact tolerance, BH_NEAR_TOL3_LATE).
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF,
-                   double *dz, const int32_t *qlist = nullptr);
+                   double *dz, const int32_t *qlist = nullptr, bool late = false);
 
 }  // namespace tsne

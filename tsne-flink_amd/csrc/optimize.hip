@@ -1746,9 +1746,9 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     if (ctx->world > 1) {
         build_qlist(ctx, s, s->otree.idx_sorted);
-        oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist);
+        oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist, ex == 1.0);
     } else {
-        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z);
+        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z, nullptr, ex == 1.0);
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     reduce_Z(ctx, s, s->z);
@@ -1967,7 +1967,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // 1. tree (identical on every rank)
     // insertion rows = original indices; the root-tile shortcut while the
     // embedding is small
-    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled());
+    // the strict near-exact tolerance while P is exaggerated (the dynamics
+    // amplify any difference fastest there), the late one after
+    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(), bh_near_tol(ex == 1.0));
     if (overlap && ov_mode == 1) side_attract();
     if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
