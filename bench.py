@@ -51,8 +51,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
-                    help="c3: 1M x 128 GMM (the metric's workload); c5: 50,000-point precomputed distance matrix "
+    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
+                    help="c3: 1M x 128 GMM (the metric's workload); c4: 500k x 300 sparse rows, cosine kNN, 3-D "
+                         "embedding (octree); c5: 50,000-point precomputed distance matrix "
                          "(--inputDistanceMatrix: affinities + joint + optimizer, no kNN)")
     ap.add_argument("--steps", type=int, default=20,
                     help="the timed schedule t=1..T as K steps of T/K iterations (0 = one step per iteration)")
@@ -120,17 +121,24 @@ def trace_entry(ctx, t, rows, Y, n):
             "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()}
 
 
-def setup_c3(ctx, a, dev, world, rank, r0, r1):
+def setup_c3(ctx, a, dev, world, rank, r0, r1, metric="sqeuclidean"):
     """C3: device-generated GMM -> kNN (query rows of this rank) -> affinities
-    -> (all-gather of the conditional graph) -> symmetrised P on every rank."""
+    -> (all-gather of the conditional graph) -> symmetrised P on every rank.
+    C4 (BASELINE configs[3]): the same stages on tests/configs.py c4's 500k x
+    300 sparse rows (dense on the device, its nonzeros the COO input) with the
+    cosine metric."""
     n, d, k = a.n, a.dim, a.k
     kk = min(k, n - 1)
-    X = gmm(n, d, 2, dev)
+    if a.config == "c4":
+        import configs
+        X = torch.from_numpy(configs.c4(n=n, d=d)).to(dev)
+    else:
+        X = gmm(n, d, 2, dev)
     sync_barrier(world)
     t0 = time.perf_counter()
     idx = torch.empty((r1 - r0, kk), dtype=torch.int32, device=dev)
     dist = torch.empty((r1 - r0, kk), dtype=torch.float64, device=dev)
-    ctx.dev_knn(X, k, "sqeuclidean", r0, r1, idx, dist)
+    ctx.dev_knn(X, k, metric, r0, r1, idx, dist)
     sync_barrier(world)
     t_knn = max_over_ranks(time.perf_counter() - t0, world)
     knn_filter_ms = float(sum(ctx.stage_ms("knn.filter")))
@@ -225,6 +233,14 @@ def main():
         if a.n == 1_000_000:
             a.n = 50_000
         a.dim = 64
+    C, metric = 2, "sqeuclidean"
+    if a.config == "c4":
+        if a.n == 1_000_000:
+            a.n = 500_000
+        if a.dim == 128:
+            a.dim = 300
+        C, metric = 3, "cosine"
+        a.no_cpu_baseline = True   # the CPU baseline leg restates the 2-D path (oracle_gradient); C3 carries it
     n, d, k = a.n, a.dim, a.k
     kk = min(k, n - 1)
     r0, r1 = T.shard_rows(n, world, rank)
@@ -238,16 +254,17 @@ def main():
         e0, e1 = 0, nnz
         kk = n - 1
     else:
-        orp, oc, ov, nnz, e0, e1, t_knn, knn_filter_ms, t_aff, X_host = setup_c3(ctx, a, dev, world, rank, r0, r1)
-    Y = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+        orp, oc, ov, nnz, e0, e1, t_knn, knn_filter_ms, t_aff, X_host = setup_c3(ctx, a, dev, world, rank, r0, r1,
+                                                                                  metric)
+    Y = torch.zeros((n, C), dtype=torch.float64, device=dev)
     upd = torch.zeros_like(Y)
     gains = torch.ones_like(Y)
-    Yh, _, _ = ctx.initWorkingSet(n, 2, seed=a.y0_seed)
+    Yh, _, _ = ctx.initWorkingSet(n, C, seed=a.y0_seed)
     if a.y0_perturb:
         Yh = Yh * (1.0 + a.y0_perturb * np.random.default_rng(a.y0_perturb_seed).normal(size=Yh.shape))
     Y[:n].copy_(torch.from_numpy(Yh))
     snap = (Y.clone(), upd.clone(), gains.clone())
-    params = default_params(iterations=a.iterations, theta=a.theta)
+    params = default_params(iterations=a.iterations, theta=a.theta, n_components=C, metric=metric)
     sync_barrier(world)
     t0 = time.perf_counter()
     ctx.dev_opt_setup(params, orp, oc, ov, n, Y, upd, gains)
@@ -322,7 +339,7 @@ def main():
     # bytes per launch = nnz*(4 col + 8 val) + (rows+1)*8 row_ptr
     #   + rows*(16 own Y + 16 attr out) + n*16 (gathered Y_j, counted once)
     rows = r1 - r0
-    attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 32 + n * 16
+    attr_bytes = (e1 - e0) * 12 + (rows + 1) * 8 + rows * 16 * C + n * 8 * C
     # log flags: 0 = non-loss launch on the side stream (beside the tree build / BH),
     # 1 = launch alone on the context stream, 2 = loss launch on the side stream
     # (Z-free KL terms), 3 = non-loss launch alone on the context stream
@@ -338,9 +355,11 @@ def main():
     dense_small = nnz // max(n, 1) > 1024 and n * 16 <= (2 << 20)
     tiles_on = os.environ.get("TSNE_ATTRACT_TILES", "1")[:1] != "0" and not dense_small
     attr_kernel = "attract_tiles<LOSS=false>" if tiles_on else "attract_rows<64,4,LOSS=false>"
+    if C == 3:
+        attr_kernel = "attract3<LOSS=false>"
     knn_flops = 2.0 * (r1 - r0) * n * d
     knn_mode = "f32" if os.environ.get("TSNE_KNN_BF16", "1")[:1] == "0" else "bf16x3"
-    upd_bytes = 128 * rows   # N*C*(5 reads + 3 writes)*8 B, C = 2
+    upd_bytes = 64 * C * rows   # N*C*(5 reads + 3 writes)*8 B
     upd_avg = float(np.mean(upd_ms)) if upd_ms else None
     prof = window_profile + timeline
     bh_ms_sum = sum(e["bh_ms"] for e in prof)
@@ -348,9 +367,11 @@ def main():
     def bh_rate(key):
         return sum(e[key] for e in prof) / (bh_ms_sum * 1e-3) if bh_ms_sum > 0 else None
 
-    workload = (f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, theta {a.theta}" if a.config == "c3"
-                else f"C5: {n}-point precomputed distance matrix ({n}x{n - 1} entries), perplexity {a.perplexity}, "
-                     f"theta {a.theta}")
+    workload = {"c3": f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, theta {a.theta}",
+                "c4": f"C4: {n}x{d} sparse rows (30 nonzeros each), cosine, k={k}, perplexity {a.perplexity}, "
+                      f"theta {a.theta}, 3-D embedding (octree)",
+                "c5": f"C5: {n}-point precomputed distance matrix ({n}x{n - 1} entries), perplexity {a.perplexity}, "
+                      f"theta {a.theta}"}[a.config]
     workload += (f"; timed region = the reference's whole schedule t=1..{a.iterations} (TsneHelpers.scala:396-430) "
                  f"as {steps} steps of {a.iterations // steps} iterations, value = T / loop seconds; the "
                  f"pre-expansion window t=1..{win} (root-tile phase) is reported apart as window_it_s")
@@ -368,10 +389,10 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)"
-                 if a.config == "c3" else
-                 "full sqeuclidean distance matrix (diagonal excluded) of a synthetic 10-blob 64-D Gaussian "
-                 "mixture (seed 4), seeded Y0 ~ N(0, 1e-4^2)"),
+        "data": {"c3": "synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)",
+                 "c4": "synthetic 20-topic sparse count rows (tests/configs.py c4, seed 3), seeded Y0 ~ N(0, 1e-4^2)",
+                 "c5": "full sqeuclidean distance matrix (diagonal excluded) of a synthetic 10-blob 64-D Gaussian "
+                       "mixture (seed 4), seeded Y0 ~ N(0, 1e-4^2)"}[a.config],
         "config": {"workload": workload, "n": n, "dim": d, "k": k, "theta": a.theta, "iterations": a.iterations,
                    "parallelism": f"rows{world}", "nnz_P": int(nnz),
                    "loop_full_s": t_loop, "full_schedule_it_s": value, "end_to_end_s": e2e,
@@ -410,7 +431,9 @@ def main():
                      "loss_launch": {"kernel": attr_kernel.replace("LOSS=false", "LOSS=true") + " + KL terms",
                                      "avg_ms": float(np.mean(loss_l)) if loss_l else None,
                                      "launches": len(loss_l)}},
-        "update_centre": {"kernels": "combine_update<1> (+ centring mean partials) + mean2_final + center_scatter",
+        "update_centre": {"kernels": ("combine_update<1> (+ centring mean, finalised by its last block) + "
+                                      "center_scatter") if C == 2 else
+                                     "combine_update3<1> + 3 x (reduce_partial + reduce_final) + center_apply + copy",
                           "avg_ms": upd_avg, "bytes_per_iteration": upd_bytes,
                           "achieved_GBs": upd_bytes / (upd_avg * 1e-3) / 1e9 if upd_avg else None,
                           "frac": upd_bytes / (upd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if upd_avg else None},
@@ -438,6 +461,12 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as fh:
                 out["bh"]["valu_pmc"] = json.load(fh)
+    if a.config == "c4":
+        out["metric"] = "t-SNE iterations/sec at C4 (500k x 300 sparse, cosine, 3-D embedding); end-to-end s"
+        out["bh"]["note"] = ("octree Barnes-Hut repulsion (QuadTree.scala:123-152 generalised to 3-D, DESIGN 3b); "
+                             "the 2-D work counters do not apply")
+        for key in ("pops_per_s", "lane_child_evals_per_s", "dense_pair_terms_per_s", "moment_evals_per_s"):
+            out["bh"].pop(key, None)
     if a.config == "c5":
         out["metric"] = "t-SNE iterations/sec at the 50k precomputed-distance-matrix config (C5); affinities+joint s"
         for key in ("knn_s", "knn_pts_per_s", "knn_filter_ms", "knn_mfma_tflops", "knn_mfma_frac_of_peak",

@@ -67,8 +67,10 @@ template <class Fn> static void run_group(tsne_ctx *g, Fn &&fn) {
             try {
                 DeviceGuard dg(g->group[r]->device);
                 fn(g->group[r], r);
+                comm_release(g->group[r]);
             } catch (...) {
                 err[r] = std::current_exception();
+                comm_release(g->group[r]);
                 // release every rank: a loopback barrier, or the peers' RCCL
                 // collectives still waiting for this rank (ncclCommAbort)
                 for (tsne_ctx *c : g->group) comm_abort(c);

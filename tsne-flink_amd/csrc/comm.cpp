@@ -18,7 +18,10 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <map>
 #include <mutex>
 
 #include "common.hpp"
@@ -35,6 +38,11 @@ struct Comm {
     // a rank failed: make every pending and later collective of this rank
     // fail (TSNE_ERR_COMM) instead of waiting for it; callable from another thread
     virtual void abort() {}
+    // the calling rank's work in a group call has ended (loopback serial mode:
+    // hand the device turn on); called on the rank's own thread
+    virtual void release(tsne_ctx *) {}
+    // a phase boundary inside a rank's work (loopback serial mode: timed)
+    virtual void mark(tsne_ctx *, const char *) {}
 };
 
 namespace {
@@ -82,6 +90,15 @@ struct RcclComm : Comm {
 };
 
 // Shared state of the ranks of one loopback group (one device).
+//
+// TSNE_LOOP_SERIAL=<file>: the ranks take turns on the device.  A rank holds
+// the turn from the end of one collective to the start of the next, drains
+// the device before it lets go, and logs the wall time of that segment of its
+// own work.  With the segments of one collective aligned across ranks, the
+// sum over collectives of the slowest rank's segment is the compute span a
+// world-size group of devices would take (collectives excluded: they are the
+// loopback's host copies here).  The summary goes to <file> (JSON) when the
+// group ends: a projection tool for N GPUs measured on one.
 struct LoopGroup {
     int world;
     std::mutex mu;
@@ -90,7 +107,85 @@ struct LoopGroup {
     uint64_t generation = 0;
     bool aborted = false;
     std::vector<void *> ptr;
-    explicit LoopGroup(int w) : world(w), ptr(w, nullptr) {}
+    // serial timing mode
+    std::string serial_path;
+    std::mutex turn;
+    std::vector<char> holding;
+    std::vector<std::chrono::steady_clock::time_point> t_acq;
+    std::vector<std::vector<std::pair<std::string, double>>> segs;   // per rank: (collective, ms)
+    explicit LoopGroup(int w) : world(w), ptr(w, nullptr), holding(w, 0), t_acq(w), segs(w) {
+        const char *e = getenv("TSNE_LOOP_SERIAL");
+        if (e && e[0]) serial_path = e;
+    }
+    ~LoopGroup() {
+        if (serial_path.empty()) return;
+        if (FILE *f = fopen(serial_path.c_str(), "w")) {
+            // collectives are issued in the same sequence on every rank
+            size_t m = segs[0].size();
+            for (int r = 1; r < world; ++r) m = std::min(m, segs[r].size());
+            std::map<std::string, std::vector<double>> lab;   // [sum of max, sum of mean, count]
+            double span = 0.0;
+            std::vector<double> tot(world, 0.0);
+            for (size_t i = 0; i < m; ++i) {
+                double mx = 0.0, sm = 0.0;
+                for (int r = 0; r < world; ++r) {
+                    mx = std::max(mx, segs[r][i].second);
+                    sm += segs[r][i].second;
+                    tot[r] += segs[r][i].second;
+                }
+                auto &v = lab[segs[0][i].first];
+                if (v.empty()) v.assign(3, 0.0);
+                v[0] += mx; v[1] += sm / world; v[2] += 1.0;
+                span += mx;
+            }
+            fprintf(f, "{\"world\": %d, \"segments\": %zu, \"span_ms\": %.6f, \"rank_total_ms\": [", world, m, span);
+            for (int r = 0; r < world; ++r) fprintf(f, "%s%.6f", r ? ", " : "", tot[r]);
+            fprintf(f, "], \"by_collective\": {");
+            bool first = true;
+            for (auto &kv : lab) {
+                fprintf(f, "%s\"%s\": {\"max_ms\": %.6f, \"mean_ms\": %.6f, \"count\": %.0f}", first ? "" : ", ",
+                        kv.first.c_str(), kv.second[0], kv.second[1], kv.second[2]);
+                first = false;
+            }
+            fprintf(f, "}}\n");
+            fclose(f);
+        }
+    }
+    // serial mode: the end of a segment of this rank's work (before a collective)
+    void seg_end(tsne_ctx *ctx, const char *what) {
+        if (serial_path.empty()) return;
+        TSNE_HIP(hipDeviceSynchronize());   // the side stream too
+        const int r = ctx->rank;
+        if (holding[r]) {
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_acq[r]).count();
+            segs[r].emplace_back(what, ms);
+            holding[r] = 0;
+            turn.unlock();
+        }
+    }
+    // serial mode: a phase boundary -- the stretch so far is logged as `what`
+    // and the next one starts (the turn is kept)
+    void seg_mark(tsne_ctx *ctx, const char *what) {
+        if (serial_path.empty() || !holding[ctx->rank]) return;
+        TSNE_HIP(hipDeviceSynchronize());
+        const int r = ctx->rank;
+        const auto now = std::chrono::steady_clock::now();
+        segs[r].emplace_back(what, std::chrono::duration<double, std::milli>(now - t_acq[r]).count());
+        t_acq[r] = now;
+    }
+    void seg_release(tsne_ctx *ctx) {
+        if (serial_path.empty() || !holding[ctx->rank]) return;
+        holding[ctx->rank] = 0;
+        turn.unlock();
+    }
+    // serial mode: the start of the next segment (after a collective)
+    void seg_begin(tsne_ctx *ctx) {
+        if (serial_path.empty()) return;
+        const int r = ctx->rank;
+        turn.lock();
+        holding[r] = 1;
+        t_acq[r] = std::chrono::steady_clock::now();
+    }
     // all ranks meet; throws on every rank once one rank has aborted
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
@@ -117,14 +212,17 @@ struct LoopComm : Comm {
     explicit LoopComm(std::shared_ptr<LoopGroup> grp) : g(std::move(grp)) {}
 
     // publish this rank's pointer once its stream has produced the data
-    void publish(tsne_ctx *ctx, void *p) {
+    void publish(tsne_ctx *ctx, void *p, const char *what) {
         TSNE_HIP(hipStreamSynchronize(ctx->stream));
+        g->seg_end(ctx, what);
         g->ptr[ctx->rank] = p;
         g->barrier();
     }
     template <class T> void allreduce(tsne_ctx *ctx, T *buf, size_t count) {
         if (count == 0) return;
-        publish(ctx, buf);
+        const std::string what = std::string(sizeof(T) == 8 && T(0.5) != T(0) ? "allreduce_f64[" : "allreduce_u64[") +
+                                 std::to_string(count) + "]";
+        publish(ctx, buf, what.c_str());
         std::vector<T> acc(count, T(0)), tmp(count);
         for (int r = 0; r < g->world; ++r) {   // fixed rank order: identical sums on every rank
             TSNE_HIP(hipMemcpy(tmp.data(), g->ptr[r], sizeof(T) * count, hipMemcpyDeviceToHost));
@@ -132,12 +230,15 @@ struct LoopComm : Comm {
         }
         g->barrier();   // every rank has read every buffer before any is overwritten
         TSNE_HIP(hipMemcpy(buf, acc.data(), sizeof(T) * count, hipMemcpyHostToDevice));
+        g->seg_begin(ctx);
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override { allreduce(ctx, buf, count); }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override { allreduce(ctx, buf, count); }
     void abort() override { g->abort(); }
+    void release(tsne_ctx *ctx) override { g->seg_release(ctx); }
+    void mark(tsne_ctx *ctx, const char *what) override { g->seg_mark(ctx, what); }
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
-        publish(ctx, buf);
+        publish(ctx, buf, "allgatherv");
         uint8_t *b = static_cast<uint8_t *>(buf);
         for (int r = 0; r < g->world; ++r) {
             if (r == ctx->rank || off[r + 1] == off[r]) continue;
@@ -145,6 +246,7 @@ struct LoopComm : Comm {
             TSNE_HIP(hipMemcpy(b + off[r], src + off[r], (size_t)(off[r + 1] - off[r]), hipMemcpyDeviceToDevice));
         }
         g->barrier();
+        g->seg_begin(ctx);
     }
 };
 
@@ -256,6 +358,14 @@ void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback) {
 // barrier) fail from now on instead of waiting.
 void comm_abort(tsne_ctx *ctx) {
     if (ctx->comm) ctx->comm->abort();
+}
+
+void comm_mark(tsne_ctx *ctx, const char *what) {
+    if (ctx->comm) ctx->comm->mark(ctx, what);
+}
+
+void comm_release(tsne_ctx *ctx) {
+    if (ctx->comm) ctx->comm->release(ctx);
 }
 
 void comm_destroy(tsne_ctx *ctx) {

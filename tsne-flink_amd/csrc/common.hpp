@@ -239,6 +239,8 @@ void comm_destroy(tsne_ctx *ctx);
 void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback);
 void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops *ops, void *user);
 void comm_abort(tsne_ctx *ctx);
+void comm_release(tsne_ctx *ctx);
+void comm_mark(tsne_ctx *ctx, const char *what);   // phase boundary (loopback serial timing)   // end of a rank's group call (loopback serial timing)
 // in place: rank r's bytes [off_bytes[r], off_bytes[r+1]) of buf reach every rank
 void comm_allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off_bytes);
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count);

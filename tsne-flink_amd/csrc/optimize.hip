@@ -114,6 +114,7 @@ struct OptState {
         while (attract_iter.size() > StageTimers::CAP) attract_iter.pop_front();
     }
     double *mpart = nullptr;  // centring mean: block partials of combine_update
+    uint32_t *mcnt = nullptr; // its arrival counter (last block finalises the mean)
     // tiled attraction layout of the owned rows (attract_tiles), rebuilt with them
     bool at_on = false;
     int64_t at_nrb = 0, at_ncb = 0;
@@ -655,14 +656,27 @@ __global__ void at_ranges(const ATile *__restrict__ tiles, int32_t nt, int64_t n
 // per row, all accesses coalesced except F[inv[i]] (near-identity gather).
 // With `mpart` (MODE 1) each block also writes the sum of its rows' Ynew
 // (x, y) to mpart[2 * block]: the centring mean's partials, fused into the
-// update so that centerEmbedding costs one more pass (center_scatter).
+// update so that centerEmbedding costs one more pass (center_scatter).  With
+// `mcnt` as well, the last block to arrive sums the partials (mean2_final's
+// order, so the same bits) into mean[0..1] and re-arms the counter: one
+// launch fewer per step.  The partials cross XCDs (separate L2s) as
+// system-scope stores / loads, drained before the agent-scope arrival atomic
+// (as bottom_up_top in bhtree.hip), with no L2 write-back fence.
+__device__ __forceinline__ void st_sys_o(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys_o(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 template <int MODE>
 __global__ __launch_bounds__(256) void combine_update(
     int64_t r0, int64_t r1, const double2 *__restrict__ attr, const int32_t *__restrict__ inv,
     const double2 *__restrict__ F, const double *__restrict__ scal, const double *__restrict__ Y,
     double *__restrict__ grad, double *__restrict__ Ynew, double *__restrict__ upd, double *__restrict__ gains,
-    double min_gain, double mom, double lr, double *__restrict__ mpart) {
+    double min_gain, double mom, double lr, double *__restrict__ mpart, uint32_t *__restrict__ mcnt,
+    double ntot, double *__restrict__ mean) {
     __shared__ double sm[2][4];
+    __shared__ int last;
     const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i < r1;
     double yn[2] = {0.0, 0.0};
@@ -697,8 +711,35 @@ __global__ __launch_bounds__(256) void combine_update(
         if (lane_id() == 0) { sm[0][threadIdx.x >> 6] = sx; sm[1][threadIdx.x >> 6] = sy; }
         __syncthreads();
         if (threadIdx.x == 0) {
-            mpart[2 * blockIdx.x] = (sm[0][0] + sm[0][1]) + (sm[0][2] + sm[0][3]);
-            mpart[2 * blockIdx.x + 1] = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
+            const double px = (sm[0][0] + sm[0][1]) + (sm[0][2] + sm[0][3]);
+            const double py = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
+            if (mcnt) {
+                st_sys_o(mpart + 2 * blockIdx.x, px);
+                st_sys_o(mpart + 2 * blockIdx.x + 1, py);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                last = __hip_atomic_fetch_add(mcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       gridDim.x - 1;
+            } else {
+                mpart[2 * blockIdx.x] = px;
+                mpart[2 * blockIdx.x + 1] = py;
+            }
+        }
+        if (mcnt) {
+            __syncthreads();
+            if (!last) return;
+            double s[2] = {0.0, 0.0};
+            for (int64_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+                s[0] += ld_sys_o(mpart + 2 * b);
+                s[1] += ld_sys_o(mpart + 2 * b + 1);
+            }
+            s[0] = wave_sum(s[0]);
+            s[1] = wave_sum(s[1]);
+            __syncthreads();   // sm is reused
+            if (lane_id() == 0) { sm[0][threadIdx.x >> 6] = s[0]; sm[1][threadIdx.x >> 6] = s[1]; }
+            __syncthreads();
+            if (threadIdx.x < 2)
+                mean[threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3])) / ntot;
+            if (threadIdx.x == 0) *mcnt = 0u;   // the next launch is stream-ordered after this one
         }
     }
 }
@@ -1123,10 +1164,11 @@ template <int MODE>
 static void combine_launch(hipStream_t st, int64_t r0, int64_t r1, const double2 *attr, const int32_t *inv,
                            const double2 *F, const double *scal, const double *Y, double *grad, double *Ynew,
                            double *upd, double *gains, double min_gain, double mom, double lr,
-                           double *mpart = nullptr) {
+                           double *mpart = nullptr, uint32_t *mcnt = nullptr, double ntot = 0.0,
+                           double *mean = nullptr) {
     if (r1 <= r0) return;
     hipLaunchKernelGGL(combine_update<MODE>, dim3(ceil_div(r1 - r0, 256)), dim3(256), 0, st, r0, r1, attr, inv, F,
-                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr, mpart);
+                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr, mpart, mcnt, ntot, mean);
 }
 
 // Upper bound of attract_launch's block count for rows rows.
@@ -1598,6 +1640,8 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(rows_cap)));
     s->part2 = ws.get<double>("opt.part2", NPART);
     s->mpart = ws.get<double>("opt.mpart", 2 * ceil_div(rows_cap, 256) + 2);
+    s->mcnt = ws.get<uint32_t>("opt.mcnt", 1);
+    TSNE_HIP(hipMemsetAsync(s->mcnt, 0, sizeof(uint32_t), st));
     s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
     s->bounds = ws.get<int64_t>("opt.bounds", world + 1);
     s->lscore = ws.get<unsigned long long>("opt.lscore", 2);
@@ -1757,7 +1801,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     const int64_t blocks = attract3_launch(st, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex,
                                            s->attr3, s->part, want_loss);
     ctx->timers.end("opt.attract", st);
-    s->log_attract(t, 1);
+    s->log_attract(t, want_loss ? 1 : 3);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     ctx->timers.begin("opt.update", st);
     if (s->L1 > s->L0)
@@ -1970,6 +2014,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // the strict near-exact tolerance while P is exaggerated (the dynamics
     // amplify any difference fastest there), the late one after
     bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(), bh_near_tol(ex == 1.0));
+    if (world > 1) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
     if (overlap && ov_mode == 1) side_attract();
     if (overlap && ov_mode == 2) side_wait();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
@@ -1982,6 +2027,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         build_qlist(ctx, s, s->tree.idx_sorted);
         bh_repulsion(ctx, s->tree, p.theta, 0, s->L1 - s->L0, s->F, s->z, s->profile ? s->visits : nullptr, s->qlist,
                      bcost, recut_mode(ctx, s));
+        comm_mark(ctx, s->tree.root_tile ? "bh_rt" : "bh");
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
@@ -2006,13 +2052,20 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     ctx->timers.begin("opt.update", st);
     const bool fused_mean = world == 1;
     const int c = s->cur;
+    // (one rank: mean2_final; TSNE_MEAN_LASTBLOCK=1 finalises the mean in
+    // combine_update's last block instead -- one launch fewer, but 3907
+    // same-address arrival atomics at 1M rows: update 0.062 -> 0.085 ms)
+    static const bool lastblk = [] { const char *e = getenv("TSNE_MEAN_LASTBLOCK"); return e && e[0] == '1'; }();
+    const bool last_block = fused_mean && lastblk;
     combine_launch<1>(st, s->L0, s->L1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
-                      s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
+                      s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr,
+                      last_block ? s->mcnt : nullptr, (double)n, s->scal + 2);
     if (want_loss) record_loss(ctx, s, t, blocks, overlap, ex);
     // 5. exchange (all-gather of the owned slices) + 6. centre
     if (fused_mean) {
-        hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256), (double)n,
-                           s->scal + 2);
+        if (!last_block)
+            hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256),
+                               (double)n, s->scal + 2);
     } else {
         gather_Ynew(ctx, s);
         for (int k = 0; k < 2; ++k) {
