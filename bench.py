@@ -374,7 +374,7 @@ def main():
                       f"theta {a.theta}"}[a.config]
     workload += (f"; timed region = the reference's whole schedule t=1..{a.iterations} (TsneHelpers.scala:396-430) "
                  f"as {steps} steps of {a.iterations // steps} iterations, value = T / loop seconds; the "
-                 f"pre-expansion window t=1..{win} (root-tile phase) is reported apart as window_it_s")
+                 f"pre-expansion window t=1..{win} is reported apart as window_it_s")
     e2e = t_knn + t_aff + t_setup + t_loop + t_out
 
     out = {
@@ -463,6 +463,8 @@ def main():
                 out["bh"]["valu_pmc"] = json.load(fh)
     if a.config == "c4":
         out["metric"] = "t-SNE iterations/sec at C4 (500k x 300 sparse, cosine, 3-D embedding); end-to-end s"
+        out["window_note"] = (f"t=1..{win}, timed inside the warmup from the same initial state: the small-embedding "
+                              "phase (octree moments per query); not the metric's workload")
         out["bh"]["note"] = ("octree Barnes-Hut repulsion (QuadTree.scala:123-152 generalised to 3-D, DESIGN 3b); "
                              "the 2-D work counters do not apply")
         for key in ("pops_per_s", "lane_child_evals_per_s", "dense_pair_terms_per_s", "moment_evals_per_s"):
