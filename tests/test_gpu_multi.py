@@ -93,6 +93,38 @@ def test_multi_optimize_loopback_matches_single(world):
     assert close(Y, Ys) and close(u, us) and close(g, gs)
 
 
+def test_multi_optimize_loopback_serial_timing(tmp_path, monkeypatch):
+    """TSNE_LOOP_SERIAL (comm.cpp LoopGroup): the ranks take turns on the
+    device and log each stretch of work between collectives, with the tree /
+    BH phase marks -- the same results as world 1, and a summary whose
+    per-collective counts follow the schedule (scripts/loop_projection.py)."""
+    import json
+    P, Y0 = problem()
+    prm = default_params(iterations=40, theta=0.5, learning_rate=200.0)
+    Ys, _, _, ls = run_single(P, Y0, prm)
+    path = tmp_path / "serial.json"
+    monkeypatch.setenv("TSNE_LOOP_SERIAL", str(path))
+    m = T.Context.multi([0, 0])
+    try:
+        Y, u, g = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+        lm = m.optimize(*P, Y, u, g, prm)
+    finally:
+        m.close()
+    for t in ls:
+        assert abs(lm[t] - ls[t]) <= TOL * abs(ls[t]), t
+    assert close(Y, Ys)
+    rep = json.loads(path.read_text())
+    assert rep["world"] == 2 and len(rep["rank_total_ms"]) == 2 and rep["span_ms"] > 0
+    lab = rep["by_collective"]
+    # one Z all-reduce per iteration + the loss every 10th; one Y all-gather per iteration
+    # (+ the gathers of a relabel); a tree and a BH mark per iteration
+    assert lab["allreduce_f64[1]"]["count"] >= 40 + 4
+    assert lab["allgatherv"]["count"] >= 40
+    marks = sum(v["count"] for k, v in lab.items() if k.startswith("tree"))
+    assert marks == 40 and sum(v["count"] for k, v in lab.items() if k.startswith("bh")) == 40
+    assert all(v["max_ms"] >= v["mean_ms"] >= 0 for v in lab.values())
+
+
 def test_multi_optimize3_loopback_matches_single():
     P, Y0 = problem(n=900, c=3, seed=8)
     prm = default_params(n_components=3, iterations=40, theta=0.5, learning_rate=200.0)
