@@ -3228,8 +3228,9 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the wave's pops and tile points
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    auto kern = kp >= 8 ? (mode == 2 ? bh_traverse<8, 2, false> : mode == 1 ? bh_traverse<8, 1, false> : bh_traverse<8, 0, false>)
-                        : (mode == 2 ? bh_traverse<4, 2, false> : mode == 1 ? bh_traverse<4, 1, false> : bh_traverse<4, 0, false>);
+    auto kern = kp >= 16  ? (mode == 2 ? bh_traverse<16, 2, false> : mode == 1 ? bh_traverse<16, 1, false> : bh_traverse<16, 0, false>)
+                : kp >= 8 ? (mode == 2 ? bh_traverse<8, 2, false> : mode == 1 ? bh_traverse<8, 1, false> : bh_traverse<8, 0, false>)
+                          : (mode == 2 ? bh_traverse<4, 2, false> : mode == 1 ? bh_traverse<4, 1, false> : bh_traverse<4, 0, false>);
     auto tkern = mode == 2 ? bh_traverse<4, 2, true> : mode == 1 ? bh_traverse<4, 1, true> : bh_traverse<4, 0, true>;
     // dynamic splitting of heavy waves (TSNE_BH_SPILL=1: on; off by default --
     // measured without gain over the C3 schedule); budget =
