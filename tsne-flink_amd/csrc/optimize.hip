@@ -1010,7 +1010,12 @@ __device__ __forceinline__ double qterm3(const double *a, const double *b) {
 
 // One wave per row (grid-stride), lanes over the row's entries, then a
 // wave reduction: attr_i = sum_j ex P_ij q_ij (y_i - y_j); LOSS adds the KL
-// terms into one partial per block (TsneHelpers.scala:269-306).
+// terms into one partial per block (TsneHelpers.scala:269-306).  A lane's
+// entries e, e + 64, ... are taken ATTR3_U at a time: their column and value
+// loads, then their Y_j gathers, are all in flight before the first term is
+// summed (C4: ~163 entries per row, one round); the sums keep the lane's
+// entry order, so the result is the same to the bit.
+constexpr int ATTR3_U = 4;
 template <bool LOSS, int MET>
 __global__ __launch_bounds__(256) void attract3(const int64_t *__restrict__ row_ptr, const int32_t *__restrict__ col,
                                                 const double *__restrict__ val, int64_t r0, int64_t r1,
@@ -1024,14 +1029,30 @@ __global__ __launch_bounds__(256) void attract3(const int64_t *__restrict__ row_
     for (int64_t i = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < r1; i += nw) {
         const double yi[3] = {Y[3 * i], Y[3 * i + 1], Y[3 * i + 2]};
         double f[3] = {0.0, 0.0, 0.0};
-        for (int64_t e = row_ptr[i] + lane; e < row_ptr[i + 1]; e += 64) {
-            const int64_t j = col[e];
-            const double yj[3] = {Y[3 * j], Y[3 * j + 1], Y[3 * j + 2]};
-            const double pij = __dmul_rn(val[e], ex);
-            const double q = qterm3<MET>(yi, yj);
-            const double sc = __dmul_rn(pij, q);
-            for (int k = 0; k < 3; ++k) f[k] = __dadd_rn(f[k], __dmul_rn(sc, __dsub_rn(yi[k], yj[k])));
-            if (LOSS) lsum += pij * log(pij / (q / Z));
+        const int64_t e1 = row_ptr[i + 1];
+        for (int64_t eb = row_ptr[i] + lane; eb < e1; eb += 64 * ATTR3_U) {
+            int64_t j[ATTR3_U];
+            double pv[ATTR3_U];
+#pragma unroll
+            for (int u = 0; u < ATTR3_U; ++u) {
+                const int64_t e = eb + 64 * u;
+                j[u] = e < e1 ? (int64_t)col[e] : i;
+                pv[u] = e < e1 ? val[e] : 0.0;
+            }
+            double yj[ATTR3_U][3];
+#pragma unroll
+            for (int u = 0; u < ATTR3_U; ++u)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) yj[u][k] = Y[3 * j[u] + k];
+#pragma unroll
+            for (int u = 0; u < ATTR3_U; ++u) {
+                if (eb + 64 * u >= e1) break;
+                const double pij = __dmul_rn(pv[u], ex);
+                const double q = qterm3<MET>(yi, yj[u]);
+                const double sc = __dmul_rn(pij, q);
+                for (int k = 0; k < 3; ++k) f[k] = __dadd_rn(f[k], __dmul_rn(sc, __dsub_rn(yi[k], yj[u][k])));
+                if (LOSS) lsum += pij * log(pij / (q / Z));
+            }
         }
         for (int k = 0; k < 3; ++k) {
             const double v = wave_sum(f[k]);
