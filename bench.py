@@ -433,7 +433,7 @@ def main():
                                      "launches": len(loss_l)}},
         "update_centre": {"kernels": ("combine_update<1> (+ centring mean, finalised by its last block) + "
                                       "center_scatter") if C == 2 else
-                                     "combine_update3<1> + 3 x (reduce_partial + reduce_final) + center_apply + copy",
+                                     "combine_update3<1> (+ centring mean partials) + mean3_final + center3_scatter",
                           "avg_ms": upd_avg, "bytes_per_iteration": upd_bytes,
                           "achieved_GBs": upd_bytes / (upd_avg * 1e-3) / 1e9 if upd_avg else None,
                           "frac": upd_bytes / (upd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if upd_avg else None},

@@ -1067,30 +1067,78 @@ __global__ __launch_bounds__(256) void attract3(const int64_t *__restrict__ row_
     }
 }
 
-// grad = attr - F / Z, then (MODE 1) updateEmbedding -> Ynew (3 components)
+// grad = attr - F / Z, then (MODE 1) updateEmbedding -> Ynew (3 components).
+// With `mpart` (MODE 1, one rank) each block also writes the sums of its
+// rows' Ynew to mpart[3 * block + c]: the centring mean's partials, as
+// combine_update in 2-D (meanC_final, center3_scatter).
 template <int MODE>
 __global__ __launch_bounds__(256) void combine_update3(int64_t r0, int64_t r1, const double *__restrict__ attr,
                                                        const int32_t *__restrict__ inv, const double *__restrict__ F,
                                                        const double *__restrict__ scal, const double *__restrict__ Y,
                                                        double *__restrict__ grad, double *__restrict__ Ynew,
                                                        double *__restrict__ upd, double *__restrict__ gains,
-                                                       double min_gain, double mom, double lr) {
+                                                       double min_gain, double mom, double lr,
+                                                       double *__restrict__ mpart) {
+    __shared__ double sm[3][4];
     const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= r1) return;
-    const double Z = scal[0];
-    const int64_t si = inv[i];
+    double yn[3] = {0.0, 0.0, 0.0};
+    if (i < r1) {
+        const double Z = scal[0];
+        const int64_t si = inv[i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double g = attr[3 * (i - r0) + c] - F[3 * si + c] / Z;
+            const int64_t o = 3 * i + c;
+            if (MODE == 0) { grad[o] = g; continue; }
+            const double u = upd[o], gn0 = gains[o];
+            const double gn = ((g > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain) : jmax(gn0 + 0.2, min_gain);
+            const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g));
+            gains[o] = gn;
+            upd[o] = un;
+            yn[c] = __dadd_rn(un, Y[o]);
+            Ynew[o] = yn[c];
+        }
+    }
+    if (MODE == 1 && mpart) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double v = wave_sum(yn[c]);
+            if (lane_id() == 0) sm[c][threadIdx.x >> 6] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3)
+            mpart[3 * blockIdx.x + threadIdx.x] =
+                (sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3]);
+    }
+}
+
+// mean[c] = (sum of the nb block partials mpart[3 b + c], fixed order) / n
+__global__ __launch_bounds__(256) void mean3_final(const double *__restrict__ mpart, int64_t nb, double n,
+                                                   double *__restrict__ mean) {
+    __shared__ double sm[3][4];
+    double s[3] = {0.0, 0.0, 0.0};
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x)
+        for (int c = 0; c < 3; ++c) s[c] += mpart[3 * b + c];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const double g = attr[3 * (i - r0) + c] - F[3 * si + c] / Z;
-        const int64_t o = 3 * i + c;
-        if (MODE == 0) { grad[o] = g; continue; }
-        const double u = upd[o], gn0 = gains[o];
-        const double gn = ((g > 0.0) == (u > 0.0)) ? jmax(gn0 * 0.8, min_gain) : jmax(gn0 + 0.2, min_gain);
-        const double un = __dsub_rn(__dmul_rn(mom, u), __dmul_rn(__dmul_rn(lr, gn), g));
-        gains[o] = gn;
-        upd[o] = un;
-        Ynew[o] = __dadd_rn(un, Y[o]);
+        const double v = wave_sum(s[c]);
+        if (lane_id() == 0) sm[c][threadIdx.x >> 6] = v;
     }
+    __syncthreads();
+    if (threadIdx.x < 3)
+        mean[threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3])) / n;
+}
+
+// centerEmbedding (TsneHelpers.scala:320-329) + the caller's copy (3-D: the
+// labels are the original indices): Y = Yu = Ynew - mean
+__global__ __launch_bounds__(256) void center3_scatter(const double *__restrict__ Ynew, int64_t n,
+                                                       const double *__restrict__ mean, double *__restrict__ Y,
+                                                       double *__restrict__ Yu) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 3 * n) return;
+    const double v = Ynew[e] - mean[e % 3];
+    Y[e] = v;
+    Yu[e] = v;
 }
 
 static int64_t attract3_blocks(int64_t rows) { return std::max<int64_t>(1, std::min<int64_t>(8192, ceil_div(rows, 4))); }
@@ -1333,7 +1381,7 @@ void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_
     const int64_t blocks = attract3_launch(st, d_row_ptr, d_col, d_P, 0, n, dY, scal, metric, exaggeration, attr,
                                            lpart, want_loss);
     hipLaunchKernelGGL(combine_update3<0>, dim3(ceil_div(n, 256)), dim3(256), 0, st, 0, n, attr, t.inv, F, scal, dY,
-                       d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0);
+                       d_grad, nullptr, nullptr, nullptr, 0.0, 0.0, 0.0, nullptr);
     TSNE_LAUNCH_CHECK();
     if (want_loss) {
         hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, lpart, blocks, 1, 0, part);
@@ -1660,7 +1708,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->scal = ws.get<double>("opt.scal", 8);
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(rows_cap)));
     s->part2 = ws.get<double>("opt.part2", NPART);
-    s->mpart = ws.get<double>("opt.mpart", 2 * ceil_div(rows_cap, 256) + 2);
+    s->mpart = ws.get<double>("opt.mpart", 3 * ceil_div(rows_cap, 256) + 3);   // C <= 3 components
     s->mcnt = ws.get<uint32_t>("opt.mcnt", 1);
     TSNE_HIP(hipMemsetAsync(s->mcnt, 0, sizeof(uint32_t), st));
     s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
@@ -1825,19 +1873,29 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     s->log_attract(t, want_loss ? 1 : 3);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     ctx->timers.begin("opt.update", st);
+    // one rank: the mean's block partials from combine_update3, one
+    // workgroup for the mean, one pass for centre + the caller's copy
+    const bool fused_mean = ctx->world == 1;
     if (s->L1 > s->L0)
         hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->L1 - s->L0, 256)), dim3(256), 0, st, s->L0, s->L1,
                            s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[0], s->gains[0],
-                           p.min_gain, mom, p.learning_rate);
+                           p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
     TSNE_LAUNCH_CHECK();
     if (want_loss) record_loss(ctx, s, t, blocks);
-    if (ctx->world > 1) gather_Ynew(ctx, s);
-    for (int k = 0; k < 3; ++k) {
-        hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 3, k, s->part2);
-        hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 2 + k, (double)n);
+    if (fused_mean) {
+        hipLaunchKernelGGL(mean3_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256), (double)n,
+                           s->scal + 2);
+        hipLaunchKernelGGL(center3_scatter, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, s->scal + 2, Y,
+                           s->Yu);
+    } else {
+        gather_Ynew(ctx, s);
+        for (int k = 0; k < 3; ++k) {
+            hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->Ynew, n, 3, k, s->part2);
+            hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 2 + k, (double)n);
+        }
+        hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, 3, s->scal + 2, Y);
+        TSNE_HIP(hipMemcpyAsync(s->Yu, Y, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st));
     }
-    hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, 3, s->scal + 2, Y);
-    TSNE_HIP(hipMemcpyAsync(s->Yu, Y, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st));
     ctx->timers.end("opt.update", st);
     TSNE_LAUNCH_CHECK();
     if (s->profile) finish_profile(ctx, s, t);
