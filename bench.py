@@ -46,6 +46,8 @@ METRIC = "t-SNE iterations/sec + end-to-end sec at N=1M×128 on 1/2/4/8 MI355X; 
 FP32_MFMA_PEAK_TF = 157.3
 BF16_MFMA_PEAK_TF = 2500.0   # dense (MI355X_MICROARCH.md); the kNN filter's bf16x3 passes run 3 bf16 MFMAs per product
 HBM_PEAK_GBS = 8000.0
+PMC_ATTRACT = "r03_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
+PMC_BH = "r03_bh_valu.json"
 
 
 def parse():
@@ -76,6 +78,8 @@ def parse():
                     help="relative N(0, eps^2) perturbation of Y0 (measures the chaotic spread of the final KL)")
     ap.add_argument("--y0-perturb-seed", type=int, default=1)
     ap.add_argument("--y0-seed", type=int, default=0, help="initWorkingSet seed (the reference is unseeded)")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="tsne_ctx_set_option on the bench's context (A/B of a tunable; repeatable)")
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
@@ -118,6 +122,7 @@ def trace_entry(ctx, t, rows, Y, n):
             "lane_utilisation": vis_t[5] / max(1, 64 * vis_t[6]),
             "heaviest_wave_vs_mean": vis_t[7] / max(1e-9, (vis_t[3] + vis_t[4] / 16) / per_wave),
             "max_wave_pops": vis_t[8], "max_wave_dense_points": vis_t[9],
+            "narrow_groups": ctx.counter("opt.narrow_groups"),
             "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()}
 
 
@@ -224,6 +229,9 @@ def main():
     if world > 1:
         torch.distributed.init_process_group("nccl", device_id=dev)
     ctx = T.Context(local)
+    for kv in a.option:
+        key, val = kv.split("=", 1)
+        ctx.set_option(key, float(val))
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     if world > 1:
         obj = [T.Context.unique_id() if rank == 0 else None]
@@ -385,6 +393,7 @@ def main():
         "steps": steps,
         "warmup": a.warmup,
         "ms_per_step": 1e3 * t_loop / steps,
+        "ms_per_iteration": 1e3 * t_loop / a.iterations,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -395,6 +404,8 @@ def main():
                        "mixture (seed 4), seeded Y0 ~ N(0, 1e-4^2)"}[a.config],
         "config": {"workload": workload, "n": n, "dim": d, "k": k, "theta": a.theta, "iterations": a.iterations,
                    "parallelism": f"rows{world}", "nnz_P": int(nnz),
+                   "step": f"{a.iterations // steps} iterations (ms_per_step is per step; ms_per_iteration apart)",
+                   "options": {kv.split("=", 1)[0]: float(kv.split("=", 1)[1]) for kv in a.option},
                    "loop_full_s": t_loop, "full_schedule_it_s": value, "end_to_end_s": e2e,
                    "window_it_s": (win / t_win) if t_win else None},
         "loop_full_s": t_loop,
@@ -431,7 +442,7 @@ def main():
                      "loss_launch": {"kernel": attr_kernel.replace("LOSS=false", "LOSS=true") + " + KL terms",
                                      "avg_ms": float(np.mean(loss_l)) if loss_l else None,
                                      "launches": len(loss_l)}},
-        "update_centre": {"kernels": ("combine_update<1> (+ centring mean, finalised by its last block) + "
+        "update_centre": {"kernels": ("combine_update<1> (+ the centring mean's block partials) + mean2_final + "
                                       "center_scatter") if C == 2 else
                                      "combine_update3<1> (+ centring mean partials) + mean3_final + center3_scatter",
                           "avg_ms": upd_avg, "bytes_per_iteration": upd_bytes,
@@ -446,18 +457,21 @@ def main():
         "window_profile": window_profile,
         "timeline": timeline,
     }
-    # HBM bytes per non-loss attraction launch over the same command's timed
-    # region, from committed PMC passes (profiles/r03_attract_traffic.json);
-    # BH VALU utilisation from committed PMC passes (profiles/r03_bh_valu.json)
+    # HBM bytes per non-loss attraction launch and BH VALU utilisation: PMC
+    # counters cannot be collected by the process they count (rocprofv3 runs
+    # the bench as its child), so these come from committed PMC passes over
+    # this same command, each file naming the commit it was measured at
+    # (profiles/PMC_ATTRACT, profiles/PMC_BH below)
     here = os.path.dirname(os.path.abspath(__file__))
     if n == 1_000_000 and d == 128 and world == 1 and a.config == "c3":
-        tf = os.path.join(here, "profiles", "r03_attract_traffic.json")
+        tf = os.path.join(here, "profiles", PMC_ATTRACT)
         if os.path.exists(tf):
             with open(tf) as fh:
                 tj = json.load(fh)
             out["roofline"]["traffic"] = tj.get("traffic_bytes_per_launch")
-            out["roofline"]["traffic_source"] = tj.get("source")
-        pmc = os.path.join(here, "profiles", "r03_bh_valu.json")
+            out["roofline"]["traffic_source"] = {"file": "profiles/" + PMC_ATTRACT, "commit": tj.get("commit"),
+                                                 "how": tj.get("source")}
+        pmc = os.path.join(here, "profiles", PMC_BH)
         if os.path.exists(pmc):
             with open(pmc) as fh:
                 out["bh"]["valu_pmc"] = json.load(fh)

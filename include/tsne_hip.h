@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TSNE_HIP_ABI_VERSION 1
+#define TSNE_HIP_ABI_VERSION 2
 #define TSNE_UNIQUE_ID_BYTES 128
 
 typedef enum {
@@ -116,6 +116,41 @@ int tsne_ctx_destroy(tsne_ctx *ctx);
 int tsne_ctx_set_stream(tsne_ctx *ctx, void *hip_stream);
 void *tsne_ctx_stream(tsne_ctx *ctx);
 int tsne_ctx_synchronize(tsne_ctx *ctx);
+/* Per-handle tunables (no reference counterpart: the reference has no BH
+ * shortcuts).  The defaults are the library's choices; a setting applies to
+ * every later call on this handle (every rank of a tsne_ctx_create_multi
+ * handle), never to other handles or threads.  Keys:
+ *   "near_tol_early" 1e-6, "near_tol_late" 5e-6   near-exact BH subtrees:
+ *       relative bound per summarised cell, for single gradients and the
+ *       optimizer's early-exaggeration phase / after it (0: the test is off);
+ *   "mom_tol" 1e-12           subtree-moment truncation bound (2-D);
+ *   "near_tol3_early" 1e-7, "near_tol3_late" 5e-6, "mom3_tol" 1e-12, and
+ *   "oct_moments" 1           the same for the 3-D octree;
+ *   "root_tile" 1             root-tile shortcut of the small-embedding phase;
+ *   "attract_tiles" 1         tiled attraction where the labels allow it;
+ *   "attract_cfg" -1          its tile shape (-1 automatic, 0..3);
+ *   "graph_order" 1           P's graph order as the initial labels;
+ *   "relabel" -1              Morton relabels: -1 automatic, 0 never, 1 by
+ *                             locality score, 2 always;
+ *   "recut" 0                 several ranks on the tiled layout: re-cut the
+ *                             row ownership by BH cost instead of relabels;
+ *   "knn_bf16" 1              kNN threshold filter on bf16x3 MFMA (0: the
+ *                             f32-input MFMA; results are identical);
+ *   "narrow" 3                BH: 64-query groups costing >= this x the mean
+ *                             run in the narrow layout (0: off).
+ * Unknown keys and out-of-range values return TSNE_ERR_ARG. */
+int tsne_ctx_set_option(tsne_ctx *ctx, const char *key, double value);
+/* HIP runtime versions (HIP_VERSION encoding, major * 10^7 + minor * 10^5 +
+ * patch): the headers this library was built with, and the runtime the
+ * process loaded (e.g. a host framework's bundled libamdhip64).  The
+ * bindings refuse a different major version.  No device needed. */
+int tsne_hip_versions(int32_t *built_out, int32_t *runtime_out);
+int tsne_ctx_get_option(tsne_ctx *ctx, const char *key, double *value_out);
+/* Diagnostic counters of the last call (synchronises the context's stream):
+ *   "bh.narrow_groups"   64-query groups the last single-call BH traversal
+ *                        (tsne_gradient / tsne_repulsion) ran in the narrow layout;
+ *   "opt.narrow_groups"  the same for the optimizer's last iteration. */
+int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);
 
 /* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls
  * tsne_comm_unique_id and ships the bytes to the other ranks out of band

@@ -285,6 +285,13 @@ object TsneHipOperators {
           val ri = new Ints(); val ci = new Ints(); val pv = new Doubles()
           it.asScala.foreach { case (_, (id, sv)) =>
             val r = index(id)
+            // a row is indexed by point ids: Tsne.scala:121 sizes it inputDimension^2,
+            // which is shorter than the ids whenever N > D^2 (INTEGRATION.md section 1)
+            if (sv.length <= maxId)
+              throw new IllegalArgumentException(
+                s"row $id of P is a SparseVector of length ${sv.length}, but the point ids reach $maxId: " +
+                "build the rows with VectorBuilder(number of points), not inputDimension * inputDimension " +
+                "(Tsne.scala:121; INTEGRATION.md section 1)")
             var o = 0
             while (o < sv.activeSize) { ri += r; ci += index(sv.indexAt(o)); pv += sv.valueAt(o); o += 1 }
           }

@@ -24,9 +24,13 @@ def main():
     ap.add_argument("snaps", nargs="+")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--theta", type=float, default=0.5)
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE", help="tsne_ctx_set_option")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     with T.Context(0) as ctx:
+        for kv in a.option:
+            key, val = kv.split("=", 1)
+            ctx.set_option(key, float(val))
         for path in a.snaps:
             Y = torch.from_numpy(np.load(path)).to(dev, torch.float64).contiguous()
             n = Y.shape[0]
@@ -39,9 +43,10 @@ def main():
                 ctx.dev_repulsion(Y, a.theta, F, z)
                 ctx.synchronize()
                 times.append(time.perf_counter() - t0)
+            narrow = ctx.counter("bh.narrow_groups")
             times = sorted(times[1:])
             print(json.dumps({"snapshot": os.path.basename(path), "n": n, "ms_median": 1e3 * times[len(times) // 2],
-                              "ms_min": 1e3 * times[0], "sum_abs_F": float(F.abs().sum()),
+                              "ms_min": 1e3 * times[0], "narrow_groups": narrow, "sum_abs_F": float(F.abs().sum()),
                               "sum_z": float(z.sum())}), flush=True)
 
 

@@ -19,7 +19,7 @@ with T.Context(0) as ctx:
         gi, gd = ctx.kNearestNeighbors(X, 90)
         oi, od = O.knn(X, 90)
         bad = np.where((gi != oi).any(1) | (gd != od).any(1))[0]
-        print(os.environ.get("TSNE_KNN_BF16"), name, "rows differing:", len(bad), flush=True)
+        print(name, "rows differing:", len(bad), flush=True)
         for r in bad[:3]:
             miss = sorted(set(oi[r].tolist()) - set(gi[r].tolist()))
             extra = sorted(set(gi[r].tolist()) - set(oi[r].tolist()))

@@ -28,7 +28,17 @@ def test_header_symbols_exported():
 
 
 def test_abi_version():
-    assert T.lib().tsne_abi_version() == 1
+    assert T.lib().tsne_abi_version() == 2
+
+
+def test_hip_runtime_version_matches_build():
+    """The HIP runtime the process loaded (torch's bundled one when torch is
+    imported first) has the major version the library was built against
+    (tsne_amd.lib() refuses it otherwise).  No device needed."""
+    import ctypes as C
+    b, r = C.c_int32(), C.c_int32()
+    assert T.lib().tsne_hip_versions(C.byref(b), C.byref(r)) == 0
+    assert b.value // 10 ** 7 == r.value // 10 ** 7 >= 6
 
 
 @pytest.mark.parametrize("name,val", [("sqeuclidean", 0), ("euclidean", 1), ("cosine", 2)])

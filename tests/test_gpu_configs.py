@@ -22,17 +22,19 @@ identities -- and end to end where the whole problem is small (C1):
       affinity rows at 1e-12, joint rows (pattern exact, values 1e-13
       relative) against a restatement of jointDistribution on the sampled
       rows, and at snapshots of the real optimizer trajectory the per-point
-      repulsion (z at BH_NEAR_TOL = 1e-6 relative, the gradient of a row block
-      at 1e-4 x max|grad|: north_star), Z == sum of the per-point z, and the
-      KL loss over all rows at 1e-9 (the oracle's attraction + loss with the
-      same Z).
+      repulsion (z at the library's near-exact bound "near_tol_early" = 1e-6
+      relative; the gradient of a row block at 1e-4 x max|grad| and, per row
+      with |g_i| >= 1e-3 max|g|, at 1e-4 x |g_i|: north_star's "per-iteration
+      gradients within 1e-4 relative"; the measured per-row figures go to
+      gpurun_out/grad_row_rel.json), Z == sum of the per-point z, and the KL
+      loss over all rows at 1e-9 (the oracle's attraction + loss with the same
+      Z).
 """
+import json
 import math
 import re
 import subprocess
 from pathlib import Path
-
-import os
 
 import numpy as np
 import pytest
@@ -47,7 +49,27 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 CLI = ROOT / "tsne-flink_amd" / "tsne_hip"
 THREADS = 16
-NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "5e-6"))   # BH_NEAR_TOL (bhtree.hip)
+ROW_REL = {}   # config/snapshot -> measured per-row relative gradient error (written to gpurun_out/)
+
+
+def near_tol(c, late=False):
+    """The library's near-exact bound, read from the context: single gradients
+    (tsne_gradient / tsne_repulsion) and the optimizer's exaggerated phase run
+    at "near_tol_early", the optimizer after it at "near_tol_late"."""
+    return c.get_option("near_tol_late" if late else "near_tol_early")
+
+
+def row_relative(g, g_ref, key):
+    """max over rows with |g_i| >= 1e-3 max|g| of |g_i - g_ref_i| / |g_ref_i|
+    (2-norms per row); recorded under `key` and returned."""
+    nrm = np.linalg.norm(g_ref, axis=1)
+    sel = nrm >= 1e-3 * nrm.max()
+    rel = float((np.linalg.norm(g - g_ref, axis=1)[sel] / nrm[sel]).max())
+    ROW_REL[key] = {"max_row_rel": rel, "rows": int(sel.sum()), "of": int(len(nrm))}
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    (out / "grad_row_rel.json").write_text(json.dumps(ROW_REL, indent=1, sort_keys=True))
+    return rel
 
 
 @pytest.fixture(scope="module")
@@ -96,7 +118,7 @@ def check_joint_rows(idx, p, orp, oc, ov, rows):
             assert abs(got[j] - v / tot) <= 1e-13 * (v / tot), (i, j)
 
 
-def check_gradient_snapshot(ctx, P, Y, theta, ex, metric, r0, nr, c=2, loss=True):
+def check_gradient_snapshot(ctx, P, Y, theta, ex, metric, r0, nr, c=2, loss=True, key="snapshot"):
     rp, col, val = P
     n = Y.shape[0]
     F, z = ctx.repulsion(Y, theta)
@@ -107,12 +129,14 @@ def check_gradient_snapshot(ctx, P, Y, theta, ex, metric, r0, nr, c=2, loss=True
         rep_o, z_o = O.repulsion_queries(Y, theta, Q, threads=THREADS)
     else:
         rep_o, z_o = O.repulsion3_queries(Y, theta, Q, threads=THREADS)
-    assert np.abs(z[r0:r0 + nr] - z_o).max() <= NEAR_TOL * z_o.max(), "per-point z"
+    assert np.abs(z[r0:r0 + nr] - z_o).max() <= near_tol(ctx) * z_o.max(), "per-point z"
     rep = np.zeros((n, c))
     rep[r0:r0 + nr] = rep_o
     attr = O.attraction_rows if c == 2 else O.attraction3_rows
     g_o, _ = attr(rp, col, val, Y, rep, Z, r0, r0 + nr, metric=metric, exaggeration=ex)
     assert np.abs(g[r0:r0 + nr] - g_o).max() <= 1e-4 * np.abs(g_o).max(), "gradient rows"
+    rel = row_relative(g[r0:r0 + nr], g_o, key)
+    assert rel <= 1e-4, (key, "per-row relative gradient", rel)
     if loss:
         _, l_o = attr(rp, col, val, Y, np.zeros((n, c)), Z, 0, n, metric=metric, exaggeration=ex, want_loss=True)
         assert abs(L - l_o) <= 1e-9 * abs(l_o), (L, l_o)
@@ -176,7 +200,7 @@ def momentum(t, T_):
 
 
 def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, loss_gpu=None, lr=1000.0,
-                   all_rows=True):
+                   all_rows=True, key="step"):
     """The optimizer's OWN iteration t (attract_tiles / attract_rows, the
     Z-free loss terms, combine_update, centring -- tsne_dev_opt_step) against
     the oracle from the same state: TsneHelpers.scala:269-317 (gradient),
@@ -196,13 +220,13 @@ def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, 
         every row of P with the same Z, at 1e-9.
     Z is the step's own BH normaliser (tsne_dev_opt_last_z); it must equal the
     sum of the per-point z of the same state (tsne_repulsion, whose sampled
-    rows are checked against the oracle) to BH_NEAR_TOL."""
+    rows are checked against the oracle) to the two builds' near-exact bounds."""
     Y0, u0, g0 = before
     Y1, u1, g1 = after
     n = Y0.shape[0]
     ex, mom = exaggeration(t, T_), momentum(t, T_)
     F, z = ctx.repulsion(Y0, theta)
-    assert abs(z.sum() - Z) <= NEAR_TOL * Z, (t, "Z", Z, z.sum())
+    assert abs(z.sum() - Z) <= (near_tol(ctx) + near_tol(ctx, ex == 1.0)) * Z, (t, "Z", Z, z.sum())
     # every row: the step's attraction (its gradient + F / Z, F the device BH of
     # the same state) against the oracle's attraction over the whole of P
     attr = O.attraction_rows if c == 2 else O.attraction3_rows
@@ -216,7 +240,7 @@ def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, 
                                                            a_opt[i].tolist(), a_o[i].tolist()) for i in bad])
     Q = np.ascontiguousarray(Y0[r0:r0 + nr])
     rep_o, z_o = (O.repulsion_queries if c == 2 else O.repulsion3_queries)(Y0, theta, Q, threads=THREADS)
-    assert np.abs(z[r0:r0 + nr] - z_o).max() <= NEAR_TOL * z_o.max(), (t, "per-point z")
+    assert np.abs(z[r0:r0 + nr] - z_o).max() <= near_tol(ctx) * z_o.max(), (t, "per-point z")
     rep = np.zeros((n, c))
     rep[r0:r0 + nr] = rep_o
     g_o, _ = attr(*P, Y0, rep, Z, r0, r0 + nr, metric=metric, exaggeration=ex)
@@ -224,6 +248,8 @@ def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, 
     tol = 1e-4 * np.abs(g_o).max()
     grad = (mom * u0[rows] - u1[rows]) / (lr * g1[rows])
     assert np.abs(grad - g_o).max() <= tol, (t, np.abs(grad - g_o).max(), tol)
+    rel = row_relative(grad, g_o, "%s step t=%d" % (key, t))
+    assert rel <= 1e-4, (t, "per-row relative gradient", rel)
     Yn, un, gn = (x[rows].copy() for x in (Y0, u0, g0))   # O.update works in place: copies, not views
     O.update(np.ascontiguousarray(g_o), Yn, un, gn, 0.01, mom, lr)
     assert ((gn == g1[rows]) | (np.abs(g_o) <= tol)).all(), (t, "gains")
@@ -250,7 +276,8 @@ def check_opt_step(ctx, P, before, after, Z, t, T_, theta, metric, r0, nr, c=2, 
             assert False, repr(info)
 
 
-def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, grad_rows, q0, stop=None, steps=()):
+def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, grad_rows, q0, stop=None, steps=(),
+                name="config"):
     n = Xd.shape[0]
     host, Pd = pipeline(ctx, Xd, k, metric, perplexity)
     check_knn_rows(X_host, host["idx"], host["dist"], k, metric, q0)
@@ -263,10 +290,10 @@ def full_config(ctx, Xd, X_host, k, metric, perplexity, theta, T_, c, snaps, gra
     for t, nr in snaps.items():
         r0 = grad_rows
         check_gradient_snapshot(ctx, host["P"], Ys[t], theta, exaggeration(t + 1, T_), metric, r0, nr, c=c,
-                                loss=(t == max(snaps)))
+                                loss=(t == max(snaps)), key="%s snapshot t=%d" % (name, t))
     for t in sorted(steps):   # the optimizer's own step at config size
         check_opt_step(ctx, host["P"], *st[t], t, T_, theta, metric, grad_rows + 64, 64, c=c,
-                       loss_gpu=losses.get(t))
+                       loss_gpu=losses.get(t), key=name)
     return losses
 
 
@@ -330,7 +357,7 @@ def test_c2_mnist_shaped_full_size(ctx):
     Xd = torch.from_numpy(X).cuda()
     losses = full_config(ctx, Xd, X, 90, "sqeuclidean", 30.0, 0.5, 1000, 2,
                          snaps={1: 32, 100: 64, 300: 64, 1000: 64}, grad_rows=40_000, q0=12_345,
-                         steps=(300, 1000))
+                         steps=(300, 1000), name="C2")
     assert sorted(losses) == list(range(10, 1001, 10))
     assert all(np.isfinite(v) for v in losses.values())
 
@@ -341,7 +368,7 @@ def test_c3_gmm_1m_full_size(ctx):
     X = Xd.cpu().numpy()
     losses = full_config(ctx, Xd, X, 90, "sqeuclidean", 30.0, 0.5, 1000, 2,
                          snaps={1: 16, 200: 64, 400: 64, 1000: 64}, grad_rows=654_321, q0=123_456,
-                         steps=(1, 200, 400, 1000))
+                         steps=(1, 200, 400, 1000), name="C3")
     assert sorted(losses) == list(range(10, 1001, 10))
     assert all(np.isfinite(v) for v in losses.values())
 
@@ -351,7 +378,7 @@ def test_c4_sparse_cosine_3d_full_size(ctx):
     X = CF.c4()
     Xd = torch.from_numpy(X).cuda()
     full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 150: 32}, grad_rows=250_000,
-                q0=77_777, stop=300, steps=(1, 120, 150, 300))
+                q0=77_777, stop=300, steps=(1, 120, 150, 300), name="C4")
 
 
 # ------------------------------------------------------------------- C5
@@ -414,7 +441,7 @@ def test_c5_distance_matrix_5k_matches_oracle(ctx):
             gg, Zg, Lg = ctx.gradient(*P, Yt, 0.5, exaggeration=ex, want_loss=True)
             r = O.gradient(*P, Yt, 0.5, exaggeration=ex, want_loss=True, threads=THREADS)
             assert np.abs(gg - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max(), t
-            assert abs(Zg - r["Z"]) <= NEAR_TOL * r["Z"], t
+            assert abs(Zg - r["Z"]) <= near_tol(ctx) * r["Z"], t
             assert np.isnan(Lg) and np.isnan(r["loss"])
             _, _, kg = ctx.gradient(*S, Yt, 0.5, exaggeration=ex, want_loss=True)
             ro = O.gradient(*S, Yt, 0.5, exaggeration=ex, want_loss=True, threads=THREADS)
@@ -496,7 +523,7 @@ def test_c5_distance_matrix_50k_full_size(ctx):
     rps = np.clip(orp.cpu().numpy() - a, 0, b - a)
     Ps = (rps, oc[a:b].cpu().numpy(), ov[a:b].cpu().numpy())
     for t in (1, 60):
-        check_opt_step(ctx, Ps, *st[t], t, T_, 0.5, "sqeuclidean", r0, nr, all_rows=False)
+        check_opt_step(ctx, Ps, *st[t], t, T_, 0.5, "sqeuclidean", r0, nr, all_rows=False, key="C5")
     assert sorted(losses) == list(range(10, T_ + 1, 10))
     assert all(np.isnan(losses[t]) == underflow for t in losses)
     del Pd, orp, oc, ov

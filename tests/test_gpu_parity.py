@@ -2,8 +2,6 @@
 reference goldens.  Tolerances: kNN indices bit-exact (ties ordered by
 (d, j)), kNN distances bit-exact fp64; goldens at the reference suite's own
 tolerances; BH gradients at 1e-4 relative to max|grad| (north_star)."""
-import os
-
 import numpy as np
 import pytest
 
@@ -160,7 +158,12 @@ def test_gradient_golden(ctx):
     assert abs(Z - G["denseSumQ"]) <= 1e-9
 
 
-NEAR_TOL = float(os.environ.get("TSNE_BH_NEAR_TOL", "5e-6"))   # BH_NEAR_TOL (bhtree.hip): per-cell relative bound of the near-exact tiles
+def near_tol(c, late=False):
+    """The library's own near-exact bound (per summarised cell, relative), read
+    from the context: single gradients and the optimizer's early-exaggeration
+    phase run at "near_tol_early" (1e-6), the optimizer after it at
+    "near_tol_late" (5e-6)."""
+    return c.get_option("near_tol_late" if late else "near_tol_early")
 
 
 def random_problem(n, k, seed):
@@ -182,7 +185,7 @@ def test_gradient_matches_oracle(ctx, scale, theta, metric):
     r = O.gradient(rp, col, val, Y, theta, metric, exaggeration=4.0, want_loss=True)
     scale_g = np.abs(r["grad"]).max()
     assert np.abs(g - r["grad"]).max() <= 1e-4 * scale_g
-    assert abs(Z - r["Z"]) <= NEAR_TOL * r["Z"]
+    assert abs(Z - r["Z"]) <= near_tol(ctx) * r["Z"]
     assert abs(loss - r["loss"]) <= 1e-6 * abs(r["loss"])
 
 
@@ -196,9 +199,9 @@ def test_gradient_large_near_exact(ctx, n, scale):
     g, Z, loss = ctx.gradient(rp, col, val, Y, 0.5, exaggeration=12.0, want_loss=True)
     r = O.gradient(rp, col, val, Y, 0.5, exaggeration=12.0, want_loss=True)
     assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
-    # near-exact subtrees: each summarised cell within BH_NEAR_TOL of its exact leaf sum
-    assert np.abs(g - r["grad"]).max() <= 10 * NEAR_TOL * np.abs(r["grad"]).max()
-    assert abs(Z - r["Z"]) <= NEAR_TOL * r["Z"]
+    # near-exact subtrees: each summarised cell within near_tol of its exact leaf sum
+    assert np.abs(g - r["grad"]).max() <= 10 * near_tol(ctx) * np.abs(r["grad"]).max()
+    assert abs(Z - r["Z"]) <= near_tol(ctx) * r["Z"]
     if np.isnan(r["loss"]):   # some P_ij underflowed to 0: 0 * ln 0 (TsneHelpers.scala:300)
         assert np.isnan(loss)
     else:
@@ -219,8 +222,8 @@ def test_root_tile_mode_per_point(ctx, n, scale, dups):
         Y[[99, 98]] = Y[99]
     F, z = ctx.repulsion(Y, 0.5)
     rep, zi = O.repulsion(Y, 0.5, threads=8)
-    assert np.abs(z - zi).max() <= NEAR_TOL * zi.max()
-    assert np.abs(F - rep).max() <= NEAR_TOL * np.abs(rep).max()
+    assert np.abs(z - zi).max() <= near_tol(ctx) * zi.max()
+    assert np.abs(F - rep).max() <= near_tol(ctx) * np.abs(rep).max()
 
 
 @pytest.mark.parametrize("theta,scale", [(0.0, 1.0), (0.5, 1.0), (0.25, 30.0), (0.5, 1e-3)])
@@ -239,7 +242,7 @@ def test_gradient_duplicate_multiplicity(ctx, theta, scale):
         Y[g] = Y[g[0]]
     g_, Z, loss = ctx.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
     r = O.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
-    tol = 1e-12 if theta == 0.0 else NEAR_TOL
+    tol = 1e-12 if theta == 0.0 else near_tol(ctx)
     assert np.abs(g_ - r["grad"]).max() <= tol * np.abs(r["grad"]).max()
     assert abs(Z - r["Z"]) <= tol * r["Z"]
     F, z = ctx.repulsion(Y, theta)
@@ -280,7 +283,7 @@ def test_gradient_points_outside_root_and_duplicates(ctx):
     g, Z, _ = ctx.gradient(rp, col, val, Y, 0.5)
     r = O.gradient(rp, col, val, Y, 0.5)
     assert np.abs(g - r["grad"]).max() <= 1e-4 * np.abs(r["grad"]).max()
-    assert abs(Z - r["Z"]) <= NEAR_TOL * r["Z"]
+    assert abs(Z - r["Z"]) <= near_tol(ctx) * r["Z"]
 
 
 # ---------------------------------------------------------- update / centre
@@ -358,10 +361,9 @@ def test_optimize_loss_matches_oracle(ctx):
         runs.append(O.optimize(rp, col, val, Yo, uo, go, iterations=200, theta=0.5))
     lo = runs[0]
     assert sorted(lg) == sorted(lo) == list(range(10, 201, 10))
-    # a looser near-exact bound moves the early trajectory sooner (chaotic
-    # growth of any per-iteration difference): at 1e-5 the 1% window is t <= 30
-    early = (10, 20, 30, 40, 50) if NEAR_TOL <= 5e-6 else (10, 20, 30)
-    for t in early:
+    # the exaggerated phase runs at the strict near-exact bound (near_tol_early)
+    assert near_tol(ctx) <= 1e-6
+    for t in (10, 20, 30, 40, 50):
         assert abs(lg[t] - lo[t]) <= 0.01 * abs(lo[t]), t
     final = np.array([r[200] for r in runs])
     mu, sd = final.mean(), final.std()
@@ -386,6 +388,24 @@ def test_host_api_converts_csr_types(ctx):
     assert np.array_equal(Ya, Yb) and la == lb
     with pytest.raises(ValueError):
         ctx.optimize(rp, col, val, Y0.astype(np.float32), ua, ga, p)
+
+
+def test_context_options():
+    """tsne_ctx_set_option / get_option: per-handle, range-checked, unknown
+    keys refused (TSNE_ERR_ARG); another handle keeps the defaults."""
+    with T.Context(0) as a, T.Context(0) as b:
+        assert a.get_option("near_tol_early") == 1e-6 and a.get_option("near_tol_late") == 5e-6
+        assert a.get_option("mom_tol") == 1e-12 and a.get_option("narrow") == 3.0
+        a.set_option("near_tol_late", 2e-6)
+        a.set_option("relabel", 2)
+        assert a.get_option("near_tol_late") == 2e-6 and a.get_option("relabel") == 2.0
+        assert b.get_option("near_tol_late") == 5e-6 and b.get_option("relabel") == -1.0
+        for key, v in (("relabel", 3), ("relabel", 0.5), ("near_tol_late", -1.0), ("no_such_key", 1.0)):
+            with pytest.raises(T.TsneError) as e:
+                a.set_option(key, v)
+            assert e.value.status == -1
+        with pytest.raises(T.TsneError):
+            a.counter("no_such_counter")
 
 
 def test_unsupported_components(ctx):
@@ -462,100 +482,67 @@ def test_tiled_attraction_matches_oracle(ctx, metric):
     assert abs(lg[10] - lo[10]) <= 1e-9 * abs(lo[10])
 
 
-_TILE_CFG_CHILD = r"""
-import sys, numpy as np
-sys.path[:0] = [sys.argv[1], sys.argv[2]]
-import tsne_amd as T
-from tsne_amd.api import default_params
-from test_gpu_parity import hub_problem
-rp, col, val = hub_problem(12000)
-Y = np.random.default_rng(74).normal(size=(12000, 2)) * 5.0
-u, g = np.zeros_like(Y), np.ones_like(Y)
-with T.Context(0) as c:
-    l = c.optimize(rp, col, val, Y, u, g, default_params(iterations=10, theta=0.0, learning_rate=200.0))
-np.save(sys.argv[3], np.concatenate([Y.ravel(), [l[10]]]))
-"""
-
-
-def test_tiled_attraction_every_config(tmp_path):
+def test_tiled_attraction_every_config():
     """Each row-block configuration of attract_tiles (512 ... 4096 rows; a run
-    picks one by its owned rows, TSNE_AT_CFG forces it) and attract_rows
-    (TSNE_ATTRACT_TILES=0), in child processes, against the oracle."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    picks one by its owned rows, the "attract_cfg" option forces it) and
+    attract_rows ("attract_tiles" 0), each on its own context, against the
+    oracle."""
     n = 12000
     rp, col, val = hub_problem(n)
-    Yo = np.random.default_rng(74).normal(size=(n, 2)) * 5.0
-    uo, go = np.zeros_like(Yo), np.ones_like(Yo)
+    Y0 = np.random.default_rng(74).normal(size=(n, 2)) * 5.0
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
     lo = O.optimize(rp, col, val, Yo, uo, go, learning_rate=200.0, iterations=10, theta=0.0, threads=8)
-    for env in ({"TSNE_AT_CFG": "0"}, {"TSNE_AT_CFG": "1"}, {"TSNE_AT_CFG": "2"}, {"TSNE_AT_CFG": "3"},
-                {"TSNE_ATTRACT_TILES": "0"}):
-        out = tmp_path / ("r_%s.npy" % "_".join(env.values()))
-        subprocess.run([sys.executable, "-c", _TILE_CFG_CHILD, os.path.join(root, "tsne-flink_amd"),
-                        os.path.join(root, "tests"), str(out)], env=dict(os.environ, **env), check=True, timeout=120)
-        r = np.load(out)
-        Yg, lg = r[:-1].reshape(n, 2), r[-1]
-        assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max(), env
-        assert abs(lg - lo[10]) <= 1e-9 * abs(lo[10]), env
+    for opt in ({"attract_cfg": 0}, {"attract_cfg": 1}, {"attract_cfg": 2}, {"attract_cfg": 3},
+                {"attract_tiles": 0}):
+        with T.Context(0) as c:
+            for k, v in opt.items():
+                c.set_option(k, v)
+            Yg, ug, gg = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+            lg = c.optimize(rp, col, val, Yg, ug, gg, default_params(iterations=10, theta=0.0, learning_rate=200.0))
+        assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max(), opt
+        assert abs(lg[10] - lo[10]) <= 1e-9 * abs(lo[10]), opt
 
 
-_RELABEL_CHILD = r"""
-import sys, numpy as np, torch
-sys.path[:0] = [sys.argv[1], sys.argv[2]]
-import tsne_amd as T
-from tsne_amd.api import default_params
-from test_gpu_parity import random_problem
-n = 700
-rp, col, val = random_problem(n, 20, seed=41)
-Y0 = np.random.default_rng(8).normal(size=(n, 2)) * 1e-3
-p = default_params(iterations=60, theta=0.5)
-with T.Context(0) as c:
-    Yh, uh, gh = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
-    lh = c.optimize(rp, col, val, Yh, uh, gh, p)
-    dev = torch.device("cuda", 0)
-    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
-    dY = t(Y0, torch.float64)
-    du = torch.zeros((n, 2), dtype=torch.float64, device=dev)
-    dg = torch.ones((n, 2), dtype=torch.float64, device=dev)
-    c.dev_opt_setup(p, t(rp, torch.int64), t(col, torch.int32), t(val, torch.float64), n, dY, du, dg)
-    for it in range(1, 61):
-        c.dev_opt_step(it)
-    c.dev_opt_sync()
-    c.synchronize()
-    assert np.array_equal(dY.cpu().numpy(), Yh) and c.dev_opt_losses() == lh
-np.save(sys.argv[3], np.concatenate([Yh.ravel(), [lh[60]]]))
-"""
+def _relabel_run(relabel):
+    """60 iterations host API and device API with the given "relabel" option:
+    both bit-equal; returns (Y, loss at t = 60)."""
+    import torch
+    n = 700
+    rp, col, val = random_problem(n, 20, seed=41)
+    Y0 = np.random.default_rng(8).normal(size=(n, 2)) * 1e-3
+    p = default_params(iterations=60, theta=0.5)
+    with T.Context(0) as c:
+        c.set_option("relabel", relabel)
+        Yh, uh, gh = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+        lh = c.optimize(rp, col, val, Yh, uh, gh, p)
+        dev = torch.device("cuda", 0)
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)  # noqa: E731
+        dY = t(Y0, torch.float64)
+        du = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+        dg = torch.ones((n, 2), dtype=torch.float64, device=dev)
+        c.dev_opt_setup(p, t(rp, torch.int64), t(col, torch.int32), t(val, torch.float64), n, dY, du, dg)
+        for it in range(1, 61):
+            c.dev_opt_step(it)
+        c.dev_opt_sync()
+        c.synchronize()
+        assert np.array_equal(dY.cpu().numpy(), Yh) and c.dev_opt_losses() == lh
+    return Yh, lh[60]
 
 
-def test_relabel_modes_agree(tmp_path):
+def test_relabel_modes_agree():
     """One rank with the tiled layout keeps P's graph order by default (no
-    Morton relabel); TSNE_RELABEL=2 relabels at every check (t % 25 == 0) and
-    hands the attraction to attract_rows.  Both, in child processes: device
-    path == host path bit for bit, and the two trajectories agree within
-    1e-6 relative after 60 iterations (two relabels).  They differ only in
-    summation orders (~1e-16), which the BH decisions amplify: on this
-    problem the oracle's own runs from Y0 perturbed by 1e-15 (relative)
-    differ by 2e-8..2e-6 at t = 30 and 3e-2..0.9 at t = 60; the two modes
-    measured 5e-9 at t = 60 (deterministic runs: a stable check)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for mode in ("", "2"):
-        out = tmp_path / ("relabel_%s.npy" % (mode or "default"))
-        env = dict(os.environ)
-        env.pop("TSNE_RELABEL", None)
-        if mode:
-            env["TSNE_RELABEL"] = mode
-        subprocess.run([sys.executable, "-c", _RELABEL_CHILD, os.path.join(root, "tsne-flink_amd"),
-                        os.path.join(root, "tests"), str(out)], env=env, check=True, timeout=120)
-        res[mode] = np.load(out)
-    a, b = res[""], res["2"]
-    assert np.abs(a[:-1] - b[:-1]).max() <= 1e-6 * np.abs(b[:-1]).max()
-    assert abs(a[-1] - b[-1]) <= 1e-6 * abs(b[-1])
+    Morton relabel); "relabel" 2 relabels at every check (t % 25 == 0) and
+    hands the attraction to attract_rows.  Both: device path == host path bit
+    for bit, and the two trajectories agree within 1e-6 relative after 60
+    iterations (two relabels).  They differ only in summation orders
+    (~1e-16), which the BH decisions amplify: on this problem the oracle's own
+    runs from Y0 perturbed by 1e-15 (relative) differ by 2e-8..2e-6 at t = 30
+    and 3e-2..0.9 at t = 60; the two modes measured 5e-9 at t = 60
+    (deterministic runs: a stable check)."""
+    ya, la = _relabel_run(-1)
+    yb, lb = _relabel_run(2)
+    assert np.abs(ya - yb).max() <= 1e-6 * np.abs(yb).max()
+    assert abs(la - lb) <= 1e-6 * abs(lb)
 
 
 def test_moment_path_engaged(ctx):

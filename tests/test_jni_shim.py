@@ -66,3 +66,18 @@ def test_scala_bodies_call_declared_natives_with_reference_signatures():
                 rf"learningRate: Double, iterations: Int, {metric},"):
         assert re.search(sig, scala), sig
     assert "allocateDirect" not in scala and "java.nio" not in scala   # off-heap, 64-bit indexes
+
+
+def test_optimize_rejects_rows_shorter_than_the_point_ids():
+    """Tsne.scala:121 sizes each row of P as inputDimension^2 while its indices
+    are point ids: the operator refuses a row shorter than the largest id with
+    an IllegalArgumentException naming the caller line and INTEGRATION.md 1
+    (which documents the one-line caller change)."""
+    scala = (JNI / "TsneHipOperators.scala").read_text()
+    body = scala[scala.index("def optimize("):]
+    m = re.search(r"if \(sv\.length <= maxId\)\s+throw new IllegalArgumentException\(", body)
+    assert m, "length check missing in optimize"
+    msg = body[m.end():body.index(")\n", m.end())]
+    assert "VectorBuilder(number of points)" in msg and "Tsne.scala:121" in msg and "INTEGRATION.md" in msg
+    integ = (ROOT / "INTEGRATION.md").read_text()
+    assert "new VectorBuilder[Double](numberOfPoints)" in integ

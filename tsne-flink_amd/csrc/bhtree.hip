@@ -49,7 +49,7 @@ constexpr int QREC_V4 = sizeof(QRec) / 16; // 16-byte pieces of a record
 // Truncated at k = MOM_ORDER, every term is a polynomial of degree <= 2k+1 in
 // u, so the subtree sums follow from its moments sum u_x^a u_y^b
 // (a + b <= MOM_DEG), shifted to the query.  The path is taken only when the
-// truncation bound (MOM_ORDER+2) rho^(MOM_ORDER+1) / (1-rho)^2 <= MOM_TOL,
+// truncation bound (MOM_ORDER+2) rho^(MOM_ORDER+1) / (1-rho)^2 <= Options::mom_tol (1e-12),
 // i.e. the result equals the reference's exact leaf sum to ~1e-14 relative
 // (fp64 rounding level); otherwise the dense leaf tile runs.  This turns the
 // near-exact O(N^2) phase of a small embedding into
@@ -59,15 +59,7 @@ constexpr int MOM_DEG = 2 * MOM_ORDER + 1;
 constexpr int MOM_K = (MOM_DEG + 1) * (MOM_DEG + 2) / 2;
 constexpr int MOM_MIN_POINTS = 64;
 constexpr int MOM_CHUNK = 2048;
-constexpr double MOM_TOL = 1e-12;
-__device__ double g_mom_tol = MOM_TOL;   // TSNE_MOM_TOL (experiments): the bound moment_ok applies
 constexpr int MOM_TASKS = 128;  // moment evaluations recorded per query; more -> dense tiles
-constexpr double BH_NEAR_TOL = 1e-6;    // near-exact subtree test (bh_traverse): 100x below
-                                        // the north-star 1e-4 gradient tolerance -- single
-                                        // gradients and the optimizer's early-exaggeration phase
-constexpr double BH_NEAR_TOL_LATE = 5e-6;   // ... the optimizer after early exaggeration (20x
-                                        // below; DESIGN.md 3a: the early phase amplifies any
-                                        // per-iteration difference fastest)
 // moment (a, b), a + b <= MOM_DEG: rows of decreasing length
 __host__ __device__ constexpr int midx(int a, int b) { return a * (MOM_DEG + 1) - a * (a - 1) / 2 + b; }
 __host__ __device__ constexpr double fact(int k) { return k <= 1 ? 1.0 : k * fact(k - 1); }
@@ -316,8 +308,17 @@ __global__ void karras_build(const uint64_t *__restrict__ k, int64_t n, const in
 // the per-node aggregates that a sibling thread reads are written and read
 // with system-scope (sc0 sc1, write-through / cache-bypassing) 8-byte
 // accesses; every thread drains its stores (s_waitcnt vmcnt(0)) before its
-// relaxed arrival atomic.  Agent-scope __threadfence() here wrote back the
-// whole XCD L2 per wave and cost ~8 ms per build at 1M points.
+// relaxed arrival atomic.  Agent-scope __threadfence() (or an acq_rel
+// arrival: buffer_wbl2 + buffer_inv at agent scope) here wrote back the whole
+// XCD L2 per wave and cost ~8 ms per build at 1M points.  What orders the
+// hand-off instead: the writer's stores complete (vmcnt(0), an asm with a
+// memory clobber: also a compiler barrier) before its arrival is issued; the
+// reader's loads are issued after its arrival returned (a branch on the
+// result, plus a compiler-only signal fence so that the relaxed loads cannot
+// be hoisted above the relaxed atomic), and they bypass the non-coherent
+// caches (system scope).  This relies on gfx950's in-order issue and
+// write-through / bypassing system-scope accesses, not on the HIP memory
+// model's release / acquire; it is gfx950-only code like the rest.
 __device__ __forceinline__ void st_sys(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -334,112 +335,6 @@ constexpr int AGG = 10;   // sx, sy, x0, x1, y0, y1, hmin, cnt, rball, (pad)
 // ball(c_c, R_c) when R_v + |c_v - c_c| <= R_c, hence
 // R_v = min(sqrt(h_v/theta) [real v], R_c - |c_v - c_c| over children c),
 // shrunk by a relative 1e-9 per level for rounding.  Leaves impose nothing.
-// Nodes whose leaf range lies inside the workgroup's own BLK leaves (the
-// lowest ~log2(BLK) levels) hand off through LDS: workgroup-scope arrival
-// counters and aggregates, no cache-bypassing HBM round trip per level.  Only
-// a node whose parent spans several workgroups publishes its aggregates to
-// the system-scope array (its parent is combined as before).
-template <int BLK>
-__global__ __launch_bounds__(BLK) void bottom_up(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
-                          const double *__restrict__ Wp, double inv_theta, BHNode *nodes, double *agg,
-                          const int32_t *__restrict__ parent_leaf,
-                          const int32_t *__restrict__ parent_node, int32_t *arrive) {
-    __shared__ double lagg[AGG - 1][BLK];
-    __shared__ int32_t larr[BLK];
-    const int m = meta[0];
-    const int S0 = blockIdx.x * BLK;
-    larr[threadIdx.x] = 0;
-    __syncthreads();
-    const int s = S0 + threadIdx.x;
-    if (s >= m || m < 2) return;
-    const double W = *Wp;
-    auto in_blk = [&](int q) { return nodes[q].first >= S0 && nodes[q].last < S0 + BLK; };
-    int p = parent_leaf[s];
-    bool intra = p >= 0 && in_blk(p);
-    while (p >= 0) {
-        if (intra) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (__hip_atomic_fetch_add(&larr[p - S0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-                return;                                  // first arriver stops
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-                return;
-        }
-        const int32_t l = nodes[p].left, r = nodes[p].right, dl = nodes[p].delta;
-        double a[2][7];                                  // sx, sy, x0, x1, y0, y1, hmin
-        double c[2], rb[2];
-        const int32_t ch[2] = {l, r};
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (ch[k] < 0) {
-                const double2 q = pos[~ch[k]];
-                a[k][0] = q.x; a[k][1] = q.y; a[k][2] = q.x; a[k][3] = q.x; a[k][4] = q.y; a[k][5] = q.y;
-                a[k][6] = __builtin_inf();
-                c[k] = 1.0;
-                rb[k] = __builtin_inf();
-            } else if (intra) {                          // children of an in-block node are in-block
-                const int o = ch[k] - S0;
-#pragma unroll
-                for (int f = 0; f < 7; ++f) a[k][f] = lagg[f][o];
-                c[k] = lagg[7][o];
-                rb[k] = lagg[8][o];
-            } else {
-                const double *g = agg + AGG * (int64_t)ch[k];
-#pragma unroll
-                for (int f = 0; f < 7; ++f) a[k][f] = ld_sys(g + f);
-                c[k] = ld_sys(g + 7);
-                rb[k] = ld_sys(g + 8);
-            }
-        }
-        const double cnt = c[0] + c[1];
-        const double sx = a[0][0] + a[1][0], sy = a[0][1] + a[1][1];
-        const double x0 = fmin(a[0][2], a[1][2]), x1 = fmax(a[0][3], a[1][3]);
-        const double y0 = fmin(a[0][4], a[1][4]), y1 = fmax(a[0][5], a[1][5]);
-        const int par = parent_node[p];
-        const int dlev = dl >> 1;
-        bool real;
-        if (dl >= 62) real = false;                      // keys tie below 31 levels
-        else if (par < 0) real = true;                   // root cell chain
-        else real = (nodes[par].delta >> 1) < dlev;      // first node of its quad level
-        const double h = real ? ldexp(W, -dlev) : -1.0;  // -1 = transparent
-        const double hmin = fmin(real ? h : __builtin_inf(), fmin(a[0][6], a[1][6]));
-        const double cx = sx / cnt, cy = sy / cnt;       // centerOfMass = sum / cumSize
-        double rball = real ? sqrt(h * inv_theta) : __builtin_inf();
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (ch[k] >= 0) {
-                const double ccx = a[k][0] / c[k], ccy = a[k][1] / c[k];
-                const double dd = sqrt((cx - ccx) * (cx - ccx) + (cy - ccy) * (cy - ccy));
-                rball = fmin(rball, rb[k] - dd);
-            }
-        }
-        rball = rball > 0.0 ? rball * (1.0 - 1e-9) : 0.0;
-        const bool pintra = par >= 0 && in_blk(par);
-        if (pintra) {
-            const int o = p - S0;
-            lagg[0][o] = sx; lagg[1][o] = sy;
-            lagg[2][o] = x0; lagg[3][o] = x1; lagg[4][o] = y0; lagg[5][o] = y1;
-            lagg[6][o] = hmin; lagg[7][o] = cnt; lagg[8][o] = rball;
-        } else {
-            double *g = agg + AGG * (int64_t)p;
-            st_sys(g + 0, sx); st_sys(g + 1, sy);
-            st_sys(g + 2, x0); st_sys(g + 3, x1); st_sys(g + 4, y0); st_sys(g + 5, y1);
-            st_sys(g + 6, hmin); st_sys(g + 7, cnt); st_sys(g + 8, rball);
-        }
-        BHNode &nd = nodes[p];                           // read by the traversal (next launch)
-        nd.cx = cx;
-        nd.cy = cy;
-        nd.cnt = (int32_t)cnt;
-        nd.h = h;
-        nd.hmin = hmin;
-        nd.rball = rball;
-        nd.bx0 = x0; nd.bx1 = x1; nd.by0 = y0; nd.by1 = y1;
-        p = par;
-        intra = pintra;
-    }
-}
-
 // Node p's aggregates from its two children's (child order fixed: the sums
 // are deterministic whichever thread combines them); writes nodes[p] and
 // returns the nine aggregates in o[] (sx, sy, x0, x1, y0, y1, hmin, cnt,
@@ -601,8 +496,8 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
 
 // Phase 2: the nodes above the frontier.  Each arrival of phase 1 (a child
 // published, the parent listed) starts a climb; the second arriver at a node
-// combines it (agent-scope arrival counters, system-scope aggregates, as
-// bottom_up) and climbs on.  Only the top ~log2(m / BU_FRONT) levels remain
+// combines it (agent-scope arrival counters, system-scope aggregates: the
+// hand-off described above st_sys) and climbs on.  Only the top ~log2(m / BU_FRONT) levels remain
 // for this cross-workgroup hand-off.
 __global__ __launch_bounds__(256) void bottom_up_top(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
                                                      const double *__restrict__ Wp, double inv_theta, BHNode *nodes,
@@ -617,6 +512,7 @@ __global__ __launch_bounds__(256) void bottom_up_top(const double2 *__restrict__
         while (p >= 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) break;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);   // the sibling's aggregates are read after the arrival
             const int32_t ch[2] = {nodes[p].left, nodes[p].right};
             const int32_t dl = nodes[p].delta;
             double a[2][7], c[2], rb[2];
@@ -1217,7 +1113,8 @@ __device__ __forceinline__ void poly_moment_eval(const double *__restrict__ coef
 }
 
 // Truncation test of the moment path for query q and a subtree's bounding box.
-__device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, double by1, double qx, double qy) {
+__device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, double by1, double qx, double qy,
+                                          double tol) {
     double cx, cy, R;
     box_centre(bx0, bx1, by0, by1, cx, cy, R);
     const double vx = qx - cx, vy = qy - cy;
@@ -1227,7 +1124,7 @@ __device__ __forceinline__ bool moment_ok(double bx0, double bx1, double by0, do
     double rp = rho;
 #pragma unroll
     for (int k = 0; k < MOM_ORDER; ++k) rp *= rho;
-    return (MOM_ORDER + 2) * rp <= g_mom_tol * (1.0 - rho) * (1.0 - rho);
+    return (MOM_ORDER + 2) * rp <= tol * (1.0 - rho) * (1.0 - rho);
 }
 
 // Moment tasks of each query (query slots [g0, g1): sorted positions, or
@@ -1244,8 +1141,6 @@ struct ChunkView {
     double *Zp = nullptr;
 };
 constexpr int CHUNK_MAX = 32;
-constexpr int LW_CHUNK = 256;   // tile_apply pack 3: small tiles per lane-wise chunk
-constexpr int LW_D = 6;         // ... point loads in flight per lane
 constexpr int CHUNK_MIN = 4096;
 __global__ void chunk_total(const int32_t *__restrict__ tcost, int64_t waves, unsigned long long *__restrict__ total) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1442,6 +1337,37 @@ __global__ __launch_bounds__(256) void moment_apply(const double2 *__restrict__ 
     Zo[e] = Zo[e] + zs;
 }
 
+// Moment tasks of the narrow groups' queries (their own lists, entry = heavy
+// slot x 64 + query), added to F, Z after the narrow traversal's sums.
+__global__ __launch_bounds__(256) void narrow_moment_apply(const double2 *__restrict__ pos,
+                                                           const BHNode *__restrict__ nodes,
+                                                           const double *__restrict__ mom,
+                                                           const int32_t *__restrict__ hlist,
+                                                           const int32_t *__restrict__ hcount,
+                                                           const int32_t *__restrict__ mtask,
+                                                           const int32_t *__restrict__ mtask_n, int64_t g0, int64_t g1,
+                                                           const int32_t *__restrict__ qlist, double2 *__restrict__ F,
+                                                           double *__restrict__ Z) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((e >> 6) >= (int64_t)*hcount) return;
+    const int64_t k = g0 + (int64_t)hlist[e >> 6] * 64 + (e & 63);
+    if (k >= g1) return;
+    const int nt = mtask_n[e];
+    if (nt == 0) return;
+    const int64_t s = qlist ? (int64_t)qlist[k] : k;
+    const double2 q = pos[s];
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    for (int t = 0; t < nt; ++t) {
+        const int node = mtask[e * MOM_TASKS + t];
+        double cx, cy, R;
+        box_centre(nodes[node], cx, cy, R);
+        moment_eval(mom + (int64_t)node * MOM_K, q.x - cx, q.y - cy, fx, fy, zs);
+    }
+    const double2 f = F[s];
+    F[s] = make_double2(f.x + fx, f.y + fy);
+    Z[s] = Z[s] + zs;
+}
+
 // fl(h / D) < theta -- the reference's max(hHeigth, hWidth) / D < theta with
 // an IEEE division -- decided by comparing h with theta * D outside a 1e-14
 // relative band (where the rounded quotient cannot cross theta), and by the
@@ -1614,583 +1540,627 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
 // dense_apply sums the tiles afterwards.  This keeps the traversal at <= 64
 // VGPRs (8 waves per SIMD to hide the record fetches) instead of ~100.
 
-// ---- Dynamic splitting of heavy traversal waves (spill tasks).
-// A wave's BH work is the depth-first walk of its shared stack.  In dense
-// clusters a few waves carry many times the mean work and set the grid's
-// span (the longest wave is the span from t ~ 350 on).  A wave
-// whose cost (pops + tile points / 64) reaches the iteration's budget
-// (TSNE_BH_BUDGET x the previous traversal's mean wave cost) hands its whole
-// remaining stack to the next pass as tasks: contiguous runs of stack entries
-// of about gfac x budget points each (<= TASK_ENT entries); a task is the same
-// 64 queries over those subtrees.  Task passes run on a fixed grid; a task
-// over budget spills again into the next region (the last pass never
-// spills).  Each task writes its 64 lanes' partial (F, z).  The combine adds
-// every task's children (its spill, in stack-entry order) bottom-up by
-// region, then a wave's children into F, Z: the summation order is fixed by
-// the spill structure, not by which wave ran what (deterministic).  Subtree
-// sums are additive, so the result is the reference's sum over the same
-// cells; only its association changes.  Tasks sum their all-open / near-exact
-// tiles densely inline (the exact leaf sum, as tile_apply's dense path).
+// ---- Narrow layout for heavy 64-query groups.
+// A wave's BH work is the depth-first walk of its shared stack; its span is
+// the serial chain pop -> record fetch -> child tests -> push.  In dense
+// clusters a few 64-query groups carry 10-20x the mean work (DESIGN.md 6,
+// "BH mid phase") and that chain alone sets the grid's span.  Such groups
+// (previous traversal cost >= Options::narrow x the mean, narrow_select) run
+// as NPARTS waves of NQ queries each, with the lanes laid out as (record k,
+// query q, child c): one pass takes NKP stack entries at once and evaluates
+// the 4 children of each for NQ queries in ONE sweep of the lanes, where the
+// 64-query layout spends 4 sweeps (one per child) per entry with most lanes
+// masked off.  The stack entries carry NQ-bit query masks.  All-open /
+// near-exact tiles are summed inline (the 4 child lanes of a query split the
+// subtree's points) or become moment tasks on the group's own lists
+// (narrow_moment_apply).  Each lane keeps its own partial sums; the NKP x 4
+// lanes of a query are added by a fixed xor butterfly at the end, so the
+// result does not depend on timing (it differs from the 64-query layout's
+// association only at rounding level: the same cells are summarised, the
+// same leaves and tiles summed).
+constexpr int NQ = 4;              // queries per narrow wave
+constexpr int NQ_LOG = 2;
+constexpr int NKP = 16 / NQ;       // stack entries per narrow pass
+constexpr int NPARTS = 64 / NQ;    // narrow waves per 64-query group (NPARTS / 4 workgroups)
+static_assert(NQ == (1 << NQ_LOG) && NKP * NQ * 4 == 64 && NPARTS % 4 == 0, "narrow lane layout");
 
-// Hand the stack [0, sp) of one wave to region r as tasks (wave-uniform);
-// false, and nothing handed over, when the region is full.
-__device__ bool spill_stack(const SpillView &sv, int r, int lane, int sp, const int32_t *sref_w,
-                            const uint64_t *smask_w, uint64_t *sbm_w, const QRec *__restrict__ qrec, int32_t wid,
-                            int32_t gpts, int32_t &c0, int32_t &nc) {
-    static_assert(STACK % 64 == 0, "spill rounds");
-    const int nr = (sp + 63) >> 6;
-    const double inv = 1.0 / (double)gpts;
-    int32_t carry_incl = 0, carry_g = -1, ng = 0;
-#pragma unroll 1
-    for (int q = 0; q < nr; ++q) {   // group boundaries, 64 entries a round (lane masks in LDS)
-        const int i = q * 64 + lane;
-        const bool in = i < sp;
-        const int32_t c = in ? qrec[sref_w[i]].cnt : 0;
-        int32_t incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t v = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += v;
+// bits {4 i : i < NQ} of x (one query per 4 lanes) -> bits {i}
+__device__ __forceinline__ uint32_t narrow_compress(uint64_t x) {
+    static_assert(NQ == 4, "narrow_compress: 4 queries per record");
+    x &= 0x1111ull;
+    x = (x | (x >> 3)) & 0x0303ull;
+    x = (x | (x >> 6)) & 0x000Full;
+    return (uint32_t)x;
+}
+
+struct NarrowView {
+    const int32_t *hlist = nullptr;    // heavy slot -> 64-query group
+    const int32_t *hcount = nullptr;   // [0] heavy groups this traversal
+    int32_t *ncost = nullptr;          // per heavy slot x part: the narrow wave's cost (next selection)
+    int32_t *mtask = nullptr;          // per heavy slot x 64 queries: moment tasks (MOM_TASKS each)
+    int32_t *mtask_n = nullptr;
+    const int32_t *nflag = nullptr;    // per group: heavy slot + 1, or 0 (the 64-query layout)
+    int32_t nbn = 0;                   // workgroups of the narrow part of the grid (hmax x NPARTS / 4)
+};
+
+// The traversal kernel's state shared by both layouts (LDS per 4-wave block).
+struct TravLDS {
+    int32_t sref[4][STACK];
+    uint64_t smask[4][STACK];
+    QRec srec[4][4];
+    int32_t bref[4][4];
+    uint64_t bmask[4][4];
+};
+
+// Stage the records of stack entries [sp, sp + k) of wave w into LDS (one
+// round of coalesced 16-byte loads; their latencies overlap).
+__device__ __forceinline__ void stage_records(TravLDS &L, int w, int lane, int sp, int k,
+                                              const QRec *__restrict__ qrec) {
+    if (lane < k) { L.bref[w][lane] = L.sref[w][sp + lane]; L.bmask[w][lane] = L.smask[w][sp + lane]; }
+    for (int e = lane; e < QREC_V4 * k; e += 64) {
+        const int rr = e / QREC_V4, part = e - rr * QREC_V4;
+        const int rf = L.sref[w][sp + rr];
+        reinterpret_cast<uint4 *>(&L.srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
+    __builtin_amdgcn_wave_barrier();
+}
+
+// All-open / near-exact test of one (query, record) pair (see the comment above
+// bh_traverse): the subtree's exact leaf sum replaces its walk.
+__device__ __forceinline__ bool tile_test(const QRec &nd, double qx, double qy, double qmag) {
+    const double cdx = qx - nd.cx, cdy = qy - nd.cy;
+    const double dc = cdx * cdx + cdy * cdy;
+    bool tile = dc <= nd.rball;   // rball^2 (1 - 1e-9)
+    if (!tile) {
+        const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+        const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+        const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+        const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
+        tile = dmax <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax)
+    }
+    return tile;
+}
+
+// The root: a single point, a key-tie group, or a cell tested like any child.
+// Lanes with `eval` take its term for their query (qx, qy); returns the lanes
+// that open it (the caller pushes the root record) and its record ref.
+template <bool STATS>
+__device__ __forceinline__ uint64_t root_step(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+                                              const QRec *__restrict__ qrec, const int32_t *__restrict__ meta,
+                                              int32_t virt, bool eval, double qx, double qy, double theta,
+                                              double th_lo, double th_hi, double &fx, double &fy, double &zs,
+                                              unsigned long long &nvis, int32_t &rpush) {
+    const int root = meta[1];
+    rpush = root;
+    if (root == ~0) {
+        if (eval) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
+        return 0;
+    }
+    if (root < 0) return 0;
+    const BHNode &rt = nodes[root];
+    if (rt.delta >= 62) {
+        for (int p = rt.first; p <= rt.last; ++p) {
+            const double2 pp = pos[p];
+            if (eval) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
         }
-        incl += carry_incl;
-        const int32_t g = (int32_t)((double)(incl - c) * inv);   // group of the exclusive prefix
-        int32_t gp = __shfl_up(g, 1, 64);
-        if (lane == 0) gp = carry_g;
-        const uint64_t bm = __ballot(in && (i == 0 || g != gp || i % TASK_ENT == 0));
-        if (lane == 0) sbm_w[q] = bm;
-        ng += (int)__popcll(bm);
-        carry_incl = __shfl(incl, 63, 64);
-        carry_g = __shfl(g, 63, 64);
+        return 0;
     }
-    int32_t tb = 0, eb = 0;
-    if (lane == 0) {
-        tb = atomicAdd(&sv.cnt[2 * r], ng);
-        eb = atomicAdd(&sv.cnt[2 * r + 1], sp);
+    // the root cell; with duplicates whose copies the reference root counts
+    // differently from the cells below it: its virtual record (h = W, every
+    // copy), opened into the real root node
+    double rh = rt.h, rcx = rt.cx, rcy = rt.cy;
+    int32_t rcnt = rt.cnt;
+    if (meta[3]) {
+        const QRec &vq = qrec[virt + root];
+        rh = ldexp(rt.h, rt.delta >> 1);
+        rcx = vq.cx; rcy = vq.cy; rcnt = vq.cnt; rpush = virt + root;
     }
-    tb = __shfl(tb, 0, 64);
-    eb = __shfl(eb, 0, 64);
-    BHTask *T = sv.task + (int64_t)(r - 1) * sv.task_cap;
-    if ((int64_t)tb + ng > sv.task_cap || (int64_t)eb + sp > sv.ent_cap) {
-        // region full: the slots reserved inside it stay empty tasks (ne = 0),
-        // which no combine reads; the wave keeps its stack
-        for (int j = lane; j < ng; j += 64)
-            if ((int64_t)tb + j < sv.task_cap) {
-                BHTask e{};
-                e.wid = wid;
-                T[tb + j] = e;
-            }
-        return false;
+    bool open = false;
+    if (eval) {
+        if (STATS) ++nvis;
+        const double dx = qx - rcx, dy = qy - rcy;
+        const double D = __fma_rn(dx, dx, dy * dy);
+        if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rcnt, fx, fy, zs);
+        else open = true;
     }
-    int32_t *ER = sv.tent_ref + (int64_t)(r - 1) * sv.ent_cap;
-    uint64_t *EM = sv.tent_mask + (int64_t)(r - 1) * sv.ent_cap;
-    for (int i = lane; i < sp; i += 64) {
-        ER[eb + i] = sref_w[i];
-        EM[eb + i] = smask_w[i];
+    return __ballot(open);
+}
+
+// One narrow wave: part `part` (queries part*NQ .. +NQ-1) of heavy group `grp`
+// (heavy slot h).  See "Narrow layout" above.
+template <int MODE>
+__device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const int32_t *__restrict__ dupc,
+                            const BHNode *__restrict__ nodes, const QRec *__restrict__ qrec,
+                            const int32_t *__restrict__ meta, const double *__restrict__ unused_mom, bool mom_on,
+                            double mom_tol, double theta, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
+                            int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
+                            unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost,
+                            const int32_t *__restrict__ cost_lab, int32_t *__restrict__ ttask_n,
+                            int32_t *__restrict__ tcost, int32_t *__restrict__ mom_flag, const NarrowView &nv,
+                            int64_t h, int part, int w) {
+    constexpr bool STATS = MODE == 2, COST = MODE >= 1;
+    (void)unused_mom;
+    const int lane = lane_id();
+    const int c = lane & 3, q = (lane >> 2) & (NQ - 1), k = lane >> (2 + NQ_LOG);
+    const int64_t grp = nv.hlist[h];
+    const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
+    const int64_t kq = g0 + grp * 64 + part * NQ + q;
+    const bool valid = kq < g1;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
+    const int64_t e = h * 64 + part * NQ + q;   // this query's moment list
+    if (part == 0 && lane == 0) { ttask_n[grp] = 0; tcost[grp] = 0; }   // tile_apply: nothing for this group
+    const long long t_start = COST ? clock64() : 0;
+    const unsigned long long w_start = STATS ? wall_clock64() : 0;
+    double qx = 0.0, qy = 0.0;
+    if (valid) { const double2 qq = pos[s]; qx = qq.x; qy = qq.y; }
+    const double qmag = fabs(qx) + fabs(qy);
+    const int ndup = valid ? dupc[s] : 0;
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    unsigned long long nvis = 0;
+    int32_t npops = 0, ntilepts = 0, ntask = 0, nwant = 0;
+    int sp = 0;
+    {
+        int32_t rpush;
+        const uint64_t om = root_step<STATS>(pos, nodes, qrec, meta, virt, valid && k == 0 && c == 0, qx, qy, theta,
+                                             th_lo, th_hi, fx, fy, zs, nvis, rpush);
+        const uint32_t qm = narrow_compress(om);
+        if (qm) {
+            if (lane == 0) { L.sref[w][0] = rpush; L.smask[w][0] = qm; }
+            sp = 1;
+        }
     }
-    int before = 0;
-#pragma unroll 1
-    for (int q = 0; q < nr; ++q) {   // one task per group: its first entry and length
-        const uint64_t v = sbm_w[q];   // wave-uniform: its two halves to scalar registers (zero-extended)
-        const uint64_t bm = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
-        const int i = q * 64 + lane;
-        if ((bm >> lane) & 1ull) {
-            const int gi = before + (int)__popcll(bm & lanemask_lt());
-            const uint64_t above = lane < 63 ? (bm >> (lane + 1)) : 0ull;
-            int nxt = sp;
-            if (above) {
-                nxt = i + __ffsll((long long)above);
-            } else {
-                for (int q2 = q + 1; q2 < nr; ++q2) {
-                    const uint64_t b2 = sbm_w[q2];
-                    if (b2) { nxt = q2 * 64 + __ffsll((long long)b2) - 1; break; }
+    // same-query lanes of earlier records (moment-task order within a pass)
+    const uint64_t qcol = 0x0001000100010001ull << (4 * q);
+    while (sp > 0) {
+        const int kn = sp > STACK / 2 ? 1 : (sp < NKP ? sp : NKP);
+        sp -= kn;
+        stage_records(L, w, lane, sp, kn, qrec);
+        npops += kn;
+        const bool kin = k < kn;
+        const int kk = kin ? k : 0;
+        const QRec &nd = L.srec[w][kk];
+        const uint32_t msk = (uint32_t)L.bmask[w][kk];
+        bool act = kin && valid && ((msk >> q) & 1u);
+        const int nflags = nd.nch;
+        bool tile = false;
+        if ((nflags & QNCH_TILE) && act) tile = tile_test(nd, qx, qy, qmag);
+        if (__ballot(tile)) {
+            const int a = nd.first, b = nd.last, cnt = nd.cnt;
+            // moment path: decided once per (record, query) by its child-0 lane,
+            // tasks appended per query in record order (capped at MOM_TASKS)
+            const bool mw = tile && c == 0 && cnt >= MOM_MIN_POINTS && moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy, mom_tol);
+            nwant += mw ? 1 : 0;
+            const uint64_t U = __ballot(mw && mom_on);
+            const int before = __popcll(U & qcol & lanemask_lt());
+            const bool usem = mw && mom_on && ntask + before < MOM_TASKS;
+            if (usem) nv.mtask[e * MOM_TASKS + ntask + before] = L.bref[w][kk];
+            ntask = min(MOM_TASKS, ntask + (int)__popcll(U & qcol));
+            const uint64_t UM = __ballot(usem);
+            const bool dense = tile && !((UM >> (lane & ~3)) & 1ull);
+            // the range holds whole equal-key runs: the query's duplicates (itself
+            // included) add exactly 1 each to z in the leaf sum, taken off here
+            if (tile && c == 0 && s >= a && s <= b) zs -= (double)ndup;
+            if (STATS && tile && c == 0) nvis += (unsigned long long)(b - a + 1);
+            // dense: the query's 4 lanes split the subtree's points
+            int p = dense ? a + c : 1, last = dense ? b : 0;
+            while (__ballot(p <= last)) {
+                if (p <= last) {
+                    const double2 pp = pos[p];
+                    pair_force(qx, qy, pp.x, pp.y, fx, fy, zs);
+                    p += 4;
                 }
             }
-            BHTask e{};
-            e.wid = wid;
-            e.e0 = eb + i;
-            e.ne = nxt - i;
-            T[tb + gi] = e;
+            const uint64_t tm = __ballot(tile && c == 0);
+            for (uint64_t r = tm; r; r &= r - 1) {   // cost: points per (record, query), as the 64-query layout's
+                const int l = __ffsll((long long)r) - 1;
+                ntilepts += __shfl(b - a + 1, l, 64);
+            }
+            act = act && !tile;
         }
-        before += (int)__popcll(bm);
+        if (__ballot(act) == 0) continue;
+        // child c of record k for query q
+        const int nch = nflags & 0xff;
+        const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
+        const bool has = act && c < nch;
+        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+        const double D = __fma_rn(dx, dx, dy * dy);
+        const bool isleaf = has && kind == QK_LEAF, iscell = has && kind == QK_CELL;
+        const double A = nd.ca[c];
+        bool acc = D > A;
+        if (iscell && !acc && !(D < A * QACC_BAND))
+            acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+        const bool takel = isleaf && !(dx == 0.0 && dy == 0.0);
+        const bool takec = iscell && acc;
+        const double wm = takel ? 1.0 : (takec ? (double)nd.ccnt[c] : 0.0);
+        if (STATS && (isleaf || iscell)) ++nvis;
+        const double Qv = recip_bh(1.0 + D);
+        const double mult = wm * Qv;
+        const double sc = mult * Qv;
+        fx = __fma_rn(sc, dx, fx);
+        fy = __fma_rn(sc, dy, fy);
+        zs += mult;
+        // duplicate kinds (rare)
+        const bool dupk = has && (kind == QK_MULTI || kind == QK_TIE);
+        if (__builtin_expect(__ballot(dupk) != 0, 0)) {
+            if (dupk && kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                if (!(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
+                    if (STATS) ++nvis;
+                    cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                }
+            } else if (dupk) {                // a key-tie group: every point directly
+                const BHNode &tn = nodes[nd.cref[c]];
+                for (int p = tn.first; p <= tn.last; ++p) {
+                    const double2 pp = pos[p];
+                    if (STATS) ++nvis;
+                    leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs);
+                }
+            }
+        }
+        // pushes: one entry per (record, child) that some query opens, in lane order
+        const uint64_t O = __ballot(iscell && !acc);
+        const bool pl = q == 0 && kin;
+        const uint32_t m = pl ? narrow_compress(O >> (k * 4 * NQ + c)) : 0u;
+        const uint64_t P = __ballot(m != 0u);
+        if (m) {
+            const int at = sp + (int)__popcll(P & lanemask_lt());
+            L.sref[w][at] = nd.cref[c];
+            L.smask[w][at] = m;
+        }
+        sp += (int)__popcll(P);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the pushes landed before the next pop
+        __builtin_amdgcn_wave_barrier();
     }
-    c0 = tb;
-    nc = ng;
-    return true;
+    // the query's NKP x 4 lanes, in a fixed xor butterfly (every lane the same bits)
+#pragma unroll
+    for (int o = 1; o <= 2; o <<= 1) {
+        fx += __shfl_xor(fx, o, 64); fy += __shfl_xor(fy, o, 64); zs += __shfl_xor(zs, o, 64);
+    }
+#pragma unroll
+    for (int o = 4 * NQ; o < 64; o <<= 1) {
+        fx += __shfl_xor(fx, o, 64); fy += __shfl_xor(fy, o, 64); zs += __shfl_xor(zs, o, 64);
+    }
+    if (k == 0 && c == 0 && valid) {
+        F[s] = make_double2(fx, fy);
+        Z[s] = zs;
+    }
+    if (k == 0 && c == 0) nv.mtask_n[e] = valid ? ntask : 0;
+    const int wwant = wave_sum(nwant);
+    if (lane == 0) {
+        nv.ncost[h * NPARTS + part] = npops + (ntilepts >> 6);
+        if (wwant && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
+            atomicAdd(&mom_flag[1], wwant);
+    }
+    if (COST && bcost) {   // this wave's run time into its queries' buckets (multi-GPU balancing)
+        const unsigned long long cc = ((unsigned long long)(clock64() - t_start) >> 6) + 1;
+        if (cost_lab) {
+            if (valid && k == 0 && c == 0) atomicAdd(&bcost[cost_lab[s] >> 8], (cc + NQ - 1) / NQ);
+        } else {
+            const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
+            if (lane == 0) atomicAdd(&bcost[sf >> 8], cc);
+        }
+    }
+    if (STATS && visits) {
+        const unsigned long long tv = wave_sum(nvis);
+        if (lane == 0) {
+            atomicAdd(visits, tv);
+            atomicAdd(visits + 3, (unsigned long long)npops);
+            atomicAdd(visits + 4, (unsigned long long)ntilepts);
+            atomicMax(visits + 8, (unsigned long long)npops);
+            atomicAdd(visits + 30, 1ull);   // narrow waves run
+            const unsigned long long w_end = wall_clock64();
+            atomicMax(visits + 15, w_end - w_start);
+            atomicMax(visits + 16, ~0ull - w_start);
+            atomicMax(visits + 17, w_end);
+            atomicAdd(visits + 18, w_end - w_start);
+            atomicMax(visits + 31, w_end - w_start);   // longest narrow wave
+        }
+    }
 }
 
-// The next 64-query group of a persistent traversal wave: group g (blocks with
-// blockIdx % 8 == g, which the dispatcher places on one XCD) takes the g-th
-// eighth of the waves in Morton order, so each XCD's L2 serves a contiguous
-// part of the tree; an exhausted eighth moves on to the next ones.  -1 when
-// every group is done.  (Which wave runs which group does not change any
-// result: a group's sums and tile list are its own.)
-__device__ __forceinline__ int64_t bh_dequeue(int32_t *qhead, int64_t nw, int grp) {
-    for (int k = 0; k < 8; ++k) {
-        const int g = (grp + k) & 7;
-        const int64_t lo = nw * g / 8, len = nw * (g + 1) / 8 - lo;
-        if (__hip_atomic_load(&qhead[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= len) continue;
-        int32_t v = 0;
-        if (lane_id() == 0) v = atomicAdd(&qhead[g], 1);
-        v = __shfl(v, 0, 64);
-        if (v < len) return lo + v;
-    }
-    return -1;
+// The narrow waves of the heavy groups: 4 per workgroup, idle beyond the
+// heavy count.  A kernel of its own (its ~78 VGPRs would cost the 64-query
+// layout's 8 waves per SIMD), launched on a second stream beside bh_traverse.
+template <int MODE>
+__global__ __launch_bounds__(256) void bh_traverse_narrow(
+    const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
+    const QRec *__restrict__ qrec, int32_t *__restrict__ ttask_n, const int32_t *__restrict__ meta,
+    int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0, int64_t g1,
+    const int32_t *__restrict__ qlist, int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
+    unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost, int32_t *__restrict__ tcost,
+    const int32_t *__restrict__ cost_lab, NarrowView nv) {
+    __shared__ TravLDS L;
+    const int w = threadIdx.x >> 6;
+    const int64_t slot = (int64_t)blockIdx.x * 4 + w;   // heavy slot x part
+    const int64_t h = slot / NPARTS;
+    if (h >= (int64_t)*nv.hcount) return;
+    narrow_wave<MODE>(L, pos, dupc, nodes, qrec, meta, nullptr, mom_flag[0] != 0, mom_tol, theta, g0, g1, qlist, virt,
+                      F, Z, visits, bcost, cost_lab, ttask_n, tcost, mom_flag, nv, h, (int)(slot % NPARTS), w);
 }
 
-// Traversal kernel (see the comment above).  STATS: per-wave work counters
-// (profiling, and the bucket costs of the multi-GPU balancing); the
-// production instantiation carries none.  TASK = false: one wave per 64
-// query slots (pass 0), spilling into region 1 when sv.task is set; TASK =
-// true: the tasks of `region`, grid-stride over a fixed grid, spilling into
-// region + 1 (none from the last region), tiles summed inline.
-template <int KPOP, int MODE, bool TASK>   // MODE 0 plain, 1 wave times for bcost only, 2 all counters
+// Traversal kernel (see the comment above), one 64-query group per wave;
+// groups the narrow waves take (nv.nflag) return at once.  MODE 0 plain; 1
+// wave run times into the multi-GPU cost buckets; 2 every counter (profiling).
+template <int MODE>
 __global__ __launch_bounds__(256) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
-    const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double theta, double near_dmax, int64_t g0,
-    int64_t g1, const int32_t *__restrict__ qlist, int xcd_chunk, int32_t virt, double2 *__restrict__ F,
-    double *__restrict__ Z, unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost,
-    const int32_t *__restrict__ border, int32_t *__restrict__ wcost, int32_t *__restrict__ tcost, SpillView sv,
-    int region, int32_t *__restrict__ qhead, const int32_t *__restrict__ cost_lab) {
+    const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0,
+    int64_t g1, const int32_t *__restrict__ qlist, int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
+    unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost, int32_t *__restrict__ wcost,
+    int32_t *__restrict__ tcost, const int32_t *__restrict__ cost_lab, NarrowView nv) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
-    __shared__ int32_t sref[4][STACK];
-    __shared__ uint64_t smask[4][STACK];
-    __shared__ QRec srec[4][KPOP];
-    __shared__ int32_t bref[4][KPOP];
-    __shared__ uint64_t bmask[4][KPOP];
-    __shared__ double2 tbuf[4][TASK ? 64 : 1];
-    __shared__ uint64_t sbm[4][STACK / 64];   // spill: group boundary masks
+    __shared__ TravLDS L;
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
-    // the pop budget of this traversal and the spill group size (points)
-    // region SPILL_PASSES + 1 (TASK): the finish pass over saved stacks (sv.ovf), without budget
-    const bool finish = TASK && region > SPILL_PASSES;
-    const bool can_spill = sv.task != nullptr && (!TASK || region < SPILL_PASSES);
-    const int32_t budget0 = can_spill ? sv.budget[0] : INT32_MAX;
-    const int32_t gpts = (int32_t)min((int64_t)INT32_MAX, max((int64_t)1, (int64_t)budget0 * sv.gfac));
-    const int64_t nsrc_w = sv.nwaves;   // saved-stack sources: waves [0, nwaves), then tasks by global id
-    // persistent query waves (qhead, !TASK): the grid is what fits on the chip
-    // and each wave dequeues 64-query groups (bh_dequeue) until none is left
-    const int64_t nqw = (g1 - g0 + 63) / 64;
-    const int64_t ntask = !TASK ? (qhead ? INT64_MAX : 1)
-                        : finish ? (int64_t)sv.cnt[0] : min((int64_t)sv.cnt[2 * region], (int64_t)sv.task_cap);
-    const int64_t gstride = TASK ? (int64_t)gridDim.x * 4 : 1;
-    for (int64_t ti = TASK ? (int64_t)blockIdx.x * 4 + w : 0; ti < ntask; ti += gstride) {
-        BHTask tk{};
-        int64_t wid, src = 0;
-        if constexpr (TASK) {
-            if (finish) {   // a saved stack: entries from its save area
-                const int2 o = sv.ovf[ti];
-                src = o.x;
-                tk.ne = o.y;
-                tk.wid = src < nsrc_w ? (int32_t)src : sv.task[src - nsrc_w].wid;
-            } else {
-                tk = sv.task[(int64_t)(region - 1) * sv.task_cap + ti];
-                if (tk.ne == 0) continue;   // an empty slot of a full region (uniform)
-            }
-            wid = tk.wid;
-        } else if (qhead) {
-            wid = bh_dequeue(qhead, nqw, (int)(blockIdx.x & 7));
-            if (wid < 0) break;
-        } else {
-            const int64_t blk = border ? (int64_t)border[blockIdx.x]
-                              : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk)
-                                              : (int64_t)blockIdx.x;
-            wid = blk * 4 + w;   // wave slot: query slots g0 + 64 wid .. + 63, tile list wid
+    const int64_t wid = (int64_t)blockIdx.x * 4 + w;   // query slots g0 + 64 wid .. + 63, tile list wid
+    // query slot k -> sorted position s (the identity, or this rank's list of
+    // its own queries in sorted order: the waves stay Morton-coherent)
+    const int64_t k = g0 + wid * 64 + lane;
+    const bool valid = k < g1;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
+    if (__ballot(valid) == 0) return;
+    if (nv.nflag && nv.nflag[wid]) return;   // a heavy group: the narrow waves take it
+    if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
+    const long long t_start = COST ? clock64() : 0;
+    const unsigned long long w_start = STATS ? wall_clock64() : 0;
+    int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next selection
+    double qx = 0.0, qy = 0.0;
+    if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
+    const double qmag = fabs(qx) + fabs(qy);
+    const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
+    double fx = 0.0, fy = 0.0, zs = 0.0;
+    unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
+    unsigned long long wfull = 0, wpart = 0;                                   // STATS only
+    int sp = 0;
+    int ntt = 0;
+    TileTask *mytt = ttask + wid * TILE_CAP;
+    {
+        int32_t rpush;
+        const uint64_t om = root_step<STATS>(pos, nodes, qrec, meta, virt, valid, qx, qy, theta, th_lo, th_hi, fx, fy,
+                                             zs, nvis, rpush);
+        if (om) {
+            if (lane == 0) { L.sref[w][0] = rpush; L.smask[w][0] = om; }
+            sp = 1;
         }
-        // query slot k -> sorted position s (the identity, or this rank's list of
-        // its own queries in sorted order: the waves stay Morton-coherent)
-        const int64_t k = g0 + wid * 64 + lane;
-        const bool valid = k < g1;
-        const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
-        if constexpr (!TASK) {
-            if (lane == 0) {
-                ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0;
-                if (sv.wspill) sv.wspill[wid] = make_int2(0, 0);
-            }
-            if (__ballot(valid) == 0) {
-                if (qhead) continue;
-                return;
-            }
-        }
-        const long long t_start = COST ? clock64() : 0;
-        const unsigned long long w_start = STATS ? wall_clock64() : 0;
-        int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next block orders
-        int32_t budget = budget0;
-        double qx = 0.0, qy = 0.0;
-        if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
-        const double qmag = fabs(qx) + fabs(qy);
-        const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
-        double fx = 0.0, fy = 0.0, zs = 0.0;
-        unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
-        unsigned long long wfull = 0, wpart = 0;                                   // STATS only
-        int sp = 0;
-        int ntt = 0;
-        TileTask *mytt = TASK ? nullptr : ttask + wid * TILE_CAP;
-        if constexpr (TASK) {   // the task's stack entries, in their original stack order
-            const int32_t *er = finish ? sv.save_ref + src * STACK : sv.tent_ref + (int64_t)(region - 1) * sv.ent_cap + tk.e0;
-            const uint64_t *em = finish ? sv.save_mask + src * STACK : sv.tent_mask + (int64_t)(region - 1) * sv.ent_cap + tk.e0;
-            for (int i = lane; i < tk.ne; i += 64) { sref[w][i] = er[i]; smask[w][i] = em[i]; }
-            sp = tk.ne;
-        } else {
-            // ---- the root: a single point, a key-tie group, or a cell tested like any child
-            const int root = meta[1];
-            if (root == ~0) {
-                if (valid) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
-            } else if (root >= 0) {
-                const BHNode &rt = nodes[root];
-                if (rt.delta >= 62) {
-                    for (int p = rt.first; p <= rt.last; ++p) {
-                        const double2 pp = pos[p];
-                        if (valid) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
-                    }
-                } else {
-                    // the root cell; with duplicates whose copies the reference root
-                    // counts differently from the cells below it: its virtual record
-                    // (h = W, every copy), opened into the real root node
-                    double rh = rt.h, rcx = rt.cx, rcy = rt.cy;
-                    int32_t rcnt = rt.cnt, rpush = root;
-                    if (meta[3]) {
-                        const QRec &vq = qrec[virt + root];
-                        rh = ldexp(rt.h, rt.delta >> 1);
-                        rcx = vq.cx; rcy = vq.cy; rcnt = vq.cnt; rpush = virt + root;
-                    }
-                    bool open = false;
-                    if (valid) {
-                        if (STATS) ++nvis;
-                        const double dx = qx - rcx, dy = qy - rcy;
-                        const double D = __fma_rn(dx, dx, dy * dy);
-                        if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rcnt, fx, fy, zs);
-                        else open = true;
-                    }
-                    const uint64_t om = __ballot(open);
-                    if (om) {
-                        if (lane == 0) { sref[w][0] = rpush; smask[w][0] = om; }
-                        sp = 1;
-                    }
-                }
-            }
-        }
-        // Pop up to KPOP cells at a time: their records are fetched with one
-        // round of coalesced 16-byte vector loads into LDS (the pops' memory
-        // latencies overlap), then processed one by one from LDS broadcasts.
-        while (sp > 0) {
-            if (sp >= 2 && npops + (ntilepts >> 6) >= budget) break;   // over budget: spilled at the end
-            const int k = sp > STACK / 2 ? 1 : (sp < KPOP ? sp : KPOP);
-            sp -= k;
-            if (lane < k) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
-            for (int e = lane; e < QREC_V4 * k; e += 64) {
-                const int rr = e / QREC_V4, part = e - rr * QREC_V4;
-                const int rf = sref[w][sp + rr];
-                reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
-            __builtin_amdgcn_wave_barrier();
-            npops += k;
-            for (int r = 0; r < k; ++r) {
-                if (STATS) ++wpops;
-                const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
-                const uint64_t msk = bmask[w][r];
-                bool act = (msk >> lane) & 1ull;
-                const QRec &nd = srec[w][r];
-                // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
-                bool tile = false;
-                const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
-                if ((nflags & QNCH_TILE) && act) {
-                    const double cdx = qx - nd.cx, cdy = qy - nd.cy;
-                    const double dc = cdx * cdx + cdy * cdy;
-                    tile = dc <= nd.rball;   // rball^2 (1 - 1e-9)
-                    if (!tile) {
-                        const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-                        const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
-                        const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-                        const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-                        tile = dmax <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax)
-                    }
-                }
-                const uint64_t tm = __ballot(tile);
-                if (tm) {
-                    const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
-                    if constexpr (TASK) {
-                        // the tile's exact leaf sum, densely, by the tile lanes (points
-                        // staged through LDS 64 at a time); the range holds whole
-                        // equal-key runs: the query's duplicates (itself included) add
-                        // exactly 1 each to z and are taken off
-                        double ux = 0.0, uy = 0.0, uz = 0.0;
-                        for (int c0 = a; c0 <= b; c0 += 64) {
-                            const int cn = min(64, b - c0 + 1);
-                            __builtin_amdgcn_wave_barrier();
-                            tbuf[w][lane] = lane < cn ? pos[c0 + lane] : make_double2(0.0, 0.0);
-                            __builtin_amdgcn_wave_barrier();
-                            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes landed
-                            __builtin_amdgcn_wave_barrier();
-                            for (int j = 0; j < cn; ++j) {
-                                const double2 pp = tbuf[w][j];
-                                pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
-                            }
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                        if (tile) {
-                            fx += ux; fy += uy; zs += uz;
-                            if (s >= a && s <= b) zs -= (double)ndup;
-                            if (STATS) nvis += (unsigned long long)(b - a + 1);
-                        }
-                        ntilepts += b - a + 1;
-                        if (STATS) wtile += (unsigned long long)(b - a + 1);
-                        act = act && !tile;
-                    } else if (ntt < TILE_CAP) {
-                        // The wave records (subtree, lanes) for tile_apply, or, when its
-                        // list is full, the lanes keep traversing (the reference's path).
-                        // The range holds whole equal-key runs, so either all of the
-                        // query's exact duplicates (itself included) are in it or none
-                        // is; they add exactly 1 each to z in the leaf sum: taken off here.
-                        if (lane == 0) {
-                            TileTask tt; tt.ref = ref; tt.first = a; tt.last = b; tt.pad = nd.cnt; tt.mask = tm;
-                            mytt[ntt] = tt;
-                        }
-                        ++ntt;
-                        ntilepts += b - a + 1;
-                        if (STATS) wtile += (unsigned long long)(b - a + 1);
-                        if (tile) {
-                            if (STATS) nvis += (unsigned long long)(b - a + 1);
-                            if (s >= a && s <= b) zs -= (double)ndup;
-                        }
-                        act = act && !tile;
-                    }
-                }
-                if (__ballot(act) == 0) continue;
-                // the opened cell's quad children, from its record
-                const int nch = nflags & 0xff;
-                if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    if (c >= nch) break;
-                    const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
-                    if (kind == QK_CELL || kind == QK_LEAF) {
-                        // A leaf (cumSize 1, com = the point) always interacts, zero if
-                        // it is the query's own point (x - y == 0 iff x == y).  A cell is
-                        // summarised when ch / D < theta (QACC_BAND: two compares against
-                        // the record's bound, the exact quotient only inside the band;
-                        // at D = 0 never).  wm = the term's multiplicity where taken, else
-                        // 0: a zero term leaves the sums bit-equal.  Only wm is computed
-                        // per kind (uniform branch), so the accumulators stay in place.
-                        if (STATS && act) ++nvis;
-                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                        const double D = __fma_rn(dx, dx, dy * dy);
-                        bool take;
-                        double wm;
-                        if (kind == QK_LEAF) {
-                            take = act && !(dx == 0.0 && dy == 0.0);
-                            wm = take ? 1.0 : 0.0;
-                        } else {
-                            const double A = nd.ca[c];
-                            bool acc = D > A;
-                            if (act && !acc && !(D < A * QACC_BAND))
-                                acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
-                            take = act && acc;
-                            wm = (double)(take ? nd.ccnt[c] : 0);
-                            const uint64_t om = __ballot(act && !acc);
-                            if (om) {
-                                if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
-                                ++sp;
-                            }
-                        }
-                        const double Q = recip_bh(1.0 + D);
-                        const double mult = wm * Q;
-                        const double sc = mult * Q;
-                        fx = __fma_rn(sc, dx, fx);
-                        fy = __fma_rn(sc, dy, fy);
-                        zs += mult;
-                        if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
-                            const uint64_t am = __ballot(act), tk2 = __ballot(take);
-                            if (am && tk2 == am) {
-                                if (am == __ballot(valid)) ++wfull; else ++wpart;
-                            }
-                        }
-                    }
-                }
-                // duplicate kinds (rare), after the others: out of the main loop,
-                // whose accumulators then stay in place
-                if (__builtin_expect((nflags & (0xAA << QNCH_KIND)) != 0, 0)) {
-                    for (int c = 0; c < nch; ++c) {
-                        const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
-                        if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
-                            if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
-                                if (STATS) ++nvis;
-                                const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                                cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
-                            }
-                        } else if (kind == QK_TIE) {
-                            const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
-                            for (int p = tn.first; p <= tn.last; ++p) {
-                                const double2 pp = pos[p];
-                                if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
-                            }
-                        }
-                    }
-                }
-            }
-        }
-        if constexpr (TASK) {   // the task's partial sums; its cost onto the origin wave (next budget)
-            if (finish && src < nsrc_w) {   // a saved wave stack: into the wave's own sums
-                if (valid) {
-                    const double2 f = F[s];
-                    F[s] = make_double2(f.x + fx, f.y + fy);
-                    Z[s] = Z[s] + zs;
-                }
-            } else if (finish) {            // a saved task stack: into that task's partial
-                const int64_t gid = src - nsrc_w;
-                const double2 f = sv.tF[gid * 64 + lane];
-                sv.tF[gid * 64 + lane] = make_double2(f.x + fx, f.y + fy);
-                sv.tZ[gid * 64 + lane] += zs;
-            } else {
-                const int64_t gid = (int64_t)(region - 1) * sv.task_cap + ti;
-                sv.tF[gid * 64 + lane] = make_double2(fx, fy);
-                sv.tZ[gid * 64 + lane] = zs;
-            }
-            if (lane == 0) atomicAdd(&wcost[wid], npops + (ntilepts >> 6));
-        } else {
-            if (valid) {
-                F[s] = make_double2(fx, fy);
-                Z[s] = zs;
-            }
-            if (lane == 0) {
-                ttask_n[wid] = ntt;
-                wcost[wid] = npops + (ntilepts >> 6);
-                tcost[wid] = ntilepts + 16 * ntt;
-            }
-        }
-        if (COST && bcost) {   // cost of this wave (or task) into its first query's 256-query bucket
-            // MODE 1: the wave's own run time (shader clock / 64; the slices only
-            // move work between ranks, every query's sums are unchanged);
-            // MODE 2: cell pops + tile points / 48
-            const unsigned long long c =
-                MODE == 1 ? ((unsigned long long)(clock64() - t_start) >> 6) + 1 : wpops + wtile / 48 + 4;
-            if (cost_lab) {   // by label: an equal share into each query's label bucket
-                if (valid) atomicAdd(&bcost[cost_lab[s] >> 8], (c + 63) >> 6);
-            } else {
-                const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
-                if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
-            }
-        }
-        if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
-                                 // [4] wave-level tile points, [5] lane child evaluations, [6] wave
-                                 // child slots, [7..9] heaviest wave or task ([1], [2]: tile_apply),
-                                 // [23] spill tasks run
-            const unsigned long long tv = wave_sum(nvis), te = wave_sum(nevals);
-            if (lane == 0) {
-                atomicAdd(visits, tv);
-                atomicAdd(visits + 3, wpops);
-                atomicAdd(visits + 4, wtile);
-                atomicAdd(visits + 5, te);
-                atomicAdd(visits + 6, wslots);
-                atomicMax(visits + 7, wpops + wtile / 16);   // heaviest wave (pops + tile points/16)
-                atomicMax(visits + 8, wpops);
-                atomicMax(visits + 9, wtile);
-                atomicAdd(visits + 13, wfull);
-                atomicAdd(visits + 14, wpart);
-                if (TASK) atomicAdd(visits + 23, 1ull);
-                const unsigned long long w_end = wall_clock64();   // [15] longest wave, [16] ~first start,
-                atomicMax(visits + 15, w_end - w_start);            // [17] last end, [18] sum of wave times
-                atomicMax(visits + 16, ~0ull - w_start);
-                atomicMax(visits + 17, w_end);
-                atomicAdd(visits + 18, w_end - w_start);
-            }
-        }
-        if (sp > 0) {   // stopped over budget: hand the remaining stack to the next region
-            int32_t c0 = 0, nc = 0;
-            if (spill_stack(sv, TASK ? region + 1 : 1, lane, sp, sref[w], smask[w], sbm[w], qrec, (int32_t)wid, gpts,
-                            c0, nc)) {
+    }
+    // Pop up to 4 cells at a time: their records are fetched with one round of
+    // coalesced 16-byte vector loads into LDS, then processed one by one from
+    // LDS broadcasts.
+    while (sp > 0) {
+        const int kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
+        sp -= kb;
+        stage_records(L, w, lane, sp, kb, qrec);
+        npops += kb;
+        for (int r = 0; r < kb; ++r) {
+            if (STATS) ++wpops;
+            const int ref = __builtin_amdgcn_readfirstlane(L.bref[w][r]);
+            const uint64_t msk = L.bmask[w][r];
+            bool act = (msk >> lane) & 1ull;
+            const QRec &nd = L.srec[w][r];
+            // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
+            bool tile = false;
+            const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
+            if ((nflags & QNCH_TILE) && act) tile = tile_test(nd, qx, qy, qmag);
+            const uint64_t tm = __ballot(tile);
+            if (tm && ntt < TILE_CAP) {
+                // The wave records (subtree, lanes) for tile_apply, or, when its
+                // list is full, the lanes keep traversing (the reference's path).
+                // The range holds whole equal-key runs, so either all of the
+                // query's exact duplicates (itself included) are in it or none
+                // is; they add exactly 1 each to z in the leaf sum: taken off here.
+                const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
                 if (lane == 0) {
-                    if constexpr (TASK) {
-                        BHTask &me = sv.task[(int64_t)(region - 1) * sv.task_cap + ti];
-                        me.c0 = c0;
-                        me.nc = nc;
+                    TileTask tt; tt.ref = ref; tt.first = a; tt.last = b; tt.pad = nd.cnt; tt.mask = tm;
+                    mytt[ntt] = tt;
+                }
+                ++ntt;
+                ntilepts += b - a + 1;
+                if (STATS) wtile += (unsigned long long)(b - a + 1);
+                if (tile) {
+                    if (STATS) nvis += (unsigned long long)(b - a + 1);
+                    if (s >= a && s <= b) zs -= (double)ndup;
+                }
+                act = act && !tile;
+            }
+            if (__ballot(act) == 0) continue;
+            // the opened cell's quad children, from its record
+            const int nch = nflags & 0xff;
+            if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (c >= nch) break;
+                const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;   // uniform: scalar branches
+                if (kind == QK_CELL || kind == QK_LEAF) {
+                    // A leaf (cumSize 1, com = the point) always interacts, zero if
+                    // it is the query's own point (x - y == 0 iff x == y).  A cell is
+                    // summarised when ch / D < theta (QACC_BAND: two compares against
+                    // the record's bound, the exact quotient only inside the band;
+                    // at D = 0 never).  wm = the term's multiplicity where taken, else
+                    // 0: a zero term leaves the sums bit-equal.  Only wm is computed
+                    // per kind (uniform branch), so the accumulators stay in place.
+                    if (STATS && act) ++nvis;
+                    const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                    const double D = __fma_rn(dx, dx, dy * dy);
+                    bool take;
+                    double wm;
+                    if (kind == QK_LEAF) {
+                        take = act && !(dx == 0.0 && dy == 0.0);
+                        wm = take ? 1.0 : 0.0;
                     } else {
-                        sv.wspill[wid] = make_int2(c0, nc);
+                        const double A = nd.ca[c];
+                        bool acc = D > A;
+                        if (act && !acc && !(D < A * QACC_BAND))
+                            acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                        take = act && acc;
+                        wm = (double)(take ? nd.ccnt[c] : 0);
+                        const uint64_t om = __ballot(act && !acc);
+                        if (om) {
+                            if (lane == 0) { L.sref[w][sp] = nd.cref[c]; L.smask[w][sp] = om; }
+                            ++sp;
+                        }
+                    }
+                    const double Q = recip_bh(1.0 + D);
+                    const double mult = wm * Q;
+                    const double sc = mult * Q;
+                    fx = __fma_rn(sc, dx, fx);
+                    fy = __fma_rn(sc, dy, fy);
+                    zs += mult;
+                    if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
+                        const uint64_t am = __ballot(act), tk2 = __ballot(take);
+                        if (am && tk2 == am) {
+                            if (am == __ballot(valid)) ++wfull; else ++wpart;
+                        }
                     }
                 }
-            } else {   // the region is full: save the stack for the finish pass (never full)
-                const int64_t src = TASK ? nsrc_w + (int64_t)(region - 1) * sv.task_cap + ti : wid;
-                for (int i = lane; i < sp; i += 64) {
-                    sv.save_ref[src * STACK + i] = sref[w][i];
-                    sv.save_mask[src * STACK + i] = smask[w][i];
+            }
+            // duplicate kinds (rare), after the others: out of the main loop,
+            // whose accumulators then stay in place
+            if (__builtin_expect((nflags & (0xAA << QNCH_KIND)) != 0, 0)) {
+                for (int c = 0; c < nch; ++c) {
+                    const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
+                    if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                        if (act && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
+                            if (STATS) ++nvis;
+                            const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                            cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
+                        }
+                    } else if (kind == QK_TIE) {
+                        const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
+                        for (int p = tn.first; p <= tn.last; ++p) {
+                            const double2 pp = pos[p];
+                            if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                        }
+                    }
                 }
-                if (lane == 0) sv.ovf[atomicAdd(&sv.cnt[0], 1)] = make_int2((int32_t)src, sp);
             }
         }
     }
-}
-
-// A task's sum = its own partial + its children's sums in spill order (region
-// `region`; its children in region + 1 are final already: bottom-up launches).
-__global__ void task_combine(SpillView sv, int region) {
-    const int64_t ntask = min((int64_t)sv.cnt[2 * region], (int64_t)sv.task_cap);
-    const BHTask *T = sv.task + (int64_t)(region - 1) * sv.task_cap;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ntask * 64;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t ti = e >> 6, lane = e & 63;
-        const BHTask tk = T[ti];
-        if (tk.ne == 0 || tk.nc == 0) continue;
-        const int64_t gid = (int64_t)(region - 1) * sv.task_cap + ti;
-        double2 f = sv.tF[gid * 64 + lane];
-        double z = sv.tZ[gid * 64 + lane];
-        for (int j = 0; j < tk.nc; ++j) {
-            const int64_t cg = (int64_t)region * sv.task_cap + tk.c0 + j;
-            const double2 g = sv.tF[cg * 64 + lane];
-            f.x += g.x;
-            f.y += g.y;
-            z += sv.tZ[cg * 64 + lane];
+    if (valid) {
+        F[s] = make_double2(fx, fy);
+        Z[s] = zs;
+    }
+    if (lane == 0) {
+        ttask_n[wid] = ntt;
+        wcost[wid] = npops + (ntilepts >> 6);
+        tcost[wid] = ntilepts + 16 * ntt;
+    }
+    if (COST && bcost) {   // cost of this wave into its queries' 256-query buckets
+        // the wave's own run time (shader clock / 64; the slices only move work
+        // between ranks, every query's sums are unchanged)
+        const unsigned long long c = ((unsigned long long)(clock64() - t_start) >> 6) + 1;
+        if (cost_lab) {   // by label: an equal share into each query's label bucket
+            if (valid) atomicAdd(&bcost[cost_lab[s] >> 8], (c + 63) >> 6);
+        } else {
+            const int64_t sf = wave_min(valid ? s : ((int64_t)1 << 62));
+            if (lane == 0) atomicAdd(&bcost[sf >> 8], c);
         }
-        sv.tF[gid * 64 + lane] = f;
-        sv.tZ[gid * 64 + lane] = z;
+    }
+    if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
+                             // [4] wave-level tile points, [5] lane child evaluations, [6] wave
+                             // child slots, [7..9] heaviest wave ([1], [2]: tile_apply)
+        const unsigned long long tv = wave_sum(nvis), te = wave_sum(nevals);
+        if (lane == 0) {
+            atomicAdd(visits, tv);
+            atomicAdd(visits + 3, wpops);
+            atomicAdd(visits + 4, wtile);
+            atomicAdd(visits + 5, te);
+            atomicAdd(visits + 6, wslots);
+            atomicMax(visits + 7, wpops + wtile / 16);   // heaviest wave (pops + tile points/16)
+            atomicMax(visits + 8, wpops);
+            atomicMax(visits + 9, wtile);
+            atomicAdd(visits + 13, wfull);
+            atomicAdd(visits + 14, wpart);
+            const unsigned long long w_end = wall_clock64();   // [15] longest wave, [16] ~first start,
+            atomicMax(visits + 15, w_end - w_start);            // [17] last end, [18] sum of wave times
+            atomicMax(visits + 16, ~0ull - w_start);
+            atomicMax(visits + 17, w_end);
+            atomicAdd(visits + 18, w_end - w_start);
+        }
     }
 }
 
-// F, Z of each query += its wave's spilled tasks' sums, in spill order.
-__global__ void wave_spill_combine(SpillView sv, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
-                                   double2 *__restrict__ F, double *__restrict__ Z) {
-    const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= g1) return;
-    const int64_t wid = (k - g0) >> 6, lane = (k - g0) & 63;
-    const int2 sp = sv.wspill[wid];
-    if (sp.y == 0) return;
-    const int64_t s = qlist ? (int64_t)qlist[k] : k;
-    double fx = 0.0, fy = 0.0, z = 0.0;
-    for (int j = 0; j < sp.y; ++j) {
-        const int64_t cg = (int64_t)sp.x + j;   // region 1
-        const double2 g = sv.tF[cg * 64 + lane];
-        fx += g.x;
-        fy += g.y;
-        z += sv.tZ[cg * 64 + lane];
-    }
-    const double2 f = F[s];
-    F[s] = make_double2(f.x + fx, f.y + fy);
-    Z[s] = Z[s] + z;
-}
-
-__global__ void set_i32(int32_t *p, int32_t v) {
-    if (threadIdx.x == 0) *p = v;
-}
-
-// The next traversal's pop budget: fac x the mean wave cost of this one (its
-// spilled tasks' costs included), at least bmin.
-__global__ __launch_bounds__(1024) void spill_budget(const int32_t *__restrict__ wcost, int64_t waves,
-                                                     int32_t *__restrict__ budget, double fac, int32_t bmin) {
-    __shared__ long long part[16];
-    long long s = 0;
-    for (int64_t w = threadIdx.x; w < waves; w += blockDim.x) s += max(wcost[w], 0);
-    s = wave_sum(s);
-    if (lane_id() == 0) part[threadIdx.x >> 6] = s;
+// The heavy groups of the next traversal, from this one's costs (one
+// workgroup): a group's cost is its wave's (pops + tile points / 64), or for a
+// group that ran narrow 2 x its heaviest narrow wave's (hysteresis: the
+// narrow waves each walk a part of the 64-query union).  Heavy: cost >= fac x
+// the mean over all groups (and >= NARROW_MIN); at most hmax of them, listed
+// in group order.  nflag[g] = heavy slot + 1 or 0.
+// Fill mode (hfill > 0: too few 64-query waves to occupy the chip, e.g. one
+// rank's share of the queries): also the hfill most costly groups, whatever
+// the factor -- the threshold is lowered to the cost bucket (4 per doubling,
+// plan_bucket) where the count from the top reaches hfill.
+constexpr int32_t NARROW_MIN = 32;
+__global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcost, int64_t waves,
+                                                      int32_t *__restrict__ nflag, const int32_t *__restrict__ ncost,
+                                                      int32_t *__restrict__ hlist, int32_t *__restrict__ hcount,
+                                                      int64_t hmax, double fac, int64_t hfill) {
+    __shared__ unsigned long long red[16];
+    __shared__ int32_t wtot[16];
+    __shared__ int32_t hist[PLAN_BUCKETS];
+    __shared__ int32_t sbucket;
+    __shared__ double sthr;
+    const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    if (t < PLAN_BUCKETS) hist[t] = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        long long t = 0;
-        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k];
-        const double b = fac * (double)t / (double)max<int64_t>(waves, 1);
-        budget[0] = (int32_t)min(2e9, max((double)bmin, b));
+    unsigned long long acc = 0;
+    for (int64_t g = t; g < waves; g += 1024) {
+        int32_t c = wcost[g];
+        const int32_t f = nflag[g];
+        if (f > 0) {
+            int32_t mx = 0;
+            for (int p = 0; p < NPARTS; ++p) mx = max(mx, ncost[(int64_t)(f - 1) * NPARTS + p]);
+            c = 2 * mx;
+            wcost[g] = c;
+        }
+        acc += (unsigned long long)max(c, 0);
+        if (hfill > 0) atomicAdd(&hist[plan_bucket(c)], 1);
     }
+    acc = wave_sum(acc);
+    if (lane == 0) red[w] = acc;
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long total = 0;
+        for (int j = 0; j < 16; ++j) total += red[j];
+        sthr = fmax((double)NARROW_MIN, fac * (double)total / (double)max<int64_t>(waves, 1));
+        // fill mode: buckets >= sbucket hold at most hfill groups
+        int64_t run = 0;
+        int b = PLAN_BUCKETS;
+        if (hfill > 0)
+            while (b > 1 && run + hist[b - 1] <= hfill) run += hist[--b];
+        sbucket = b;
+    }
+    __syncthreads();
+    const double thr = sthr;
+    const int bmin = sbucket;
+    int32_t base = 0;
+    for (int64_t g0 = 0; g0 < waves; g0 += 1024) {
+        const int64_t g = g0 + t;
+        bool hv = false;
+        if (fac > 0.0 && g < waves) {
+            const int32_t c = wcost[g];
+            hv = c >= NARROW_MIN && ((double)c >= thr || plan_bucket(c) >= bmin);
+        }
+        const uint64_t b = __ballot(hv);
+        if (lane == 0) wtot[w] = (int32_t)__popcll(b);
+        __syncthreads();
+        int32_t off = base, tot = 0;
+        for (int j = 0; j < 16; ++j) {
+            if (j < w) off += wtot[j];
+            tot += wtot[j];
+        }
+        const int32_t slot = off + (int32_t)__popcll(b & lanemask_lt());
+        if (g < waves) {
+            const bool take = hv && slot < hmax;
+            nflag[g] = take ? slot + 1 : 0;
+            if (take) hlist[slot] = (int32_t)g;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (t == 0) *hcount = (int32_t)min<int64_t>(base, hmax);
 }
 
 // The traversal waves' tiles, in recording order: one wave per traversal
@@ -2202,27 +2172,18 @@ __global__ __launch_bounds__(1024) void spill_budget(const int32_t *__restrict__
 // coalesced dwordx4 load per lane, the next chunk prefetched into registers)
 // and read back as wave-uniform broadcasts.  Lanes whose bound holds are
 // counted for the next iteration's moment gate.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void tile_apply(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
-                                                  const double *__restrict__ mom,
-                                                  const TileTask *__restrict__ ttask,
-                                                  const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1,
-                                                  const int32_t *__restrict__ qlist, int xcd_chunk,
-                                                  int32_t *__restrict__ mom_flag,
-                                                  int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
-                                                  double2 *__restrict__ F, double *__restrict__ Z,
-                                                  unsigned long long *__restrict__ visits, int qmajor, int pack,
-                                                  float lw_cost, const int32_t *__restrict__ torder, ChunkView cv) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void tile_apply(
+    const double2 *__restrict__ pos, const BHNode *__restrict__ nodes, const TileTask *__restrict__ ttask,
+    const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
+    int32_t *__restrict__ mom_flag, double mom_tol, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
+    double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits,
+    const int32_t *__restrict__ torder, ChunkView cv) {
     __shared__ double2 tbuf[4][64];
-    __shared__ uint64_t sbm[4][64];
     __shared__ int smark[4][64];
     __shared__ int2 srng[4][64];
-    __shared__ int2 crng[4][LW_CHUNK];          // pack 3: the chunk's small-tile ranges
-    __shared__ uint64_t cmask[4][LW_CHUNK / 64][64];   // pack 3: per window, each lane's tiles (transposed masks)
+    constexpr float LW_COST = 1.6f;   // lane-wise cost per point relative to a sweep slot (gathers, refills)
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const bool pklw = (pack & 4) == 0;   // packed rounds walked lane-wise (pack | 4: the masked sweep)
-    pack &= 3;
-    const int64_t blk = torder ? (int64_t)torder[blockIdx.x]
-                      : xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t blk = torder ? (int64_t)torder[blockIdx.x] : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
     int64_t qw = wid;   // chunks: slot wid = chunk c of C of traversal wave qw's tile list
     int ch = 0, C = 1;
@@ -2260,14 +2221,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     unsigned long long ps_steps[4] = {0, 0, 0, 0}, ps_pairs[4] = {0, 0, 0, 0};
     double2 *buf = tbuf[w];
     const TileTask *mytt = ttask + qw * TILE_CAP;
-    int masked_until = tb;   // pack 2: tiles before this one take the masked sweep
+    int masked_until = tb;   // tiles before this one take the masked sweep
     for (int t = tb; t < nt;) {
         const TileTask tt = mytt[t];
-        if (pack == 3 && tt.last - tt.first + 1 < MOM_MIN_POINTS) {   // small tiles: the lane-wise pass below
-            ++t;
-            continue;
-        }
-        if (pack == 2 && t >= masked_until && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
+        if (t >= masked_until && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
             // Lane-wise window: the run of <= 64 consecutive small tiles
             // starting at t.  Each lane walks only the points of ITS tiles
             // (its bits of the 64 masks, transposed by 64 ballots), gathering
@@ -2301,7 +2258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             }
             // W bit i: tile t + i is one of mine.  Lane-wise costs the busiest
             // lane's points, the masked 64-slot sweep every point: take the
-            // cheaper (lw_cost: lane-wise cost per point relative to a sweep
+            // cheaper (LW_COST: lane-wise cost per point relative to a sweep
             // slot, gathers and refills included), the sweep for the whole window.
             const int cnt_i = b_i - a_i + 1;
             __builtin_amdgcn_wave_barrier();
@@ -2315,7 +2272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 cl += r.y - r.x + 1;
             }
             const int cmax = wave_max(cl), ctot = wave_sum(lane < wn ? cnt_i : 0);
-            if ((float)cmax * lw_cost >= (float)ctot) {
+            if ((float)cmax * LW_COST >= (float)ctot) {
                 masked_until = t + wn;
                 goto masked;
             }
@@ -2353,7 +2310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             continue;
         }
     masked:
-        if (pack && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
+        if (tt.last - tt.first + 1 < MOM_MIN_POINTS) {
             // Packed round: the run of consecutive small tiles (no moments below
             // MOM_MIN_POINTS) whose points fit 64 slots is staged as one batch of
             // (point, tile lane mask) and swept once, each lane taking the points
@@ -2392,51 +2349,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             const uint64_t mk = __shfl(m_i, own, 64);
             __builtin_amdgcn_wave_barrier();
             buf[lane] = lane < total ? pos[fa + lane - st] : make_double2(0.0, 0.0);
-            sbm[w][lane] = lane < total ? mk : 0ull;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_wave_barrier();
             double ux = 0.0, uy = 0.0, uz = 0.0;
             int nmine = 0;
-            if (pklw) {
-                // lane-wise over the staged slots: each lane walks only ITS slots
-                // (the round's 64 slot masks transposed), two at a time, so the
-                // round costs its busiest lane's slots instead of all of them;
-                // a lane's order is still slot order (the same sums as the sweep)
-                uint64_t M = lane < total ? mk : 0ull;
+            // lane-wise over the staged slots: each lane walks only ITS slots
+            // (the round's 64 slot masks transposed), two at a time, so the
+            // round costs its busiest lane's slots instead of all of them;
+            // a lane's order is still slot order (the same sums as the sweep)
+            uint64_t M = lane < total ? mk : 0ull;
 #pragma unroll
-                for (int st2 = 0; st2 < 6; ++st2) {
-                    const int j = 32 >> st2;
-                    const uint64_t lo = st2 == 0 ? 0x00000000FFFFFFFFull : st2 == 1 ? 0x0000FFFF0000FFFFull
-                                      : st2 == 2 ? 0x00FF00FF00FF00FFull : st2 == 3 ? 0x0F0F0F0F0F0F0F0Full
-                                      : st2 == 4 ? 0x3333333333333333ull : 0x5555555555555555ull;
-                    const uint32_t ylo = __shfl_xor((uint32_t)M, j, 64), yhi = __shfl_xor((uint32_t)(M >> 32), j, 64);
-                    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
-                    M = (lane & j) ? ((M & ~lo) | ((y & ~lo) >> j)) : ((M & lo) | ((y & lo) << j));
+            for (int st2 = 0; st2 < 6; ++st2) {
+                const int j = 32 >> st2;
+                const uint64_t lo = st2 == 0 ? 0x00000000FFFFFFFFull : st2 == 1 ? 0x0000FFFF0000FFFFull
+                                  : st2 == 2 ? 0x00FF00FF00FF00FFull : st2 == 3 ? 0x0F0F0F0F0F0F0F0Full
+                                  : st2 == 4 ? 0x3333333333333333ull : 0x5555555555555555ull;
+                const uint32_t ylo = __shfl_xor((uint32_t)M, j, 64), yhi = __shfl_xor((uint32_t)(M >> 32), j, 64);
+                const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+                M = (lane & j) ? ((M & ~lo) | ((y & ~lo) >> j)) : ((M & lo) | ((y & lo) << j));
+            }
+            while (__ballot(M != 0ull)) {
+                if (M) {
+                    const int j0 = __ffsll((long long)M) - 1;
+                    M &= M - 1;
+                    const int j1 = M ? __ffsll((long long)M) - 1 : -1;
+                    if (M) M &= M - 1;
+                    const double2 p0 = buf[j0];
+                    const double2 p1 = buf[j1 < 0 ? j0 : j1];
+                    pair_force(qx, qy, p0.x, p0.y, ux, uy, uz);
+                    if (j1 >= 0) pair_force(qx, qy, p1.x, p1.y, ux, uy, uz);
+                    if (visits) nmine += j1 >= 0 ? 2 : 1;
                 }
-                while (__ballot(M != 0ull)) {
-                    if (M) {
-                        const int j0 = __ffsll((long long)M) - 1;
-                        M &= M - 1;
-                        const int j1 = M ? __ffsll((long long)M) - 1 : -1;
-                        if (M) M &= M - 1;
-                        const double2 p0 = buf[j0];
-                        const double2 p1 = buf[j1 < 0 ? j0 : j1];
-                        pair_force(qx, qy, p0.x, p0.y, ux, uy, uz);
-                        if (j1 >= 0) pair_force(qx, qy, p1.x, p1.y, ux, uy, uz);
-                        if (visits) nmine += j1 >= 0 ? 2 : 1;
-                    }
-                    if (visits) ps_steps[1] += 2;
-                }
-            } else {
-                for (int j = 0; j < total; ++j) {
-                    const double2 pp = buf[j];
-                    if ((sbm[w][j] >> lane) & 1ull) {
-                        pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
-                        ++nmine;
-                    }
-                }
-                if (visits) ps_steps[1] += (unsigned long long)total;
+                if (visits) ps_steps[1] += 2;
             }
             __builtin_amdgcn_wave_barrier();
             fx += ux; fy += uy; zs += uz;
@@ -2456,7 +2401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
         bool usem = false;
         if (mine && cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
             const BHNode &nd = nodes[ref];
-            if (moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy)) {
+            if (moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy, mom_tol)) {
                 ++nwant;
                 if (mom_on) {
                     usem = true;
@@ -2472,7 +2417,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             if (dm) wt_dense_pts += (unsigned long long)cnt_t;
             if (cnt >= MOM_MIN_POINTS && (tt.mask != 0)) ++wt_momchk;
         }
-        if (dm && qmajor && kq * ((cnt_t + 63) / 64 + 6) < cnt_t) {
+        if (dm && kq * ((cnt_t + 63) / 64 + 6) < cnt_t) {
             // Few lanes, many points: query-major.  For each dense lane j in
             // turn, all 64 lanes split the tile's points and a butterfly sum
             // (fixed order: deterministic) hands lane j its total -- kq passes
@@ -2532,100 +2477,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 if (dense) ps_pairs[3] += (unsigned long long)(b - a + 1);
             }
         }
-    }
-    if (pack == 3) {
-        // Small tiles (< MOM_MIN_POINTS points, always dense), lane-wise: in
-        // chunks of LW_CHUNK tiles each lane walks the points of ITS tiles (its
-        // bits of the masks, transposed 64 tiles at a time) in tile order, so a
-        // chunk costs its busiest lane's points and the lanes' imbalance
-        // averages over the whole chunk.  The walk keeps LW_D point loads in
-        // flight (a rotating register pipeline), so the gathers' latency hides
-        // behind the pair terms; the order per lane is fixed (tile, then point).
-        double ux = 0.0, uy = 0.0, uz = 0.0;
-        int nmine = 0;
-        for (int c0 = tb; c0 < nt; c0 += LW_CHUNK) {
-            const int c1 = min(nt, c0 + LW_CHUNK);
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll 1
-            for (int k = 0; k < LW_CHUNK / 64; ++k) {
-                const int ti = c0 + k * 64 + lane;
-                uint64_t m_i = 0;
-                int2 r = make_int2(0, -1);
-                if (ti < c1) {
-                    const TileTask h = mytt[ti];
-                    if (h.last - h.first + 1 < MOM_MIN_POINTS) { m_i = h.mask; r = make_int2(h.first, h.last); }
-                }
-                crng[w][k * 64 + lane] = r;
-                uint64_t W = m_i;   // 64 x 64 bit transpose, as the pack-2 windows
-#pragma unroll
-                for (int st = 0; st < 6; ++st) {
-                    const int j = 32 >> st;
-                    const uint64_t lo = st == 0 ? 0x00000000FFFFFFFFull : st == 1 ? 0x0000FFFF0000FFFFull
-                                      : st == 2 ? 0x00FF00FF00FF00FFull : st == 3 ? 0x0F0F0F0F0F0F0F0Full
-                                      : st == 4 ? 0x3333333333333333ull : 0x5555555555555555ull;
-                    const uint32_t ylo = __shfl_xor((uint32_t)W, j, 64), yhi = __shfl_xor((uint32_t)(W >> 32), j, 64);
-                    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
-                    W = (lane & j) ? ((W & ~lo) | ((y & ~lo) >> j)) : ((W & lo) | ((y & lo) << j));
-                }
-                cmask[w][k][lane] = W;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
-            const int nwin = (c1 - c0 + 63) / 64;
-            int kw = 0, p = 0, last = -1;
-            uint64_t Wc = cmask[w][0][lane];
-            // the range after the current one, fetched ahead (np > nlast: none left)
-            auto fetch_next = [&](int &np, int &nl) {
-                while (Wc == 0 && kw + 1 < nwin) Wc = cmask[w][++kw][lane];
-                if (Wc == 0) { np = 1; nl = 0; return; }
-                const int i = __ffsll((long long)Wc) - 1;
-                Wc &= Wc - 1;
-                const int2 r = crng[w][kw * 64 + i];
-                np = r.x;
-                nl = r.y;
-            };
-            int np, nl;
-            fetch_next(np, nl);
-            // the next point of this lane's walk, -1 at its end
-            auto advance = [&]() -> int {
-                if (p < last) return ++p;
-                if (np > nl) return -1;
-                p = np;
-                last = nl;
-                fetch_next(np, nl);
-                return p;
-            };
-            double2 v[LW_D];
-            bool o[LW_D];
-            int c = advance();
-#pragma unroll
-            for (int k = 0; k < LW_D; ++k) {
-                o[k] = c >= 0;
-                v[k] = make_double2(0.0, 0.0);
-                if (o[k]) { v[k] = pos[c]; c = advance(); }
-            }
-            while (true) {
-                bool any = false;
-#pragma unroll
-                for (int k = 0; k < LW_D; ++k) any = any || o[k];
-                if (__ballot(any) == 0) break;
-                if (visits) ps_steps[0] += LW_D;
-#pragma unroll
-                for (int k = 0; k < LW_D; ++k) {
-                    if (o[k]) {
-                        pair_force(qx, qy, v[k].x, v[k].y, ux, uy, uz);
-                        ++nmine;
-                    }
-                    o[k] = c >= 0;
-                    if (o[k]) { v[k] = pos[c]; c = advance(); }
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        fx += ux; fy += uy; zs += uz;
-        ndense += (unsigned long long)nmine;
-        if (visits) ps_pairs[0] += (unsigned long long)nmine;
     }
     if (valid && cv.slot_w) {
         mtask_n[e] = ntask;
@@ -2805,7 +2656,7 @@ __global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict_
                                                       const double *__restrict__ coef, const int32_t *__restrict__ meta,
                                                       int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
                                                       double2 *__restrict__ F, double *__restrict__ Z,
-                                                      unsigned long long *__restrict__ visits) {
+                                                      unsigned long long *__restrict__ visits, double mom_tol) {
     const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool valid = k < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : 0;
@@ -2815,7 +2666,7 @@ __global__ __launch_bounds__(256) void root_tile_eval(const double2 *__restrict_
     double fx = 0.0, fy = 0.0, zs = 0.0;
     if (valid) {
         const double2 q = pos[s];
-        usem = moment_ok(rt.bx0, rt.bx1, rt.by0, rt.by1, q.x, q.y);
+        usem = moment_ok(rt.bx0, rt.bx1, rt.by0, rt.by1, q.x, q.y, mom_tol);
         if (usem) {
             double cx, cy, R;
             box_centre(rt, cx, cy, R);
@@ -2858,24 +2709,26 @@ __global__ void block_cost_keys(const int32_t *__restrict__ cost, int64_t nwaves
     val[b] = (int32_t)b;
 }
 
-}  // namespace
-
-// Longest-first order of nblocks blocks by the per-wave costs -> order.
-// The Morton sort (64-bit keys, int32 payload).  rocPRIM's radix sort picks
-// its merge sort below 2^20 items (22 launches, ~200 us at 1M);
-// TSNE_SORT=onesweep forces Onesweep (merge_sort_limit = 0: 8 scatter passes
-// of ~24 us plus two lookback-state fills each, ~300 us at 1M, measured).
-using onesweep_cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                rocprim::default_config, 0>;
-static void morton_sort(void *tmp, size_t &bytes, const uint64_t *k_in, uint64_t *k_out, const int32_t *v_in,
-                        int32_t *v_out, int64_t n, hipStream_t st) {
-    static const bool merge = [] { const char *e = getenv("TSNE_SORT"); return !(e && std::string(e) == "onesweep"); }();
-    if (merge)
-        TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, k_in, k_out, v_in, v_out, (int)n, 0, 64, st));
-    else
-        TSNE_HIP(rocprim::radix_sort_pairs<onesweep_cfg>(tmp, bytes, k_in, k_out, v_in, v_out, (size_t)n, 0, 64, st));
+// Heavy groups a traversal of `waves` 64-query waves turns narrow to fill the
+// chip: narrowing h groups adds (NPARTS - 1) h waves; up to 8 waves per SIMD
+// (32 per CU) in all.  0 once the 64-query waves alone fill it (one rank of
+// 1M points: 15,625 waves).
+int64_t narrow_fill(const tsne_ctx *ctx, int64_t waves) {
+    const int64_t cap = 32 * (int64_t)ctx->cu_count;
+    return waves >= cap ? 0 : (cap - waves) / (NPARTS - 1);
 }
 
+}  // namespace
+
+// The Morton sort (64-bit keys, int32 payload).  rocPRIM's radix sort picks
+// its merge sort below 2^20 items (22 launches, ~200 us at 1M; Onesweep
+// measured ~300 us at 1M).
+static void morton_sort(void *tmp, size_t &bytes, const uint64_t *k_in, uint64_t *k_out, const int32_t *v_in,
+                        int32_t *v_out, int64_t n, hipStream_t st) {
+    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, k_in, k_out, v_in, v_out, (int)n, 0, 64, st));
+}
+
+// Longest-first order of nblocks blocks by the per-wave costs -> order.
 static void block_order(tsne_ctx *ctx, BHTree &t, const int32_t *cost, int64_t nwaves, int64_t nblocks,
                         int32_t *order) {
     hipStream_t st = ctx->stream;
@@ -2886,134 +2739,135 @@ static void block_order(tsne_ctx *ctx, BHTree &t, const int32_t *cost, int64_t n
                                                           (int)nblocks, 0, 32, st));
 }
 
-void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n) {
+void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
     Workspace &ws = ctx->ws;
-    if (const char *e = getenv("TSNE_MOM_TOL")) {
-        const double v = atof(e);
-        TSNE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mom_tol), &v, sizeof(double)));
-    }
     t.n = n;
-    t.keys = ws.get<uint64_t>("bh.keys", n);
-    t.keys_sorted = ws.get<uint64_t>("bh.keys_sorted", n);
-    t.idx = ws.get<int32_t>("bh.idx", n);
-    t.idx_sorted = ws.get<int32_t>("bh.idx_sorted", n);
-    t.inv = ws.get<int32_t>("bh.inv", n);
-    t.dupc = ws.get<int32_t>("bh.dupc", n);
-    t.vid = ws.get<int32_t>("bh.vid", n);
-    t.dflag = ws.get<int32_t>("bh.dflag", 1);
-    t.rmin = ws.get<int32_t>("bh.rmin", n);
-    t.rvid = ws.get<int32_t>("bh.rvid", n);
-    t.rt2 = ws.get<int32_t>("bh.rt2", n);
-    t.arrive2 = ws.get<int32_t>("bh.arrive2", n);
-    t.cntcorr = ws.get<int32_t>("bh.cntcorr", n);
-    t.tiecnt = ws.get<int32_t>("bh.tiecnt", n);
-    t.notile = ws.get<int32_t>("bh.notile", n);
-    t.sumcorr = ws.get<double>("bh.sumcorr", 2 * (size_t)n);
-    t.vflag = ws.get<int32_t>("bh.vflag", n);
-    t.vcnt = ws.get<int32_t>("bh.vcnt", n);
-    t.vcntf = ws.get<int32_t>("bh.vcntf", n);
-    t.vsum = ws.get<double>("bh.vsum", 2 * (size_t)n);
-    t.vcom = ws.get<double>("bh.vcom", 2 * (size_t)n);
-    t.pos = ws.get<double2>("bh.pos", n);
-    t.nodes = ws.get<BHNode>("bh.nodes", n);
-    t.qrec = ws.get<QRec>("bh.qrec", 2 * (size_t)n);   // [n, 2n): virtual chain-top records (duplicates)
-    t.agg = ws.get<double>("bh.agg", AGG * (size_t)n);
-    t.parent_leaf = ws.get<int32_t>("bh.parent_leaf", n);
-    t.parent_node = ws.get<int32_t>("bh.parent_node", n);
-    t.arrive = ws.get<int32_t>("bh.arrive", n);
-    t.fstart = ws.get<int32_t>("bh.fstart", n);
+    t.keys = ws.get<uint64_t>(pre + "keys", n);
+    t.keys_sorted = ws.get<uint64_t>(pre + "keys_sorted", n);
+    t.idx = ws.get<int32_t>(pre + "idx", n);
+    t.idx_sorted = ws.get<int32_t>(pre + "idx_sorted", n);
+    t.inv = ws.get<int32_t>(pre + "inv", n);
+    t.dupc = ws.get<int32_t>(pre + "dupc", n);
+    t.vid = ws.get<int32_t>(pre + "vid", n);
+    t.dflag = ws.get<int32_t>(pre + "dflag", 1);
+    t.rmin = ws.get<int32_t>(pre + "rmin", n);
+    t.rvid = ws.get<int32_t>(pre + "rvid", n);
+    t.rt2 = ws.get<int32_t>(pre + "rt2", n);
+    t.arrive2 = ws.get<int32_t>(pre + "arrive2", n);
+    t.cntcorr = ws.get<int32_t>(pre + "cntcorr", n);
+    t.tiecnt = ws.get<int32_t>(pre + "tiecnt", n);
+    t.notile = ws.get<int32_t>(pre + "notile", n);
+    t.sumcorr = ws.get<double>(pre + "sumcorr", 2 * (size_t)n);
+    t.vflag = ws.get<int32_t>(pre + "vflag", n);
+    t.vcnt = ws.get<int32_t>(pre + "vcnt", n);
+    t.vcntf = ws.get<int32_t>(pre + "vcntf", n);
+    t.vsum = ws.get<double>(pre + "vsum", 2 * (size_t)n);
+    t.vcom = ws.get<double>(pre + "vcom", 2 * (size_t)n);
+    t.pos = ws.get<double2>(pre + "pos", n);
+    t.nodes = ws.get<BHNode>(pre + "nodes", n);
+    t.qrec = ws.get<QRec>(pre + "qrec", 2 * (size_t)n);   // [n, 2n): virtual chain-top records (duplicates)
+    t.agg = ws.get<double>(pre + "agg", AGG * (size_t)n);
+    t.parent_leaf = ws.get<int32_t>(pre + "parent_leaf", n);
+    t.parent_node = ws.get<int32_t>(pre + "parent_node", n);
+    t.arrive = ws.get<int32_t>(pre + "arrive", n);
+    t.fstart = ws.get<int32_t>(pre + "fstart", n);
     TSNE_HIP(hipMemsetAsync(t.fstart, 0, sizeof(int32_t) * n, ctx->stream));
     t.gen = 0;
     t.rt_skip = 0;
-    t.top_list = ws.get<int32_t>("bh.top_list", 2 * (size_t)n);
-    t.top_cnt = ws.get<int32_t>("bh.top_cnt", 1);
-    t.qhead = ws.get<int32_t>("bh.qhead", 8);
-    t.meta = ws.get<int32_t>("bh.meta", 4);
-    t.mom = ws.get<double>("bh.mom", (size_t)n * MOM_K);
-    t.mom_cnt = ws.get<int32_t>("bh.mom_cnt", n + 1);
-    t.mom_off = ws.get<int32_t>("bh.mom_off", n + 1);
-    t.mom_list = ws.get<int32_t>("bh.mom_list", n);
+    t.top_list = ws.get<int32_t>(pre + "top_list", 2 * (size_t)n);
+    t.top_cnt = ws.get<int32_t>(pre + "top_cnt", 1);
+    t.meta = ws.get<int32_t>(pre + "meta", 4);
+    t.mom = ws.get<double>(pre + "mom", (size_t)n * MOM_K);
+    t.mom_cnt = ws.get<int32_t>(pre + "mom_cnt", n + 1);
+    t.mom_off = ws.get<int32_t>(pre + "mom_off", n + 1);
+    t.mom_list = ws.get<int32_t>(pre + "mom_list", n);
     // items <= sum over moment nodes of (cnt / MOM_CHUNK + 1); every point lies in
     // at most 94 nested nodes (62 key bits + 32 tie-break bits)
     t.mom_items_cap = n + ceil_div(n * 94, MOM_CHUNK);
-    t.mom_item = ws.get<int32_t>("bh.mom_item", t.mom_items_cap);
-    t.mom_part = ws.get<double>("bh.mom_part", (size_t)t.mom_items_cap * MOM_K);
-    t.mom_flag = ws.get<int32_t>("bh.mom_flag", 3);
+    t.mom_item = ws.get<int32_t>(pre + "mom_item", t.mom_items_cap);
+    t.mom_part = ws.get<double>(pre + "mom_part", (size_t)t.mom_items_cap * MOM_K);
+    t.mom_flag = ws.get<int32_t>(pre + "mom_flag", 3);
     const int32_t flag_init[3] = {1, INT32_MAX, (int32_t)std::min<int64_t>(INT32_MAX, (n >> 6) + 1)};   // first build: moments on
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, flag_init, sizeof(flag_init), hipMemcpyHostToDevice, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     // tile_apply slots: traversal waves + at most half as many extra chunks (+ margin)
     const int64_t qwaves = ceil_div(n, 64) + 4;
     t.tile_waves = qwaves + qwaves / 2 + 64;
-    t.mtask = ws.get<int32_t>("bh.mtask", (size_t)std::max<int64_t>(n, t.tile_waves * 64) * MOM_TASKS);
-    t.mtask_n = ws.get<int32_t>("bh.mtask_n", std::max<int64_t>(n, t.tile_waves * 64));
-    t.ttask = ws.get<TileTask>("bh.ttask", (size_t)t.tile_waves * TILE_CAP);
-    t.ttask_n = ws.get<int32_t>("bh.ttask_n", t.tile_waves);
+    t.mtask = ws.get<int32_t>(pre + "mtask", (size_t)std::max<int64_t>(n, t.tile_waves * 64) * MOM_TASKS);
+    t.mtask_n = ws.get<int32_t>(pre + "mtask_n", std::max<int64_t>(n, t.tile_waves * 64));
+    t.ttask = ws.get<TileTask>(pre + "ttask", (size_t)t.tile_waves * TILE_CAP);
+    t.ttask_n = ws.get<int32_t>(pre + "ttask_n", t.tile_waves);
     size_t sb = 0;
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, t.mom_cnt, t.mom_off, (int)(n + 1), ctx->stream));
     t.scan_tmp_bytes = sb;
-    t.scan_tmp = ws.get<uint8_t>("bh.scan_tmp", sb);
+    t.scan_tmp = ws.get<uint8_t>(pre + "scan_tmp", sb);
     t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
-    t.bbox_part = ws.get<double>("bh.bbox_part", 4 * (size_t)t.bbox_blocks);
-    t.W = ws.get<double>("bh.W", 1);
-    t.bb = ws.get<double>("bh.bb", 4);
-    t.status = ws.get<int32_t>("bh.status", 4);
+    t.bbox_part = ws.get<double>(pre + "bbox_part", 4 * (size_t)t.bbox_blocks);
+    t.W = ws.get<double>(pre + "W", 1);
+    t.bb = ws.get<double>(pre + "bb", 4);
+    t.status = ws.get<int32_t>(pre + "status", 4);
     t.status_h = ctx->pinned;
-    t.rcoef = ws.get<double>("bh.rcoef", POLY_K);
+    t.rcoef = ws.get<double>(pre + "rcoef", POLY_K);
     t.dup_mask = ((uint64_t)1 << (64 - __builtin_clzll((uint64_t)std::max<int64_t>(2, 4 * n) - 1))) - 1;
-    t.dup_tab = ws.get<int32_t>("bh.dup_tab", t.dup_mask + 1);
-    t.dup_open = ws.get<uint8_t>("bh.dup_open", n);
+    t.dup_tab = ws.get<int32_t>(pre + "dup_tab", t.dup_mask + 1);
+    t.dup_open = ws.get<uint8_t>(pre + "dup_open", n);
     size_t tb = 0;
     morton_sort(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, n, ctx->stream);
     t.sort_tmp_bytes = tb;
-    t.sort_tmp = ws.get<uint8_t>("bh.sort_tmp", tb);
+    t.sort_tmp = ws.get<uint8_t>(pre + "sort_tmp", tb);
     const int64_t nb = ceil_div(t.tile_waves, 4);
-    t.wcost = ws.get<int32_t>("bh.wcost", t.tile_waves);
-    t.tcost = ws.get<int32_t>("bh.tcost", t.tile_waves);
-    t.okey = ws.get<int32_t>("bh.okey", nb);
-    t.okey2 = ws.get<int32_t>("bh.okey2", nb);
-    t.oval = ws.get<int32_t>("bh.oval", nb);
-    t.border = ws.get<int32_t>("bh.border", nb);
-    t.torder = ws.get<int32_t>("bh.torder", nb);
+    t.wcost = ws.get<int32_t>(pre + "wcost", t.tile_waves);
+    t.tcost = ws.get<int32_t>(pre + "tcost", t.tile_waves);
+    t.okey = ws.get<int32_t>(pre + "okey", nb);
+    t.okey2 = ws.get<int32_t>(pre + "okey2", nb);
+    t.oval = ws.get<int32_t>(pre + "oval", nb);
+    t.border = ws.get<int32_t>(pre + "border", nb);
+    t.torder = ws.get<int32_t>(pre + "torder", nb);
     size_t ob = 0;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, ob, t.okey, t.okey2, t.oval, t.border, (int)nb, 0,
                                                           32, ctx->stream));
     t.osort_tmp_bytes = ob;
-    t.osort_tmp = ws.get<uint8_t>("bh.osort_tmp", ob);
+    t.osort_tmp = ws.get<uint8_t>(pre + "osort_tmp", ob);
     t.have_cost = false;
-    t.ch_C = ws.get<int32_t>("bh.ch_C", qwaves + 1);
-    t.ch_slot0 = ws.get<int32_t>("bh.ch_slot0", qwaves + 1);
-    t.ch_slot_w = ws.get<int32_t>("bh.ch_slot_w", t.tile_waves);
-    t.ch_slot_c = ws.get<int32_t>("bh.ch_slot_c", t.tile_waves);
-    t.ch_scost = ws.get<int32_t>("bh.ch_scost", t.tile_waves);
-    t.ch_nslots = ws.get<int32_t>("bh.ch_nslots", 1);
-    t.ch_total = ws.get<unsigned long long>("bh.ch_total", 1);
-    t.ch_Fp = ws.get<double2>("bh.ch_Fp", (size_t)t.tile_waves * 64);
-    t.ch_Zp = ws.get<double>("bh.ch_Zp", (size_t)t.tile_waves * 64);
+    t.ch_C = ws.get<int32_t>(pre + "ch_C", qwaves + 1);
+    t.ch_slot0 = ws.get<int32_t>(pre + "ch_slot0", qwaves + 1);
+    t.ch_slot_w = ws.get<int32_t>(pre + "ch_slot_w", t.tile_waves);
+    t.ch_slot_c = ws.get<int32_t>(pre + "ch_slot_c", t.tile_waves);
+    t.ch_scost = ws.get<int32_t>(pre + "ch_scost", t.tile_waves);
+    t.ch_nslots = ws.get<int32_t>(pre + "ch_nslots", 1);
+    t.ch_total = ws.get<unsigned long long>(pre + "ch_total", 1);
+    t.ch_Fp = ws.get<double2>(pre + "ch_Fp", (size_t)t.tile_waves * 64);
+    t.ch_Zp = ws.get<double>(pre + "ch_Zp", (size_t)t.tile_waves * 64);
     size_t cb = 0;
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, cb, t.ch_C, t.ch_slot0, (int)(qwaves + 1), ctx->stream));
     t.ch_scan_bytes = cb;
-    t.ch_scan_tmp = ws.get<uint8_t>("bh.ch_scan_tmp", cb);
-    // spill tasks: per region up to n / 16 tasks (>= 4096) and 4 entries per task
-    SpillView &sv = t.spill;
-    sv.task_cap = (int32_t)std::max<int64_t>(4096, std::min<int64_t>(1 << 22, ceil_div(n, 16)));
-    sv.ent_cap = 4 * sv.task_cap;
-    sv.task = ws.get<BHTask>("bh.sp_task", (size_t)SPILL_PASSES * sv.task_cap);
-    sv.tent_ref = ws.get<int32_t>("bh.sp_eref", (size_t)SPILL_PASSES * sv.ent_cap);
-    sv.tent_mask = ws.get<uint64_t>("bh.sp_emask", (size_t)SPILL_PASSES * sv.ent_cap);
-    sv.cnt = ws.get<int32_t>("bh.sp_cnt", 2 * (SPILL_PASSES + 1));
-    sv.wspill = ws.get<int2>("bh.sp_wave", t.tile_waves);
-    sv.tF = ws.get<double2>("bh.sp_F", (size_t)SPILL_PASSES * sv.task_cap * 64);
-    sv.tZ = ws.get<double>("bh.sp_Z", (size_t)SPILL_PASSES * sv.task_cap * 64);
-    sv.budget = ws.get<int32_t>("bh.sp_budget", 2);
-    sv.nwaves = t.tile_waves;
-    const int64_t nsrc = t.tile_waves + (int64_t)SPILL_PASSES * sv.task_cap;
-    sv.save_ref = ws.get<int32_t>("bh.sp_sref", (size_t)nsrc * STACK);
-    sv.save_mask = ws.get<uint64_t>("bh.sp_smask", (size_t)nsrc * STACK);
-    sv.ovf = ws.get<int2>("bh.sp_ovf", (size_t)nsrc);
-    const int32_t no_budget[2] = {INT32_MAX, 0};   // the first traversal: no spill (no wave costs yet)
-    TSNE_HIP(hipMemcpyAsync(sv.budget, no_budget, sizeof(no_budget), hipMemcpyHostToDevice, ctx->stream));
+    t.ch_scan_tmp = ws.get<uint8_t>(pre + "ch_scan_tmp", cb);
+    // narrow layout of heavy groups: at most 1/8 of the groups, their moment lists
+    t.nar_hmax = std::max<int64_t>({(int64_t)1, ceil_div(qwaves, 8), std::min<int64_t>(qwaves, narrow_fill(ctx, 0))});
+    t.nflag = ws.get<int32_t>(pre + "nflag", t.tile_waves);
+    TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * t.tile_waves, ctx->stream));
+    t.hlist = ws.get<int32_t>(pre + "hlist", t.nar_hmax);
+    t.hcount = ws.get<int32_t>(pre + "hcount", 1);
+    TSNE_HIP(hipMemsetAsync(t.hcount, 0, sizeof(int32_t), ctx->stream));
+    t.ncost = ws.get<int32_t>(pre + "ncost", (size_t)t.nar_hmax * NPARTS);
+    t.nmtask = ws.get<int32_t>(pre + "nmtask", (size_t)t.nar_hmax * 64 * MOM_TASKS);
+    t.nmtask_n = ws.get<int32_t>(pre + "nmtask_n", (size_t)t.nar_hmax * 64);
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t) {
+    if (!t.nflag_set || !t.hcount) return 0;
+    int32_t h = 0;
+    TSNE_HIP(hipMemcpyAsync(&h, t.hcount, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    return h;
+}
+
+BHTree &bh_single_tree(tsne_ctx *ctx, int64_t n) {
+    if (!ctx->single_tree) ctx->single_tree = new BHTree();
+    BHTree &t = *ctx->single_tree;
+    if (t.n != n) bh_alloc(ctx, t, n, "bh1.");
+    return t;
 }
 
 // Cost-balanced query slices for the next iteration: one 1024-thread block
@@ -3063,13 +2917,9 @@ void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int w
     TSNE_LAUNCH_CHECK();
 }
 
-// The near-exact tolerances (TSNE_BH_NEAR_TOL_EARLY / TSNE_BH_NEAR_TOL: experiment
-// overrides of BH_NEAR_TOL / BH_NEAR_TOL_LATE; 0 disables the test)
-double bh_near_tol(bool late) {
-    static const double early = [] { const char *e = getenv("TSNE_BH_NEAR_TOL_EARLY"); return e ? atof(e) : BH_NEAR_TOL; }();
-    static const double lt = [] { const char *e = getenv("TSNE_BH_NEAR_TOL"); return e ? atof(e) : BH_NEAR_TOL_LATE; }();
-    return late ? lt : early;
-}
+// The near-exact tolerance of a build (Options::near_tol_early / near_tol_late;
+// 0 disables the test)
+double bh_near_tol(const tsne_ctx *ctx, bool late) { return late ? ctx->opts.near_tol_late : ctx->opts.near_tol_early; }
 
 // Largest D for which 48 theta^2 D^2 (1 + 8 D) <= tol (see bh_traverse).
 double bh_near_dmax(double theta, double tol) {
@@ -3082,7 +2932,7 @@ double bh_near_dmax(double theta, double tol) {
 
 void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap, bool root_tile_ok,
               double near_tol) {
-    if (near_tol < 0.0) near_tol = bh_near_tol(false);
+    if (near_tol < 0.0) near_tol = bh_near_tol(ctx, false);
     t.near_dmax = bh_near_dmax(theta, near_tol);
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
@@ -3110,8 +2960,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
         TSNE_HIP(hipStreamSynchronize(st));
         if (!t.status_h[0]) {
             root_tile_ok = false;
-            static const bool noskip = getenv("TSNE_RT_NOSKIP") != nullptr;
-            if (!noskip && t.status_h[1] >= 3) t.rt_skip = std::min(64, 4 * (t.status_h[1] - 2));
+            if (t.status_h[1] >= 3) t.rt_skip = std::min(64, 4 * (t.status_h[1] - 2));
         }
     }
     if (root_tile_ok) {
@@ -3150,26 +2999,17 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
     hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc, t.vid,
                        t.dflag);
-    // TSNE_BU=old: the one-launch bottom-up (every level above a 1024-leaf
-    // block through the cross-workgroup hand-off)
-    static const bool bu_old = [] { const char *e = getenv("TSNE_BU"); return e && std::string(e) == "old"; }();
     if (++t.gen <= 0) {   // wrapped: clear the marks once
         TSNE_HIP(hipMemsetAsync(t.fstart, 0, sizeof(int32_t) * n, st));
         t.gen = 1;
     }
     hipLaunchKernelGGL(karras_build, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.keys_sorted, n, t.meta,
-                       t.nodes, t.parent_leaf, t.parent_node, t.arrive, t.arrive2, bu_old ? nullptr : t.fstart, t.gen,
-                       t.top_cnt);
+                       t.nodes, t.parent_leaf, t.parent_node, t.arrive, t.arrive2, t.fstart, t.gen, t.top_cnt);
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
-    if (bu_old) {
-        hipLaunchKernelGGL(bottom_up<1024>, dim3(ceil_div(n, 1024)), dim3(1024), 0, st, t.pos, t.meta, t.W, inv_theta,
-                           t.nodes, t.agg, t.parent_leaf, t.parent_node, t.arrive);
-    } else {
-        hipLaunchKernelGGL(bottom_up_intra, dim3(ceil_div(n, BU_NB)), dim3(BU_NB), 0, st, t.pos, t.meta, t.W, inv_theta,
-                           t.nodes, t.agg, t.parent_leaf, t.parent_node, t.fstart, t.gen, t.top_list, t.top_cnt);
-        hipLaunchKernelGGL(bottom_up_top, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.meta, t.W,
-                           inv_theta, t.nodes, t.agg, t.parent_node, t.arrive, t.top_list, t.top_cnt);
-    }
+    hipLaunchKernelGGL(bottom_up_intra, dim3(ceil_div(n, BU_NB)), dim3(BU_NB), 0, st, t.pos, t.meta, t.W, inv_theta,
+                       t.nodes, t.agg, t.parent_leaf, t.parent_node, t.fstart, t.gen, t.top_list, t.top_cnt);
+    hipLaunchKernelGGL(bottom_up_top, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.meta, t.W,
+                       inv_theta, t.nodes, t.agg, t.parent_node, t.arrive, t.top_list, t.top_cnt);
     // exact duplicates: the reference's multiplicities (each kernel returns
     // at once unless dup_count saw a duplicate)
     hipLaunchKernelGGL(dup_bottom_up, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.meta, t.dflag, t.idx_sorted, rowmap,
@@ -3187,13 +3027,8 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 1024)), dim3(1024), 0, st, t.nodes, n, t.meta, t.mom_flag,
                        t.mom_cnt, t.mom_list, t.meta, t.mom_off, t.mom_item);
     const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
-    static const bool ldsred = [] { const char *e = getenv("TSNE_MOMRED"); return !(e && std::string(e) == "shuffle"); }();
-    if (ldsred)
-        hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n,
-                           t.mom_item, t.mom_part);
-    else
-        hipLaunchKernelGGL(moment_items<false>, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n,
-                           t.mom_item, t.mom_part);
+    hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n, t.mom_item,
+                       t.mom_part);
     hipLaunchKernelGGL(moment_reduce, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
                        t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
@@ -3203,108 +3038,65 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist,
                   unsigned long long *bcost, bool cost_by_label) {
     if (s1 <= s0) return;
+    hipStream_t st = ctx->stream;
+    const double mom_tol = ctx->opts.mom_tol;
     if (t.root_tile) {
         if (visits)
-            hipLaunchKernelGGL(root_tile_eval<true>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream,
-                               t.root_pos, t.nodes, t.rcoef, t.meta, s0, s1, qlist, dF, dz, visits);
+            hipLaunchKernelGGL(root_tile_eval<true>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.root_pos,
+                               t.nodes, t.rcoef, t.meta, s0, s1, qlist, dF, dz, visits, mom_tol);
         else
-            hipLaunchKernelGGL(root_tile_eval<false>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream,
-                               t.root_pos, t.nodes, t.rcoef, t.meta, s0, s1, qlist, dF, dz, visits);
+            hipLaunchKernelGGL(root_tile_eval<false>, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.root_pos,
+                               t.nodes, t.rcoef, t.meta, s0, s1, qlist, dF, dz, visits, mom_tol);
         TSNE_LAUNCH_CHECK();
         return;
     }
-    const double near_dmax = t.near_dmax;
-    // variant: records per batch (TSNE_BH_KPOP = 1/4/8) and XCD block order (TSNE_BH_XCD = run
-    // length C in blocks of chunked XCD placement, 0 = dispatcher round-robin)
-    static const int kp = [] { const char *e = getenv("TSNE_BH_KPOP"); return e ? atoi(e) : 4; }();
-    static const int xcd = [] { const char *e = getenv("TSNE_BH_XCD"); return e ? atoi(e) : 0; }();
-    // dense tiles: query-major passes for sparse lane masks (TSNE_TILE_QMAJOR=0: lane-major only)
-    static const int qmajor = [] { const char *e = getenv("TSNE_TILE_QMAJOR"); return e ? atoi(e) : 1; }();
-    // small tiles (TSNE_TILE_PACK): 2 per 64-tile window the cheaper of lane-wise walks and
-    // packed 64-slot masked sweeps (C3 snapshots: tile_apply -6 % at t = 250, -18 % at t = 500),
-    // 1 packed sweeps only, 0 one round per tile
-    static const int pack = [] { const char *e = getenv("TSNE_TILE_PACK"); return e ? atoi(e) : 2; }();
-    static const float lw_cost = [] { const char *e = getenv("TSNE_TILE_LW"); return e ? (float)atof(e) : 1.6f; }();
     // counters only when asked for: visits need every counter, the multi-GPU
-    // cost buckets only the wave's pops and tile points
+    // cost buckets only the waves' run times
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    auto kern = kp >= 16  ? (mode == 2 ? bh_traverse<16, 2, false> : mode == 1 ? bh_traverse<16, 1, false> : bh_traverse<16, 0, false>)
-                : kp >= 8 ? (mode == 2 ? bh_traverse<8, 2, false> : mode == 1 ? bh_traverse<8, 1, false> : bh_traverse<8, 0, false>)
-                          : (mode == 2 ? bh_traverse<4, 2, false> : mode == 1 ? bh_traverse<4, 1, false> : bh_traverse<4, 0, false>);
-    auto tkern = mode == 2 ? bh_traverse<4, 2, true> : mode == 1 ? bh_traverse<4, 1, true> : bh_traverse<4, 0, true>;
-    // dynamic splitting of heavy waves (TSNE_BH_SPILL=1: on; off by default --
-    // measured without gain over the C3 schedule); budget =
-    // TSNE_BH_BUDGET (default 2) x the previous traversal's mean wave cost,
-    // spill groups of TSNE_BH_GROUP (default 2) x budget points
-    const bool spill_on = [] { const char *e = getenv("TSNE_BH_SPILL"); return e && e[0] == '1'; }();   // per call
-    static const double bfac = [] { const char *e = getenv("TSNE_BH_BUDGET"); return e ? atof(e) : 2.0; }();
-    static const int gfac = [] { const char *e = getenv("TSNE_BH_GROUP"); return e ? std::max(1, atoi(e)) : 2; }();
-    static const int32_t bmin = [] { const char *e = getenv("TSNE_BH_BUDGET_MIN"); return e ? std::max(1, atoi(e)) : 256; }();
-    SpillView sv;
-    if (spill_on) {
-        sv = t.spill;
-        sv.gfac = gfac;
-        TSNE_HIP(hipMemsetAsync(sv.cnt, 0, sizeof(int32_t) * 2 * (SPILL_PASSES + 1), ctx->stream));
-        // TSNE_BH_BUDGET_FIXED=N (read per call; tests): this traversal's budget is N pops
-        if (const char *e = getenv("TSNE_BH_BUDGET_FIXED"))
-            hipLaunchKernelGGL(set_i32, dim3(1), dim3(64), 0, ctx->stream, sv.budget, std::max(1, atoi(e)));
-    }
-    // longest-first block orders, TSNE_BH_ORDER bits: 1 traversal (by the
-    // previous traversal's wave costs), 2 tile_apply (by this traversal's
-    // tile points); default 2 -- the traversal keeps launch order, whose
-    // Morton-contiguous blocks share tree records in each XCD's L2 (full C3
-    // schedule 8.08 s in launch order vs 8.35 s longest-first)
-    static const int lpt_bits = [] { const char *e = getenv("TSNE_BH_ORDER"); return e ? atoi(e) : 2; }();
+    auto kern = mode == 2 ? bh_traverse<2> : mode == 1 ? bh_traverse<1> : bh_traverse<0>;
     const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
-    const int32_t *border = nullptr, *torder = nullptr;
-    if ((lpt_bits & 1) && t.have_cost) {
-        block_order(ctx, t, t.wcost, waves, nblocks, t.border);
-        border = t.border;
+    // heavy groups of this traversal from the previous one's costs (narrow
+    // layout; none on a tree's first traversal or with Options::narrow = 0)
+    NarrowView nv;
+    const double nfac = ctx->opts.narrow;
+    const bool narrow = nfac > 0.0 && t.have_cost && t.cost_waves == waves;
+    if (narrow) {
+        hipLaunchKernelGGL(narrow_select, dim3(1), dim3(1024), 0, st, t.wcost, waves, t.nflag, t.ncost, t.hlist,
+                           t.hcount, t.nar_hmax, nfac, std::min<int64_t>(t.nar_hmax, narrow_fill(ctx, waves)));
+        nv.hlist = t.hlist; nv.hcount = t.hcount; nv.ncost = t.ncost; nv.mtask = t.nmtask; nv.mtask_n = t.nmtask_n;
+        nv.nflag = t.nflag;
+        nv.nbn = (int32_t)ceil_div(t.nar_hmax * NPARTS, 4);
+    } else if (t.nflag_set) {
+        TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * t.tile_waves, st));
     }
-    // persistent query waves (TSNE_BH_PERSIST=1; default: one block per 4 query waves):
-    // cu_count x 8 blocks (the traversal's occupancy: 20 KB of LDS and 58
-    // VGPRs per 4-wave block) dequeue 64-query groups, per XCD group in
-    // Morton order (bh_dequeue)
-    static const bool persist = [] { const char *e = getenv("TSNE_BH_PERSIST"); return e && e[0] == '1'; }();
-    const bool pq = persist && !border;
-    if (pq) TSNE_HIP(hipMemsetAsync(t.qhead, 0, 8 * sizeof(int32_t), ctx->stream));
-    const int64_t tgrid0 = pq ? std::min<int64_t>(nblocks, (int64_t)ctx->cu_count * 8) : nblocks;
-    hipLaunchKernelGGL(kern, dim3(tgrid0), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes,
-                       t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd,
-                       (int32_t)t.n, dF, dz, visits, bcost, border, t.wcost, t.tcost, sv, 0, pq ? t.qhead : nullptr,
-                       cost_by_label ? t.idx_sorted : nullptr);
-    if (spill_on) {   // task passes over regions 1..P (fixed grid: one wave per SIMD slot of every CU)
-        const int tgrid = ctx->cu_count * 8;
-        // regions 1..P, then the finish pass (region P + 1) over stacks saved when a region was full
-        for (int r = 1; r <= SPILL_PASSES + 1; ++r)
-            hipLaunchKernelGGL(tkern, dim3(tgrid), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.qrec, t.ttask,
-                               t.ttask_n, t.meta, t.mom_flag, theta, near_dmax, s0, s1, qlist, xcd, (int32_t)t.n, dF,
-                               dz, visits, bcost, border, t.wcost, t.tcost, sv, r, nullptr,
-                               cost_by_label ? t.idx_sorted : nullptr);
+    t.nflag_set = narrow;
+    const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
+    if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
+        TSNE_HIP(hipEventRecord(ctx->aux_ev[0], st));
+        TSNE_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
+        auto nk = mode == 2 ? bh_traverse_narrow<2> : mode == 1 ? bh_traverse_narrow<1> : bh_traverse_narrow<0>;
+        hipLaunchKernelGGL(nk, dim3(nv.nbn), dim3(256), 0, ctx->aux_stream, t.pos, t.dupc, t.nodes, t.qrec, t.ttask_n,
+                           t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost,
+                           t.tcost, clab, nv);
+        TSNE_HIP(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
     }
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
+                       t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
+                       t.tcost, clab, nv);
+    if (narrow) TSNE_HIP(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
     t.have_cost = true;
-    // tile chunks of heavy waves (ChunkView; TSNE_TILE_CHUNK=0: one tile_apply wave per traversal wave)
-    static const bool chunk_on = [] { const char *e = getenv("TSNE_TILE_CHUNK"); return !(e && e[0] == '0'); }();
+    t.cost_waves = waves;
+    // tile chunks of heavy waves (ChunkView): the single-workgroup plan while
+    // the per-wave costs fit its LDS, else the multi-launch plan and block sort
     ChunkView cv;
-    int64_t tslots = waves;
-    const int32_t *tcost = t.tcost;
-    // TSNE_TILE_PLAN=0: the multi-launch chunk plan and block sort
-    static const bool plan1 = [] { const char *e = getenv("TSNE_TILE_PLAN"); return !(e && e[0] == '0'); }();
-    bool planned = false;
-    if (chunk_on && plan1 && waves <= PLAN_WAVES_MAX &&
-        ceil_div(std::min<int64_t>(t.tile_waves, waves + waves / 2 + 64), 4) <= PLAN_BLOCKS_MAX) {
-        tslots = std::min<int64_t>(t.tile_waves, waves + waves / 2 + 64);
-        hipLaunchKernelGGL(tile_plan, dim3(1), dim3(1024), 0, ctx->stream, t.tcost, waves, tslots, t.ch_C, t.ch_slot0,
-                           t.ch_slot_w, t.ch_slot_c, t.ch_nslots, (lpt_bits & 2) ? t.torder : nullptr);
-        cv.slot_w = t.ch_slot_w; cv.slot_c = t.ch_slot_c; cv.nslots = t.ch_nslots;
-        cv.Fp = t.ch_Fp; cv.Zp = t.ch_Zp;
-        if (lpt_bits & 2) torder = t.torder;
-        planned = true;
-    } else if (chunk_on) {
-        hipStream_t st = ctx->stream;
+    const int64_t tslots = std::min<int64_t>(t.tile_waves, waves + waves / 2 + 64);
+    const int32_t *torder = t.torder;
+    if (waves <= PLAN_WAVES_MAX && ceil_div(tslots, 4) <= PLAN_BLOCKS_MAX) {
+        hipLaunchKernelGGL(tile_plan, dim3(1), dim3(1024), 0, st, t.tcost, waves, tslots, t.ch_C, t.ch_slot0,
+                           t.ch_slot_w, t.ch_slot_c, t.ch_nslots, t.torder);
+    } else {
         const int64_t wb = ceil_div(waves + 1, 256);
-        tslots = std::min<int64_t>(t.tile_waves, waves + waves / 2 + 64);
         TSNE_HIP(hipMemsetAsync(t.ch_total, 0, sizeof(unsigned long long), st));
         hipLaunchKernelGGL(chunk_total, dim3(wb), dim3(256), 0, st, t.tcost, waves, t.ch_total);
         hipLaunchKernelGGL(chunk_parts, dim3(wb), dim3(256), 0, st, t.tcost, t.ch_total, waves, t.ch_C);
@@ -3312,31 +3104,19 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.ch_scan_tmp, tb, t.ch_C, t.ch_slot0, (int)(waves + 1), st));
         hipLaunchKernelGGL(chunk_fill, dim3(wb), dim3(256), 0, st, t.ch_C, t.ch_slot0, t.tcost, waves, t.ch_slot_w,
                            t.ch_slot_c, t.ch_scost, tslots, t.ch_nslots);
-        cv.slot_w = t.ch_slot_w; cv.slot_c = t.ch_slot_c; cv.nslots = t.ch_nslots;
-        cv.Fp = t.ch_Fp; cv.Zp = t.ch_Zp;
-        tcost = t.ch_scost;
+        block_order(ctx, t, t.ch_scost, tslots, ceil_div(tslots, 4), t.torder);
     }
-    const int64_t tblocks = ceil_div(tslots, 4);
-    if ((lpt_bits & 2) && !planned) {
-        block_order(ctx, t, tcost, tslots, tblocks, t.torder);
-        torder = t.torder;
-    }
-    hipLaunchKernelGGL(tile_apply, dim3(tblocks), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
-                       t.ttask, t.ttask_n, s0, s1, qlist, xcd, t.mom_flag, t.mtask, t.mtask_n, dF, dz, visits, qmajor,
-                       pack, lw_cost, torder, cv);
-    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(cv.slot_w ? tslots * 64 : s1 - s0, 256)), dim3(256), 0,
-                       ctx->stream, t.pos, t.nodes, t.mom, t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
-    if (cv.slot_w)
-        hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.ch_Fp, t.ch_Zp,
-                           t.ch_C, t.ch_slot0, s0, s1, qlist, dF, dz);
-    if (spill_on) {   // spilled tasks' sums, bottom-up, then into F, Z; the next budget
-        const int cgrid = ctx->cu_count * 4;
-        for (int r = SPILL_PASSES - 1; r >= 1; --r)
-            hipLaunchKernelGGL(task_combine, dim3(cgrid), dim3(256), 0, ctx->stream, sv, r);
-        hipLaunchKernelGGL(wave_spill_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, sv, s0, s1,
-                           qlist, dF, dz);
-        hipLaunchKernelGGL(spill_budget, dim3(1), dim3(1024), 0, ctx->stream, t.wcost, waves, sv.budget, bfac, bmin);
-    }
+    cv.slot_w = t.ch_slot_w; cv.slot_c = t.ch_slot_c; cv.nslots = t.ch_nslots;
+    cv.Fp = t.ch_Fp; cv.Zp = t.ch_Zp;
+    hipLaunchKernelGGL(tile_apply, dim3(ceil_div(tslots, 4)), dim3(256), 0, st, t.pos, t.nodes, t.ttask, t.ttask_n,
+                       s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits, torder, cv);
+    hipLaunchKernelGGL(moment_apply, dim3(ceil_div(tslots * 64, 256)), dim3(256), 0, st, t.pos, t.nodes, t.mom,
+                       t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
+    hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.ch_Fp, t.ch_Zp, t.ch_C,
+                       t.ch_slot0, s0, s1, qlist, dF, dz);
+    if (narrow)
+        hipLaunchKernelGGL(narrow_moment_apply, dim3(ceil_div(t.nar_hmax * 64, 256)), dim3(256), 0, st, t.pos,
+                           t.nodes, t.mom, t.hlist, t.hcount, t.nmtask, t.nmtask_n, s0, s1, qlist, dF, dz);
     TSNE_LAUNCH_CHECK();
 }
 

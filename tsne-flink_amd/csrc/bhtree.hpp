@@ -12,34 +12,6 @@ struct TileTask {
     uint64_t mask;
 };
 
-// Spill tasks of the traversal (bhtree.hip "Dynamic splitting"): a task is
-// the 64 queries of wave `wid` over a contiguous run of stack entries of its
-// region; its own spill (children in the next region) is [c0, c0 + nc).
-constexpr int SPILL_PASSES = 4;   // task regions 1..SPILL_PASSES after the query-wave pass
-constexpr int TASK_ENT = 16;      // stack entries per task at most
-struct BHTask {
-    int32_t wid;
-    int32_t e0, ne;
-    int32_t c0, nc;
-    int32_t pad[3];
-};
-struct SpillView {
-    BHTask *task = nullptr;          // region r (1..SPILL_PASSES) at (r - 1) * task_cap
-    int32_t *tent_ref = nullptr;     // stack entries, region r at (r - 1) * ent_cap
-    uint64_t *tent_mask = nullptr;
-    int32_t *cnt = nullptr;          // [2 r]: tasks, [2 r + 1]: entries allocated in region r
-    int2 *wspill = nullptr;          // per query wave: its spill (children in region 1)
-    double2 *tF = nullptr;           // per task (global id (r - 1) * task_cap + i) x 64 lanes
-    double *tZ = nullptr;
-    int32_t *budget = nullptr;       // [0] the traversal's pop budget
-    int32_t *save_ref = nullptr;     // saved stacks (a spill that found its region full), STACK per source:
-    uint64_t *save_mask = nullptr;   //   waves [0, nwaves), then tasks by global id
-    int2 *ovf = nullptr;             // (source, depth) of every saved stack; cnt[0] of them
-    int64_t nwaves = 0;
-    int32_t task_cap = 0, ent_cap = 0;
-    int32_t gfac = 2;                // spill group size: gfac x budget points
-};
-
 // Internal node of the binary radix tree over sorted Morton keys.  A node
 // whose common prefix ends inside a quad level is "transparent" (h == 0:
 // always opened); otherwise it IS the reference quadtree cell of half width
@@ -124,7 +96,6 @@ struct BHTree {
     int32_t gen = 0;
     int rt_skip = 0;            // builds left before the root-tile test is tried again
     double near_dmax = 0.0;     // this build's near-exact radius (squared distance), bh_near_dmax
-    int32_t *qhead = nullptr;   // persistent traversal: per XCD group, query waves handed out
     int32_t *meta = nullptr;    // [0] = m (in-root points), [1] = root ref, [2] = moment nodes
     // subtree moments (see bhtree.hip "Subtree moments"): per internal node
     // MOM_K scaled moments about its bounding-box centre, for nodes of
@@ -176,12 +147,24 @@ struct BHTree {
     double *ch_Zp = nullptr;
     void *ch_scan_tmp = nullptr;
     size_t ch_scan_bytes = 0;
-    // spill tasks of heavy traversal waves (SpillView)
-    SpillView spill;
+    // narrow layout of heavy 64-query groups (bhtree.hip "Narrow layout"):
+    // per group its heavy slot + 1 (or 0), the heavy list and count, per
+    // narrow wave its cost, per narrow query its moment tasks
+    int32_t *nflag = nullptr, *hlist = nullptr, *hcount = nullptr, *ncost = nullptr;
+    int32_t *nmtask = nullptr, *nmtask_n = nullptr;
+    int64_t nar_hmax = 0;
+    bool nflag_set = false;      // some nflag may be set (cleared before a traversal without selection)
+    int64_t cost_waves = 0;      // query waves of the traversal the costs came from
 };
 
-// Allocate (from ctx->ws) for n points.
-void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
+// Allocate (from ctx->ws, buffers named pre + field) for n points.  One
+// prefix per tree that must persist alongside another (the optimizer's "bh.",
+// the single-call operators' "bh1.").
+void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre = "bh.");
+// The single-call operators' tree (tsne_gradient / tsne_repulsion): kept in
+// the context, so that consecutive calls of one size reuse its buffers and the
+// previous traversal's wave costs (the narrow layout's selection).
+BHTree &bh_single_tree(tsne_ctx *ctx, int64_t n);
 // Build the tree of all n points of Y (n x 2, device).  rowmap (device,
 // nullable = identity) gives each point's insertion row in the reference
 // (its original index): the order that decides duplicate multiplicities.
@@ -189,10 +172,10 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n);
 // tree is one near-exact subtree evaluated from the root's moments (the
 // small-embedding phase, see bh_root_tile): t.root_tile tells which.
 // near_tol: the near-exact tolerance of this build and the traversals on it
-// (< 0: bh_near_tol(false), the strict one).
+// (< 0: bh_near_tol(ctx, false), the strict one).
 void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const int32_t *rowmap = nullptr,
               bool root_tile_ok = false, double near_tol = -1.0);
-double bh_near_tol(bool late);
+double bh_near_tol(const tsne_ctx *ctx, bool late);
 // Repulsion for the query slots [s0, s1): sorted positions, or with qlist
 // (device, ascending sorted positions: one rank's own queries) the positions
 // qlist[s0..s1).  F (double2) and z (sum of Q) are written at the sorted
@@ -202,6 +185,8 @@ double bh_near_tol(bool late);
 void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist = nullptr,
                   unsigned long long *bcost = nullptr, bool cost_by_label = false);
+// Heavy groups the last traversal on t ran narrow (synchronises the stream).
+int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).
 void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int world, int64_t *bounds);
 

@@ -102,6 +102,49 @@ template <class T> static void download(tsne_ctx *ctx, T *h, const T *d, size_t 
 
 static void sync(tsne_ctx *ctx) { TSNE_HIP(hipStreamSynchronize(ctx->stream)); }
 
+// The Options fields by key (tsne_ctx_set_option); values range-checked.
+struct OptionField {
+    const char *key;
+    double Options::*d;
+    int Options::*i;
+    double lo, hi;
+};
+static const OptionField k_options[] = {
+    {"near_tol_early", &Options::near_tol_early, nullptr, 0.0, 1e-2},
+    {"near_tol_late", &Options::near_tol_late, nullptr, 0.0, 1e-2},
+    {"mom_tol", &Options::mom_tol, nullptr, 0.0, 1e-4},
+    {"near_tol3_early", &Options::near_tol3_early, nullptr, 0.0, 1e-2},
+    {"near_tol3_late", &Options::near_tol3_late, nullptr, 0.0, 1e-2},
+    {"mom3_tol", &Options::mom3_tol, nullptr, 0.0, 1e-4},
+    {"oct_moments", nullptr, &Options::oct_moments, 0, 1},
+    {"root_tile", nullptr, &Options::root_tile, 0, 1},
+    {"attract_tiles", nullptr, &Options::attract_tiles, 0, 1},
+    {"attract_cfg", nullptr, &Options::attract_cfg, -1, 3},
+    {"graph_order", nullptr, &Options::graph_order, 0, 1},
+    {"relabel", nullptr, &Options::relabel, -1, 2},
+    {"recut", nullptr, &Options::recut, 0, 1},
+    {"knn_bf16", nullptr, &Options::knn_bf16, 0, 1},
+    {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
+};
+static const OptionField &option_field(const char *key) {
+    for (const OptionField &f : k_options)
+        if (std::strcmp(f.key, key) == 0) return f;
+    fail(TSNE_ERR_ARG, std::string("unknown option '") + key + "'");
+}
+static void set_option(Options &o, const char *key, double v) {
+    const OptionField &f = option_field(key);
+    TSNE_REQUIRE(v >= f.lo && v <= f.hi, std::string("option '") + key + "' out of range");
+    if (f.d) o.*f.d = v;
+    else {
+        TSNE_REQUIRE(v == std::floor(v), std::string("option '") + key + "' takes an integer");
+        o.*f.i = (int)v;
+    }
+}
+static double get_option(const Options &o, const char *key) {
+    const OptionField &f = option_field(key);
+    return f.d ? o.*f.d : (double)(o.*f.i);
+}
+
 }  // namespace tsne
 
 using namespace tsne;
@@ -222,6 +265,8 @@ int tsne_ctx_create(int32_t device, tsne_ctx **out) {
         c->cu_count = prop.multiProcessorCount;
         TSNE_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
+        TSNE_HIP(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+        for (auto &e : c->aux_ev) TSNE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         TSNE_HIP(hipHostMalloc(reinterpret_cast<void **>(&c->pinned), 64 * sizeof(int32_t)));
         *out = c.release();
     });
@@ -274,12 +319,18 @@ int tsne_ctx_destroy(tsne_ctx *ctx) {
         DeviceGuard g(ctx->device);
         (void)hipStreamSynchronize(ctx->stream);
         opt_destroy(ctx);
+        delete ctx->single_tree;
+        ctx->single_tree = nullptr;
         comm_destroy(ctx);
         ctx->timers.clear();
         ctx->ws.clear();
         if (ctx->pinned) (void)hipHostFree(ctx->pinned);
         ctx->pinned = nullptr;
         if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+        if (ctx->aux_stream) (void)hipStreamSynchronize(ctx->aux_stream);
+        if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
+        for (auto &e : ctx->aux_ev)
+            if (e) (void)hipEventDestroy(e);
     });
     delete ctx;
     return rc;
@@ -305,6 +356,48 @@ int tsne_ctx_set_stream(tsne_ctx *ctx, void *hip_stream) {
 }
 
 void *tsne_ctx_stream(tsne_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int tsne_ctx_set_option(tsne_ctx *ctx, const char *key, double value) {
+    return guard([&] {
+        check_ctx(ctx);
+        TSNE_REQUIRE(key != nullptr, "option key is NULL");
+        TSNE_REQUIRE(value == value, "option value is NaN");
+        Options o = ctx->opts;
+        set_option(o, key, value);
+        ctx->opts = o;
+        for (tsne_ctx *c : ctx->group) c->opts = o;
+    });
+}
+
+int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        TSNE_REQUIRE(name != nullptr && value_out != nullptr, "NULL argument");
+        ctx = primary(ctx);
+        DeviceGuard g(ctx->device);
+        const std::string k = name;
+        if (k == "bh.narrow_groups") *value_out = ctx->single_tree ? bh_narrow_groups(ctx, *ctx->single_tree) : 0;
+        else if (k == "opt.narrow_groups") *value_out = opt_tree(ctx) ? bh_narrow_groups(ctx, *opt_tree(ctx)) : 0;
+        else fail(TSNE_ERR_ARG, "unknown counter '" + k + "'");
+    });
+}
+
+int tsne_hip_versions(int32_t *built_out, int32_t *runtime_out) {
+    return guard([&] {
+        int rt = 0;
+        TSNE_HIP(hipRuntimeGetVersion(&rt));
+        if (built_out) *built_out = HIP_VERSION;
+        if (runtime_out) *runtime_out = rt;
+    });
+}
+
+int tsne_ctx_get_option(tsne_ctx *ctx, const char *key, double *value_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        TSNE_REQUIRE(key != nullptr && value_out != nullptr, "NULL argument");
+        *value_out = get_option(primary(ctx)->opts, key);
+    });
+}
 
 int tsne_ctx_synchronize(tsne_ctx *ctx) {
     return guard([&] {

@@ -53,30 +53,44 @@ void nccl_check(ncclResult_t r, const char *what) {
 
 struct RcclComm : Comm {
     ncclComm_t comm = nullptr;
-    std::atomic<bool> aborted{false};
+    // mu orders abort() against this rank's own collective calls: abort runs
+    // on a failing peer's thread (run_group), and ncclCommAbort frees the
+    // communicator, so no enqueue may be inside RCCL with it then.  The
+    // enqueues are asynchronous (the waiting happens later, in a stream
+    // synchronisation that the abort ends), so the lock is held briefly.
+    std::mutex mu;
+    bool aborted = false;
     ~RcclComm() override {
-        if (comm && !aborted.load()) (void)ncclCommDestroy(comm);
+        if (comm && !aborted) (void)ncclCommDestroy(comm);
     }
     // ncclCommAbort stops this rank's in-flight collective kernels and frees
     // the communicator: a peer blocked in a collective with it then fails
     // instead of hanging (run_group aborts every rank of a group once one
     // rank has thrown).  Later calls report TSNE_ERR_COMM.
     void abort() override {
-        if (comm && !aborted.exchange(true)) (void)ncclCommAbort(comm);
+        std::lock_guard<std::mutex> lk(mu);
+        if (comm && !aborted) {
+            aborted = true;
+            (void)ncclCommAbort(comm);
+        }
     }
+    // caller holds mu
     void live() {
-        if (aborted.load()) fail(TSNE_ERR_COMM, "RCCL communicator aborted (another rank failed)");
+        if (aborted) fail(TSNE_ERR_COMM, "RCCL communicator aborted (another rank failed)");
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override {
+        std::lock_guard<std::mutex> lk(mu);
         live();
         nccl_check(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, ctx->stream), "ncclAllReduce");
     }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override {
+        std::lock_guard<std::mutex> lk(mu);
         live();
         nccl_check(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm, ctx->stream), "ncclAllReduce");
     }
     // ragged all-gather: one in-place broadcast per root, fused into one group
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
+        std::lock_guard<std::mutex> lk(mu);
         live();
         uint8_t *b = static_cast<uint8_t *>(buf);
         nccl_check(ncclGroupStart(), "ncclGroupStart");

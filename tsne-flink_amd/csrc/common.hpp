@@ -156,6 +156,28 @@ struct StageTimers {
 
 struct Comm;      // collective backend: RCCL or in-process loopback (comm.cpp)
 struct OptState;  // device-resident optimizer state (optimize.hip)
+struct BHTree;    // Barnes-Hut tree (bhtree.hpp)
+
+// Per-context tunables (tsne_ctx_set_option): the library's defaults, set per
+// handle by the caller -- nothing here is process-static.  DESIGN.md 3a gives
+// the tolerances' derivations and measurements.
+struct Options {
+    // near-exact BH subtrees (bh_traverse): relative bound per summarised cell,
+    // single gradients and the early-exaggeration phase / the optimizer after it
+    double near_tol_early = 1e-6, near_tol_late = 5e-6;
+    double mom_tol = 1e-12;                               // subtree-moment truncation bound (2-D)
+    double near_tol3_early = 1e-7, near_tol3_late = 5e-6;  // the 3-D octree's
+    double mom3_tol = 1e-12;
+    int oct_moments = 1;      // 3-D subtree moments
+    int root_tile = 1;        // root-tile shortcut of the small-embedding phase
+    int attract_tiles = 1;    // tiled attraction (attract_tiles) where the labels allow it
+    int attract_cfg = -1;     // its tile shape: -1 by rows per rank, else ATCfg0..3
+    int graph_order = 1;      // P's graph order (components + BFS) as the initial labels
+    int relabel = -1;         // -1 automatic, 0 never, 1 by the locality score, 2 always
+    int recut = 0;            // several ranks on the tiled layout: re-cut by BH cost instead of relabels
+    int knn_bf16 = 1;         // kNN threshold filter: bf16x3 MFMA (0: f32-input MFMA)
+    double narrow = 3.0;      // BH: 64-query groups costing >= narrow x the mean run in the narrow layout (0: off)
+};
 
 }  // namespace tsne
 
@@ -163,10 +185,14 @@ struct tsne_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    hipStream_t aux_stream = nullptr;   // second stream of one operator (the narrow BH waves)
+    hipEvent_t aux_ev[2] = {nullptr, nullptr};
     int rank = 0, world = 1;
     tsne::Comm *comm = nullptr;
     tsne::Workspace ws;
     tsne::OptState *opt = nullptr;
+    tsne::Options opts;
+    tsne::BHTree *single_tree = nullptr;   // bh_single_tree (owned; freed by tsne_ctx_destroy)
     tsne::StageTimers timers;
     int32_t *pinned = nullptr;   // small pinned host scratch (per-iteration read-backs)
     int cu_count = 256;
@@ -231,6 +257,7 @@ void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits);
 double opt_last_z(tsne_ctx *ctx);
 int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap);
 void opt_destroy(tsne_ctx *ctx);
+BHTree *opt_tree(tsne_ctx *ctx);   // the optimizer's 2-D tree (nullptr without one)
 
 // comm.cpp
 void comm_unique_id(uint8_t *out);

@@ -38,11 +38,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));   // 8 bf16: one 32x32x16 MFMA operand fragment
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// bf16x3 filter tiles (knn_filter_bf): 256 queries x 256 candidates per
-// 512-thread workgroup, dims staged 32 at a time (two 16-deep MFMA steps).
+// bf16x3 filter tiles (knn_filter_glds): 256 queries x 256 candidates per
+// 1024-thread workgroup, dims staged 32 at a time (two 16-deep MFMA steps).
 constexpr int FT = 256;
 constexpr int FK = 32;
-constexpr int FROW = FK + 8;   // LDS row in bf16 elements (80 B): rows 20 banks apart
 constexpr int FTPB = 8;        // candidate tiles per workgroup (cross-tile prefetch)
 constexpr int FSQ = 64, FSC = 4;   // super-tile: query tiles x candidate groups
 
@@ -272,160 +271,9 @@ __global__ __launch_bounds__(256) void knn_filter(
 // knn_run's delta_coef covers both, and the exact fp64 re-rank restores
 // the exact order -- the filter only decides who is re-ranked.
 // Workgroup: 16 waves as 4 (queries) x 4 (candidates), wave tile 64 x 64 =
-// 2 x 2 MFMA 32x32 tiles (<= 128 registers: 4 waves/SIMD hide the loads);
-// each 32-dim stage is loaded into registers one stage ahead (across
-// candidate tiles too) and written to LDS between two barriers.
-__global__ __launch_bounds__(1024) void knn_filter_bf(
-    const unsigned short *__restrict__ Xh, const unsigned short *__restrict__ Xm, const float *__restrict__ norm32,
-    int64_t npad_rows, int32_t dpad, int64_t q0, int64_t q1, int64_t c0, int64_t c1, float dot_scale,
-    const float *__restrict__ tau,
-    int32_t *__restrict__ cnt, float *__restrict__ cand_d, int32_t *__restrict__ cand_j, int32_t *__restrict__ flags,
-    int32_t cap) {
-    __shared__ unsigned short sm[4][FT * FROW];   // Qh, Qm, Ch, Cm
-    __shared__ float nq_s[FT], tau_s[FT], nc_s[2][FT];
-    __shared__ int64_t qoff_s[FT];   // candidate-buffer offset of each query row (read in the rare append path)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 2, wc = wave & 3;   // wave tile: rows 64 wr.., cols 64 wc..
-    // Super-tile raster over a 1-D grid: FSQ query tiles x FSC candidate
-    // groups per super-tile, query tile fastest -- the XCD (block % 8) keeps
-    // the same FSQ/8 query tiles in its L2 across the super-tile's candidate
-    // groups, and each candidate group is re-read from the MALL, not HBM.
-    const int64_t nqt = (q1 - q0 + FT - 1) / FT;
-    const int64_t ncg = (c1 - c0 + (int64_t)FT * FTPB - 1) / ((int64_t)FT * FTPB);
-    const int64_t nqt_pad = (nqt + FSQ - 1) / FSQ * FSQ;
-    const int64_t b = blockIdx.x;
-    const int64_t sts = (int64_t)FSQ * FSC;
-    const int64_t st = b / sts, inner = b % sts;
-    const int64_t nst_q = nqt_pad / FSQ;
-    const int64_t qt = (st % nst_q) * FSQ + inner % FSQ, cg = (st / nst_q) * FSC + inner / FSQ;
-    if (qt >= nqt || cg >= ncg) return;   // uniform over the workgroup
-    const int64_t qb = q0 + qt * FT;
-    // FTPB consecutive candidate tiles per workgroup: the next tile's first
-    // stage is loaded during the current tile's last one
-    const int64_t cfirst = c0 + cg * FTPB * FT;
-    const int ntile = (int)min<int64_t>(FTPB, (c1 - cfirst + FT - 1) / FT);
-    if (tid < FT) {
-        const int64_t q = qb + tid;
-        nq_s[tid] = norm32[q];
-        tau_s[tid] = q < q1 ? tau[q - q0] : 0.f;
-        qoff_s[tid] = (q - q0) * (int64_t)cap;
-    }
-    // per-element tests in 32-bit tile coordinates (wave-uniform limits):
-    // 64-bit row offsets would be hoisted out of the tile loop and spilled
-    const int qlim = (int)min<int64_t>(FT, q1 - qb), qi0 = (int)(qb - q0);
-    // stage: 4 arrays x 256 rows x 4 pieces of 8 bf16 = 4096 x 16 B; thread
-    // tid loads piece (row tid / 4, part tid % 4) of every array (Qh, Qm, Ch,
-    // Cm) -- 32-bit element offsets (knn_run: npad * dpad < 2^32) on uniform
-    // bases
-    const int srow = tid >> 2, spart = tid & 3;
-    const uint32_t qoff = 2u * ((uint32_t)(qb + srow) * (uint32_t)dpad + (uint32_t)(spart * 8));   // bytes
-    // Buffer loads: 32-bit byte offsets on a uniform descriptor (knn_run:
-    // 2 npad dpad < 2^31).  Flat loads' 64-bit addresses spilled, and every
-    // spill reload's vmcnt(0) drained the stage prefetch.  Four named
-    // registers, not an array (a private array captured by a lambda was
-    // promoted to LDS).
-    const int nbytes = 2 * (int)(npad_rows * dpad);
-    const auto rh = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short *>(Xh), (short)0, nbytes, 0x00020000);
-    const auto rm = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short *>(Xm), (short)0, nbytes, 0x00020000);
-    u32x4 p0, p1, p2, p3;
-#define TSNE_KNN_LOAD_STAGE(CB, K0)                                                                    \
-    do {                                                                                             \
-        const uint32_t coff_ = 2u * ((uint32_t)((CB) + srow) * (uint32_t)dpad + (uint32_t)(spart * 8)); \
-        const uint32_t k_ = 2u * (uint32_t)(K0);                                                     \
-        p0 = __builtin_amdgcn_raw_buffer_load_b128(rh, qoff + k_, 0, 0);                              \
-        p1 = __builtin_amdgcn_raw_buffer_load_b128(rm, qoff + k_, 0, 0);                              \
-        p2 = __builtin_amdgcn_raw_buffer_load_b128(rh, coff_ + k_, 0, 0);                             \
-        p3 = __builtin_amdgcn_raw_buffer_load_b128(rm, coff_ + k_, 0, 0);                             \
-    } while (0)
-    TSNE_KNN_LOAD_STAGE(cfirst, 0);
-    const int lr = lane & 31, lh = lane >> 5;
-    for (int it = 0; it < ntile; ++it) {
-        const int64_t cb = cfirst + (int64_t)it * FT;
-        float *ncb = nc_s[it & 1];
-        if (tid >= FT && tid < 2 * FT) ncb[tid - FT] = norm32[cb + (tid - FT)];
-        floatx16 acc[2][2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-            for (int nn = 0; nn < 2; ++nn)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[m][nn][r] = 0.f;
-        for (int k0 = 0; k0 < dpad; k0 += FK) {
-            *reinterpret_cast<u32x4 *>(&sm[0][srow * FROW + spart * 8]) = p0;
-            *reinterpret_cast<u32x4 *>(&sm[1][srow * FROW + spart * 8]) = p1;
-            *reinterpret_cast<u32x4 *>(&sm[2][srow * FROW + spart * 8]) = p2;
-            *reinterpret_cast<u32x4 *>(&sm[3][srow * FROW + spart * 8]) = p3;
-            __syncthreads();
-            if (k0 + FK < dpad) TSNE_KNN_LOAD_STAGE(cb, k0 + FK);
-            else if (it + 1 < ntile) TSNE_KNN_LOAD_STAGE(cb + FT, 0);
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                const int kc = st * 16 + 8 * lh;
-                // fragments loaded per (m, nn): 16 live operand registers
-                // (B re-read once per m: the LDS has the bandwidth, the
-                // register file -- 128 per lane at 4 waves/SIMD -- does not)
-#pragma unroll
-                for (int m = 0; m < 2; ++m) {
-                    const int qrow = wr * 64 + m * 32 + lr;
-                    const bf16x8 ah = *reinterpret_cast<const bf16x8 *>(&sm[0][qrow * FROW + kc]);
-                    const bf16x8 am = *reinterpret_cast<const bf16x8 *>(&sm[1][qrow * FROW + kc]);
-#pragma unroll
-                    for (int nn = 0; nn < 2; ++nn) {
-                        const int crow = wc * 64 + nn * 32 + lr;
-                        const bf16x8 bh = *reinterpret_cast<const bf16x8 *>(&sm[2][crow * FROW + kc]);
-                        const bf16x8 bm = *reinterpret_cast<const bf16x8 *>(&sm[3][crow * FROW + kc]);
-                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[m][nn], 0, 0, 0);
-                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[m][nn], 0, 0, 0);
-                        acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[m][nn], 0, 0, 0);
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        // epilogue: C/D layout col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-        const int clim = (int)min<int64_t>(FT, c1 - cb);
-        const int64_t dqc = qb - cb;   // self pair: lc == lrow + dqc
-        const int dself = (dqc > -FT && dqc < FT) ? (int)dqc : (1 << 20);
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-#pragma unroll
-            for (int nn = 0; nn < 2; ++nn) {
-                const int lc = wc * 64 + nn * 32 + lr;
-                const float ncv = ncb[lc];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int lrow = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    const float dv = nq_s[lrow] + ncv - dot_scale * acc[m][nn][r];
-                    const bool ok = lrow < qlim && lc < clim && lc != lrow + dself && dv <= tau_s[lrow];
-                    const uint64_t msk = __ballot(ok);
-                    if (msk) {
-                        const uint32_t mine = lh ? (uint32_t)(msk >> 32) : (uint32_t)msk;
-                        const int leader = __ffs(mine) - 1;
-                        int base = 0;
-                        if (ok && lr == leader) base = atomicAdd(&cnt[qi0 + lrow], __popc(mine));
-                        base = __shfl(base, (lh << 5) + (leader < 0 ? 0 : leader), 64);
-                        if (ok) {
-                            const int slot = base + __popc(mine & ((1u << lr) - 1u));
-                            if (slot < cap) {
-                                const int64_t o = qoff_s[lrow] + slot;
-                                cand_d[o] = dv;
-                                cand_j[o] = (int32_t)(cb + lc);
-                            } else {
-                                flags[qi0 + lrow] = 1;
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-#undef TSNE_KNN_LOAD_STAGE
-
-// knn_filter_bf with the stages copied global -> LDS by the LDS DMA
-// (global_load_lds_dwordx4): no staging registers (the register-staged form
-// spilled at 4 waves/SIMD, and each spill reload's vmcnt(0) drained the
+// 2 x 2 MFMA 32x32 tiles.  The 32-dim stages are copied global -> LDS by the
+// LDS DMA (global_load_lds_dwordx4): no staging registers (a register-staged
+// form spilled at 4 waves/SIMD, and each spill reload's vmcnt(0) drained the
 // prefetch), two LDS stage buffers, stage g+1 issued before stage g is
 // waited for.  LDS rows are 64 B with the 16-B slots XOR-swizzled by row
 // bits 2..3 (conflict-free ds_read_b128 fragment reads); the DMA writes each
@@ -456,7 +304,9 @@ __global__ __launch_bounds__(1024) void knn_filter_glds(
     float *nc_s = reinterpret_cast<float *>(lds + G_NC);
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
-    // super-tile raster (see knn_filter_bf)
+    // Super-tile raster over a 1-D grid: FSQ query tiles x FSC candidate
+    // groups per super-tile, query tile fastest (the XCD = block % 8 keeps
+    // neighbouring query tiles' candidate stages in its L2)
     const int64_t nqt = (q1 - q0 + FT - 1) / FT;
     const int64_t ncg = (c1 - c0 + (int64_t)FT * FTPB - 1) / ((int64_t)FT * FTPB);
     const int64_t nqt_pad = (nqt + FSQ - 1) / FSQ * FSQ;
@@ -844,10 +694,8 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     const int32_t dpad = (int32_t)round_up(d, KC);
     // rows up to the last 256-tile of a candidate range starting anywhere
     const int64_t npad = round_up(n, FT) + FT;
-    // bf16x3 threshold passes (TSNE_KNN_BF16=0: f32-input MFMA only)
-    // TSNE_KNN_BF16: 0 f32-input MFMA only, 1 (default) bf16x3 with LDS-DMA
-    // staging, 2 bf16x3 with register staging
-    static const int bf_mode = [] { const char *e = getenv("TSNE_KNN_BF16"); return e ? atoi(e) : 1; }();
+    // bf16x3 threshold passes (Options::knn_bf16 = 0: f32-input MFMA only)
+    const int bf_mode = ctx->opts.knn_bf16;
     const bool use_bf = bf_mode != 0 && 2 * npad * (int64_t)round_up(d, KC) < ((int64_t)1 << 31);   // 32-bit offsets
 
     // --- prep
@@ -919,17 +767,11 @@ void knn_run(tsne_ctx *ctx, const double *dX, int64_t n, int32_t d, int32_t metr
     while (seen < n) {
         int64_t r = std::min<int64_t>(seen, n - seen);
         ctx->timers.begin("knn.filter", st);
-        if (use_bf && bf_mode == 1)
+        if (use_bf)
             hipLaunchKernelGGL(knn_filter_glds,
                                dim3(round_up(ceil_div(nq, FT), FSQ) * round_up(ceil_div(r, (int64_t)FT * FTPB), FSC)),
                                dim3(1024), 0, st, Xh, Xm, norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt,
                                cand_d, cand_j, flags, (int32_t)CAP, nmax);
-        else if (use_bf)
-            hipLaunchKernelGGL(knn_filter_bf,
-                               dim3(round_up(ceil_div(nq, FT), FSQ) * round_up(ceil_div(r, (int64_t)FT * FTPB), FSC)),
-                               dim3(1024), 0, st, Xh, Xm,
-                               norm32, npad, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d, cand_j, flags,
-                               (int32_t)CAP);
         else
             hipLaunchKernelGGL(knn_filter<1>, dim3(ceil_div(r, TC), qtiles), dim3(256), 0, st, X32,
                                norm32, dpad, q0, q1, seen, seen + r, dot_scale, tau, cnt, cand_d,

@@ -11,8 +11,9 @@
 // points outside the root cell are queries only.  Deviations:
 // exact duplicates count with full multiplicity, cells deeper than 21 levels
 // are not split (all their points interact directly), and subtrees entirely
-// within D <= near_dmax of a query are summed exactly (<= BH_NEAR_TOL3
-// relative from the restatement's cell sums).
+// within D <= near_dmax of a query are summed exactly (<= Options::
+// near_tol3_early (1e-7) / near_tol3_late (5e-6: C4 loop 29.7 -> 19.5 s,
+// losses to 6 digits) relative from the restatement's cell sums).
 //
 // The traversal is the 2-D design without its quad-collapsed records and
 // moments: a wave of 64 Morton-consecutive queries shares an LDS stack of
@@ -29,9 +30,6 @@ namespace {
 constexpr int LEVELS3 = 21;                 // 63 key bits
 constexpr uint64_t OUT_KEY3 = 1ull << 63;   // outside the root cell: sorts last
 constexpr int STACK3 = 256;                 // single pops, <= 2 pushes each: depth-bounded
-constexpr double BH_NEAR_TOL3 = 1e-7;        // single gradients and the early-exaggeration phase
-constexpr double BH_NEAR_TOL3_LATE = 5e-6;   // the optimizer after early exaggeration, as 2-D's
-                                             // BH_NEAR_TOL_LATE (C4 loop 29.7 -> 19.5 s, losses to 6 digits)
 constexpr int AGG3 = 12;                    // sx, sy, sz, x0, x1, y0, y1, z0, z1, hmin, cnt, rball
 
 __global__ void bbox3_partial(const double *__restrict__ Y, int64_t n, double *__restrict__ part) {
@@ -408,15 +406,13 @@ __device__ __forceinline__ bool summarise3(double h, double dx, double dy, doubl
 // M(a; b) = sum_p s^a P^b (a + |b| <= MOM3_ORDER + 1).  Truncated at
 // k <= MOM3_ORDER; with rho = B (R^2 + 2 |v| R) >= |B delta| (R: the box's
 // half-diagonal) the remainder is below (K + 2) rho^(K+1) / (1 - rho)^2
-// relative, taken only when that is <= MOM3_TOL (fp64 rounding level).  A
+// relative, taken only when that is <= Options::mom3_tol (1e-12).  A
 // subtree evaluated this way is one the traversal sums exactly (an all-open or
 // near-exact tile), so the result equals that exact leaf sum to 1e-14.
 constexpr int MOM3_ORDER = 3;
 constexpr int MOM3_K = 70;          // (a, bx, by, bz) with a + bx + by + bz <= 4
 constexpr int MOM3_MIN = 64;        // nodes of >= 64 points carry moments
 constexpr int MOM3_CHUNK = 1024;    // points per moment item
-constexpr double MOM3_TOL = 1e-12;   // round 3 (1e-14 before): >= 1e5 below the near-exact tolerances
-__device__ double g_mom3_tol = MOM3_TOL;   // TSNE_MOM3_TOL (experiments): the bound oct moment_ok applies
 constexpr int MOM3_GROUP = 10;      // moments accumulated per pass over an item's points
 constexpr int MOM3_TASKS = 512;     // moment tiles recorded per query; more -> dense tiles
 constexpr int DENSE3_MAX = 2048;    // larger tiles only by moments (else traversed)
@@ -531,14 +527,14 @@ __global__ void oct_mom_gate(int32_t *mom_flag) {
     mom_flag[1] = 0;
 }
 
-__device__ __forceinline__ bool mom3_ok(double vx, double vy, double vz, double R) {
+__device__ __forceinline__ bool mom3_ok(double vx, double vy, double vz, double R, double tol) {
     const double A = vx * vx + vy * vy + vz * vz;
     const double rho = (R * R + 2.0 * sqrt(A) * R) / (1.0 + A) * (1.0 + 1e-12);
     if (!(rho < 0.25)) return false;
     double rp = rho;
 #pragma unroll
     for (int k = 0; k < MOM3_ORDER; ++k) rp *= rho;
-    return (MOM3_ORDER + 2) * rp <= g_mom3_tol * (1.0 - rho) * (1.0 - rho);
+    return (MOM3_ORDER + 2) * rp <= tol * (1.0 - rho) * (1.0 - rho);
 }
 // z += sum 1/(1+D), F += sum (q - p)/(1+D)^2 over the node's points from its
 // moments mu (wave-uniform: scalar loads), the query itself included (D = 0:
@@ -607,7 +603,8 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
                                                     int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
                                                     int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
                                                     int32_t *__restrict__ mtask_n, double *__restrict__ F,
-                                                    double *__restrict__ Z, unsigned long long *__restrict__ dbg) {
+                                                    double *__restrict__ Z, unsigned long long *__restrict__ dbg,
+                                                    double mom_tol) {
     __shared__ int32_t sref[4][STACK3];
     __shared__ uint64_t smask[4][STACK3];
     __shared__ double4 tbuf[4][64];
@@ -683,7 +680,7 @@ __global__ __launch_bounds__(256) void oct_traverse(const double4 *__restrict__ 
         if (tile && mom3_node(nd)) {
             double cx, cy, cz, R;
             box3(nd, cx, cy, cz, R);
-            if (mom3_ok(qx - cx, qy - cy, qz - cz, R)) {
+            if (mom3_ok(qx - cx, qy - cy, qz - cz, R, mom_tol)) {
                 ++nwant;
                 if (mom_on && ntask < MOM3_TASKS) {
                     usem = true;
@@ -830,10 +827,6 @@ __global__ __launch_bounds__(256) void oct_mom_apply(const double4 *__restrict__
 }  // namespace
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
-    if (const char *e = getenv("TSNE_MOM3_TOL")) {
-        const double v = atof(e);
-        TSNE_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mom3_tol), &v, sizeof(double)));
-    }
     Workspace &ws = ctx->ws;
     t.n = n;
     t.keys = ws.get<uint64_t>("oct.keys", n);
@@ -871,8 +864,8 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
     t.mscan_tmp_bytes = mb;
     t.mscan_tmp = ws.get<uint8_t>("oct.mscan_tmp", mb);
     // the first build computes moments (demand := threshold); threshold n / 64
-    // lanes; TSNE_OCT_MOMENTS=0 turns the path off
-    static const bool on = [] { const char *e = getenv("TSNE_OCT_MOMENTS"); return !(e && e[0] == '0'); }();
+    // lanes; Options::oct_moments = 0 turns the path off
+    const bool on = ctx->opts.oct_moments != 0;
     const int32_t thr = (int32_t)std::max<int64_t>(1, n / 64);
     const int32_t f[4] = {0, on ? thr : 0, on ? thr : INT32_MAX, 0};
     TSNE_HIP(hipMemcpyAsync(t.mom_flag, f, sizeof(f), hipMemcpyHostToDevice, ctx->stream));
@@ -912,15 +905,13 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
     TSNE_LAUNCH_CHECK();
 }
 
-// Largest D with 72 theta^2 D^2 (1 + 8 D) <= BH_NEAR_TOL3: the 2-D bound
-// (bhtree.hip bh_near_dmax) scaled by 12/8 for the larger 3-D cell diagonal
-// (second-order remainder (2 + 8D) r^2 / 2 with r^2 <= 12 h^2 instead of 8 h^2).
-static double oct_near_dmax(double theta, bool late) {
+// Largest D with 72 theta^2 D^2 (1 + 8 D) <= the near-exact tolerance
+// (Options::near_tol3_early / near_tol3_late): the 2-D bound (bhtree.hip
+// bh_near_dmax) scaled by 12/8 for the larger 3-D cell diagonal (second-order
+// remainder (2 + 8D) r^2 / 2 with r^2 <= 12 h^2 instead of 8 h^2).
+static double oct_near_dmax(const tsne_ctx *ctx, double theta, bool late) {
     if (!(theta > 0.0)) return __builtin_inf();
-    // TSNE_BH_NEAR_TOL3 / TSNE_BH_NEAR_TOL3_EARLY: experiment overrides of the late / early tolerance
-    static const double tl = [] { const char *e = getenv("TSNE_BH_NEAR_TOL3"); return e ? atof(e) : BH_NEAR_TOL3_LATE; }();
-    static const double te = [] { const char *e = getenv("TSNE_BH_NEAR_TOL3_EARLY"); return e ? atof(e) : BH_NEAR_TOL3; }();
-    const double tol = late ? tl : te;
+    const double tol = late ? ctx->opts.near_tol3_late : ctx->opts.near_tol3_early;
     if (!(tol > 0.0)) return -1.0;
     double d = std::sqrt(tol / (72.0 * theta * theta));
     while (72.0 * theta * theta * d * d * (1.0 + 8.0 * d) > tol) d *= 0.99;
@@ -939,12 +930,12 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
     const int64_t waves = ceil_div(s1 - s0, 64);
     if (debug)
         hipLaunchKernelGGL(oct_traverse<true>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, oct_near_dmax(theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
-                           dF, dz, dbg);
+                           t.nodes, t.meta, theta, oct_near_dmax(ctx, theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                           dF, dz, dbg, ctx->opts.mom3_tol);
     else
         hipLaunchKernelGGL(oct_traverse<false>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, oct_near_dmax(theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
-                           dF, dz, dbg);
+                           t.nodes, t.meta, theta, oct_near_dmax(ctx, theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                           dF, dz, dbg, ctx->opts.mom3_tol);
     hipLaunchKernelGGL(oct_mom_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
     if (debug) {

@@ -114,7 +114,6 @@ struct OptState {
         while (attract_iter.size() > StageTimers::CAP) attract_iter.pop_front();
     }
     double *mpart = nullptr;  // centring mean: block partials of combine_update
-    uint32_t *mcnt = nullptr; // its arrival counter (last block finalises the mean)
     // tiled attraction layout of the owned rows (attract_tiles), rebuilt with them
     bool at_on = false;
     int64_t at_nrb = 0, at_ncb = 0;
@@ -129,6 +128,13 @@ struct OptState {
     double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits[10] = {};
 };
+
+// TSNE_DEBUG_TILES=1: layout and per-iteration BH / tile diagnostics on stderr
+// (synchronises; a debug print, no effect on results)
+static bool debug_tiles() {
+    static const bool on = getenv("TSNE_DEBUG_TILES") != nullptr;
+    return on;
+}
 
 namespace {
 
@@ -656,27 +662,16 @@ __global__ void at_ranges(const ATile *__restrict__ tiles, int32_t nt, int64_t n
 // per row, all accesses coalesced except F[inv[i]] (near-identity gather).
 // With `mpart` (MODE 1) each block also writes the sum of its rows' Ynew
 // (x, y) to mpart[2 * block]: the centring mean's partials, fused into the
-// update so that centerEmbedding costs one more pass (center_scatter).  With
-// `mcnt` as well, the last block to arrive sums the partials (mean2_final's
-// order, so the same bits) into mean[0..1] and re-arms the counter: one
-// launch fewer per step.  The partials cross XCDs (separate L2s) as
-// system-scope stores / loads, drained before the agent-scope arrival atomic
-// (as bottom_up_top in bhtree.hip), with no L2 write-back fence.
-__device__ __forceinline__ void st_sys_o(double *p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ double ld_sys_o(const double *p) {
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+// update so that centerEmbedding costs one more pass (center_scatter); the
+// mean itself is mean2_final (finalising it in the last block instead saved a
+// launch but cost 3,907 same-address arrival atomics: 0.062 -> 0.085 ms).
 template <int MODE>
 __global__ __launch_bounds__(256) void combine_update(
     int64_t r0, int64_t r1, const double2 *__restrict__ attr, const int32_t *__restrict__ inv,
     const double2 *__restrict__ F, const double *__restrict__ scal, const double *__restrict__ Y,
     double *__restrict__ grad, double *__restrict__ Ynew, double *__restrict__ upd, double *__restrict__ gains,
-    double min_gain, double mom, double lr, double *__restrict__ mpart, uint32_t *__restrict__ mcnt,
-    double ntot, double *__restrict__ mean) {
+    double min_gain, double mom, double lr, double *__restrict__ mpart) {
     __shared__ double sm[2][4];
-    __shared__ int last;
     const int64_t i = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i < r1;
     double yn[2] = {0.0, 0.0};
@@ -713,33 +708,8 @@ __global__ __launch_bounds__(256) void combine_update(
         if (threadIdx.x == 0) {
             const double px = (sm[0][0] + sm[0][1]) + (sm[0][2] + sm[0][3]);
             const double py = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
-            if (mcnt) {
-                st_sys_o(mpart + 2 * blockIdx.x, px);
-                st_sys_o(mpart + 2 * blockIdx.x + 1, py);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                last = __hip_atomic_fetch_add(mcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                       gridDim.x - 1;
-            } else {
-                mpart[2 * blockIdx.x] = px;
-                mpart[2 * blockIdx.x + 1] = py;
-            }
-        }
-        if (mcnt) {
-            __syncthreads();
-            if (!last) return;
-            double s[2] = {0.0, 0.0};
-            for (int64_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
-                s[0] += ld_sys_o(mpart + 2 * b);
-                s[1] += ld_sys_o(mpart + 2 * b + 1);
-            }
-            s[0] = wave_sum(s[0]);
-            s[1] = wave_sum(s[1]);
-            __syncthreads();   // sm is reused
-            if (lane_id() == 0) { sm[0][threadIdx.x >> 6] = s[0]; sm[1][threadIdx.x >> 6] = s[1]; }
-            __syncthreads();
-            if (threadIdx.x < 2)
-                mean[threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3])) / ntot;
-            if (threadIdx.x == 0) *mcnt = 0u;   // the next launch is stream-ordered after this one
+            mpart[2 * blockIdx.x] = px;
+            mpart[2 * blockIdx.x + 1] = py;
         }
     }
 }
@@ -1176,10 +1146,7 @@ static int64_t attract_grid(int64_t rows, int lpr, int bpc_req) {
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
         return c;
     }();
-    // TSNE_ATTRACT_BPC: blocks per CU (experiment: < 8 leaves wave slots to
-    // concurrent kernels)
-    static const int bpc_env = [] { const char *e = getenv("TSNE_ATTRACT_BPC"); return e ? std::max(1, atoi(e)) : 0; }();
-    const int bpc = bpc_env ? bpc_env : bpc_req > 0 ? std::min(bpc_req, 8) : 8;
+    const int bpc = bpc_req > 0 ? std::min(bpc_req, 8) : 8;
     const int64_t full = round_up(cus * bpc, NUM_XCD);
     const int64_t need = round_up(std::max<int64_t>(1, ceil_div(rows * lpr, 256)), NUM_XCD);
     return std::min(full, need);
@@ -1207,37 +1174,20 @@ static int64_t attract_launch_v(hipStream_t st, const AttractArgs &a, bool loss)
     }
 }
 
-static int attract_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("TSNE_ATTRACT");
-        const std::string s = e ? e : "";
-        v = s == "16x4" ? 0 : s == "32x4" ? 1 : s == "64x4" ? 2 : s == "16x8" ? 3 : s == "32x8" ? 4
-          : s == "16x12" ? 5 : 2;
-    }
-    return v;
-}
-
+// attract_rows: 64 lanes per row, 4 (col, val) loads then 4 Y_j gathers in
+// flight per lane (16/32 lanes, 8/12 in flight measured slower, round 1)
 static int64_t attract_launch(hipStream_t st, const AttractArgs &a, bool loss) {
-    switch (attract_variant()) {
-        case 0: return attract_launch_v<16, 4>(st, a, loss);
-        case 1: return attract_launch_v<32, 4>(st, a, loss);
-        case 3: return attract_launch_v<16, 8>(st, a, loss);
-        case 4: return attract_launch_v<32, 8>(st, a, loss);
-        case 5: return attract_launch_v<16, 12>(st, a, loss);
-        default: return attract_launch_v<64, 4>(st, a, loss);
-    }
+    return attract_launch_v<64, 4>(st, a, loss);
 }
 
 template <int MODE>
 static void combine_launch(hipStream_t st, int64_t r0, int64_t r1, const double2 *attr, const int32_t *inv,
                            const double2 *F, const double *scal, const double *Y, double *grad, double *Ynew,
                            double *upd, double *gains, double min_gain, double mom, double lr,
-                           double *mpart = nullptr, uint32_t *mcnt = nullptr, double ntot = 0.0,
-                           double *mean = nullptr) {
+                           double *mpart = nullptr) {
     if (r1 <= r0) return;
     hipLaunchKernelGGL(combine_update<MODE>, dim3(ceil_div(r1 - r0, 256)), dim3(256), 0, st, r0, r1, attr, inv, F,
-                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr, mpart, mcnt, ntot, mean);
+                       scal, Y, grad, Ynew, upd, gains, min_gain, mom, lr, mpart);
 }
 
 // Upper bound of attract_launch's block count for rows rows.
@@ -1283,20 +1233,16 @@ void init_working_set_device(tsne_ctx *ctx, int64_t n, int32_t c, uint64_t seed,
 }
 
 // The root-tile shortcut of bh_build while the embedding is small
-// (TSNE_ROOT_TILE=0: always the full tree).
-static bool root_tile_enabled() {
-    static const bool on = [] { const char *e = getenv("TSNE_ROOT_TILE"); return !(e && e[0] == '0'); }();
-    return on;
-}
+// (Options::root_tile = 0: always the full tree).
+static bool root_tile_enabled(const tsne_ctx *ctx) { return ctx->opts.root_tile != 0; }
 
 void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col,
                      const double *d_P, int64_t n, const double *dY, int32_t metric, double theta,
                      double exaggeration, double *d_grad, double *h_sumq, double *h_loss) {
     TSNE_REQUIRE(n >= 1, "empty embedding");
     hipStream_t st = ctx->stream;
-    BHTree t;
-    bh_alloc(ctx, t, n);
-    bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled());
+    BHTree &t = bh_single_tree(ctx, n);
+    bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled(ctx));
     double2 *F = ctx->ws.get<double2>("grad.F", n);
     double *z = ctx->ws.get<double>("grad.z", n);
     double *part = ctx->ws.get<double>("grad.part", NPART);
@@ -1343,9 +1289,8 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
     double *zs = ctx->ws.get<double>("rep.z", n);
     const int32_t *inv;
     if (c == 2) {
-        BHTree t;
-        bh_alloc(ctx, t, n);
-        bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled());
+        BHTree &t = bh_single_tree(ctx, n);
+        bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled(ctx));
         bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, nullptr);
         inv = t.inv;
     } else {
@@ -1430,10 +1375,9 @@ static void gather_working_set(tsne_ctx *ctx, OptState *s) {
     comm_allgatherv(ctx, s->gains[c], off.data());
 }
 
-// Tile configuration for `rows` owned rows (TSNE_AT_CFG=0..3 forces one)
+// Tile configuration for `rows` owned rows (Options::attract_cfg 0..3 forces one)
 static int at_cfg(tsne_ctx *ctx, int64_t rows) {
-    static const int forced = [] { const char *e = getenv("TSNE_AT_CFG"); return e ? std::max(0, std::min(3, atoi(e))) : -1; }();
-    if (forced >= 0) return forced;
+    if (ctx->opts.attract_cfg >= 0) return ctx->opts.attract_cfg;
     for (int c = 3; c > 0; --c)
         if (ceil_div(rows, (int64_t)512 << c) >= ctx->cu_count - ctx->cu_count / 16) return c;
     return 0;
@@ -1445,9 +1389,9 @@ static int at_cfg(tsne_ctx *ctx, int64_t rows) {
 // (a second radix sort of the (tile, row) segments), 64-row slices, and the
 // jagged-diagonal scatter of the column offsets and values.
 // Skipped (attract_rows runs) for dense rows over a small embedding (C5: all
-// of Y sits in one L2), for >= 2^31 owned entries, or with TSNE_ATTRACT_TILES=0.
+// of Y sits in one L2), for >= 2^31 owned entries, or with Options::attract_tiles = 0.
 static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
-    static const bool on = [] { const char *e = getenv("TSNE_ATTRACT_TILES"); return !(e && e[0] == '0'); }();
+    const bool on = ctx->opts.attract_tiles != 0;
     hipStream_t st = ctx->stream;
     Workspace &ws = ctx->ws;
     const int64_t rows = s->L1 - s->L0, n = s->n;
@@ -1540,8 +1484,7 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
     s->at_rbt = ws.get<int32_t>("opt.at.rbt", nrb + 1);
     hipLaunchKernelGGL(at_ranges, dim3(ceil_div(nt + 1, 256)), dim3(256), 0, st, s->at_tiles, nt, nrb, s->at_rbt);
     TSNE_LAUNCH_CHECK();
-    static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;
-    if (dbg) {   // layout statistics: tiles, segments, slices, slice widths
+    if (debug_tiles()) {   // layout statistics: tiles, segments, slices, slice widths
         std::vector<ASlice> hs(nsl);
         TSNE_HIP(hipMemcpyAsync(hs.data(), s->at_slices, sizeof(ASlice) * nsl, hipMemcpyDeviceToHost, st));
         TSNE_HIP(hipStreamSynchronize(st));
@@ -1709,8 +1652,6 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->part = ws.get<double>("opt.part", std::max<int64_t>(NPART, attract_max_blocks(rows_cap)));
     s->part2 = ws.get<double>("opt.part2", NPART);
     s->mpart = ws.get<double>("opt.mpart", 3 * ceil_div(rows_cap, 256) + 3);   // C <= 3 components
-    s->mcnt = ws.get<uint32_t>("opt.mcnt", 1);
-    TSNE_HIP(hipMemsetAsync(s->mcnt, 0, sizeof(uint32_t), st));
     s->bcost = ws.get<unsigned long long>("opt.bcost", ceil_div(n, 256) + 1);
     s->bounds = ws.get<int64_t>("opt.bounds", world + 1);
     s->lscore = ws.get<unsigned long long>("opt.lscore", 2);
@@ -1742,8 +1683,8 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         s->rpw = ws.get<int64_t>("opt.rpw", rows_cap + 1);
         s->colw = ws.get<int32_t>("opt.colw", nnz + 1);
         s->valw = ws.get<double>("opt.valw", nnz + 1);
-        // initial labels in P's graph order (TSNE_GRAPH_ORDER=0: the original order)
-        static const bool gorder = [] { const char *e = getenv("TSNE_GRAPH_ORDER"); return !(e && e[0] == '0'); }();
+        // initial labels in P's graph order (Options::graph_order = 0: the original order)
+        const bool gorder = ctx->opts.graph_order != 0;
         const bool dense_small = s->nnz / n > 1024 && n * 16 <= (2 << 20);   // see maybe_relabel
         if (gorder && n >= 2 && !(dense_small && world == 1)) {
             int32_t *order = ws.get<int32_t>("opt.g.order", n);
@@ -1754,16 +1695,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         }
     }
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
-    {   // side stream (attraction); TSNE_SIDE_PRIO=high|low picks a stream priority
-        const char *e = getenv("TSNE_SIDE_PRIO");
-        const std::string v = e ? e : "";
-        int least = 0, greatest = 0;
-        TSNE_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        if (v == "high" || v == "low")
-            TSNE_HIP(hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, v == "high" ? greatest : least));
-        else
-            TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));
-    }
+    TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));   // the attraction's (stream priorities: no gain, round 1)
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_attr, hipEventDisableTiming));
     ctx->timers.reset("opt.attract");
@@ -1822,7 +1754,7 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
     unsigned long long v[32] = {};
     TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
     for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
-    static const bool dbg = getenv("TSNE_DEBUG_TILES") != nullptr;   // tile_apply diagnostics
+    const bool dbg = debug_tiles();   // tile_apply diagnostics
     if (dbg)
         fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu "
                 "pops=%llu child_slots=%llu all_take_full=%llu all_take_partial=%llu\n", t,
@@ -1909,9 +1841,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
 // equal cost, applied (owned rows and their tiles rebuilt) when a cut moves
 // by more than 1/16 of a rank's share.
 static bool recut_mode(tsne_ctx *ctx, OptState *s) {
-    static const int mode = [] { const char *e = getenv("TSNE_RELABEL"); return e ? atoi(e) : -1; }();
-    static const bool on = [] { const char *e = getenv("TSNE_RECUT"); return e && e[0] == '1'; }();
-    return on && mode == -1 && ctx->world > 1 && s->at_on && !s->morton_labels;
+    return ctx->opts.recut && ctx->opts.relabel == -1 && ctx->world > 1 && s->at_on && !s->morton_labels;
 }
 static void recut(tsne_ctx *ctx, OptState *s, const std::vector<int64_t> &cuts) {
     gather_working_set(ctx, s);   // full upd / gains under the old cuts
@@ -1952,12 +1882,12 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     // row gathers all of Y, which sits in one XCD's L2 (n * 16 B <= 2 MiB)
     // whatever the labels, so a relabel (a copy of the whole P) buys nothing
     if (ctx->world == 1 && s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
-    // TSNE_RELABEL: 0 never, 1 by the locality score, 2 always; unset: by the
+    // Options::relabel: 0 never, 1 by the locality score, 2 always; -1: by the
     // score, except on one rank with the tiled layout, which keeps P's graph
     // order (attract_tiles reads Y in label windows; a Morton relabel hands
     // the attraction back to attract_rows: whole C3 schedule 7.23 -> 7.01 s
     // without relabels, A/B on one box)
-    static const int mode = [] { const char *e = getenv("TSNE_RELABEL"); return e ? atoi(e) : -1; }();
+    const int mode = ctx->opts.relabel;
     if (mode == 0 || (mode == -1 && ctx->world == 1 && s->at_on)) return;
     // a fixed sample of rows, ~1 << 22 entries at most (dense rows: fewer rows)
     const int64_t avg = std::max<int64_t>(1, s->nnz / std::max<int64_t>(1, n));
@@ -2017,10 +1947,9 @@ static void attract_tiles_launch_l(hipStream_t st, const OptState *s, const Attr
 // concurrent launch vs 3.1 for attract_rows), and there the attraction is
 // hidden behind the traversal anyway.
 static int64_t attract_launch_opt(hipStream_t st, const OptState *s, const AttractArgs &a, bool loss) {
-    // tiles in every phase while the labels are P's graph order
-    // (TSNE_AT_PHASE=root: only while the tree takes the root-tile path)
-    static const bool at_root = [] { const char *e = getenv("TSNE_AT_PHASE"); return e && std::string(e) == "root"; }();
-    if (!s->at_on || (!s->tree.root_tile && at_root)) return attract_launch(st, a, loss);
+    // tiles in every phase while the labels are P's graph order (only in the
+    // root-tile phase, attract_rows after it: whole C3 schedule 5.94 -> 6.40 s)
+    if (!s->at_on) return attract_launch(st, a, loss);
     if (loss) attract_tiles_launch_l<true>(st, s, a);
     else attract_tiles_launch_l<false>(st, s, a);
     return s->at_nrb;
@@ -2054,31 +1983,19 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     AttractArgs aa{s->rpw - s->L0, s->colw, s->valw, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr, s->part};
     // 0. attraction sums on the side stream, concurrent with the BH
     // traversal (in loss iterations with Z-free KL terms, P ln(P (1 + metric)):
-    // ln(Z) sum P is added once Z is known; TSNE_LOSS_ALONE=1 instead runs the
-    // loss launch after Z on the context stream) -- or, while the last
-    // build took the root-tile path, already with the tree build, on 3 blocks
-    // per CU (as fast as 8: miss-bound) so that the build's short kernels
-    // keep the other slots.  A full build is not overlapped: its latency-bound
-    // kernels stretch under the attraction (morton_keys 15 -> 800 us; whole
-    // schedule 8.53 -> 8.97 s).  TSNE_OVERLAP=tree / after / bh forces a mode.
-    static const bool loss_alone = [] { const char *e = getenv("TSNE_LOSS_ALONE"); return e && e[0] == '1'; }();
-    static const int ov_env = [] {
-        const char *e = getenv("TSNE_OVERLAP");
-        const std::string v = e ? e : "";
-        return v == "tree" ? 0 : v == "after" ? 1 : v == "bh" ? 2 : v == "none" ? 3 : -1;
-    }();
-    const int ov_mode = ov_env >= 0 ? ov_env : s->tree.root_tile ? 0 : 1;
-    // serial: the attraction on the context stream after Z, alone on the GPU
-    const bool overlap = ov_mode != 3 && (!want_loss || !loss_alone);
-    if (want_loss && overlap) aa.scal = s->scal + 7;   // Z = 1 in the kernel
+    // ln(Z) sum P is added once Z is known; the loss launch alone after Z:
+    // whole schedule +1 %) -- or, while the last build took the root-tile
+    // path, already with the tree build, on 3 blocks per CU (as fast as 8:
+    // miss-bound) so that the build's short kernels keep the other slots.  A
+    // full build is not overlapped: its latency-bound kernels stretch under
+    // the attraction (morton_keys 15 -> 800 us; whole schedule 8.53 -> 8.97 s).
+    const bool rt_phase = s->tree.root_tile;
+    if (want_loss) aa.scal = s->scal + 7;   // Z = 1 in the kernel
     int64_t blocks = 0;
-    if (overlap && ov_mode == 0 && s->tree.root_tile) aa.bpc = 3;
-    auto side_wait = [&] {
+    if (rt_phase) aa.bpc = 3;
+    auto side_attract = [&] {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
         TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
-    };
-    auto side_attract = [&] {
-        if (ov_mode != 2) side_wait();
         ctx->timers.begin("opt.attract", s->side);
         blocks = attract_launch_opt(s->side, s, aa, want_loss != 0);
         TSNE_LAUNCH_CHECK();
@@ -2086,16 +2003,15 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         s->log_attract(t, want_loss ? 2 : 0);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
-    if (overlap && ov_mode == 0) side_attract();
+    if (rt_phase) side_attract();
     // 1. tree (identical on every rank)
     // insertion rows = original indices; the root-tile shortcut while the
     // embedding is small
     // the strict near-exact tolerance while P is exaggerated (the dynamics
     // amplify any difference fastest there), the late one after
-    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(), bh_near_tol(ex == 1.0));
+    bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(ctx), bh_near_tol(ctx, ex == 1.0));
     if (world > 1) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
-    if (overlap && ov_mode == 1) side_attract();
-    if (overlap && ov_mode == 2) side_wait();
+    if (!rt_phase) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
@@ -2110,41 +2026,25 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
-    if (overlap && ov_mode == 2) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
     reduce_Z(ctx, s, s->z);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
-    // 4. attraction (TSNE_LOSS_ALONE loss iterations: here, after Z) + update for owned rows
-    if (overlap) {
-        TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
-    } else {
-        ctx->timers.begin("opt.attract", st);
-        blocks = attract_launch_opt(st, s, aa, want_loss != 0);
-        TSNE_LAUNCH_CHECK();
-        ctx->timers.end("opt.attract", st);
-        s->log_attract(t, want_loss ? 1 : 3);
-    }
+    // 4. the attraction's sums + update for owned rows
+    TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     // update + centre: combine_update (with the mean's block partials when one
     // rank holds every row), mean, centre + write-back of the caller's Y
     ctx->timers.begin("opt.update", st);
     const bool fused_mean = world == 1;
     const int c = s->cur;
-    // (one rank: mean2_final; TSNE_MEAN_LASTBLOCK=1 finalises the mean in
-    // combine_update's last block instead -- one launch fewer, but 3907
-    // same-address arrival atomics at 1M rows: update 0.062 -> 0.085 ms)
-    static const bool lastblk = [] { const char *e = getenv("TSNE_MEAN_LASTBLOCK"); return e && e[0] == '1'; }();
-    const bool last_block = fused_mean && lastblk;
     combine_launch<1>(st, s->L0, s->L1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
-                      s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr,
-                      last_block ? s->mcnt : nullptr, (double)n, s->scal + 2);
-    if (want_loss) record_loss(ctx, s, t, blocks, overlap, ex);
+                      s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
+    if (want_loss) record_loss(ctx, s, t, blocks, true, ex);
     // 5. exchange (all-gather of the owned slices) + 6. centre
     if (fused_mean) {
-        if (!last_block)
-            hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256),
-                               (double)n, s->scal + 2);
+        hipLaunchKernelGGL(mean2_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256),
+                           (double)n, s->scal + 2);
     } else {
         gather_Ynew(ctx, s);
         for (int k = 0; k < 2; ++k) {
@@ -2207,6 +2107,11 @@ int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, doub
         if (ms) ms[e] = v[e];
     }
     return k;
+}
+
+BHTree *opt_tree(tsne_ctx *ctx) {
+    OptState *s = ctx->opt;
+    return (s && s->C == 2) ? &s->tree : nullptr;
 }
 
 double opt_last_z(tsne_ctx *ctx) {

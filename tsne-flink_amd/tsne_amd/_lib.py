@@ -80,6 +80,10 @@ SIGNATURES = {
     "tsne_dev_opt_last_z": (C.c_int, [P, PD]),
     "tsne_dev_opt_attract_log": (C.c_int, [P, P, P, P, I32, PI32]),
     "tsne_ctx_stage_ms": (C.c_int, [P, C.c_char_p, P, I32, PI32]),
+    "tsne_ctx_set_option": (C.c_int, [P, C.c_char_p, D]),
+    "tsne_ctx_get_option": (C.c_int, [P, C.c_char_p, PD]),
+    "tsne_hip_versions": (C.c_int, [PI32, PI32]),
+    "tsne_ctx_counter": (C.c_int, [P, C.c_char_p, PI64]),
 }
 
 _lib = None
@@ -101,16 +105,24 @@ def lib():
         # (same soname as /opt/rocm's).  Loaded first, it is the one this
         # library binds to; if this library initialised /opt/rocm's runtime
         # first, torch's own would later find no GPU ("No HIP GPUs are
-        # available", measured on the GPU box).  So torch, when present, goes first.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # available", measured on the GPU box).  So torch, when present, goes
+        # first (TSNE_NO_TORCH_PRELOAD=1: not; a broken torch install only
+        # skips the preload).  The runtime that was loaded must then be of the
+        # major version the library was built against (checked below).
+        if not os.environ.get("TSNE_NO_TORCH_PRELOAD"):
+            try:
+                import torch  # noqa: F401
+            except Exception:  # noqa: BLE001 -- any failure: load without it
+                pass
         L = C.CDLL(str(path))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        built, rt = C.c_int32(), C.c_int32()
+        if L.tsne_hip_versions(C.byref(built), C.byref(rt)) == 0 and rt.value // 10**7 != built.value // 10**7:
+            raise TsneError(-2, f"{path} was built for HIP {built.value} but the process loaded HIP runtime "
+                                f"{rt.value} (major versions differ)")
         _lib = L
     return _lib
 

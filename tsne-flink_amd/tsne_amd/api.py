@@ -71,6 +71,21 @@ class Context:
         check(lib().tsne_ctx_create_multi(_ptr(devs), len(devs), C.byref(self._h)))
         return self
 
+    def set_option(self, key, value):
+        """tsne_ctx_set_option: a per-handle tunable (include/tsne_hip.h lists the keys)."""
+        check(lib().tsne_ctx_set_option(self._h, key.encode(), float(value)))
+
+    def get_option(self, key):
+        out = C.c_double()
+        check(lib().tsne_ctx_get_option(self._h, key.encode(), C.byref(out)))
+        return out.value
+
+    def counter(self, name):
+        """tsne_ctx_counter: a diagnostic counter of the last call (e.g. "bh.narrow_groups")."""
+        out = C.c_int64()
+        check(lib().tsne_ctx_counter(self._h, name.encode(), C.byref(out)))
+        return out.value
+
     def rank_world(self):
         r, w = C.c_int32(), C.c_int32()
         check(lib().tsne_ctx_rank(self._h, C.byref(r), C.byref(w)))
