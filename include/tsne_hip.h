@@ -126,6 +126,8 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "mom_tol" 1e-12           subtree-moment truncation bound (2-D);
  *   "near_tol3_early" 1e-7, "near_tol3_late" 5e-6, "mom3_tol" 1e-12, and
  *   "oct_moments" 1           the same for the 3-D octree;
+ *   "oct_records" 1           3-D: octal records and the 8-query record
+ *                             traversal (0: the binary-node walk);
  *   "root_tile" 1             root-tile shortcut of the small-embedding phase;
  *   "attract_tiles" 1         tiled attraction where the labels allow it;
  *   "attract_cfg" -1          its tile shape (-1 automatic, 0..3);
@@ -137,7 +139,14 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "knn_bf16" 1              kNN threshold filter on bf16x3 MFMA (0: the
  *                             f32-input MFMA; results are identical);
  *   "narrow" 3                BH: 64-query groups costing >= this x the mean
- *                             run in the narrow layout (0: off).
+ *                             run in the narrow layout (0: off).  The
+ *                             selection reads the previous traversal's costs:
+ *                             the optimizer's previous iteration, and for the
+ *                             single-call operators only with
+ *   "reuse_costs" 0           1: tsne_gradient / tsne_repulsion select from the
+ *                             previous call's costs (results then depend on
+ *                             the call history at rounding level; 0 keeps
+ *                             every single call a function of its input).
  * Unknown keys and out-of-range values return TSNE_ERR_ARG. */
 int tsne_ctx_set_option(tsne_ctx *ctx, const char *key, double value);
 /* HIP runtime versions (HIP_VERSION encoding, major * 10^7 + minor * 10^5 +

@@ -28,6 +28,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     with T.Context(0) as ctx:
+        ctx.set_option("reuse_costs", 1)   # repeated calls: the narrow selection from the previous call
         for kv in a.option:
             key, val = kv.split("=", 1)
             ctx.set_option(key, float(val))

@@ -75,12 +75,17 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--iterations", type=int, default=1000)
     ap.add_argument("--skip-single", action="store_true")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="tsne_ctx_set_option on both handles (e.g. narrow=0, recut=1)")
     a = ap.parse_args()
+    opts = {kv.split("=", 1)[0]: float(kv.split("=", 1)[1]) for kv in a.option}
     dev = torch.device("cuda", 0)
     P, Y0 = build_p(a.n, 128, 90, dev)
-    out = {"n": a.n, "world": a.world, "iterations": a.iterations, "recut": os.environ.get("TSNE_RECUT", "0")}
+    out = {"n": a.n, "world": a.world, "iterations": a.iterations, "options": opts}
     if not a.skip_single:
         with T.Context(0) as one:
+            for k_, v_ in opts.items():
+                one.set_option(k_, v_)
             t_setup, _ = run(one, P, Y0, 1)
             t_full, loss1 = run(one, P, Y0, a.iterations)
         out.update({"single_call_s": t_full, "single_setup_s": t_setup, "single_loop_s": t_full - t_setup,
@@ -88,6 +93,8 @@ def main():
     path = os.path.join(tempfile.mkdtemp(), "serial.json")
     os.environ["TSNE_LOOP_SERIAL"] = path
     m = T.Context.multi([0] * a.world)
+    for k_, v_ in opts.items():
+        m.set_option(k_, v_)
     try:
         t_w, lossw = run(m, P, Y0, a.iterations)
     finally:

@@ -33,6 +33,7 @@ def layouts(Y, theta, factor):
     selection reads the previous traversal's costs: a first call records them),
     and the number of narrow groups."""
     with T.Context(0) as c:
+        c.set_option("reuse_costs", 1)
         c.set_option("narrow", 0)
         F0, z0 = c.repulsion(Y, theta)
         assert c.counter("bh.narrow_groups") == 0
@@ -79,6 +80,18 @@ def test_narrow_with_duplicates_and_ties():
         tol = c.get_option("near_tol_early")
     assert np.abs(z1 - zi).max() <= tol * zi.max()
     assert np.abs(F1 - rep).max() <= tol * np.abs(rep).max()
+
+
+def test_single_calls_are_history_free():
+    """By default (reuse_costs 0) a single call is a function of its input:
+    the same call twice gives the same bits whatever ran before."""
+    Y = clustered(20_000, 7)
+    with T.Context(0) as c:
+        F0, z0 = c.repulsion(Y, 0.5)
+        c.repulsion(Y * 1.5, 0.5)
+        F1, z1 = c.repulsion(Y, 0.5)
+        assert c.counter("bh.narrow_groups") == 0
+    assert np.array_equal(F0, F1) and np.array_equal(z0, z1)
 
 
 def test_narrow_small_embedding_moments():
@@ -134,3 +147,30 @@ def test_optimizer_narrow_deterministic_and_equal():
     assert np.abs(Ya - Yc).max() <= 1e-6 * np.abs(Yc).max()
     for t in lc:
         assert abs(la[t] - lc[t]) <= 1e-7 * abs(lc[t]), t
+
+
+@pytest.mark.parametrize("n,scale,theta", [(3000, 1e-4, 0.5), (20000, 0.02, 0.5), (20000, 3.0, 0.5),
+                                           (20000, 0.1, 0.25), (600, 1.0, 0.0)])
+def test_octal_records_match_binary_walk_and_oracle(n, scale, theta):
+    """3-D: the octal-record traversal (8 queries x 8 children per wave) and the
+    binary-node walk ("oct_records" 0) against the octree restatement
+    (oracle_gradient3): the same summarised cells; tiles are taken at real
+    cells only by the records, within the near-exact bound."""
+    from test_gpu_parity import random_problem
+    rp, col, val = random_problem(n, 10, seed=n + int(scale * 100))
+    Y = np.random.default_rng(n).normal(size=(n, 3)) * scale
+    r = O.gradient3(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
+    F_o, z_o = r["rep"], r["zi"]
+    tol = 1e-12 if theta == 0.0 else 1e-6
+    out = {}
+    for rec in (1, 0):
+        with T.Context(0) as c:
+            c.set_option("oct_records", rec)
+            g, Z, loss = c.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
+            F, z = c.repulsion(Y, theta)
+        assert np.abs(g - r["grad"]).max() <= tol * np.abs(r["grad"]).max(), rec
+        assert abs(Z - r["Z"]) <= 1e-7 * r["Z"], rec
+        assert np.abs(z - z_o).max() <= 1e-7 * z_o.max(), rec
+        assert np.abs(F - F_o).max() <= 1e-6 * np.abs(F_o).max(), rec
+        out[rec] = (F, z)
+    assert np.abs(out[1][1] - out[0][1]).max() <= 2e-7 * out[0][1].max()

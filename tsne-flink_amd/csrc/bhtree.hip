@@ -1590,6 +1590,8 @@ struct TravLDS {
     QRec srec[4][4];
     int32_t bref[4][4];
     uint64_t bmask[4][4];
+    int32_t bref2[4][4];  // the 64-query layout's prefetched batch (software pipeline)
+    uint64_t bmask2[4][4];
 };
 
 // Stage the records of stack entries [sp, sp + k) of wave w into LDS (one
@@ -1688,15 +1690,12 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
     const int64_t kq = g0 + grp * 64 + part * NQ + q;
     const bool valid = kq < g1;
-    const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
-    const int64_t e = h * 64 + part * NQ + q;   // this query's moment list
+    const int32_t s = valid ? (qlist ? qlist[kq] : (int32_t)kq) : -1;   // sorted position (< 2^31)
     if (part == 0 && lane == 0) { ttask_n[grp] = 0; tcost[grp] = 0; }   // tile_apply: nothing for this group
     const long long t_start = COST ? clock64() : 0;
     const unsigned long long w_start = STATS ? wall_clock64() : 0;
     double qx = 0.0, qy = 0.0;
     if (valid) { const double2 qq = pos[s]; qx = qq.x; qy = qq.y; }
-    const double qmag = fabs(qx) + fabs(qy);
-    const int ndup = valid ? dupc[s] : 0;
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0;
     int32_t npops = 0, ntilepts = 0, ntask = 0, nwant = 0;
@@ -1711,8 +1710,6 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
             sp = 1;
         }
     }
-    // same-query lanes of earlier records (moment-task order within a pass)
-    const uint64_t qcol = 0x0001000100010001ull << (4 * q);
     while (sp > 0) {
         const int kn = sp > STACK / 2 ? 1 : (sp < NKP ? sp : NKP);
         sp -= kn;
@@ -1725,7 +1722,7 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
         bool act = kin && valid && ((msk >> q) & 1u);
         const int nflags = nd.nch;
         bool tile = false;
-        if ((nflags & QNCH_TILE) && act) tile = tile_test(nd, qx, qy, qmag);
+        if ((nflags & QNCH_TILE) && act) tile = tile_test(nd, qx, qy, fabs(qx) + fabs(qy));
         if (__ballot(tile)) {
             const int a = nd.first, b = nd.last, cnt = nd.cnt;
             // moment path: decided once per (record, query) by its child-0 lane,
@@ -1733,15 +1730,17 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
             const bool mw = tile && c == 0 && cnt >= MOM_MIN_POINTS && moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy, mom_tol);
             nwant += mw ? 1 : 0;
             const uint64_t U = __ballot(mw && mom_on);
+            // same-query lanes of earlier records: the task order within a pass
+            const uint64_t qcol = 0x0001000100010001ull << (4 * q);
             const int before = __popcll(U & qcol & lanemask_lt());
             const bool usem = mw && mom_on && ntask + before < MOM_TASKS;
-            if (usem) nv.mtask[e * MOM_TASKS + ntask + before] = L.bref[w][kk];
+            if (usem) nv.mtask[(h * 64 + part * NQ + q) * MOM_TASKS + ntask + before] = L.bref[w][kk];
             ntask = min(MOM_TASKS, ntask + (int)__popcll(U & qcol));
             const uint64_t UM = __ballot(usem);
             const bool dense = tile && !((UM >> (lane & ~3)) & 1ull);
             // the range holds whole equal-key runs: the query's duplicates (itself
             // included) add exactly 1 each to z in the leaf sum, taken off here
-            if (tile && c == 0 && s >= a && s <= b) zs -= (double)ndup;
+            if (tile && c == 0 && s >= a && s <= b) zs -= (double)dupc[s];
             if (STATS && tile && c == 0) nvis += (unsigned long long)(b - a + 1);
             // dense: the query's 4 lanes split the subtree's points
             int p = dense ? a + c : 1, last = dense ? b : 0;
@@ -1826,7 +1825,7 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
         F[s] = make_double2(fx, fy);
         Z[s] = zs;
     }
-    if (k == 0 && c == 0) nv.mtask_n[e] = valid ? ntask : 0;
+    if (k == 0 && c == 0) nv.mtask_n[h * 64 + part * NQ + q] = valid ? ntask : 0;
     const int wwant = wave_sum(nwant);
     if (lane == 0) {
         nv.ncost[h * NPARTS + part] = npops + (ntilepts >> 6);
@@ -1883,8 +1882,8 @@ __global__ __launch_bounds__(256) void bh_traverse_narrow(
 // Traversal kernel (see the comment above), one 64-query group per wave;
 // groups the narrow waves take (nv.nflag) return at once.  MODE 0 plain; 1
 // wave run times into the multi-GPU cost buckets; 2 every counter (profiling).
-template <int MODE>
-__global__ __launch_bounds__(256) void bh_traverse(
+template <int MODE, bool PIPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0,
@@ -1927,19 +1926,46 @@ __global__ __launch_bounds__(256) void bh_traverse(
         }
     }
     // Pop up to 4 cells at a time: their records are fetched with one round of
-    // coalesced 16-byte vector loads into LDS, then processed one by one from
-    // LDS broadcasts.
-    while (sp > 0) {
-        const int kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
+    // coalesced 16-byte vector loads, then processed one by one from LDS
+    // broadcasts.  Software pipeline (PIPE): while one batch is processed, the
+    // next one (the entries below it) is already popped and its records are in
+    // flight in registers (one 16-byte piece per lane), written over the
+    // processed batch in LDS afterwards -- the record latency hides behind a
+    // batch's VALU work.  Every entry is still processed once; only the order
+    // changes.
+    int cur = 0, kb = 0;
+    if (sp > 0) {
+        kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
         sp -= kb;
         stage_records(L, w, lane, sp, kb, qrec);
+    }
+    while (kb > 0) {
+        int kn = 0;
+        uint4 pre = make_uint4(0u, 0u, 0u, 0u);
+        // the next batch: popped now, its records loaded into registers (only
+        // while the stack is at most half full: beyond, strict depth-first
+        // single pops keep its depth bounded as without the pipeline)
+        if (PIPE && sp > 0 && sp <= STACK / 2) {
+            kn = sp < 4 ? sp : 4;
+            sp -= kn;
+            int32_t *nbref = cur ? L.bref[w] : L.bref2[w];
+            uint64_t *nbmask = cur ? L.bmask[w] : L.bmask2[w];
+            if (lane < kn) { nbref[lane] = L.sref[w][sp + lane]; nbmask[lane] = L.smask[w][sp + lane]; }
+            if (lane < QREC_V4 * kn) {
+                const int rr = lane / QREC_V4, part = lane - rr * QREC_V4;
+                pre = reinterpret_cast<const uint4 *>(qrec + L.sref[w][sp + rr])[part];
+            }
+        }
+        const QRec *brec = L.srec[w];
+        const int32_t *bref_c = cur ? L.bref2[w] : L.bref[w];
+        const uint64_t *bmask_c = cur ? L.bmask2[w] : L.bmask[w];
         npops += kb;
         for (int r = 0; r < kb; ++r) {
             if (STATS) ++wpops;
-            const int ref = __builtin_amdgcn_readfirstlane(L.bref[w][r]);
-            const uint64_t msk = L.bmask[w][r];
+            const int ref = __builtin_amdgcn_readfirstlane(bref_c[r]);
+            const uint64_t msk = bmask_c[r];
             bool act = (msk >> lane) & 1ull;
-            const QRec &nd = L.srec[w][r];
+            const QRec &nd = brec[r];
             // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
             bool tile = false;
             const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
@@ -2036,6 +2062,25 @@ __global__ __launch_bounds__(256) void bh_traverse(
                     }
                 }
             }
+        }
+        if (kn > 0) {   // the prefetched batch into the other buffer
+            __builtin_amdgcn_wave_barrier();   // the processed batch's LDS reads are done
+            if (lane < QREC_V4 * kn) {
+                const int rr = lane / QREC_V4, part = lane - rr * QREC_V4;
+                reinterpret_cast<uint4 *>(&L.srec[w][rr])[part] = pre;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the batch is in LDS
+            __builtin_amdgcn_wave_barrier();
+            cur ^= 1;
+            kb = kn;
+        } else if (sp > 0) {   // nothing prefetched (the stack was empty, or no pipeline): a fresh batch
+            kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
+            sp -= kb;
+            cur = 0;
+            stage_records(L, w, lane, sp, kb, qrec);
+        } else {
+            kb = 0;
         }
     }
     if (valid) {
@@ -2828,7 +2873,8 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
                                                           32, ctx->stream));
     t.osort_tmp_bytes = ob;
     t.osort_tmp = ws.get<uint8_t>(pre + "osort_tmp", ob);
-    t.have_cost = false;
+    t.sel_waves = 0;
+    t.ran_narrow = false;
     t.ch_C = ws.get<int32_t>(pre + "ch_C", qwaves + 1);
     t.ch_slot0 = ws.get<int32_t>(pre + "ch_slot0", qwaves + 1);
     t.ch_slot_w = ws.get<int32_t>(pre + "ch_slot_w", t.tile_waves);
@@ -2848,6 +2894,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
     TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * t.tile_waves, ctx->stream));
     t.hlist = ws.get<int32_t>(pre + "hlist", t.nar_hmax);
     t.hcount = ws.get<int32_t>(pre + "hcount", 1);
+    t.hran = ws.get<int32_t>(pre + "hran", 1);
     TSNE_HIP(hipMemsetAsync(t.hcount, 0, sizeof(int32_t), ctx->stream));
     t.ncost = ws.get<int32_t>(pre + "ncost", (size_t)t.nar_hmax * NPARTS);
     t.nmtask = ws.get<int32_t>(pre + "nmtask", (size_t)t.nar_hmax * 64 * MOM_TASKS);
@@ -2856,9 +2903,9 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
 }
 
 int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t) {
-    if (!t.nflag_set || !t.hcount) return 0;
+    if (!t.ran_narrow || !t.hran) return 0;
     int32_t h = 0;
-    TSNE_HIP(hipMemcpyAsync(&h, t.hcount, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipMemcpyAsync(&h, t.hran, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     return h;
 }
@@ -2867,6 +2914,10 @@ BHTree &bh_single_tree(tsne_ctx *ctx, int64_t n) {
     if (!ctx->single_tree) ctx->single_tree = new BHTree();
     BHTree &t = *ctx->single_tree;
     if (t.n != n) bh_alloc(ctx, t, n, "bh1.");
+    // a single call is a function of its input alone unless the caller asked
+    // for the previous call's costs (Options::reuse_costs): without costs the
+    // traversal takes the 64-query layout everywhere
+    if (!ctx->opts.reuse_costs) t.sel_waves = 0;
     return t;
 }
 
@@ -3053,24 +3104,24 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the waves' run times
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    auto kern = mode == 2 ? bh_traverse<2> : mode == 1 ? bh_traverse<1> : bh_traverse<0>;
+    const bool pipe = ctx->opts.bh_pipeline != 0;
+    auto kern = pipe ? (mode == 2 ? bh_traverse<2, true> : mode == 1 ? bh_traverse<1, true> : bh_traverse<0, true>)
+                     : (mode == 2 ? bh_traverse<2, false> : mode == 1 ? bh_traverse<1, false> : bh_traverse<0, false>);
     const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
-    // heavy groups of this traversal from the previous one's costs (narrow
-    // layout; none on a tree's first traversal or with Options::narrow = 0)
+    // heavy groups: selected after the previous traversal of the same query
+    // count from its costs (narrow_select at the end of this function, so
+    // that nothing delays this traversal's dispatch behind the tree build);
+    // none on a tree's first traversal or with Options::narrow = 0
     NarrowView nv;
     const double nfac = ctx->opts.narrow;
-    const bool narrow = nfac > 0.0 && t.have_cost && t.cost_waves == waves;
+    const bool narrow = nfac > 0.0 && t.sel_waves == waves;
     if (narrow) {
-        hipLaunchKernelGGL(narrow_select, dim3(1), dim3(1024), 0, st, t.wcost, waves, t.nflag, t.ncost, t.hlist,
-                           t.hcount, t.nar_hmax, nfac, std::min<int64_t>(t.nar_hmax, narrow_fill(ctx, waves)));
         nv.hlist = t.hlist; nv.hcount = t.hcount; nv.ncost = t.ncost; nv.mtask = t.nmtask; nv.mtask_n = t.nmtask_n;
         nv.nflag = t.nflag;
         nv.nbn = (int32_t)ceil_div(t.nar_hmax * NPARTS, 4);
-    } else if (t.nflag_set) {
-        TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * t.tile_waves, st));
     }
-    t.nflag_set = narrow;
+    t.ran_narrow = narrow;
     const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
     if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
         TSNE_HIP(hipEventRecord(ctx->aux_ev[0], st));
@@ -3085,8 +3136,6 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                        t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
                        t.tcost, clab, nv);
     if (narrow) TSNE_HIP(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
-    t.have_cost = true;
-    t.cost_waves = waves;
     // tile chunks of heavy waves (ChunkView): the single-workgroup plan while
     // the per-wave costs fit its LDS, else the multi-launch plan and block sort
     ChunkView cv;
@@ -3114,9 +3163,20 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
     hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.ch_Fp, t.ch_Zp, t.ch_C,
                        t.ch_slot0, s0, s1, qlist, dF, dz);
-    if (narrow)
+    if (narrow) {
         hipLaunchKernelGGL(narrow_moment_apply, dim3(ceil_div(t.nar_hmax * 64, 256)), dim3(256), 0, st, t.pos,
                            t.nodes, t.mom, t.hlist, t.hcount, t.nmtask, t.nmtask_n, s0, s1, qlist, dF, dz);
+        TSNE_HIP(hipMemcpyAsync(t.hran, t.hcount, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    }
+    // the next traversal's heavy groups (of the same query count) from this one's costs
+    if (nfac > 0.0) {
+        if (!narrow) TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * waves, st));   // no stale slots
+        hipLaunchKernelGGL(narrow_select, dim3(1), dim3(1024), 0, st, t.wcost, waves, t.nflag, t.ncost, t.hlist,
+                           t.hcount, t.nar_hmax, nfac, std::min<int64_t>(t.nar_hmax, narrow_fill(ctx, waves)));
+        t.sel_waves = waves;
+    } else {
+        t.sel_waves = 0;
+    }
     TSNE_LAUNCH_CHECK();
 }
 

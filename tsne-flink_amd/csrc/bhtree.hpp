@@ -136,7 +136,6 @@ struct BHTree {
     int32_t *border = nullptr, *torder = nullptr;  // per block: traversal / tile_apply order
     void *osort_tmp = nullptr;
     size_t osort_tmp_bytes = 0;
-    bool have_cost = false;
     // tile chunks (bhtree.hip ChunkView): chunks per traversal wave, first
     // chunk slot (waves + 1), slot -> wave and chunk | C << 16, slot costs,
     // slot count; partial sums per chunk slot lane
@@ -151,10 +150,11 @@ struct BHTree {
     // per group its heavy slot + 1 (or 0), the heavy list and count, per
     // narrow wave its cost, per narrow query its moment tasks
     int32_t *nflag = nullptr, *hlist = nullptr, *hcount = nullptr, *ncost = nullptr;
+    int32_t *hran = nullptr;     // heavy groups the last traversal ran narrow
     int32_t *nmtask = nullptr, *nmtask_n = nullptr;
     int64_t nar_hmax = 0;
-    bool nflag_set = false;      // some nflag may be set (cleared before a traversal without selection)
-    int64_t cost_waves = 0;      // query waves of the traversal the costs came from
+    int64_t sel_waves = 0;       // query waves the current selection is for (0: none)
+    bool ran_narrow = false;     // the last traversal used a selection
 };
 
 // Allocate (from ctx->ws, buffers named pre + field) for n points.  One

@@ -117,6 +117,7 @@ static const OptionField k_options[] = {
     {"near_tol3_late", &Options::near_tol3_late, nullptr, 0.0, 1e-2},
     {"mom3_tol", &Options::mom3_tol, nullptr, 0.0, 1e-4},
     {"oct_moments", nullptr, &Options::oct_moments, 0, 1},
+    {"oct_records", nullptr, &Options::oct_records, 0, 1},
     {"root_tile", nullptr, &Options::root_tile, 0, 1},
     {"attract_tiles", nullptr, &Options::attract_tiles, 0, 1},
     {"attract_cfg", nullptr, &Options::attract_cfg, -1, 3},
@@ -125,6 +126,8 @@ static const OptionField k_options[] = {
     {"recut", nullptr, &Options::recut, 0, 1},
     {"knn_bf16", nullptr, &Options::knn_bf16, 0, 1},
     {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
+    {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
+    {"bh_pipeline", nullptr, &Options::bh_pipeline, 0, 1},
 };
 static const OptionField &option_field(const char *key) {
     for (const OptionField &f : k_options)

@@ -169,6 +169,7 @@ struct Options {
     double near_tol3_early = 1e-7, near_tol3_late = 5e-6;  // the 3-D octree's
     double mom3_tol = 1e-12;
     int oct_moments = 1;      // 3-D subtree moments
+    int oct_records = 1;      // 3-D: octal records + the 8-query record traversal (0: the binary-node walk)
     int root_tile = 1;        // root-tile shortcut of the small-embedding phase
     int attract_tiles = 1;    // tiled attraction (attract_tiles) where the labels allow it
     int attract_cfg = -1;     // its tile shape: -1 by rows per rank, else ATCfg0..3
@@ -177,6 +178,9 @@ struct Options {
     int recut = 0;            // several ranks on the tiled layout: re-cut by BH cost instead of relabels
     int knn_bf16 = 1;         // kNN threshold filter: bf16x3 MFMA (0: f32-input MFMA)
     double narrow = 3.0;      // BH: 64-query groups costing >= narrow x the mean run in the narrow layout (0: off)
+    int bh_pipeline = 1;      // BH traversal: the next record batch in flight while one is processed
+    int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
+                              // previous call's costs (results then depend on the call history at rounding level)
 };
 
 }  // namespace tsne

@@ -824,6 +824,327 @@ __global__ __launch_bounds__(256) void oct_mom_apply(const double4 *__restrict__
     Z[s] += zs;
 }
 
+// ---- Octal records and the record traversal (the 2-D design of bhtree.hip:
+// quad records + batched record fetches, with the narrow lane layout).
+constexpr double OACC_MARGIN = 2.5e-14;   // sure-accept bound margin (bhtree.hpp QACC_MARGIN)
+constexpr double OACC_BAND = (1.0 - OACC_MARGIN) / (1.0 + OACC_MARGIN);
+
+// One thread per binary node: the record of every real cell (h >= 0, no key
+// tie); its children found through <= 2 levels of transparent nodes, in key
+// order.  Records are assembled in LDS and copied out as coalesced 16-byte
+// pieces (ORec is 496 bytes).
+constexpr int OREC_BLK = 64;
+__global__ __launch_bounds__(OREC_BLK) void build_orec(const OctNode *__restrict__ nodes,
+                                                       const double4 *__restrict__ pos,
+                                                       const int32_t *__restrict__ meta, double inv_theta,
+                                                       double near_dmax, ORec *__restrict__ orec) {
+    __shared__ ORec sr[OREC_BLK];
+    __shared__ int32_t sreal[OREC_BLK];
+    const int m = meta[0];
+    const int b0 = blockIdx.x * OREC_BLK;
+    const int nrec = min(OREC_BLK, m - 1 - b0);
+    if (nrec <= 0) return;
+    const int i = b0 + threadIdx.x;
+    if (threadIdx.x < nrec) {
+        const OctNode &nd = nodes[i];
+        const bool real = nd.h >= 0.0 && nd.delta < 63;
+        sreal[threadIdx.x] = real;
+        if (real) {
+            ORec &r = sr[threadIdx.x];
+            r.cx = nd.cx; r.cy = nd.cy; r.cz = nd.cz;
+            r.rball2 = nd.rball * nd.rball * (1.0 - 1e-9);
+            r.thr = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax);
+            r.bx0 = nd.bx0; r.bx1 = nd.bx1; r.by0 = nd.by0; r.by1 = nd.by1; r.bz0 = nd.bz0; r.bz1 = nd.bz1;
+            r.first = nd.first; r.last = nd.last; r.cnt = nd.cnt; r.pad = 0;
+            int nc = 0, kinds = 0;
+            auto put = [&](int32_t c) {
+                if (c < 0) {
+                    const double4 p = pos[~c];
+                    r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ccz[nc] = p.z;
+                    r.ch[nc] = 0.0; r.ca[nc] = 0.0; r.cref[nc] = c; r.ccnt[nc] = 1;
+                    kinds |= OK_LEAF << (2 * nc);
+                } else {
+                    const OctNode &cn = nodes[c];
+                    r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; r.ccz[nc] = cn.cz;
+                    r.cref[nc] = c; r.ccnt[nc] = cn.cnt;
+                    if (cn.delta >= 63) {
+                        r.ch[nc] = 0.0; r.ca[nc] = 0.0;
+                        kinds |= OK_TIE << (2 * nc);
+                    } else {
+                        r.ch[nc] = cn.h; r.ca[nc] = cn.h * inv_theta * (1.0 + OACC_MARGIN);
+                        kinds |= OK_CELL << (2 * nc);
+                    }
+                }
+                ++nc;
+            };
+            auto transparent = [&](int32_t c) { return c >= 0 && nodes[c].delta < 63 && nodes[c].h < 0.0; };
+            const int32_t top[2] = {nd.left, nd.right};
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int32_t c = top[k];
+                if (transparent(c)) {
+                    const int32_t sub[2] = {nodes[c].left, nodes[c].right};
+#pragma unroll
+                    for (int k2 = 0; k2 < 2; ++k2) {
+                        const int32_t c2 = sub[k2];
+                        if (transparent(c2)) { put(nodes[c2].left); put(nodes[c2].right); }
+                        else put(c2);
+                    }
+                } else {
+                    put(c);
+                }
+            }
+            for (int k = nc; k < 8; ++k) {
+                r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ccz[k] = 0.0; r.ch[k] = 0.0; r.ca[k] = 0.0;
+                r.cref[k] = 0; r.ccnt[k] = 0;
+            }
+            // a tile test can pass here unless the box's half-diagonal alone
+            // (the least max-corner distance of any query) exceeds both bounds
+            const double hx = 0.5 * (nd.bx1 - nd.bx0), hy = 0.5 * (nd.by1 - nd.by0), hz = 0.5 * (nd.bz1 - nd.bz0);
+            const bool tile = nd.rball > 0.0 || (hx * hx + hy * hy + hz * hz) * (1.0 - 1e-9) <= r.thr;
+            r.nch = nc | (tile ? ONCH_TILE : 0);
+            r.kinds = kinds;
+        }
+    }
+    __syncthreads();
+    constexpr int V = sizeof(ORec) / 16;
+    const uint4 *src = reinterpret_cast<const uint4 *>(sr);
+    uint4 *dst = reinterpret_cast<uint4 *>(orec + b0);
+    for (int k = threadIdx.x; k < nrec * V; k += OREC_BLK)
+        if (sreal[k / V]) dst[k] = src[k];
+}
+
+// Record traversal: one wave = 8 queries x 8 children (lane = 8 q + c).  The
+// wave's LDS stack holds (record, 8-bit query mask) entries, one per cell some
+// query opens; up to OKPOP records are fetched per round (coalesced 16-byte
+// pieces, latencies overlapped), then each is one sweep of the lanes: lane
+// (q, c) takes child c of the record for query q -- a leaf interacts (zero if
+// it is the query's own point), a cell is summarised when h / D < theta
+// (QuadTree.scala:133-134, 3-D D) or pushed, a key-tie group interacts point
+// by point.  Before that, per (record, query), the all-open / near-exact tests
+// (the 2-D path's, bhtree.hip): the subtree's exact leaf sum from its moments
+// (a task of the query's list, oct_mom_apply) or densely, the query's 8 lanes
+// splitting its points; a large tile the moments cannot take is traversed.
+// Each lane keeps its own partial sums; the query's 8 lanes are added by a
+// fixed xor butterfly at the end (deterministic).
+constexpr int OQ = 8;          // queries per wave
+constexpr int OKPOP = 4;       // records per fetch round
+constexpr int OSTACK = 512;    // batch rounds while <= OSTACK / 2 entries, then depth-first (+7 per level)
+template <bool DBG>
+__global__ __launch_bounds__(256) void oct_traverse_rec(
+    const double4 *__restrict__ pos, const int32_t *__restrict__ dupc, const OctNode *__restrict__ nodes,
+    const ORec *__restrict__ orec, const int32_t *__restrict__ meta, double theta, int64_t g0, int64_t g1,
+    const int32_t *__restrict__ qlist, int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
+    int32_t *__restrict__ mtask_n, double *__restrict__ F, double *__restrict__ Z,
+    unsigned long long *__restrict__ dbg, double mom_tol) {
+    __shared__ int32_t sref[4][OSTACK];
+    __shared__ uint32_t smask[4][OSTACK];
+    __shared__ ORec srec[4][OKPOP];
+    __shared__ int32_t bref[4][OKPOP];
+    __shared__ uint32_t bmask[4][OKPOP];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int q = lane >> 3, c = lane & 7;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + w;
+    const int64_t kq = g0 + wid * OQ + q;
+    const bool valid = kq < g1;
+    if (__ballot(valid) == 0) return;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
+    const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
+    double qx = 0.0, qy = 0.0, qz = 0.0;
+    if (valid) { const double4 p = pos[s]; qx = p.x; qy = p.y; qz = p.z; }
+    const double qmag = fabs(qx) + fabs(qy) + fabs(qz);
+    const int ndup = valid ? dupc[s] : 0;
+    const bool mom_on = mom_flag[0] != 0;
+    double fx = 0.0, fy = 0.0, fz = 0.0, zs = 0.0;
+    int ntask = 0, nwant = 0;
+    unsigned long long d_pops = 0, d_childs = 0, d_dense = 0, d_declined = 0;   // Options-free debug counters
+    int sp = 0;
+    // the root: a single point, a key-tie group, or a cell tested like any child
+    // (lane c = 0 of each query)
+    const int root = meta[1];
+    const bool r0 = valid && c == 0;
+    if (root == ~0) {
+        if (r0) { const double4 p = pos[0]; leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs); }
+    } else if (root >= 0) {
+        const OctNode &rt = nodes[root];
+        if (rt.delta >= 63) {
+            for (int p = rt.first; p <= rt.last; ++p) {
+                const double4 pp = pos[p];
+                if (r0) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+            }
+        } else {
+            bool open = false;
+            if (r0) {
+                const double dx = qx - rt.cx, dy = qy - rt.cy, dz = qz - rt.cz;
+                if (summarise3(rt.h, dx, dy, dz, th_lo, th_hi, theta))
+                    cell3(dx, dy, dz, dx * dx + dy * dy + dz * dz, rt.cnt, fx, fy, fz, zs);
+                else
+                    open = true;
+            }
+            const uint64_t om = __ballot(open);
+            uint32_t qm = 0;
+#pragma unroll
+            for (int k = 0; k < OQ; ++k) qm |= (uint32_t)((om >> (8 * k)) & 1ull) << k;
+            if (qm) {
+                if (lane == 0) { sref[w][0] = root; smask[w][0] = qm; }
+                sp = 1;
+            }
+        }
+    }
+    while (sp > 0) {
+        const int kb = sp > OSTACK / 2 ? 1 : (sp < OKPOP ? sp : OKPOP);
+        sp -= kb;
+        if (lane < kb) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
+        constexpr int V = sizeof(ORec) / 16;
+        for (int e = lane; e < V * kb; e += 64) {
+            const int rr = e / V, part = e - rr * V;
+            const int rf = sref[w][sp + rr];
+            reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(orec + rf)[part];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: the batch is in LDS
+        __builtin_amdgcn_wave_barrier();
+        for (int r = 0; r < kb; ++r) {
+            if (DBG && lane == 0) ++d_pops;
+            const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
+            const uint32_t msk = bmask[w][r];
+            bool act = valid && ((msk >> q) & 1u);
+            const ORec &nd = srec[w][r];
+            const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);
+            // all-open / near-exact tests, per (record, query): the subtree's exact leaf sum
+            bool tile = false;
+            if ((nflags & ONCH_TILE) && act) {
+                const double cdx = qx - nd.cx, cdy = qy - nd.cy, cdz = qz - nd.cz;
+                tile = cdx * cdx + cdy * cdy + cdz * cdz <= nd.rball2;
+                if (!tile) {
+                    const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1) +
+                                               fabs(nd.bz0) + fabs(nd.bz1));
+                    const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                    const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                    const double dzm = fmax(fabs(qz - nd.bz0), fabs(qz - nd.bz1)) + ex;
+                    tile = (dxm * dxm + dym * dym + dzm * dzm) * (1.0 + 1e-12) <= nd.thr;
+                }
+            }
+            if (__ballot(tile)) {
+                const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
+                const int cnt = __builtin_amdgcn_readfirstlane(nd.cnt);
+                // moments: decided by the query's lane c = 0 (one record per sweep: list order = record order)
+                bool usem = false;
+                if (tile && c == 0 && cnt >= MOM3_MIN) {
+                    double bcx, bcy, bcz, R;
+                    box3(nodes[ref], bcx, bcy, bcz, R);
+                    if (mom3_ok(qx - bcx, qy - bcy, qz - bcz, R, mom_tol)) {
+                        ++nwant;
+                        if (mom_on && ntask < MOM3_TASKS) {
+                            usem = true;
+                            mtask[s * MOM3_TASKS + ntask] = ref;
+                        }
+                    }
+                }
+                const uint64_t UM = __ballot(usem);
+                const bool mq = (UM >> (lane & ~7)) & 1ull;   // the query's moment decision
+                if (mq) ++ntask;                              // (every lane of the query: the same count)
+                // a large tile the moments cannot take: the lane keeps traversing it
+                const bool dense = tile && !mq && (b - a + 1) <= DENSE3_MAX;
+                if (DBG && tile && !mq && !dense && c == 0) ++d_declined;
+                const bool taken = mq || dense;
+                if (taken && c == 0 && s >= a && s <= b) zs -= (double)ndup;   // the query's own copies add 1 each
+                if (DBG && dense && c == 0) d_dense += (unsigned long long)(b - a + 1);
+                int p = dense ? a + c : 1, last = dense ? b : 0;
+                while (__ballot(p <= last)) {
+                    if (p <= last) {
+                        const double4 pp = pos[p];
+                        const double dx = qx - pp.x, dy = qy - pp.y, dz = qz - pp.z;
+                        const double rr = rcp2(__fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0))));
+                        const double sc = rr * rr;
+                        fx = __fma_rn(sc, dx, fx);
+                        fy = __fma_rn(sc, dy, fy);
+                        fz = __fma_rn(sc, dz, fz);
+                        zs += rr;
+                        p += 8;
+                    }
+                }
+                act = act && !taken;
+            }
+            if (__ballot(act) == 0) continue;
+            // child c of the record for query q
+            const int nch = nflags & 0xff;
+            const int kind = (__builtin_amdgcn_readfirstlane(nd.kinds) >> (2 * c)) & 3;
+            const bool has = act && c < nch;
+            if (DBG && has) ++d_childs;
+            const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c], dz = qz - nd.ccz[c];
+            const double D = __fma_rn(dx, dx, __fma_rn(dy, dy, dz * dz));
+            const bool isleaf = has && kind == OK_LEAF, iscell = has && kind == OK_CELL;
+            const double A = nd.ca[c];
+            bool acc = D > A;
+            if (iscell && !acc && !(D < A * OACC_BAND))
+                acc = nd.ch[c] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) < theta;
+            const bool takel = isleaf && !(dx == 0.0 && dy == 0.0 && dz == 0.0);
+            const bool takec = iscell && acc;
+            const double wm = takel ? 1.0 : (takec ? (double)nd.ccnt[c] : 0.0);
+            const double Qv = rcp2(1.0 + D);
+            const double mult = wm * Qv;
+            const double sc = mult * Qv;
+            fx = __fma_rn(sc, dx, fx);
+            fy = __fma_rn(sc, dy, fy);
+            fz = __fma_rn(sc, dz, fz);
+            zs += mult;
+            const bool tie = has && kind == OK_TIE;
+            if (__builtin_expect(__ballot(tie) != 0, 0) && tie) {   // a key-tie group: every point directly
+                const OctNode &tn = nodes[nd.cref[c]];
+                for (int p = tn.first; p <= tn.last; ++p) {
+                    const double4 pp = pos[p];
+                    leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+                }
+            }
+            // pushes: one entry per child some query opens, in child order
+            const uint64_t O = __ballot(iscell && !acc);
+            uint32_t mcq = 0;
+            if (q == 0 && c < nch) {
+#pragma unroll
+                for (int k = 0; k < OQ; ++k) mcq |= (uint32_t)((O >> (8 * k + c)) & 1ull) << k;
+            }
+            const uint64_t P = __ballot(mcq != 0u);
+            if (mcq) {
+                const int at = sp + (int)__popcll(P & lanemask_lt());
+                sref[w][at] = nd.cref[c];
+                smask[w][at] = mcq;
+            }
+            sp += (int)__popcll(P);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the pushes landed before the next reads
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    // the query's 8 lanes in a fixed xor butterfly (every lane the same bits)
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        fx += __shfl_xor(fx, o, 64); fy += __shfl_xor(fy, o, 64);
+        fz += __shfl_xor(fz, o, 64); zs += __shfl_xor(zs, o, 64);
+    }
+    if (valid && c == 0) {
+        F[3 * s] = fx;
+        F[3 * s + 1] = fy;
+        F[3 * s + 2] = fz;
+        Z[s] = zs;
+        mtask_n[s] = ntask;
+    }
+    if (DBG) {   // [0] wave pops, [1] lane child evaluations, [2] dense tile points, [3] declined tiles, [4] moment tasks
+        const unsigned long long a = wave_sum(d_childs), b2 = wave_sum(d_dense), c2 = wave_sum(d_declined),
+                                 e = wave_sum((unsigned long long)(c == 0 ? ntask : 0));
+        if (lane == 0) {
+            atomicAdd(dbg, d_pops * (64 / OQ));   // in 64-query-wave units, as the binary traversal's
+            atomicAdd(dbg + 1, a);
+            atomicAdd(dbg + 2, b2);
+            atomicAdd(dbg + 3, c2);
+            atomicAdd(dbg + 4, e);
+        }
+    }
+    const int ww = wave_sum(nwant);
+    if (lane == 0 && ww && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
+        atomicAdd(&mom_flag[1], ww);
+}
+
 }  // namespace
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
@@ -837,6 +1158,7 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
     t.dupc = ws.get<int32_t>("oct.dupc", n);
     t.pos = ws.get<double4>("oct.pos", n);
     t.nodes = ws.get<OctNode>("oct.nodes", n);
+    t.orec = ws.get<ORec>("oct.orec", n);
     t.agg = ws.get<double>("oct.agg", AGG3 * (size_t)n);
     t.parent_leaf = ws.get<int32_t>("oct.parent_leaf", n);
     t.parent_node = ws.get<int32_t>("oct.parent_node", n);
@@ -872,7 +1194,9 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
 }
 
-void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
+static double oct_near_dmax(const tsne_ctx *ctx, double theta, bool late);
+
+void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta, bool late) {
     hipStream_t st = ctx->stream;
     const int64_t n = t.n;
     hipLaunchKernelGGL(bbox3_partial, dim3(t.bbox_blocks), dim3(256), 0, st, dY, n, t.bbox_part);
@@ -891,6 +1215,10 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta) {
     hipLaunchKernelGGL(bottom_up3<512>, dim3(ceil_div(n, 512)), dim3(512), 0, st, t.pos, t.meta, t.W, inv_theta, t.nodes,
                        t.agg, t.parent_leaf, t.parent_node, t.arrive);
     hipLaunchKernelGGL(set_root3, dim3(1), dim3(1), 0, st, t.meta);
+    t.near_dmax = oct_near_dmax(ctx, theta, late);
+    if (ctx->opts.oct_records)
+        hipLaunchKernelGGL(build_orec, dim3(ceil_div(n, OREC_BLK)), dim3(OREC_BLK), 0, st, t.nodes, t.pos, t.meta,
+                           inv_theta, t.near_dmax, t.orec);
     // subtree moments (when the last traversal wanted them)
     hipLaunchKernelGGL(oct_mom_gate, dim3(1), dim3(1), 0, st, t.mom_flag);
     hipLaunchKernelGGL(oct_mom_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, n, t.meta, t.mom_flag, t.mcnt);
@@ -919,7 +1247,7 @@ static double oct_near_dmax(const tsne_ctx *ctx, double theta, bool late) {
 }
 
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF, double *dz,
-                   const int32_t *qlist, bool late) {
+                   const int32_t *qlist) {
     if (s1 <= s0) return;
     static const bool debug = getenv("TSNE_DEBUG_OCT") != nullptr;   // traversal counters on stderr (synchronises)
     unsigned long long *dbg = nullptr;
@@ -927,14 +1255,23 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
         dbg = ctx->ws.get<unsigned long long>("oct.dbg", 8);
         TSNE_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), ctx->stream));
     }
-    const int64_t waves = ceil_div(s1 - s0, 64);
-    if (debug)
-        hipLaunchKernelGGL(oct_traverse<true>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, oct_near_dmax(ctx, theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+    if (ctx->opts.oct_records) {   // the record traversal: 8 queries per wave
+        const int64_t rw = ceil_div(s1 - s0, OQ);
+        if (debug)
+            hipLaunchKernelGGL(oct_traverse_rec<true>, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                               t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz,
+                               dbg, ctx->opts.mom3_tol);
+        else
+            hipLaunchKernelGGL(oct_traverse_rec<false>, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos,
+                               t.dupc, t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                               dF, dz, dbg, ctx->opts.mom3_tol);
+    } else if (debug)
+        hipLaunchKernelGGL(oct_traverse<true>, dim3(ceil_div(ceil_div(s1 - s0, 64), 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                           t.nodes, t.meta, theta, t.near_dmax, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
                            dF, dz, dbg, ctx->opts.mom3_tol);
     else
-        hipLaunchKernelGGL(oct_traverse<false>, dim3(ceil_div(waves, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, oct_near_dmax(ctx, theta, late), s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+        hipLaunchKernelGGL(oct_traverse<false>, dim3(ceil_div(ceil_div(s1 - s0, 64), 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                           t.nodes, t.meta, theta, t.near_dmax, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
                            dF, dz, dbg, ctx->opts.mom3_tol);
     hipLaunchKernelGGL(oct_mom_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);

@@ -25,6 +25,28 @@ struct __attribute__((aligned(16))) OctNode {
     int32_t first, last;          // leaf range in sorted order
 };
 
+// Octal record of a real octree cell (the 2-D QRec's design, bhtree.hpp):
+// its own tile-test data plus the summaries of its <= 8 octree children,
+// found by descending through the transparent binary nodes of its level
+// (<= 2 binary levels: 3 key bits per octal level), so that the traversal
+// evaluates all children of an opened cell from one record load.  Child kinds
+// (bits 2c of `kinds`): OK_CELL a real cell (cref = node id), OK_LEAF one
+// point (cref = ~sorted index), OK_TIE a key-tie group (cref = node id: all
+// its points interact directly).
+constexpr int OK_CELL = 0, OK_LEAF = 1, OK_TIE = 2;
+constexpr int32_t ONCH_TILE = 0x100;   // nch flag: an all-open / near-exact tile test can pass here
+struct __attribute__((aligned(16))) ORec {
+    double cx, cy, cz;                     // centre of mass
+    double rball2, thr;                    // tile tests: rball^2 (1 - 1e-9); max(hmin / theta (1 - 1e-12), near_dmax)
+    double bx0, bx1, by0, by1, bz0, bz1;   // bounding box of the subtree's points
+    int32_t first, last, cnt, nch;         // leaf range, cumSize, children | ONCH_TILE
+    int32_t kinds, pad;
+    double ccx[8], ccy[8], ccz[8];         // child centres of mass (leaf: the point)
+    double ch[8], ca[8];                   // child half widths, sure-accept bounds ch / theta (1 + 2.5e-14)
+    int32_t cref[8], ccnt[8];
+};
+static_assert(sizeof(ORec) % 16 == 0, "records are fetched in 16-byte pieces");
+
 struct OctTree {
     int64_t n = 0;
     uint64_t *keys = nullptr, *keys_sorted = nullptr;
@@ -33,6 +55,8 @@ struct OctTree {
     int32_t *dupc = nullptr;                         // exact duplicates of each sorted point
     double4 *pos = nullptr;                          // sorted positions (x, y, z, 0)
     OctNode *nodes = nullptr;
+    ORec *orec = nullptr;                            // per binary node id, valid for real cells
+    double near_dmax = 0.0;                          // the records' near-exact radius (this build)
     double *agg = nullptr;
     int32_t *parent_leaf = nullptr, *parent_node = nullptr, *arrive = nullptr;
     int32_t *meta = nullptr;                         // [0] in-root points m, [1] root ref
@@ -51,13 +75,13 @@ struct OctTree {
 };
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n);
-// Octree of all n points of Y (n x 3, device).
-void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta);
+// Octree of all n points of Y (n x 3, device); late: the optimizer after
+// early exaggeration (the near-exact tolerance the records are built for).
+void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta, bool late = false);
 // Repulsion for the query slots [s0, s1) (sorted positions, or qlist[slot]:
 // a rank's own queries, ascending): F (n x 3, sorted order) and z written
-// at the sorted position.  late: the optimizer after early exaggeration
-// (the looser near-exact tolerance, BH_NEAR_TOL3_LATE).
+// at the sorted position (the near-exact tolerance of the build).
 void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, int64_t s1, double *dF,
-                   double *dz, const int32_t *qlist = nullptr, bool late = false);
+                   double *dz, const int32_t *qlist = nullptr);
 
 }  // namespace tsne

@@ -1787,13 +1787,13 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     const int64_t n = s->n;
     double *Y = s->Y[0];
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[0], st));
-    oct_build(ctx, s->otree, Y, p.theta);
+    oct_build(ctx, s->otree, Y, p.theta, ex == 1.0);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     if (ctx->world > 1) {
         build_qlist(ctx, s, s->otree.idx_sorted);
-        oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist, ex == 1.0);
+        oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist);
     } else {
-        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z, nullptr, ex == 1.0);
+        oct_repulsion(ctx, s->otree, p.theta, 0, n, s->F3, s->z, nullptr);
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     reduce_Z(ctx, s, s->z);
