@@ -1,12 +1,22 @@
-"""Summarise gpurun_out/ab_<k>.json (scripts/gpu_ab_bench.sh): loop, window,
-end to end, and the timeline's BH / attraction ms at a few iterations."""
-import json
-import os
+"""Summarise an A/B bench file of scripts/gpu_r4.sh (`# <variant>` lines, each
+followed by bench.py's JSON line): loop, end to end, and the timeline's
+tree / BH / attraction ms at a few iterations.
 
-idx = [l.split(None, 1) for l in open("gpurun_out/ab_index.txt").read().splitlines()]
-for k, name in idx:
-    d = json.load(open(f"gpurun_out/ab_{k}.json"))
+usage: python scripts/ab_summary.py gpurun_out/r4<TAG>/bench.jsonl"""
+import json
+import sys
+
+name = None
+for line in open(sys.argv[1]):
+    line = line.strip()
+    if line.startswith("#"):
+        name = line[1:].strip()
+        continue
+    if not line.startswith("{"):
+        continue
+    d = json.loads(line)
     tl = {r["t"]: r for r in d.get("timeline", [])}
     pts = " ".join(f"t{t}:{tl[t]['tree_ms']:.2f}/{tl[t]['bh_ms']:.2f}/{tl[t]['attract_ms']:.2f}"
                    for t in (250, 500, 700, 900) if t in tl)
-    print(f"{k} {name:40s} loop {d['loop_full_s']:.3f} s  window {d['window_it_s']:.0f} it/s  e2e {d['end_to_end_s']:.2f} s  {pts}")
+    print(f"{name or '-':32s} loop {d.get('loop_full_s', float('nan')):.3f} s  "
+          f"e2e {d.get('end_to_end_s', float('nan')):.2f} s  {pts}")

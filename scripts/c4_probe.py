@@ -20,9 +20,18 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=500_000)
 ap.add_argument("--cap", type=float, default=200.0)
 ap.add_argument("--iterations", type=int, default=1000)
+ap.add_argument("--trace-range", default="", help="lo:hi:step -- also trace these iterations (e.g. 100:260:5)")
+ap.add_argument("--stop", type=int, default=0, help="stop after this iteration (0: the whole schedule)")
+ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE", help="tsne_ctx_set_option")
 a = ap.parse_args()
+extra = set()
+if a.trace_range:
+    lo, hi, st = (int(v) for v in a.trace_range.split(":"))
+    extra = set(range(lo, hi, st))
 dev = torch.device("cuda", 0)
 ctx = T.Context(0)
+for kv in a.option:
+    ctx.set_option(kv.split("=", 1)[0], float(kv.split("=", 1)[1]))
 ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 X = torch.from_numpy(configs.c4(n=a.n)).to(dev)
 n, k = a.n, 90
@@ -53,7 +62,7 @@ ctx.dev_opt_setup(default_params(iterations=a.iterations, theta=0.5, n_component
 torch.cuda.synchronize()
 t_start = time.perf_counter()
 for t in range(1, a.iterations + 1):
-    trace = t in (1, 2, 5, 10, 20, 50, 100, 150, 200, 250, 300, 400, 500, 600, 700, 800, 900, 1000)
+    trace = t in (1, 2, 5, 10, 20, 50, 100, 150, 200, 250, 300, 400, 500, 600, 700, 800, 900, 1000) or t in extra
     if trace:
         ctx.dev_opt_profile(1)
     ts = time.perf_counter()
@@ -65,7 +74,7 @@ for t in range(1, a.iterations + 1):
         ext = (Y.max(0).values - Y.min(0).values).max().item()
         print(json.dumps({"t": t, "step_ms": dt * 1e3, "tree_ms": ms[0], "bh_ms": ms[1], "attract_ms": ms[3],
                           "update_ms": ms[4], "extent": ext, "elapsed_s": time.perf_counter() - t_start}), flush=True)
-    if time.perf_counter() - t_start > a.cap:
+    if time.perf_counter() - t_start > a.cap or (a.stop and t >= a.stop):
         print(json.dumps({"stopped_at": t, "elapsed_s": time.perf_counter() - t_start}), flush=True)
         break
 else:

@@ -1,5 +1,5 @@
 # PMC passes (SQ instruction mix / waits, LDS conflicts, L2) over the timed
-# window's attraction launches: bench.py --no-rest, attract_tiles / attract_rows.
+# window's attraction launches: bench.py --steps 20 --warmup 5 (whole schedule), attract_tiles.
 # Env: PMC_ARGS (extra bench arguments, e.g. --option attract_cfg=3).
 set -u
 cd "$GRAFT_REPO_ROOT"

@@ -30,14 +30,18 @@ def clustered(n, seed):
 
 def layouts(Y, theta, factor):
     """(F, z) of the 64-query layout, then of the narrow one at `factor` (the
-    selection reads the previous traversal's costs: a first call records them),
-    and the number of narrow groups."""
+    selection runs at the end of a traversal, from its costs, for the next
+    one: the first call with the option on only selects), and the number of
+    narrow groups."""
     with T.Context(0) as c:
         c.set_option("reuse_costs", 1)
         c.set_option("narrow", 0)
         F0, z0 = c.repulsion(Y, theta)
         assert c.counter("bh.narrow_groups") == 0
         c.set_option("narrow", factor)
+        Fw, zw = c.repulsion(Y, theta)
+        assert c.counter("bh.narrow_groups") == 0
+        assert np.array_equal(Fw, F0) and np.array_equal(zw, z0)
         F1, z1 = c.repulsion(Y, theta)
         ng = c.counter("bh.narrow_groups")
         F2, z2 = c.repulsion(Y, theta)   # the same selection (same costs): the same bits
