@@ -1,6 +1,7 @@
-"""Time the 2-D repulsion (tsne_dev_repulsion: tree build + BH traversal +
-tiles + moments) on embedding snapshots of the C3 schedule written by
-`bench.py --dump-y T1,T2,... --dump-dir DIR`, and print per snapshot the
+"""Time the repulsion (tsne_dev_repulsion: tree build + BH traversal +
+tiles + moments; 2-D quadtree or, for n x 3 snapshots, the octree) on
+embedding snapshots written by `bench.py --dump-y T1,T2,... --dump-dir DIR`
+(C3) or `scripts/c4_probe.py --dump-y ...` (C4), and print per snapshot the
 median wall time and checksums of F and z (to compare variants: equal
 checksums = equal results up to the printed digits).
 
@@ -35,7 +36,7 @@ def main():
         for path in a.snaps:
             Y = torch.from_numpy(np.load(path)).to(dev, torch.float64).contiguous()
             n = Y.shape[0]
-            F = torch.empty((n, 2), dtype=torch.float64, device=dev)
+            F = torch.empty((n, Y.shape[1]), dtype=torch.float64, device=dev)
             z = torch.empty(n, dtype=torch.float64, device=dev)
             times = []
             for _ in range(a.reps + 1):

@@ -22,8 +22,11 @@ ap.add_argument("--cap", type=float, default=200.0)
 ap.add_argument("--iterations", type=int, default=1000)
 ap.add_argument("--trace-range", default="", help="lo:hi:step -- also trace these iterations (e.g. 100:260:5)")
 ap.add_argument("--stop", type=int, default=0, help="stop after this iteration (0: the whole schedule)")
+ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as <dump-dir>/Y3_t<t>.npy")
+ap.add_argument("--dump-dir", default="gpurun_out")
 ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE", help="tsne_ctx_set_option")
 a = ap.parse_args()
+dumps = {int(v) for v in a.dump_y.split(",") if v}
 extra = set()
 if a.trace_range:
     lo, hi, st = (int(v) for v in a.trace_range.split(":"))
@@ -74,6 +77,8 @@ for t in range(1, a.iterations + 1):
         ext = (Y.max(0).values - Y.min(0).values).max().item()
         print(json.dumps({"t": t, "step_ms": dt * 1e3, "tree_ms": ms[0], "bh_ms": ms[1], "attract_ms": ms[3],
                           "update_ms": ms[4], "extent": ext, "elapsed_s": time.perf_counter() - t_start}), flush=True)
+    if t in dumps:
+        np.save(Path(a.dump_dir) / f"Y3_t{t}.npy", Y.cpu().numpy())
     if time.perf_counter() - t_start > a.cap or (a.stop and t >= a.stop):
         print(json.dumps({"stopped_at": t, "elapsed_s": time.perf_counter() - t_start}), flush=True)
         break

@@ -7,6 +7,7 @@
 #   smoke       __graft_entry__.smoke()
 #   pmc         scripts/gpu_pmc.sh (summarise with scripts/pmc_summary.py <tag>)
 #   c4probe     scripts/c4_probe.py C4PROBE_ARGS
+#   snap3       C4 snapshots (SNAP3_T) written by c4_probe, timed per SNAP3_VARS, debug counters, PMC
 #   proj        scripts/loop_projection.py PROJ_ARGS per PROJ_VARS entry
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -14,6 +15,8 @@ export TMPDIR=/tmp
 O=gpurun_out/r4${TAG:-x}
 mkdir -p $O
 run() { local lim=$1; shift; timeout -k 10 $lim "$@"; }
+# a test step's failures do not stop the session; a time limit, abort or crash does
+tst() { run "$@"; local rc=$?; echo "tests rc=$rc" >> $O/status.txt; case $rc in 0|1) return 0;; *) return $rc;; esac; }
 has() { [[ " ${STEPS:-} " == *" $1 "* ]]; }
 if has snap; then
   for v in ${SNAP_VARS:--}; do
@@ -23,8 +26,12 @@ if has snap; then
   done
 fi
 if has tests_narrow; then
-  run 900 python -u -m pytest tests/test_gpu_narrow.py tests/test_gpu_parity.py -x -v -p no:cacheprovider \
+  tst 900 python -u -m pytest tests/test_gpu_narrow.py tests/test_gpu_parity.py -v -p no:cacheprovider \
       --timeout 300 --timeout-method thread > $O/tests_narrow.log 2>&1 || exit $?
+fi
+if has tests_multi; then
+  tst 900 python -u -m pytest tests/test_gpu_multi.py -v -p no:cacheprovider \
+      --timeout 300 --timeout-method thread > $O/tests_multi.log 2>&1 || exit $?
 fi
 if has bench; then
   for v in ${BENCH_VARS:--}; do
@@ -34,7 +41,7 @@ if has bench; then
   done
 fi
 if has tests3d; then
-  run 900 python -u -m pytest tests/test_gpu_narrow.py tests/test_gpu_parity.py tests/test_gpu_multi.py -x -v \
+  tst 900 python -u -m pytest tests/test_gpu_narrow.py tests/test_gpu_parity.py tests/test_gpu_multi.py -v \
       -p no:cacheprovider --timeout 300 --timeout-method thread -k "octal or gradient3 or optimize3" \
       > $O/tests3d.log 2>&1 || exit $?
 fi
@@ -49,7 +56,7 @@ if has ktrace; then
   run 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o kt -- python bench.py --no-cpu-baseline --trace 0 ${KTRACE_ARGS:-} > $O/ktrace_bench.json 2> $O/ktrace.err || exit $?
 fi
 if has tests_all; then
-  run 1100 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 600 --timeout-method thread \
+  tst 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 --timeout-method thread \
       > $O/tests_all.log 2>&1 || exit $?
 fi
 if has smoke; then
@@ -60,6 +67,25 @@ if has pmc; then
 fi
 if has c4probe; then
   run 300 python scripts/c4_probe.py ${C4PROBE_ARGS:-} > $O/c4probe.log 2>&1 || exit $?
+fi
+if has snap3; then   # C4 snapshots in the transition, timed, counted and PMC-profiled
+  S3=${SNAP3_T:-120,150,180}
+  mkdir -p /tmp/snap3
+  run 400 python scripts/c4_probe.py --stop ${S3##*,} --cap 200 --dump-y $S3 --dump-dir /tmp/snap3 > $O/snap3_probe.log 2>&1 || exit $?
+  files=$(for t in $(echo $S3 | tr ',' ' '); do echo /tmp/snap3/Y3_t$t.npy; done)
+  for v in ${SNAP3_VARS:--}; do
+    opt=""; [ "$v" != "-" ] && opt="--option $v"
+    echo "# $v" >> $O/snap3.jsonl
+    run 300 python scripts/bh_snap.py $files --reps 3 $opt >> $O/snap3.jsonl 2>> $O/snap3.err || exit $?
+  done
+  TSNE_DEBUG_OCT=1 run 300 python scripts/bh_snap.py $files --reps 0 > $O/snap3_dbg.jsonl 2> $O/snap3_dbg.err || exit $?
+  k=0
+  for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
+              "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"; do
+    k=$((k+1))
+    timeout -s KILL 180 rocprofv3 --pmc $pass --kernel-include-regex "oct_" -d $O/pmc3_$k -o pmc --output-format csv -- \
+      python scripts/bh_snap.py $files --reps 0 > $O/pmc3_$k.log 2>&1 || exit $?
+  done
 fi
 if has proj; then
   for v in ${PROJ_VARS:--}; do

@@ -41,7 +41,8 @@ def layouts(Y, theta, factor):
         c.set_option("narrow", factor)
         Fw, zw = c.repulsion(Y, theta)
         assert c.counter("bh.narrow_groups") == 0
-        assert np.array_equal(Fw, F0) and np.array_equal(zw, z0)
+        # the same 64-query layout (block order from the recorded costs: re-association only)
+        assert np.all(np.abs(zw - z0) <= 1e-12 * z0) and np.abs(Fw - F0).max() <= 1e-12 * np.abs(F0).max()
         F1, z1 = c.repulsion(Y, theta)
         ng = c.counter("bh.narrow_groups")
         F2, z2 = c.repulsion(Y, theta)   # the same selection (same costs): the same bits

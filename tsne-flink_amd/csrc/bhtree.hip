@@ -1590,8 +1590,6 @@ struct TravLDS {
     QRec srec[4][4];
     int32_t bref[4][4];
     uint64_t bmask[4][4];
-    int32_t bref2[4][4];  // the 64-query layout's prefetched batch (software pipeline)
-    uint64_t bmask2[4][4];
 };
 
 // Stage the records of stack entries [sp, sp + k) of wave w into LDS (one
@@ -1832,7 +1830,9 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
         if (wwant && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
             atomicAdd(&mom_flag[1], wwant);
     }
-    if (COST && bcost) {   // this wave's run time into its queries' buckets (multi-GPU balancing)
+    // this wave's run time into its queries' buckets (multi-GPU balancing); a
+    // wave of the last, partial group may hold no query at all: nothing to add
+    if (COST && bcost && __ballot(valid)) {
         const unsigned long long cc = ((unsigned long long)(clock64() - t_start) >> 6) + 1;
         if (cost_lab) {
             if (valid && k == 0 && c == 0) atomicAdd(&bcost[cost_lab[s] >> 8], (cc + NQ - 1) / NQ);
@@ -1882,7 +1882,7 @@ __global__ __launch_bounds__(256) void bh_traverse_narrow(
 // Traversal kernel (see the comment above), one 64-query group per wave;
 // groups the narrow waves take (nv.nflag) return at once.  MODE 0 plain; 1
 // wave run times into the multi-GPU cost buckets; 2 every counter (profiling).
-template <int MODE, bool PIPE>
+template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
@@ -1925,40 +1925,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
             sp = 1;
         }
     }
-    // Pop up to 4 cells at a time: their records are fetched with one round of
+    // Pop up to 4 cells at a time (one while the stack is over half full: the
+    // depth stays bounded): their records are fetched with one round of
     // coalesced 16-byte vector loads, then processed one by one from LDS
-    // broadcasts.  Software pipeline (PIPE): while one batch is processed, the
-    // next one (the entries below it) is already popped and its records are in
-    // flight in registers (one 16-byte piece per lane), written over the
-    // processed batch in LDS afterwards -- the record latency hides behind a
-    // batch's VALU work.  Every entry is still processed once; only the order
-    // changes.
-    int cur = 0, kb = 0;
-    if (sp > 0) {
-        kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
+    // broadcasts.  (A software pipeline -- the next batch's records in flight
+    // in registers while one is processed -- measured no gain: C3 loop 5.645
+    // vs 5.643 s, BH snapshots within noise; removed.)
+    while (sp > 0) {
+        const int kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
         sp -= kb;
         stage_records(L, w, lane, sp, kb, qrec);
-    }
-    while (kb > 0) {
-        int kn = 0;
-        uint4 pre = make_uint4(0u, 0u, 0u, 0u);
-        // the next batch: popped now, its records loaded into registers (only
-        // while the stack is at most half full: beyond, strict depth-first
-        // single pops keep its depth bounded as without the pipeline)
-        if (PIPE && sp > 0 && sp <= STACK / 2) {
-            kn = sp < 4 ? sp : 4;
-            sp -= kn;
-            int32_t *nbref = cur ? L.bref[w] : L.bref2[w];
-            uint64_t *nbmask = cur ? L.bmask[w] : L.bmask2[w];
-            if (lane < kn) { nbref[lane] = L.sref[w][sp + lane]; nbmask[lane] = L.smask[w][sp + lane]; }
-            if (lane < QREC_V4 * kn) {
-                const int rr = lane / QREC_V4, part = lane - rr * QREC_V4;
-                pre = reinterpret_cast<const uint4 *>(qrec + L.sref[w][sp + rr])[part];
-            }
-        }
         const QRec *brec = L.srec[w];
-        const int32_t *bref_c = cur ? L.bref2[w] : L.bref[w];
-        const uint64_t *bmask_c = cur ? L.bmask2[w] : L.bmask[w];
+        const int32_t *bref_c = L.bref[w];
+        const uint64_t *bmask_c = L.bmask[w];
         npops += kb;
         for (int r = 0; r < kb; ++r) {
             if (STATS) ++wpops;
@@ -2062,25 +2041,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                     }
                 }
             }
-        }
-        if (kn > 0) {   // the prefetched batch into the other buffer
-            __builtin_amdgcn_wave_barrier();   // the processed batch's LDS reads are done
-            if (lane < QREC_V4 * kn) {
-                const int rr = lane / QREC_V4, part = lane - rr * QREC_V4;
-                reinterpret_cast<uint4 *>(&L.srec[w][rr])[part] = pre;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the batch is in LDS
-            __builtin_amdgcn_wave_barrier();
-            cur ^= 1;
-            kb = kn;
-        } else if (sp > 0) {   // nothing prefetched (the stack was empty, or no pipeline): a fresh batch
-            kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
-            sp -= kb;
-            cur = 0;
-            stage_records(L, w, lane, sp, kb, qrec);
-        } else {
-            kb = 0;
         }
     }
     if (valid) {
@@ -3104,9 +3064,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the waves' run times
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    const bool pipe = ctx->opts.bh_pipeline != 0;
-    auto kern = pipe ? (mode == 2 ? bh_traverse<2, true> : mode == 1 ? bh_traverse<1, true> : bh_traverse<0, true>)
-                     : (mode == 2 ? bh_traverse<2, false> : mode == 1 ? bh_traverse<1, false> : bh_traverse<0, false>);
+    auto kern = mode == 2 ? bh_traverse<2> : mode == 1 ? bh_traverse<1> : bh_traverse<0>;
     const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     // heavy groups: selected after the previous traversal of the same query

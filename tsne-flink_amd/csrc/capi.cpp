@@ -127,7 +127,6 @@ static const OptionField k_options[] = {
     {"knn_bf16", nullptr, &Options::knn_bf16, 0, 1},
     {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
     {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
-    {"bh_pipeline", nullptr, &Options::bh_pipeline, 0, 1},
 };
 static const OptionField &option_field(const char *key) {
     for (const OptionField &f : k_options)

@@ -178,7 +178,6 @@ struct Options {
     int recut = 0;            // several ranks on the tiled layout: re-cut by BH cost instead of relabels
     int knn_bf16 = 1;         // kNN threshold filter: bf16x3 MFMA (0: f32-input MFMA)
     double narrow = 3.0;      // BH: 64-query groups costing >= narrow x the mean run in the narrow layout (0: off)
-    int bh_pipeline = 1;      // BH traversal: the next record batch in flight while one is processed
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
                               // previous call's costs (results then depend on the call history at rounding level)
 };
