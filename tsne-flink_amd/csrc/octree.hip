@@ -1145,6 +1145,221 @@ __global__ __launch_bounds__(256) void oct_traverse_rec(
         atomicAdd(&mom_flag[1], ww);
 }
 
+
+// Record traversal, 64-query layout: one wave = 64 consecutive sorted queries
+// (lane = query) sharing an LDS stack of (record, 64-bit lane mask) entries,
+// the 2-D traversal's design (bhtree.hip bh_traverse) on octal records.  A
+// popped record serves every lane that opened it: one record fetch per 64
+// queries (the 8-query layout fetches it per 8), so the transition phase --
+// extents ~0.05-5, where nearly every cell near a query opens and the
+// neighbouring queries open the same ones -- moves 8x fewer record bytes.
+// Each lane evaluates the record's <= 8 children in order.  All-open /
+// near-exact tiles: per lane a moment task (oct_mom_apply) or the dense leaf
+// sum, which all lanes of the tile walk together: the points are wave-uniform
+// (scalar loads), each lane adds its own pair terms.  Identical decisions to
+// the 8-query layout (same tests, same records); the sums differ from it only
+// in association.
+constexpr int O64_STACK = 256;   // entries; batches of O64_KB while sp <= O64_BATCH, then depth-first
+constexpr int O64_KB = 2;        // records per fetch round (2 x 31 16-byte pieces: one round of the lanes)
+constexpr int O64_BATCH = 64;    // depth bound: 64 + 2 x 8 + 7 per level x 21 levels < O64_STACK
+static_assert(O64_BATCH + O64_KB * 8 + 7 * LEVELS3 < O64_STACK, "64-query octal stack bound");
+static_assert(O64_KB * (int)(sizeof(ORec) / 16) <= 64, "one fetch round per batch");
+template <bool DBG>
+__global__ __launch_bounds__(256) void oct_traverse64(
+    const double4 *__restrict__ pos, const int32_t *__restrict__ dupc, const OctNode *__restrict__ nodes,
+    const ORec *__restrict__ orec, const int32_t *__restrict__ meta, double theta, int64_t g0, int64_t g1,
+    const int32_t *__restrict__ qlist, int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
+    int32_t *__restrict__ mtask_n, double *__restrict__ F, double *__restrict__ Z,
+    unsigned long long *__restrict__ dbg, double mom_tol) {
+    __shared__ int32_t sref[4][O64_STACK];
+    __shared__ uint64_t smask[4][O64_STACK];
+    __shared__ ORec srec[4][O64_KB];
+    __shared__ int32_t bref[4][O64_KB];
+    __shared__ uint64_t bmask[4][O64_KB];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + w;
+    const int64_t kq = g0 + wid * 64 + lane;
+    const bool valid = kq < g1;
+    if (__ballot(valid) == 0) return;
+    const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
+    const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
+    double qx = 0.0, qy = 0.0, qz = 0.0;
+    if (valid) { const double4 p = pos[s]; qx = p.x; qy = p.y; qz = p.z; }
+    const double qmag = fabs(qx) + fabs(qy) + fabs(qz);
+    const int ndup = valid ? dupc[s] : 0;
+    const bool mom_on = mom_flag[0] != 0;
+    double fx = 0.0, fy = 0.0, fz = 0.0, zs = 0.0;
+    int ntask = 0, nwant = 0;
+    unsigned long long d_pops = 0, d_childs = 0, d_dense = 0, d_declined = 0;
+    int sp = 0;
+    const int root = meta[1];
+    if (root == ~0) {
+        if (valid) { const double4 p = pos[0]; leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs); }
+    } else if (root >= 0) {
+        const OctNode &rt = nodes[root];
+        if (rt.delta >= 63) {
+            for (int p = rt.first; p <= rt.last; ++p) {
+                const double4 pp = pos[p];
+                if (valid) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+            }
+        } else {
+            bool open = false;
+            if (valid) {
+                const double dx = qx - rt.cx, dy = qy - rt.cy, dz = qz - rt.cz;
+                if (summarise3(rt.h, dx, dy, dz, th_lo, th_hi, theta))
+                    cell3(dx, dy, dz, dx * dx + dy * dy + dz * dz, rt.cnt, fx, fy, fz, zs);
+                else
+                    open = true;
+            }
+            const uint64_t om = __ballot(open);
+            if (om) {
+                if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
+                sp = 1;
+            }
+        }
+    }
+    while (sp > 0) {
+        const int kb = sp > O64_BATCH ? 1 : (sp < O64_KB ? sp : O64_KB);
+        sp -= kb;
+        if (lane < kb) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
+        constexpr int V = sizeof(ORec) / 16;
+        if (lane < V * kb) {
+            const int rr = lane / V, part = lane - rr * V;
+            reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(orec + sref[w][sp + rr])[part];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: the batch is in LDS
+        __builtin_amdgcn_wave_barrier();
+        for (int r = 0; r < kb; ++r) {
+            if (DBG && lane == 0) ++d_pops;
+            const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
+            const uint64_t msk = bmask[w][r];
+            bool act = valid && ((msk >> lane) & 1ull);
+            const ORec &nd = srec[w][r];
+            const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);
+            bool tile = false;
+            if ((nflags & ONCH_TILE) && act) {
+                const double cdx = qx - nd.cx, cdy = qy - nd.cy, cdz = qz - nd.cz;
+                tile = cdx * cdx + cdy * cdy + cdz * cdz <= nd.rball2;
+                if (!tile) {
+                    const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1) +
+                                               fabs(nd.bz0) + fabs(nd.bz1));
+                    const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                    const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                    const double dzm = fmax(fabs(qz - nd.bz0), fabs(qz - nd.bz1)) + ex;
+                    tile = (dxm * dxm + dym * dym + dzm * dzm) * (1.0 + 1e-12) <= nd.thr;
+                }
+            }
+            if (__ballot(tile)) {
+                const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
+                const int cnt = __builtin_amdgcn_readfirstlane(nd.cnt);
+                bool usem = false;
+                if (tile && cnt >= MOM3_MIN) {
+                    double bcx, bcy, bcz, R;
+                    box3(nodes[ref], bcx, bcy, bcz, R);
+                    if (mom3_ok(qx - bcx, qy - bcy, qz - bcz, R, mom_tol)) {
+                        ++nwant;
+                        if (mom_on && ntask < MOM3_TASKS) {
+                            usem = true;
+                            mtask[s * MOM3_TASKS + ntask++] = ref;
+                        }
+                    }
+                }
+                // a large tile the moments cannot take: the lane keeps traversing it
+                const bool dense = tile && !usem && (b - a + 1) <= DENSE3_MAX;
+                if (DBG && tile && !usem && !dense) ++d_declined;
+                const bool taken = usem || dense;
+                if (taken && s >= a && s <= b) zs -= (double)ndup;   // the query's own copies add 1 each
+                if (__ballot(dense)) {
+                    if (DBG && dense) d_dense += (unsigned long long)(b - a + 1);
+                    // the points are the wave's (uniform index: scalar loads), every
+                    // lane of the tile adds its own terms
+                    double ux = 0.0, uy = 0.0, uz = 0.0, uq = 0.0;
+                    for (int p = a; p <= b; ++p) {
+                        const double4 pp = pos[p];
+                        const double dx = qx - pp.x, dy = qy - pp.y, dz = qz - pp.z;
+                        const double rr = rcp2(__fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0))));
+                        const double sc = rr * rr;
+                        ux = __fma_rn(sc, dx, ux);
+                        uy = __fma_rn(sc, dy, uy);
+                        uz = __fma_rn(sc, dz, uz);
+                        uq += rr;
+                    }
+                    if (dense) { fx += ux; fy += uy; fz += uz; zs += uq; }
+                }
+                act = act && !taken;
+            }
+            if (__ballot(act) == 0) continue;
+            const int nch = nflags & 0xff;
+            const int kinds = __builtin_amdgcn_readfirstlane(nd.kinds);
+            if (DBG && act) d_childs += (unsigned long long)nch;
+            for (int c = 0; c < nch; ++c) {
+                const int kind = (kinds >> (2 * c)) & 3;   // uniform: scalar branches
+                if (kind == OK_TIE) continue;                // after the loop (rare)
+                const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c], dz = qz - nd.ccz[c];
+                const double D = __fma_rn(dx, dx, __fma_rn(dy, dy, dz * dz));
+                double wm;
+                if (kind == OK_LEAF) {
+                    wm = (act && !(dx == 0.0 && dy == 0.0 && dz == 0.0)) ? 1.0 : 0.0;
+                } else {
+                    const double A = nd.ca[c];
+                    bool acc = D > A;
+                    if (act && !acc && !(D < A * OACC_BAND))
+                        acc = nd.ch[c] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
+                              theta;
+                    wm = (act && acc) ? (double)nd.ccnt[c] : 0.0;
+                    const uint64_t om = __ballot(act && !acc);
+                    if (om) {
+                        if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
+                        ++sp;
+                    }
+                }
+                const double Qv = rcp2(1.0 + D);
+                const double mult = wm * Qv;
+                const double sc = mult * Qv;
+                fx = __fma_rn(sc, dx, fx);
+                fy = __fma_rn(sc, dy, fy);
+                fz = __fma_rn(sc, dz, fz);
+                zs += mult;
+            }
+            if (__builtin_expect(kinds & 0xAAAA, 0)) {   // key-tie groups: every point directly
+                for (int c = 0; c < nch; ++c) {
+                    if (((kinds >> (2 * c)) & 3) != OK_TIE) continue;
+                    const OctNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
+                    for (int p = tn.first; p <= tn.last; ++p) {
+                        const double4 pp = pos[p];
+                        if (act) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the pushes landed before the next reads
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (valid) {
+        F[3 * s] = fx;
+        F[3 * s + 1] = fy;
+        F[3 * s + 2] = fz;
+        Z[s] = zs;
+        mtask_n[s] = ntask;
+    }
+    if (DBG) {   // [0] wave pops, [1] lane child evaluations, [2] dense tile points, [3] declined tiles, [4] moment tasks
+        const unsigned long long a = wave_sum(d_childs), b2 = wave_sum(d_dense), c2 = wave_sum(d_declined),
+                                 e = wave_sum((unsigned long long)ntask);
+        if (lane == 0) {
+            atomicAdd(dbg, d_pops);
+            atomicAdd(dbg + 1, a);
+            atomicAdd(dbg + 2, b2);
+            atomicAdd(dbg + 3, c2);
+            atomicAdd(dbg + 4, e);
+        }
+    }
+    const int ww = wave_sum(nwant);
+    if (lane == 0 && ww && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
+        atomicAdd(&mom_flag[1], ww);
+}
+
 }  // namespace
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
@@ -1255,7 +1470,17 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
         dbg = ctx->ws.get<unsigned long long>("oct.dbg", 8);
         TSNE_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), ctx->stream));
     }
-    if (ctx->opts.oct_records) {   // the record traversal: 8 queries per wave
+    if (ctx->opts.oct_records == 2) {   // the record traversal: 64 queries per wave
+        const int64_t nw = ceil_div(s1 - s0, 64);
+        if (debug)
+            hipLaunchKernelGGL(oct_traverse64<true>, dim3(ceil_div(nw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                               t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz,
+                               dbg, ctx->opts.mom3_tol);
+        else
+            hipLaunchKernelGGL(oct_traverse64<false>, dim3(ceil_div(nw, 4)), dim3(256), 0, ctx->stream, t.pos,
+                               t.dupc, t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
+                               dF, dz, dbg, ctx->opts.mom3_tol);
+    } else if (ctx->opts.oct_records) {   // the record traversal: 8 queries per wave
         const int64_t rw = ceil_div(s1 - s0, OQ);
         if (debug)
             hipLaunchKernelGGL(oct_traverse_rec<true>, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
