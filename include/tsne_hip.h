@@ -127,7 +127,11 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "near_tol3_early" 1e-7, "near_tol3_late" 5e-6, "mom3_tol" 1e-12, and
  *   "oct_moments" 1           the same for the 3-D octree;
  *   "oct_records" 1           3-D: octal records and the 8-query record
- *                             traversal (0: the binary-node walk);
+ *                             traversal (2: the 64-query one; 0: the
+ *                             binary-node walk);
+ *   "coherent_sort" 1         the trees' Morton sort from the previous build's
+ *                             order (0: rocPRIM's radix sort; the same
+ *                             permutation);
  *   "root_tile" 1             root-tile shortcut of the small-embedding phase;
  *   "attract_tiles" 1         tiled attraction where the labels allow it;
  *   "attract_cfg" -1          its tile shape (-1 automatic, 0..3);

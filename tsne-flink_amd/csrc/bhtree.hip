@@ -2820,6 +2820,8 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
     morton_sort(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, n, ctx->stream);
     t.sort_tmp_bytes = tb;
     t.sort_tmp = ws.get<uint8_t>(pre + "sort_tmp", tb);
+    csort_alloc(ctx, t.cs, n, pre);
+    t.cs_primed = false;
     const int64_t nb = ceil_div(t.tile_waves, 4);
     t.wcost = ws.get<int32_t>(pre + "wcost", t.tile_waves);
     t.tcost = ws.get<int32_t>(pre + "tcost", t.tile_waves);
@@ -3004,8 +3006,16 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     }
     hipLaunchKernelGGL(morton_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
     TSNE_LAUNCH_CHECK();
-    size_t tb = t.sort_tmp_bytes;
-    morton_sort(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, n, st);
+    // the previous full build's order buckets the keys (csort.hpp); the first
+    // build, small trees and Options::coherent_sort = 0: rocPRIM's sort (the same
+    // result: keys ascending, ties by point index)
+    if (t.cs.P > 0 && t.cs_primed && ctx->opts.coherent_sort) {
+        csort_run(ctx, t.cs, t.keys, t.idx_sorted, t.keys_sorted, t.idx_sorted, st);
+    } else {
+        size_t tb = t.sort_tmp_bytes;
+        morton_sort(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, n, st);
+    }
+    t.cs_primed = true;
     hipLaunchKernelGGL(count_in_root, dim3(1), dim3(64), 0, st, t.keys_sorted, n, t.meta);
     hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
     hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc, t.vid,

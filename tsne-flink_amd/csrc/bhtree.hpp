@@ -1,6 +1,7 @@
 // bhtree.hpp -- GPU Barnes-Hut quadtree with the reference's semantics.
 #pragma once
 #include "common.hpp"
+#include "csort.hpp"
 
 namespace tsne {
 
@@ -126,6 +127,8 @@ struct BHTree {
     uint64_t dup_mask = 0;
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
+    CoherentSort cs;             // the Morton sort from the previous build's order (csort.hpp)
+    bool cs_primed = false;      // idx_sorted holds a previous build's permutation
     int bbox_blocks = 0;
     // longest-first block order of the traversal (by each wave's pops + tile
     // points in the previous traversal) and of tile_apply (by this

@@ -1,0 +1,212 @@
+// csort.hip -- the trees' Morton sort from the previous build's order (csort.hpp).
+#include "csort.hpp"
+
+namespace tsne {
+namespace {
+
+constexpr int CS_BLK = 1024;      // elements per count / scatter workgroup
+constexpr int CS_TARGET = 1024;   // points per bucket (the previous order's step)
+constexpr int CS_PMAX = 2048;     // buckets at most (the splitter sort's LDS)
+constexpr int CS_CAP = 4096;      // bucket capacity of the LDS sort (48 KB)
+constexpr int CS_SORT_T = 512;    // threads of a bucket's sort
+
+// (k, v) < (k2, v2) lexicographically
+__device__ __forceinline__ bool kv_less(uint64_t k, int32_t v, uint64_t k2, int32_t v2) {
+    return k < k2 || (k == k2 && v < v2);
+}
+
+// Bitonic sort of N (a power of two) (key, value) pairs in a[] / b[] (LDS or
+// global memory private to the workgroup), T threads, ascending by (key, value).
+template <int T>
+__device__ void bitonic_kv(uint64_t *a, int32_t *b, int N) {
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < N; i += T) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t ka = a[i], kl = a[l];
+                    const int32_t va = b[i], vl = b[l];
+                    const bool up = (i & k) == 0;
+                    if (kv_less(kl, vl, ka, va) == up) {
+                        a[i] = kl; a[l] = ka;
+                        b[i] = vl; b[l] = va;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// P splitters from the previous order at equal steps, sorted.
+__global__ __launch_bounds__(1024) void cs_split(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
+                                                 int64_t n, int32_t P, uint64_t *__restrict__ split) {
+    __shared__ uint64_t s[CS_PMAX];
+    __shared__ int32_t v[CS_PMAX];
+    for (int j = threadIdx.x; j < CS_PMAX; j += 1024) {
+        s[j] = j < P ? keys[prev[(int64_t)j * n / P]] : ~0ull;
+        v[j] = j;
+    }
+    __syncthreads();
+    bitonic_kv<1024>(s, v, CS_PMAX);
+    for (int j = threadIdx.x; j < P; j += 1024) split[j] = s[j];
+}
+
+// bucket of key k: the number of splitters split[1..P-1] <= k; guess g first
+// (the bucket the previous order puts element j in)
+__device__ __forceinline__ int cs_find(const uint64_t *__restrict__ split, int32_t P, uint64_t k, int g) {
+    if ((g == 0 || split[g] <= k) && (g == P - 1 || k < split[g + 1])) return g;
+    int lo = 0, hi = P - 1;   // answer in [lo, hi]
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (split[mid] <= k) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(CS_BLK) void cs_count(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
+                                                   int64_t n, int32_t P, const uint64_t *__restrict__ split,
+                                                   int32_t *__restrict__ bkt, int32_t *__restrict__ cnt) {
+    __shared__ int32_t h[CS_PMAX];
+    for (int b = threadIdx.x; b < P; b += CS_BLK) h[b] = 0;
+    __syncthreads();
+    const int64_t j = (int64_t)blockIdx.x * CS_BLK + threadIdx.x;
+    if (j < n) {
+        const uint64_t k = keys[prev[j]];
+        const int b = cs_find(split, P, k, (int)(j * P / n));
+        bkt[j] = b;
+        atomicAdd(&h[b], 1);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < P; b += CS_BLK)
+        if (h[b]) atomicAdd(&cnt[b], h[b]);
+}
+
+// exclusive scan of the bucket sizes -> off[0..P], cur = off; stat[0] = oversized buckets
+__global__ __launch_bounds__(1024) void cs_scan(const int32_t *__restrict__ cnt, int32_t P, int32_t *__restrict__ off,
+                                                int32_t *__restrict__ cur, int32_t *__restrict__ stat) {
+    __shared__ int32_t s[1024];
+    __shared__ int32_t nover;
+    const int t = threadIdx.x;
+    if (t == 0) nover = 0;
+    const int per = (P + 1023) / 1024;   // <= 2
+    int loc[2] = {0, 0}, sum = 0;
+    for (int e = 0; e < per; ++e) {
+        const int b = t * per + e;
+        loc[e] = b < P ? cnt[b] : 0;
+        sum += loc[e];
+    }
+    s[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {   // inclusive Hillis-Steele scan
+        const int v = t >= d ? s[t - d] : 0;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    int run = s[t] - sum;
+    for (int e = 0; e < per; ++e) {
+        const int b = t * per + e;
+        if (b < P) {
+            off[b] = run;
+            cur[b] = run;
+            if (loc[e] > CS_CAP) atomicAdd(&nover, 1);
+        }
+        run += loc[e];
+    }
+    if (t == 1023) off[P] = s[1023];
+    __syncthreads();
+    if (t == 0) stat[0] = nover;
+}
+
+__global__ __launch_bounds__(CS_BLK) void cs_scatter(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
+                                                     int64_t n, int32_t P, const int32_t *__restrict__ bkt,
+                                                     int32_t *__restrict__ cur, uint64_t *__restrict__ kb,
+                                                     int32_t *__restrict__ vb) {
+    __shared__ int32_t h[CS_PMAX], base[CS_PMAX];
+    for (int b = threadIdx.x; b < P; b += CS_BLK) h[b] = 0;
+    __syncthreads();
+    const int64_t j = (int64_t)blockIdx.x * CS_BLK + threadIdx.x;
+    int b = 0, r = 0;
+    if (j < n) {
+        b = bkt[j];
+        r = atomicAdd(&h[b], 1);   // rank within this workgroup's share of the bucket (any order: sorted below)
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < P; c += CS_BLK)
+        if (h[c]) base[c] = atomicAdd(&cur[c], h[c]);
+    __syncthreads();
+    if (j < n) {
+        const int32_t p = prev[j];
+        const int32_t slot = base[b] + r;
+        kb[slot] = keys[p];
+        vb[slot] = p;
+    }
+}
+
+// One workgroup per bucket: its (key, point) pairs sorted and written to the
+// output at the bucket's offset.  Over CS_CAP: the same bitonic network in
+// the bucket's private scratch (kb / vb + n + 2 off: disjoint, N <= 2 m).
+__global__ __launch_bounds__(CS_SORT_T) void cs_bucket(const int32_t *__restrict__ cnt, const int32_t *__restrict__ off,
+                                                       int64_t n, uint64_t *kb, int32_t *vb,
+                                                       uint64_t *__restrict__ keys_sorted,
+                                                       int32_t *__restrict__ idx_sorted) {
+    __shared__ uint64_t sk[CS_CAP];
+    __shared__ int32_t sv[CS_CAP];
+    const int b = blockIdx.x;
+    const int m = cnt[b], o = off[b];
+    if (m == 0) return;
+    int N = 2;
+    while (N < m) N <<= 1;
+    uint64_t *a = sk;
+    int32_t *v = sv;
+    if (m > CS_CAP) { a = kb + n + 2 * (int64_t)o; v = vb + n + 2 * (int64_t)o; }
+    for (int i = threadIdx.x; i < N; i += CS_SORT_T) {
+        a[i] = i < m ? kb[o + i] : ~0ull;
+        v[i] = i < m ? vb[o + i] : INT32_MAX;
+    }
+    __syncthreads();
+    bitonic_kv<CS_SORT_T>(a, v, N);
+    for (int i = threadIdx.x; i < m; i += CS_SORT_T) {
+        keys_sorted[o + i] = a[i];
+        idx_sorted[o + i] = v[i];
+    }
+}
+
+}  // namespace
+
+void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &pre) {
+    cs.n = n;
+    cs.P = 0;
+    if (n < CSORT_MIN_N) return;
+    TSNE_REQUIRE(n < (int64_t)1 << 29, "coherent sort: n too large for 32-bit offsets into its 3n scratch");
+    cs.P = (int32_t)std::min<int64_t>(CS_PMAX, std::max<int64_t>(2, n / CS_TARGET));
+    Workspace &ws = ctx->ws;
+    cs.split = ws.get<uint64_t>(pre + "cs.split", cs.P);
+    cs.cnt = ws.get<int32_t>(pre + "cs.cnt", cs.P);
+    cs.off = ws.get<int32_t>(pre + "cs.off", cs.P + 1);
+    cs.cur = ws.get<int32_t>(pre + "cs.cur", cs.P);
+    cs.bkt = ws.get<int32_t>(pre + "cs.bkt", n);
+    cs.kb = ws.get<uint64_t>(pre + "cs.kb", 3 * (size_t)n);
+    cs.vb = ws.get<int32_t>(pre + "cs.vb", 3 * (size_t)n);
+    cs.stat = ws.get<int32_t>(pre + "cs.stat", 1);
+}
+
+void csort_run(tsne_ctx *ctx, CoherentSort &cs, const uint64_t *keys, const int32_t *prev, uint64_t *keys_sorted,
+               int32_t *idx_sorted, hipStream_t st) {
+    (void)ctx;
+    TSNE_REQUIRE(cs.P > 0, "coherent sort not allocated");
+    const int64_t n = cs.n;
+    const int64_t nb = ceil_div(n, CS_BLK);
+    hipLaunchKernelGGL(cs_split, dim3(1), dim3(1024), 0, st, keys, prev, n, cs.P, cs.split);
+    TSNE_HIP(hipMemsetAsync(cs.cnt, 0, sizeof(int32_t) * cs.P, st));
+    hipLaunchKernelGGL(cs_count, dim3(nb), dim3(CS_BLK), 0, st, keys, prev, n, cs.P, cs.split, cs.bkt, cs.cnt);
+    hipLaunchKernelGGL(cs_scan, dim3(1), dim3(1024), 0, st, cs.cnt, cs.P, cs.off, cs.cur, cs.stat);
+    hipLaunchKernelGGL(cs_scatter, dim3(nb), dim3(CS_BLK), 0, st, keys, prev, n, cs.P, cs.bkt, cs.cur, cs.kb, cs.vb);
+    hipLaunchKernelGGL(cs_bucket, dim3(cs.P), dim3(CS_SORT_T), 0, st, cs.cnt, cs.off, n, cs.kb, cs.vb, keys_sorted,
+                       idx_sorted);
+    TSNE_LAUNCH_CHECK();
+}
+
+}  // namespace tsne

@@ -1387,6 +1387,8 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
                                                64, ctx->stream));
     t.sort_tmp_bytes = tb;
     t.sort_tmp = ws.get<uint8_t>("oct.sort_tmp", tb);
+    csort_alloc(ctx, t.cs, n, "oct.");
+    t.cs_primed = false;
     t.mom = ws.get<double>("oct.mom", (size_t)MOM3_K * n);
     t.mcnt = ws.get<int32_t>("oct.mcnt", n);
     t.moff = ws.get<int32_t>("oct.moff", n);
@@ -1418,9 +1420,14 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta, bool l
     hipLaunchKernelGGL(bbox3_final, dim3(1), dim3(256), 0, st, t.bbox_part, t.bbox_blocks, t.W, t.meta);
     hipLaunchKernelGGL(morton3_keys, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, n, t.W, t.keys, t.idx, t.meta);
     TSNE_LAUNCH_CHECK();
-    size_t tb = t.sort_tmp_bytes;
-    TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n,
-                                               0, 64, st));
+    if (t.cs.P > 0 && t.cs_primed && ctx->opts.coherent_sort) {   // from the previous build's order (csort.hpp)
+        csort_run(ctx, t.cs, t.keys, t.idx_sorted, t.keys_sorted, t.idx_sorted, st);
+    } else {
+        size_t tb = t.sort_tmp_bytes;
+        TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(t.sort_tmp, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n,
+                                                   0, 64, st));
+    }
+    t.cs_primed = true;
     hipLaunchKernelGGL(count_in_root3, dim3(1), dim3(64), 0, st, t.keys_sorted, n, t.meta);
     hipLaunchKernelGGL(gather3, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
     hipLaunchKernelGGL(dup_count3, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc);

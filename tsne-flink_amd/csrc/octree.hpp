@@ -10,6 +10,7 @@
 // cells (the rest transparent), and a wave-shared traversal stack.
 #pragma once
 #include "common.hpp"
+#include "csort.hpp"
 
 namespace tsne {
 
@@ -63,6 +64,8 @@ struct OctTree {
     double *bbox_part = nullptr, *W = nullptr;
     void *sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
+    CoherentSort cs;             // the Morton sort from the previous build's order (csort.hpp)
+    bool cs_primed = false;
     int bbox_blocks = 0;
     // subtree moments (70 per node of >= MOM3_MIN points, about its box
     // centre), built in chunks; gated by the previous traversal's demand
