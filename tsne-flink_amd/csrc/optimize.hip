@@ -1789,6 +1789,20 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[0], st));
     oct_build(ctx, s->otree, Y, p.theta, ex == 1.0);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
+    // the attraction of a non-loss iteration needs no Z: on the side stream,
+    // beside the traversal (after the build, whose latency-bound kernels it
+    // would stretch; the 2-D rule); a loss iteration's after Z, as before
+    const bool side = !want_loss;
+    int64_t blocks = 0;
+    if (side) {
+        TSNE_HIP(hipEventRecord(s->ev_y, st));
+        TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
+        ctx->timers.begin("opt.attract", s->side);
+        blocks = attract3_launch(s->side, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr3,
+                                 s->part, false);
+        ctx->timers.end("opt.attract", s->side);
+        TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
+    }
     if (ctx->world > 1) {
         build_qlist(ctx, s, s->otree.idx_sorted);
         oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist);
@@ -1798,10 +1812,14 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     reduce_Z(ctx, s, s->z);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
-    ctx->timers.begin("opt.attract", st);
-    const int64_t blocks = attract3_launch(st, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex,
-                                           s->attr3, s->part, want_loss);
-    ctx->timers.end("opt.attract", st);
+    if (side) {
+        TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
+    } else {
+        ctx->timers.begin("opt.attract", st);
+        blocks = attract3_launch(st, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr3,
+                                 s->part, want_loss);
+        ctx->timers.end("opt.attract", st);
+    }
     s->log_attract(t, want_loss ? 1 : 3);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     ctx->timers.begin("opt.update", st);
