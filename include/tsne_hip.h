@@ -126,8 +126,8 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "mom_tol" 1e-12           subtree-moment truncation bound (2-D);
  *   "near_tol3_early" 1e-7, "near_tol3_late" 5e-6, "mom3_tol" 1e-12, and
  *   "oct_moments" 1           the same for the 3-D octree;
- *   "oct_records" 1           3-D: octal records and the 8-query record
- *                             traversal (2: the 64-query one; 0: the
+ *   "oct_records" 2           3-D: octal records and the 64-query record
+ *                             traversal (1: the 8-query one; 0: the
  *                             binary-node walk);
  *   "coherent_sort" 1         the trees' Morton sort from the previous build's
  *                             order (0: rocPRIM's radix sort; the same

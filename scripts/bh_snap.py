@@ -46,7 +46,7 @@ def main():
                 ctx.synchronize()
                 times.append(time.perf_counter() - t0)
             narrow = ctx.counter("bh.narrow_groups")
-            times = sorted(times[1:])
+            times = sorted(times[1:] if len(times) > 1 else times)   # --reps 0: the one (cold) call
             print(json.dumps({"snapshot": os.path.basename(path), "n": n, "ms_median": 1e3 * times[len(times) // 2],
                               "ms_min": 1e3 * times[0], "narrow_groups": narrow, "sum_abs_F": float(F.abs().sum()),
                               "sum_z": float(z.sum())}), flush=True)

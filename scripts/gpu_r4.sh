@@ -41,8 +41,9 @@ if has bench; then
   done
 fi
 if has tests3d; then
-  tst 900 python -u -m pytest tests/test_gpu_narrow.py tests/test_gpu_parity.py tests/test_gpu_multi.py -v \
-      -p no:cacheprovider --timeout 300 --timeout-method thread -k "octal or gradient3 or optimize3" \
+  tst 900 python -u -m pytest tests/test_gpu_narrow.py tests/test_gpu_parity.py tests/test_gpu_multi.py \
+      tests/test_gpu_configs.py tests/test_gpu_csort.py -v -p no:cacheprovider --timeout 300 --timeout-method thread \
+      -k "octal or gradient3 or optimize3 or c4 or C4 or 3d or csort or coherent" \
       > $O/tests3d.log 2>&1 || exit $?
 fi
 if has bench4; then

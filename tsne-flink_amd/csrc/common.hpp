@@ -170,7 +170,7 @@ struct Options {
     double mom3_tol = 1e-12;
     int oct_moments = 1;      // 3-D subtree moments
     int coherent_sort = 1;    // the trees' Morton sort from the previous build's order (csort.hpp; 0: rocPRIM's radix sort)
-    int oct_records = 1;      // 3-D: octal records + the 8-query record traversal (2: the 64-query one; 0: the binary-node walk)
+    int oct_records = 2;      // 3-D: octal records + the 64-query record traversal (1: the 8-query one; 0: the binary-node walk)
     int root_tile = 1;        // root-tile shortcut of the small-embedding phase
     int attract_tiles = 1;    // tiled attraction (attract_tiles) where the labels allow it
     int attract_cfg = -1;     // its tile shape: -1 by rows per rank, else ATCfg0..3
