@@ -162,7 +162,9 @@ int tsne_ctx_get_option(tsne_ctx *ctx, const char *key, double *value_out);
 /* Diagnostic counters of the last call (synchronises the context's stream):
  *   "bh.narrow_groups"   64-query groups the last single-call BH traversal
  *                        (tsne_gradient / tsne_repulsion) ran in the narrow layout;
- *   "opt.narrow_groups"  the same for the optimizer's last iteration. */
+ *   "opt.narrow_groups"  the same for the optimizer's last iteration;
+ *   "bh.csort_oversized", "opt.csort_oversized"  buckets of the last coherent
+ *                        Morton sort (csort.hpp) beyond its LDS capacity. */
 int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);
 
 /* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls

@@ -28,32 +28,44 @@ def run(n, C, coherent, seed, iterations=40, dups=False, scale=3.0):
         Y = torch.from_numpy(Y0.copy()).to(dev)
         u, g = torch.zeros_like(Y), torch.ones_like(Y)
         c.dev_opt_setup(p, *Pd, n, Y, u, g)
+        over = 0
         for t in range(1, p.iterations + 1):
             c.dev_opt_step(t)
+            if coherent and C == 2:
+                over += c.counter("opt.csort_oversized")
         c.synchronize()
-        return Y.cpu().numpy(), c.dev_opt_losses()
+        return Y.cpu().numpy(), c.dev_opt_losses(), over
 
 
 @pytest.mark.parametrize("n,C,dups", [(50_000, 2, False), (50_000, 2, True), (40_000, 3, False), (40_000, 3, True)])
 def test_coherent_sort_bit_identical(n, C, dups):
-    Ya, la = run(n, C, 1, 31, dups=dups)
-    Yb, lb = run(n, C, 0, 31, dups=dups)
+    Ya, la, over = run(n, C, 1, 31, dups=dups)
+    Yb, lb, _ = run(n, C, 0, 31, dups=dups)
+    assert over == 0   # oversampled splitters: every bucket within the LDS capacity
     assert la == lb
     assert np.array_equal(Ya, Yb)
 
 
-def test_coherent_sort_after_a_jump():
-    """A large move between builds (the embedding scaled x50 and shifted: the
-    previous order's buckets overflow the LDS capacity -> the global-memory
-    path) still gives rocPRIM's permutation: the repulsion is bit-identical."""
+def test_coherent_sort_after_a_jump_and_oversized_buckets():
+    """A large move between builds (half the embedding scaled x50 and shifted,
+    half shrunk), then 12k copies of one point (equal keys: no splitter can
+    cut them, the bucket exceeds the LDS capacity -> the global-memory path):
+    rocPRIM's permutation every time, so the repulsion is bit-identical."""
     n = 60_000
     rng = np.random.default_rng(4)
     Y = rng.normal(size=(n, 2))
     Y2 = np.concatenate([Y[: n // 2] * 50.0 + 7.0, Y[n // 2:] * 0.01], axis=0)
+    Y3 = Y2.copy()
+    Y3[5000:17000] = Y3[5000]
     out = {}
     for cs in (1, 0):
         with T.Context(0) as c:
             c.set_option("coherent_sort", cs)
             c.repulsion(Y, 0.5)
-            out[cs] = c.repulsion(Y2, 0.5)
-    assert np.array_equal(out[1][0], out[0][0]) and np.array_equal(out[1][1], out[0][1])
+            r2 = c.repulsion(Y2, 0.5)
+            r3 = c.repulsion(Y3, 0.5)
+            if cs:
+                assert c.counter("bh.csort_oversized") >= 1
+            out[cs] = (r2, r3)
+    for k in range(2):
+        assert np.array_equal(out[1][k][0], out[0][k][0]) and np.array_equal(out[1][k][1], out[0][k][1])

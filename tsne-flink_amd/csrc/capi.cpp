@@ -381,6 +381,8 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         const std::string k = name;
         if (k == "bh.narrow_groups") *value_out = ctx->single_tree ? bh_narrow_groups(ctx, *ctx->single_tree) : 0;
         else if (k == "opt.narrow_groups") *value_out = opt_tree(ctx) ? bh_narrow_groups(ctx, *opt_tree(ctx)) : 0;
+        else if (k == "bh.csort_oversized") *value_out = ctx->single_tree ? csort_oversized(ctx, ctx->single_tree->cs) : 0;
+        else if (k == "opt.csort_oversized") *value_out = opt_tree(ctx) ? csort_oversized(ctx, opt_tree(ctx)->cs) : 0;
         else fail(TSNE_ERR_ARG, "unknown counter '" + k + "'");
     });
 }

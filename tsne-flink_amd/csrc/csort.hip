@@ -5,8 +5,9 @@ namespace tsne {
 namespace {
 
 constexpr int CS_BLK = 1024;      // elements per count / scatter workgroup
-constexpr int CS_TARGET = 1024;   // points per bucket (the previous order's step)
-constexpr int CS_PMAX = 2048;     // buckets at most (the splitter sort's LDS)
+constexpr int CS_TARGET = 1024;   // points per bucket
+constexpr int CS_PMAX = 1024;     // buckets at most
+constexpr int CS_OVS = 8;         // samples per bucket (splitters: every CS_OVS-th sorted sample)
 constexpr int CS_CAP = 4096;      // bucket capacity of the LDS sort (48 KB)
 constexpr int CS_SORT_T = 512;    // threads of a bucket's sort
 
@@ -38,18 +39,38 @@ __device__ void bitonic_kv(uint64_t *a, int32_t *b, int N) {
     }
 }
 
-// P splitters from the previous order at equal steps, sorted.
+// Bitonic sort of N (a power of two) keys in LDS, T threads, ascending.
+template <int T>
+__device__ void bitonic_k(uint64_t *a, int N) {
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < N; i += T) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t ka = a[i], kl = a[l];
+                    if ((kl < ka) == ((i & k) == 0)) { a[i] = kl; a[l] = ka; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// P splitters: CS_OVS x P samples of the keys at equal steps of the previous
+// order, sorted; every CS_OVS-th.  The previous order keeps the coarse Morton
+// cells in place, but inside a dense cell the order is new every iteration
+// (the box moves its deep cell boundaries), so the samples there are random
+// ones: oversampling keeps the buckets within ~2x of their mean.
 __global__ __launch_bounds__(1024) void cs_split(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
                                                  int64_t n, int32_t P, uint64_t *__restrict__ split) {
-    __shared__ uint64_t s[CS_PMAX];
-    __shared__ int32_t v[CS_PMAX];
-    for (int j = threadIdx.x; j < CS_PMAX; j += 1024) {
-        s[j] = j < P ? keys[prev[(int64_t)j * n / P]] : ~0ull;
-        v[j] = j;
-    }
+    __shared__ uint64_t s[CS_OVS * CS_PMAX];
+    const int S = CS_OVS * P;
+    int N = 2;
+    while (N < S) N <<= 1;
+    for (int j = threadIdx.x; j < N; j += 1024) s[j] = j < S ? keys[prev[(int64_t)j * n / S]] : ~0ull;
     __syncthreads();
-    bitonic_kv<1024>(s, v, CS_PMAX);
-    for (int j = threadIdx.x; j < P; j += 1024) split[j] = s[j];
+    bitonic_k<1024>(s, N);
+    for (int j = threadIdx.x; j < P; j += 1024) split[j] = s[j * CS_OVS];
 }
 
 // bucket of key k: the number of splitters split[1..P-1] <= k; guess g first
@@ -179,8 +200,7 @@ __global__ __launch_bounds__(CS_SORT_T) void cs_bucket(const int32_t *__restrict
 void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &pre) {
     cs.n = n;
     cs.P = 0;
-    if (n < CSORT_MIN_N) return;
-    TSNE_REQUIRE(n < (int64_t)1 << 29, "coherent sort: n too large for 32-bit offsets into its 3n scratch");
+    if (n < CSORT_MIN_N || n > CSORT_MAX_N) return;   // rocPRIM's sort
     cs.P = (int32_t)std::min<int64_t>(CS_PMAX, std::max<int64_t>(2, n / CS_TARGET));
     Workspace &ws = ctx->ws;
     cs.split = ws.get<uint64_t>(pre + "cs.split", cs.P);
@@ -191,6 +211,15 @@ void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &
     cs.kb = ws.get<uint64_t>(pre + "cs.kb", 3 * (size_t)n);
     cs.vb = ws.get<int32_t>(pre + "cs.vb", 3 * (size_t)n);
     cs.stat = ws.get<int32_t>(pre + "cs.stat", 1);
+    TSNE_HIP(hipMemsetAsync(cs.stat, 0, sizeof(int32_t), ctx->stream));
+}
+
+int64_t csort_oversized(tsne_ctx *ctx, const CoherentSort &cs) {
+    if (cs.P <= 0 || !cs.stat) return 0;
+    int32_t h = 0;
+    TSNE_HIP(hipMemcpyAsync(&h, cs.stat, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    return h;
 }
 
 void csort_run(tsne_ctx *ctx, CoherentSort &cs, const uint64_t *keys, const int32_t *prev, uint64_t *keys_sorted,

@@ -5,7 +5,7 @@
 // n = 1M (its merge-sort path: ~20 launches), a quarter of the 2-D build.
 // The embedding moves little between iterations, so the previous build's
 // sorted order nearly sorts the new keys: P splitters taken from it at equal
-// steps cut the key range into buckets of ~1024 points, the points are
+// steps (oversampled 8x) cut the key range into buckets of ~1024 points, the points are
 // scattered to their buckets (in the previous order: a workgroup's points
 // fall into a few adjacent buckets), and each bucket is sorted in LDS.
 // Output: keys ascending, ties by point index -- exactly the stable radix
@@ -30,14 +30,17 @@ struct CoherentSort {
     int32_t *stat = nullptr;        // [0] oversized buckets of the last sort (diagnostics)
 };
 
-// Buffers for n points (ctx workspace, names pre + field).  n < CSORT_MIN_N:
-// nothing (the callers keep rocPRIM's sort).
+// Buffers for n points (ctx workspace, names pre + field).  n outside
+// [CSORT_MIN_N, CSORT_MAX_N]: nothing (the callers keep rocPRIM's sort).
 constexpr int64_t CSORT_MIN_N = 16384;
+constexpr int64_t CSORT_MAX_N = 2000000;   // <= 1024 buckets of ~2k points (LDS capacity 4k)
 void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &pre);
 // keys[p] for points p < n -> keys_sorted / idx_sorted ascending by (key, p).
 // prev_idx_sorted: the previous sort's idx_sorted (a permutation of [0, n));
 // it may be the same buffer as idx_sorted (read before it is written).
 void csort_run(tsne_ctx *ctx, CoherentSort &cs, const uint64_t *keys, const int32_t *prev_idx_sorted,
                uint64_t *keys_sorted, int32_t *idx_sorted, hipStream_t st);
+// Oversized buckets of the last csort_run (synchronises the context's stream; 0 if none ran).
+int64_t csort_oversized(tsne_ctx *ctx, const CoherentSort &cs);
 
 }  // namespace tsne
