@@ -7,31 +7,33 @@ namespace {
 constexpr int CS_BLK = 1024;      // elements per count / scatter workgroup
 constexpr int CS_TARGET = 1024;   // points per bucket
 constexpr int CS_PMAX = 1024;     // buckets at most
-constexpr int CS_OVS = 8;         // samples per bucket (splitters: every CS_OVS-th sorted sample)
+constexpr int CS_OVS = 4;         // samples per bucket (splitters: every CS_OVS-th sorted sample)
 constexpr int CS_CAP = 4096;      // bucket capacity of the LDS sort (48 KB)
-constexpr int CS_SORT_T = 512;    // threads of a bucket's sort
+constexpr int CS_SORT_T = 1024;   // threads of a bucket's sort
 
 // (k, v) < (k2, v2) lexicographically
 __device__ __forceinline__ bool kv_less(uint64_t k, int32_t v, uint64_t k2, int32_t v2) {
     return k < k2 || (k == k2 && v < v2);
 }
 
-// Bitonic sort of N (a power of two) (key, value) pairs in a[] / b[] (LDS or
-// global memory private to the workgroup), T threads, ascending by (key, value).
-template <int T>
-__device__ void bitonic_kv(uint64_t *a, int32_t *b, int N) {
+// Bitonic sorts of N (a power of two) entries, T threads: stage (k, j) has
+// N / 2 compare-exchange pairs (i, i + j), i = the pair index p with a zero
+// bit inserted at j, taken p = tid, tid + T, ... (every thread busy).
+__device__ __forceinline__ int bitonic_lo(int p, int j) { return ((p & ~(j - 1)) << 1) | (p & (j - 1)); }
+
+// (key, value) pairs ascending by (key, value); a / b in LDS or in global
+// memory private to the workgroup (one network, instantiated per space)
+template <int T, class KP, class VP>
+__device__ __forceinline__ void bitonic_kv(KP a, VP b, int N) {
     for (int k = 2; k <= N; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < N; i += T) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint64_t ka = a[i], kl = a[l];
-                    const int32_t va = b[i], vl = b[l];
-                    const bool up = (i & k) == 0;
-                    if (kv_less(kl, vl, ka, va) == up) {
-                        a[i] = kl; a[l] = ka;
-                        b[i] = vl; b[l] = va;
-                    }
+            for (int p = threadIdx.x; p < (N >> 1); p += T) {
+                const int i = bitonic_lo(p, j), l = i + j;
+                const uint64_t ka = a[i], kl = a[l];
+                const int32_t va = b[i], vl = b[l];
+                if (kv_less(kl, vl, ka, va) == ((i & k) == 0)) {
+                    a[i] = kl; a[l] = ka;
+                    b[i] = vl; b[l] = va;
                 }
             }
             __syncthreads();
@@ -39,17 +41,15 @@ __device__ void bitonic_kv(uint64_t *a, int32_t *b, int N) {
     }
 }
 
-// Bitonic sort of N (a power of two) keys in LDS, T threads, ascending.
+// keys ascending (LDS)
 template <int T>
-__device__ void bitonic_k(uint64_t *a, int N) {
+__device__ __forceinline__ void bitonic_k(uint64_t *a, int N) {
     for (int k = 2; k <= N; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < N; i += T) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const uint64_t ka = a[i], kl = a[l];
-                    if ((kl < ka) == ((i & k) == 0)) { a[i] = kl; a[l] = ka; }
-                }
+            for (int p = threadIdx.x; p < (N >> 1); p += T) {
+                const int i = bitonic_lo(p, j), l = i + j;
+                const uint64_t ka = a[i], kl = a[l];
+                if ((kl < ka) == ((i & k) == 0)) { a[i] = kl; a[l] = ka; }
             }
             __syncthreads();
         }
@@ -60,14 +60,25 @@ __device__ void bitonic_k(uint64_t *a, int N) {
 // order, sorted; every CS_OVS-th.  The previous order keeps the coarse Morton
 // cells in place, but inside a dense cell the order is new every iteration
 // (the box moves its deep cell boundaries), so the samples there are random
-// ones: oversampling keeps the buckets within ~2x of their mean.
+// ones: 4x oversampling keeps the buckets within ~3.3x of their mean on the
+// C3 snapshots (max 3290 of 1024 at t = 650, CS_CAP 4096).
 __global__ __launch_bounds__(1024) void cs_split(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
                                                  int64_t n, int32_t P, uint64_t *__restrict__ split) {
     __shared__ uint64_t s[CS_OVS * CS_PMAX];
     const int S = CS_OVS * P;
     int N = 2;
     while (N < S) N <<= 1;
-    for (int j = threadIdx.x; j < N; j += 1024) s[j] = j < S ? keys[prev[(int64_t)j * n / S]] : ~0ull;
+    int32_t pi[CS_OVS];   // every thread's gathers in flight together
+#pragma unroll
+    for (int e = 0; e < CS_OVS; ++e) {
+        const int j = threadIdx.x + 1024 * e;
+        pi[e] = j < S ? prev[(int64_t)j * n / S] : 0;
+    }
+#pragma unroll
+    for (int e = 0; e < CS_OVS; ++e) {
+        const int j = threadIdx.x + 1024 * e;
+        if (j < N) s[j] = j < S ? keys[pi[e]] : ~0ull;
+    }
     __syncthreads();
     bitonic_k<1024>(s, N);
     for (int j = threadIdx.x; j < P; j += 1024) split[j] = s[j * CS_OVS];
@@ -180,18 +191,30 @@ __global__ __launch_bounds__(CS_SORT_T) void cs_bucket(const int32_t *__restrict
     if (m == 0) return;
     int N = 2;
     while (N < m) N <<= 1;
-    uint64_t *a = sk;
-    int32_t *v = sv;
-    if (m > CS_CAP) { a = kb + n + 2 * (int64_t)o; v = vb + n + 2 * (int64_t)o; }
-    for (int i = threadIdx.x; i < N; i += CS_SORT_T) {
-        a[i] = i < m ? kb[o + i] : ~0ull;
-        v[i] = i < m ? vb[o + i] : INT32_MAX;
-    }
-    __syncthreads();
-    bitonic_kv<CS_SORT_T>(a, v, N);
-    for (int i = threadIdx.x; i < m; i += CS_SORT_T) {
-        keys_sorted[o + i] = a[i];
-        idx_sorted[o + i] = v[i];
+    if (m <= CS_CAP) {   // LDS (its own instantiation: ds_ instructions, not flat ones)
+        for (int i = threadIdx.x; i < N; i += CS_SORT_T) {
+            sk[i] = i < m ? kb[o + i] : ~0ull;
+            sv[i] = i < m ? vb[o + i] : INT32_MAX;
+        }
+        __syncthreads();
+        bitonic_kv<CS_SORT_T>(sk, sv, N);
+        for (int i = threadIdx.x; i < m; i += CS_SORT_T) {
+            keys_sorted[o + i] = sk[i];
+            idx_sorted[o + i] = sv[i];
+        }
+    } else {
+        uint64_t *a = kb + n + 2 * (int64_t)o;
+        int32_t *v = vb + n + 2 * (int64_t)o;
+        for (int i = threadIdx.x; i < N; i += CS_SORT_T) {
+            a[i] = i < m ? kb[o + i] : ~0ull;
+            v[i] = i < m ? vb[o + i] : INT32_MAX;
+        }
+        __syncthreads();
+        bitonic_kv<CS_SORT_T>(a, v, N);
+        for (int i = threadIdx.x; i < m; i += CS_SORT_T) {
+            keys_sorted[o + i] = a[i];
+            idx_sorted[o + i] = v[i];
+        }
     }
 }
 

@@ -5,7 +5,7 @@
 // n = 1M (its merge-sort path: ~20 launches), a quarter of the 2-D build.
 // The embedding moves little between iterations, so the previous build's
 // sorted order nearly sorts the new keys: P splitters taken from it at equal
-// steps (oversampled 8x) cut the key range into buckets of ~1024 points, the points are
+// steps (oversampled 4x) cut the key range into buckets of ~1024 points, the points are
 // scattered to their buckets (in the previous order: a workgroup's points
 // fall into a few adjacent buckets), and each bucket is sorted in LDS.
 // Output: keys ascending, ties by point index -- exactly the stable radix
