@@ -2717,10 +2717,14 @@ __global__ void block_cost_keys(const int32_t *__restrict__ cost, int64_t nwaves
 // Heavy groups a traversal of `waves` 64-query waves turns narrow to fill the
 // chip: narrowing h groups adds (NPARTS - 1) h waves; up to 8 waves per SIMD
 // (32 per CU) in all.  0 once the 64-query waves alone fill it (one rank of
-// 1M points: 15,625 waves).
+// 1M points: 15,625 waves).  Below half of that (one of 8 ranks at C3: 1,953
+// waves) every group: there each 64-query wave is one latency-bound chain
+// with ~2 waves per SIMD beside it, and the narrow layout cuts the chain
+// (W = 8 projection, scripts/loop_projection.py: span 4.83 -> 3.99 s).
 int64_t narrow_fill(const tsne_ctx *ctx, int64_t waves) {
     const int64_t cap = 32 * (int64_t)ctx->cu_count;
-    return waves >= cap ? 0 : (cap - waves) / (NPARTS - 1);
+    if (waves >= cap) return 0;
+    return waves < cap / 2 ? waves : (cap - waves) / (NPARTS - 1);
 }
 
 }  // namespace
@@ -2851,7 +2855,7 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
     t.ch_scan_bytes = cb;
     t.ch_scan_tmp = ws.get<uint8_t>(pre + "ch_scan_tmp", cb);
     // narrow layout of heavy groups: at most 1/8 of the groups, their moment lists
-    t.nar_hmax = std::max<int64_t>({(int64_t)1, ceil_div(qwaves, 8), std::min<int64_t>(qwaves, narrow_fill(ctx, 0))});
+    t.nar_hmax = std::max<int64_t>({(int64_t)1, ceil_div(qwaves, 8), std::min<int64_t>(qwaves, 16 * (int64_t)ctx->cu_count)});
     t.nflag = ws.get<int32_t>(pre + "nflag", t.tile_waves);
     TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * t.tile_waves, ctx->stream));
     t.hlist = ws.get<int32_t>(pre + "hlist", t.nar_hmax);
