@@ -131,9 +131,6 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             binary-node walk);
  *   "attract_overlap" 1       the 2-D attraction of a non-loss iteration runs
  *                             beside the BH kernels (0: after them);
- *   "attract_split" 0         > 0: the tiled attraction of a non-loss
- *                             iteration starts before the tree build, on this
- *                             share of the CUs;
  *   "coherent_sort" 1         the trees' Morton sort from the previous build's
  *                             order (0: rocPRIM's radix sort; the same
  *                             permutation);

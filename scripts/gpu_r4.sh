@@ -26,7 +26,7 @@ if has snap; then
   done
 fi
 if has tests_narrow; then
-  tst 900 python -u -m pytest tests/test_gpu_schedule.py tests/test_gpu_csort.py tests/test_gpu_narrow.py tests/test_gpu_parity.py -v -p no:cacheprovider \
+  tst 900 python -u -m pytest tests/test_gpu_csort.py tests/test_gpu_narrow.py tests/test_gpu_parity.py -v -p no:cacheprovider \
       --timeout 300 --timeout-method thread > $O/tests_narrow.log 2>&1 || exit $?
 fi
 if has tests_multi; then

@@ -376,31 +376,27 @@ using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
 
-// Row blocks (owned rows [b0, b0 + RB) of [0, rows), label r0 + local row) in
-// XCD-chunked order: one per workgroup, or with a grid smaller than nrb
-// (Options::attract_split: the attraction beside the tree build on part of
-// the chip) each workgroup takes every gridDim.x-th in turn.  attr / lpart
-// as attract_rows (lpart per workgroup).
+// One workgroup per row block (owned rows [b0, b0 + RB) of [0, rows), label
+// r0 + local row); XCD-chunked block order.  attr / lpart as attract_rows.
 template <class CF, bool LOSS, int MET>
 __global__ __launch_bounds__(CF::NT) void attract_tiles(
     const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
     const uint32_t *__restrict__ srow, int64_t rows, int64_t r0, int64_t n, const uint16_t *__restrict__ pk,
     const double *__restrict__ pv, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
-    int64_t xcd_chunk, int64_t nrb, double2 *__restrict__ attr, double *__restrict__ lpart) {
+    int64_t xcd_chunk, double2 *__restrict__ attr, double *__restrict__ lpart) {
     constexpr int RB = CF::RB, W = CF::W, NT = CF::NT, WAVES = CF::WAVES;
     __shared__ double2 win[W];
     __shared__ double2 acc[RB];
     __shared__ double sl[WAVES];
     const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-    const double Z = LOSS ? scal[0] : 1.0;
-    double lsum = 0.0;
-    for (int64_t v = blockIdx.x; v < nrb; v += gridDim.x) {
-    const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(v, nrb, xcd_chunk) : v;
+    const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t b0 = rb * RB;
     const int nr = (int)min((int64_t)RB, rows - b0);
     const double2 *Y2 = reinterpret_cast<const double2 *>(Y);
     const double2 *Yrow = Y2 + r0 + b0;
     for (int i = tid; i < nr; i += NT) acc[i] = make_double2(0.0, 0.0);
+    const double Z = LOSS ? scal[0] : 1.0;
+    double lsum = 0.0;
     constexpr int WL = (W + NT - 1) / NT;
     const int t0 = rbt[rb], t1 = rbt[rb + 1];
     for (int t = t0; t < t1; ++t) {
@@ -486,8 +482,6 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
         __syncthreads();
     }
     for (int i = tid; i < nr; i += NT) attr[b0 + i] = acc[i];
-    __syncthreads();   // acc is the next row block's
-    }
     if (LOSS) {
         lsum = wave_sum(lsum);
         if (lane == 0) sl[w] = lsum;
@@ -1140,7 +1134,6 @@ struct AttractArgs {
     const int64_t *rp; const int32_t *col; const double *val; int64_t r0, r1; const double *Y;
     const double *scal; int metric; double ex; double2 *attr; double *lpart;
     int bpc = 0;   // blocks per CU of the persistent grid (0: 8 = every wave slot)
-    int64_t grid = 0;   // attract_tiles: workgroups (0: one per row block)
 };
 
 // persistent grid: bpc 256-thread blocks per CU (8: every wave slot), a
@@ -1945,10 +1938,9 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
 template <class CF, bool LOSS, int MET>
 static void attract_tiles_launch_c(hipStream_t st, const OptState *s, const AttractArgs &a) {
     const int64_t nb = s->at_nrb;
-    const int64_t g = a.grid > 0 ? std::min<int64_t>(nb, a.grid) : nb;
-    hipLaunchKernelGGL((attract_tiles<CF, LOSS, MET>), dim3(g), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt,
+    hipLaunchKernelGGL((attract_tiles<CF, LOSS, MET>), dim3(nb), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt,
                        s->at_slices, s->at_srow, a.r1 - a.r0, a.r0, s->n, s->at_pk, s->at_pv, a.Y, a.scal, a.ex,
-                       nb / NUM_XCD, nb, a.attr, a.lpart);
+                       nb / NUM_XCD, a.attr, a.lpart);
 }
 template <bool LOSS, int MET>
 static void attract_tiles_launch_m(hipStream_t st, const OptState *s, const AttractArgs &a) {
@@ -1978,7 +1970,7 @@ static int64_t attract_launch_opt(hipStream_t st, const OptState *s, const Attra
     if (!s->at_on) return attract_launch(st, a, loss);
     if (loss) attract_tiles_launch_l<true>(st, s, a);
     else attract_tiles_launch_l<false>(st, s, a);
-    return a.grid > 0 ? std::min<int64_t>(s->at_nrb, a.grid) : s->at_nrb;
+    return s->at_nrb;
 }
 
 void opt_step(tsne_ctx *ctx, int32_t t) {
@@ -2029,13 +2021,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         s->log_attract(t, want_loss ? 2 : 0);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
-    // Options::attract_split > 0: a non-loss tiled attraction starts before the
-    // build on that share of the CUs (persistent grid, NUM_XCD multiples), so
-    // that the build's and the traversal's kernels keep the rest of the chip
-    const bool split_attract = !rt_phase && !want_loss && s->at_on && ctx->opts.attract_split > 0.0;
-    if (split_attract)
-        aa.grid = std::max<int64_t>(NUM_XCD, (int64_t)(ctx->opts.attract_split * ctx->cu_count) / NUM_XCD * NUM_XCD);
-    if (rt_phase || split_attract) side_attract();
+    if (rt_phase) side_attract();
     // 1. tree (identical on every rank)
     // insertion rows = original indices; the root-tile shortcut while the
     // embedding is small
@@ -2045,8 +2031,8 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (world > 1) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
     // Options::attract_overlap 0: after the BH kernels instead (attract_tiles
     // holds ~156 KB of LDS per CU: beside them it time-slices the CUs with them)
-    const bool late_attract = !rt_phase && !split_attract && ctx->opts.attract_overlap == 0;
-    if (!rt_phase && !split_attract && !late_attract) side_attract();
+    const bool late_attract = !rt_phase && ctx->opts.attract_overlap == 0;
+    if (!rt_phase && !late_attract) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
