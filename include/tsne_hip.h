@@ -129,8 +129,6 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "oct_records" 2           3-D: octal records and the 64-query record
  *                             traversal (1: the 8-query one; 0: the
  *                             binary-node walk);
- *   "attract_overlap" 1       the 2-D attraction of a non-loss iteration runs
- *                             beside the BH kernels (0: after them);
  *   "coherent_sort" 1         the trees' Morton sort from the previous build's
  *                             order (0: rocPRIM's radix sort; the same
  *                             permutation);

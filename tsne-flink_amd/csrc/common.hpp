@@ -169,7 +169,6 @@ struct Options {
     double near_tol3_early = 1e-7, near_tol3_late = 5e-6;  // the 3-D octree's
     double mom3_tol = 1e-12;
     int oct_moments = 1;      // 3-D subtree moments
-    int attract_overlap = 1;  // 2-D attraction beside the BH kernels (0: after them, still beside the Z reduce)
     int coherent_sort = 1;    // the trees' Morton sort from the previous build's order (csort.hpp; 0: rocPRIM's radix sort)
     int oct_records = 2;      // 3-D: octal records + the 64-query record traversal (1: the 8-query one; 0: the binary-node walk)
     int root_tile = 1;        // root-tile shortcut of the small-embedding phase

@@ -2029,10 +2029,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // amplify any difference fastest there), the late one after
     bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(ctx), bh_near_tol(ctx, ex == 1.0));
     if (world > 1) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
-    // Options::attract_overlap 0: after the BH kernels instead (attract_tiles
-    // holds ~156 KB of LDS per CU: beside them it time-slices the CUs with them)
-    const bool late_attract = !rt_phase && ctx->opts.attract_overlap == 0;
-    if (!rt_phase && !late_attract) side_attract();
+    if (!rt_phase) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
@@ -2047,7 +2044,6 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
-    if (late_attract) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
     reduce_Z(ctx, s, s->z);
