@@ -35,9 +35,11 @@ if has tests_multi; then
 fi
 if has bench; then
   for v in ${BENCH_VARS:--}; do
-    opt=""; [ "$v" != "-" ] && opt="--option $v"
+    # "-": defaults; "lib=PATH": another build of the library (TSNE_HIP_LIB); else KEY=VALUE options
+    opt=""; lib=""
+    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option $v" ;; esac
     echo "# $v" >> $O/bench.jsonl
-    run 400 python bench.py --no-cpu-baseline $opt >> $O/bench.jsonl 2>> $O/bench.err || exit $?
+    TSNE_HIP_LIB="$lib" run 400 python bench.py --no-cpu-baseline $opt >> $O/bench.jsonl 2>> $O/bench.err || exit $?
   done
 fi
 if has tests3d; then
@@ -48,9 +50,10 @@ if has tests3d; then
 fi
 if has bench4; then
   for v in ${BENCH4_VARS:--}; do
-    opt=""; [ "$v" != "-" ] && opt="--option $v"
+    opt=""; lib=""
+    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option $v" ;; esac
     echo "# $v" >> $O/bench4.jsonl
-    run 600 python bench.py --config c4 --no-cpu-baseline $opt >> $O/bench4.jsonl 2>> $O/bench4.err || exit $?
+    TSNE_HIP_LIB="$lib" run 600 python bench.py --config c4 --no-cpu-baseline $opt >> $O/bench4.jsonl 2>> $O/bench4.err || exit $?
   done
 fi
 if has ktrace; then
