@@ -2007,14 +2007,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                             ++sp;
                         }
                     }
-                    if (__ballot(wm != 0.0)) {   // some lane takes the term
-                        const double Q = recip_bh(1.0 + D);
-                        const double mult = wm * Q;
-                        const double sc = mult * Q;
-                        fx = __fma_rn(sc, dx, fx);
-                        fy = __fma_rn(sc, dy, fy);
-                        zs += mult;
-                    }
+                    const double Q = recip_bh(1.0 + D);
+                    const double mult = wm * Q;
+                    const double sc = mult * Q;
+                    fx = __fma_rn(sc, dx, fx);
+                    fy = __fma_rn(sc, dy, fy);
+                    zs += mult;
                     if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
                         const uint64_t am = __ballot(act), tk2 = __ballot(take);
                         if (am && tk2 == am) {

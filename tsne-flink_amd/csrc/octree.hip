@@ -1314,15 +1314,13 @@ __global__ __launch_bounds__(256) void oct_traverse64(
                         ++sp;
                     }
                 }
-                if (__ballot(wm != 0.0)) {   // some lane takes the term (in the transition most cells open)
-                    const double Qv = rcp2(1.0 + D);
-                    const double mult = wm * Qv;
-                    const double sc = mult * Qv;
-                    fx = __fma_rn(sc, dx, fx);
-                    fy = __fma_rn(sc, dy, fy);
-                    fz = __fma_rn(sc, dz, fz);
-                    zs += mult;
-                }
+                const double Qv = rcp2(1.0 + D);
+                const double mult = wm * Qv;
+                const double sc = mult * Qv;
+                fx = __fma_rn(sc, dx, fx);
+                fy = __fma_rn(sc, dy, fy);
+                fz = __fma_rn(sc, dz, fz);
+                zs += mult;
             }
             if (__builtin_expect(kinds & 0xAAAA, 0)) {   // key-tie groups: every point directly
                 for (int c = 0; c < nch; ++c) {
