@@ -70,7 +70,11 @@ if has pmc; then
   run 1300 bash scripts/gpu_pmc.sh || exit $?
 fi
 if has c4probe; then
-  run 300 python scripts/c4_probe.py ${C4PROBE_ARGS:-} > $O/c4probe.log 2>&1 || exit $?
+  for v in ${C4PROBE_VARS:--}; do
+    opt=""; [ "$v" != "-" ] && opt="--option $v"
+    echo "# $v" >> $O/c4probe.log
+    run 300 python scripts/c4_probe.py ${C4PROBE_ARGS:-} $opt >> $O/c4probe.log 2>&1 || exit $?
+  done
 fi
 if has snap3; then   # C4 snapshots in the transition, timed, counted and PMC-profiled
   S3=${SNAP3_T:-120,150,180}
