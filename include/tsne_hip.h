@@ -129,6 +129,9 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "oct_records" 2           3-D: octal records and the 64-query record
  *                             traversal (1: the 8-query one; 0: the
  *                             binary-node walk);
+ *   "oct_layout_switch" 6     3-D with oct_records 2: the 8-query layout
+ *                             while the octree's root half-width is below
+ *                             this x the near-exact radius (0: never);
  *   "coherent_sort" 1         the trees' Morton sort from the previous build's
  *                             order (0: rocPRIM's radix sort; the same
  *                             permutation);

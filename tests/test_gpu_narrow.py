@@ -173,6 +173,7 @@ def test_octal_records_match_binary_walk_and_oracle(n, scale, theta):
     for rec in (1, 2, 0):
         with T.Context(0) as c:
             c.set_option("oct_records", rec)
+            c.set_option("oct_layout_switch", 0)   # each layout at every scale
             g, Z, loss = c.gradient(rp, col, val, Y, theta, exaggeration=4.0, want_loss=True)
             F, z = c.repulsion(Y, theta)
         assert np.abs(g - r["grad"]).max() <= tol * np.abs(r["grad"]).max(), rec

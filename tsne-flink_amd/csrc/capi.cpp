@@ -119,6 +119,7 @@ static const OptionField k_options[] = {
     {"oct_moments", nullptr, &Options::oct_moments, 0, 1},
     {"oct_records", nullptr, &Options::oct_records, 0, 2},
     {"coherent_sort", nullptr, &Options::coherent_sort, 0, 1},
+    {"oct_layout_switch", &Options::oct_layout_switch, nullptr, 0, 1e6},
     {"root_tile", nullptr, &Options::root_tile, 0, 1},
     {"attract_tiles", nullptr, &Options::attract_tiles, 0, 1},
     {"attract_cfg", nullptr, &Options::attract_cfg, -1, 3},

@@ -170,6 +170,7 @@ struct Options {
     double mom3_tol = 1e-12;
     int oct_moments = 1;      // 3-D subtree moments
     int coherent_sort = 1;    // the trees' Morton sort from the previous build's order (csort.hpp; 0: rocPRIM's radix sort)
+    double oct_layout_switch = 6.0;   // 3-D: the 8-query layout while the root half-width < this x sqrt(near_dmax)
     int oct_records = 2;      // 3-D: octal records + the 64-query record traversal (1: the 8-query one; 0: the binary-node walk)
     int root_tile = 1;        // root-tile shortcut of the small-embedding phase
     int attract_tiles = 1;    // tiled attraction (attract_tiles) where the labels allow it

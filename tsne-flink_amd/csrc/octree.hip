@@ -936,7 +936,7 @@ __global__ __launch_bounds__(256) void oct_traverse_rec(
     const ORec *__restrict__ orec, const int32_t *__restrict__ meta, double theta, int64_t g0, int64_t g1,
     const int32_t *__restrict__ qlist, int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
     int32_t *__restrict__ mtask_n, double *__restrict__ F, double *__restrict__ Z,
-    unsigned long long *__restrict__ dbg, double mom_tol) {
+    unsigned long long *__restrict__ dbg, double mom_tol, const double *__restrict__ Wp, double wthr, int regime) {
     __shared__ int32_t sref[4][OSTACK];
     __shared__ uint32_t smask[4][OSTACK];
     __shared__ ORec srec[4][OKPOP];
@@ -948,6 +948,9 @@ __global__ __launch_bounds__(256) void oct_traverse_rec(
     const int64_t kq = g0 + wid * OQ + q;
     const bool valid = kq < g1;
     if (__ballot(valid) == 0) return;
+    // per-iteration layout choice (oct_repulsion): regime 1 runs below the
+    // root half-width wthr, regime 2 at or above it, 0 always
+    if (regime != 0 && (regime == 1) != (*Wp < wthr)) return;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
     double qx = 0.0, qy = 0.0, qz = 0.0;
@@ -1170,7 +1173,7 @@ __global__ __launch_bounds__(256) void oct_traverse64(
     const ORec *__restrict__ orec, const int32_t *__restrict__ meta, double theta, int64_t g0, int64_t g1,
     const int32_t *__restrict__ qlist, int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
     int32_t *__restrict__ mtask_n, double *__restrict__ F, double *__restrict__ Z,
-    unsigned long long *__restrict__ dbg, double mom_tol) {
+    unsigned long long *__restrict__ dbg, double mom_tol, const double *__restrict__ Wp, double wthr, int regime) {
     __shared__ int32_t sref[4][O64_STACK];
     __shared__ uint64_t smask[4][O64_STACK];
     __shared__ ORec srec[4][O64_KB];
@@ -1181,6 +1184,9 @@ __global__ __launch_bounds__(256) void oct_traverse64(
     const int64_t kq = g0 + wid * 64 + lane;
     const bool valid = kq < g1;
     if (__ballot(valid) == 0) return;
+    // per-iteration layout choice (oct_repulsion): regime 1 runs below the
+    // root half-width wthr, regime 2 at or above it, 0 always
+    if (regime != 0 && (regime == 1) != (*Wp < wthr)) return;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
     double qx = 0.0, qy = 0.0, qz = 0.0;
@@ -1477,34 +1483,34 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
         dbg = ctx->ws.get<unsigned long long>("oct.dbg", 8);
         TSNE_HIP(hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), ctx->stream));
     }
-    if (ctx->opts.oct_records == 2) {   // the record traversal: 64 queries per wave
+    // the record traversals: 64 queries per wave (oct_records 2), or 8 (1);
+    // with oct_layout_switch > 0 the layout follows the embedding's size each
+    // iteration (device-side: both launched, one returns at once): the
+    // 8-query one while the root half-width is below oct_layout_switch x the
+    // near-exact radius (its dense tiles have sparse lane masks there), the
+    // 64-query one above (C4 transition, profiles/r04_s16_c4_probe_layouts.jsonl)
+    const bool sw = ctx->opts.oct_records == 2 && ctx->opts.oct_layout_switch > 0.0 && t.near_dmax > 0.0;
+    const double wthr = sw ? ctx->opts.oct_layout_switch * std::sqrt(t.near_dmax) : 0.0;
+    if (ctx->opts.oct_records == 2) {
         const int64_t nw = ceil_div(s1 - s0, 64);
-        if (debug)
-            hipLaunchKernelGGL(oct_traverse64<true>, dim3(ceil_div(nw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                               t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz,
-                               dbg, ctx->opts.mom3_tol);
-        else
-            hipLaunchKernelGGL(oct_traverse64<false>, dim3(ceil_div(nw, 4)), dim3(256), 0, ctx->stream, t.pos,
-                               t.dupc, t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
-                               dF, dz, dbg, ctx->opts.mom3_tol);
-    } else if (ctx->opts.oct_records) {   // the record traversal: 8 queries per wave
+        auto k64 = debug ? oct_traverse64<true> : oct_traverse64<false>;
+        hipLaunchKernelGGL(k64, dim3(ceil_div(nw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.orec,
+                           t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz, dbg,
+                           ctx->opts.mom3_tol, t.W, wthr, sw ? 2 : 0);
+    }
+    if (ctx->opts.oct_records == 1 || sw) {
         const int64_t rw = ceil_div(s1 - s0, OQ);
-        if (debug)
-            hipLaunchKernelGGL(oct_traverse_rec<true>, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                               t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz,
-                               dbg, ctx->opts.mom3_tol);
-        else
-            hipLaunchKernelGGL(oct_traverse_rec<false>, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos,
-                               t.dupc, t.nodes, t.orec, t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
-                               dF, dz, dbg, ctx->opts.mom3_tol);
-    } else if (debug)
-        hipLaunchKernelGGL(oct_traverse<true>, dim3(ceil_div(ceil_div(s1 - s0, 64), 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, t.near_dmax, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
-                           dF, dz, dbg, ctx->opts.mom3_tol);
-    else
-        hipLaunchKernelGGL(oct_traverse<false>, dim3(ceil_div(ceil_div(s1 - s0, 64), 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
-                           t.nodes, t.meta, theta, t.near_dmax, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n,
-                           dF, dz, dbg, ctx->opts.mom3_tol);
+        auto k8 = debug ? oct_traverse_rec<true> : oct_traverse_rec<false>;
+        hipLaunchKernelGGL(k8, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.orec,
+                           t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz, dbg,
+                           ctx->opts.mom3_tol, t.W, wthr, sw ? 1 : 0);
+    }
+    if (ctx->opts.oct_records == 0) {   // the binary-node walk
+        auto kb = debug ? oct_traverse<true> : oct_traverse<false>;
+        hipLaunchKernelGGL(kb, dim3(ceil_div(ceil_div(s1 - s0, 64), 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc,
+                           t.nodes, t.meta, theta, t.near_dmax, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz,
+                           dbg, ctx->opts.mom3_tol);
+    }
     hipLaunchKernelGGL(oct_mom_apply, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, ctx->stream, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz);
     if (debug) {
