@@ -46,8 +46,8 @@ METRIC = "t-SNE iterations/sec + end-to-end sec at N=1M×128 on 1/2/4/8 MI355X; 
 FP32_MFMA_PEAK_TF = 157.3
 BF16_MFMA_PEAK_TF = 2500.0   # dense (MI355X_MICROARCH.md); the kNN filter's bf16x3 passes run 3 bf16 MFMAs per product
 HBM_PEAK_GBS = 8000.0
-PMC_ATTRACT = "r03_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
-PMC_BH = "r03_bh_valu.json"
+PMC_ATTRACT = "r04_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
+PMC_BH = "r04_bh_valu.json"
 
 
 def parse():
@@ -439,6 +439,12 @@ def main():
                      "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
                      "bytes_per_launch": attr_bytes, "avg_ms": attr_ms, "launches": len(nonloss),
                      "avg_ms_window": float(np.mean(win_nl)) if win_nl else None,
+                     # the window's launches (root-tile phase: beside the short build kernels
+                     # only); over the schedule the launches share the CUs with the BH kernels
+                     # (attract_tiles' 156 KB of LDS per CU time-slices them), so their event
+                     # time is the overlap's, not the kernel's own
+                     "frac_window": (attr_bytes / (float(np.mean(win_nl)) * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                     if win_nl else None,
                      "loss_launch": {"kernel": attr_kernel.replace("LOSS=false", "LOSS=true") + " + KL terms",
                                      "avg_ms": float(np.mean(loss_l)) if loss_l else None,
                                      "launches": len(loss_l)}},
