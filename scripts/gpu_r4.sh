@@ -8,6 +8,7 @@
 #   pmc         scripts/gpu_pmc.sh (summarise with scripts/pmc_summary.py <tag>)
 #   c4probe     scripts/c4_probe.py C4PROBE_ARGS
 #   snap3       C4 snapshots (SNAP3_T) written by c4_probe, timed per SNAP3_VARS, debug counters, PMC
+#   pmcsnap     PMC passes (SQ waits / LDS / VALU) over the BH kernels on snaps/Y_t{250,650}.npy
 #   proj        scripts/loop_projection.py PROJ_ARGS per PROJ_VARS entry
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -93,6 +94,15 @@ if has snap3; then   # C4 snapshots in the transition, timed, counted and PMC-pr
     k=$((k+1))
     timeout -s KILL 180 rocprofv3 --pmc $pass --kernel-include-regex "oct_" -d $O/pmc3_$k -o pmc --output-format csv -- \
       python scripts/bh_snap.py $files --reps 0 > $O/pmc3_$k.log 2>&1 || exit $?
+  done
+fi
+if has pmcsnap; then   # PMC passes over the 2-D BH kernels on the committed C3 snapshots
+  k=0
+  for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
+              "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
+    k=$((k+1))
+    timeout -s KILL 180 rocprofv3 --pmc $pass --kernel-include-regex "bh_traverse|tile_apply" -d $O/pmcs_$k -o pmc \
+      --output-format csv -- python scripts/bh_snap.py snaps/Y_t250.npy snaps/Y_t650.npy --reps 1 > $O/pmcs_$k.log 2>&1 || exit $?
   done
 fi
 if has proj; then
