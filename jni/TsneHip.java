@@ -21,6 +21,8 @@ public final class TsneHip {
      *  optimize fan out over them from this one call (SURVEY.md 8b "Threading"). */
     public static native long ctxCreateMulti(int[] devices);
     public static native void ctxDestroy(long ctx);
+    /** tsne_ctx_set_option: per-handle tunables (include/tsne_hip.h; the defaults are the library's choices). */
+    public static native void ctxSetOption(long ctx, String key, double value);
 
     /** Tsne.getMetric (Tsne.scala:161-168): unknown name -> IllegalArgumentException. */
     public static native int metricFromName(String name);

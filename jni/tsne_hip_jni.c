@@ -55,6 +55,16 @@ JNIEXPORT void JNI_FN(ctxDestroy)(JNIEnv *e, jclass c, jlong ctx) {
     tsne_ctx_destroy(CTX(ctx));
 }
 
+/* Per-handle tunables (tsne_ctx_set_option); unknown keys / bad values throw
+ * IllegalArgumentException. */
+JNIEXPORT void JNI_FN(ctxSetOption)(JNIEnv *e, jclass c, jlong ctx, jstring key, jdouble value) {
+    (void)c;
+    const char *k = (*e)->GetStringUTFChars(e, key, NULL);
+    const int rc = tsne_ctx_set_option(CTX(ctx), k, value);
+    (*e)->ReleaseStringUTFChars(e, key, k);
+    chk(e, rc);
+}
+
 JNIEXPORT jint JNI_FN(metricFromName)(JNIEnv *e, jclass c, jstring name) {
     (void)c;
     const char *s = (*e)->GetStringUTFChars(e, name, NULL);
