@@ -138,6 +138,7 @@ struct LoopGroup {
             size_t m = segs[0].size();
             for (int r = 1; r < world; ++r) m = std::min(m, segs[r].size());
             std::map<std::string, std::vector<double>> lab;   // [sum of max, sum of mean, count]
+            std::map<std::string, std::vector<double>> ser;   // per 100 occurrences of a label: sum of max
             double span = 0.0;
             std::vector<double> tot(world, 0.0);
             for (size_t i = 0; i < m; ++i) {
@@ -149,7 +150,11 @@ struct LoopGroup {
                 }
                 auto &v = lab[segs[0][i].first];
                 if (v.empty()) v.assign(3, 0.0);
+                const size_t occ = (size_t)v[2];
                 v[0] += mx; v[1] += sm / world; v[2] += 1.0;
+                auto &sv = ser[segs[0][i].first];
+                if (sv.size() <= occ / 100) sv.resize(occ / 100 + 1, 0.0);
+                sv[occ / 100] += mx;
                 span += mx;
             }
             fprintf(f, "{\"world\": %d, \"segments\": %zu, \"span_ms\": %.6f, \"rank_total_ms\": [", world, m, span);
@@ -159,6 +164,14 @@ struct LoopGroup {
             for (auto &kv : lab) {
                 fprintf(f, "%s\"%s\": {\"max_ms\": %.6f, \"mean_ms\": %.6f, \"count\": %.0f}", first ? "" : ", ",
                         kv.first.c_str(), kv.second[0], kv.second[1], kv.second[2]);
+                first = false;
+            }
+            fprintf(f, "}, \"max_ms_per_100\": {");
+            first = true;
+            for (auto &kv : ser) {
+                fprintf(f, "%s\"%s\": [", first ? "" : ", ", kv.first.c_str());
+                for (size_t b = 0; b < kv.second.size(); ++b) fprintf(f, "%s%.3f", b ? ", " : "", kv.second[b]);
+                fprintf(f, "]");
                 first = false;
             }
             fprintf(f, "}}\n");
