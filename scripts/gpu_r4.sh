@@ -27,7 +27,7 @@ if has snap; then
   done
 fi
 if has tests_narrow; then
-  tst 900 python -u -m pytest tests/test_gpu_csort.py tests/test_gpu_narrow.py tests/test_gpu_parity.py -v -p no:cacheprovider \
+  TSNE_HIP_LIB="${TESTS_LIB:-}" tst 900 python -u -m pytest tests/test_gpu_csort.py tests/test_gpu_narrow.py tests/test_gpu_parity.py -v -p no:cacheprovider \
       --timeout 300 --timeout-method thread > $O/tests_narrow.log 2>&1 || exit $?
 fi
 if has tests_multi; then
@@ -107,9 +107,10 @@ if has pmcsnap; then   # PMC passes over the 2-D BH kernels on the committed C3 
 fi
 if has proj; then
   for v in ${PROJ_VARS:--}; do
-    opt=""; [ "$v" != "-" ] && opt="--option $v"
+    opt=""; lib=""
+    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option $v" ;; esac
     echo "# $v" >> $O/proj.jsonl
-    run 600 python scripts/loop_projection.py ${PROJ_ARGS:-} $opt >> $O/proj.jsonl 2>> $O/proj.err || exit $?
+    TSNE_HIP_LIB="$lib" run 600 python scripts/loop_projection.py ${PROJ_ARGS:-} $opt >> $O/proj.jsonl 2>> $O/proj.err || exit $?
   done
 fi
 echo done > $O/done.txt

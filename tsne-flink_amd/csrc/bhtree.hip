@@ -1558,19 +1558,24 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
 // result does not depend on timing (it differs from the 64-query layout's
 // association only at rounding level: the same cells are summarised, the
 // same leaves and tiles summed).
-constexpr int NQ = 4;              // queries per narrow wave
 constexpr int NQ_LOG = 2;
+constexpr int NQ = 1 << NQ_LOG;    // queries per narrow wave
 constexpr int NKP = 16 / NQ;       // stack entries per narrow pass
 constexpr int NPARTS = 64 / NQ;    // narrow waves per 64-query group (NPARTS / 4 workgroups)
-static_assert(NQ == (1 << NQ_LOG) && NKP * NQ * 4 == 64 && NPARTS % 4 == 0, "narrow lane layout");
+static_assert(NKP * NQ * 4 == 64 && NPARTS % 4 == 0 && NKP <= 8, "narrow lane layout");
 
 // bits {4 i : i < NQ} of x (one query per 4 lanes) -> bits {i}
 __device__ __forceinline__ uint32_t narrow_compress(uint64_t x) {
-    static_assert(NQ == 4, "narrow_compress: 4 queries per record");
-    x &= 0x1111ull;
-    x = (x | (x >> 3)) & 0x0303ull;
-    x = (x | (x >> 6)) & 0x000Full;
-    return (uint32_t)x;
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) m |= (uint32_t)((x >> (4 * i)) & 1ull) << i;
+    return m;
+}
+// lanes (k, q, c = 0) for every record slot k: query q's first lane in each
+__host__ __device__ constexpr uint64_t narrow_qcol0() {
+    uint64_t m = 0;
+    for (int k = 0; k < NKP; ++k) m |= 1ull << (k * 4 * NQ);
+    return m;
 }
 
 struct NarrowView {
@@ -1583,18 +1588,23 @@ struct NarrowView {
     int32_t nbn = 0;                   // workgroups of the narrow part of the grid (hmax x NPARTS / 4)
 };
 
-// The traversal kernel's state shared by both layouts (LDS per 4-wave block).
-struct TravLDS {
+// The traversal kernels' state (LDS per 4-wave block): KB records per batch
+// (4 in the 64-query layout, NKP in the narrow one).
+template <int KB>
+struct TravLDS_T {
     int32_t sref[4][STACK];
     uint64_t smask[4][STACK];
-    QRec srec[4][4];
-    int32_t bref[4][4];
-    uint64_t bmask[4][4];
+    QRec srec[4][KB];
+    int32_t bref[4][KB];
+    uint64_t bmask[4][KB];
 };
+using TravLDS = TravLDS_T<4>;
+using NarrowLDS = TravLDS_T<(NKP > 4 ? NKP : 4)>;
 
 // Stage the records of stack entries [sp, sp + k) of wave w into LDS (one
 // round of coalesced 16-byte loads; their latencies overlap).
-__device__ __forceinline__ void stage_records(TravLDS &L, int w, int lane, int sp, int k,
+template <class LDS>
+__device__ __forceinline__ void stage_records(LDS &L, int w, int lane, int sp, int k,
                                               const QRec *__restrict__ qrec) {
     if (lane < k) { L.bref[w][lane] = L.sref[w][sp + lane]; L.bmask[w][lane] = L.smask[w][sp + lane]; }
     for (int e = lane; e < QREC_V4 * k; e += 64) {
@@ -1671,7 +1681,7 @@ __device__ __forceinline__ uint64_t root_step(const double2 *__restrict__ pos, c
 // One narrow wave: part `part` (queries part*NQ .. +NQ-1) of heavy group `grp`
 // (heavy slot h).  See "Narrow layout" above.
 template <int MODE>
-__device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const int32_t *__restrict__ dupc,
+__device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const int32_t *__restrict__ dupc,
                             const BHNode *__restrict__ nodes, const QRec *__restrict__ qrec,
                             const int32_t *__restrict__ meta, const double *__restrict__ unused_mom, bool mom_on,
                             double mom_tol, double theta, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
@@ -1729,7 +1739,7 @@ __device__ void narrow_wave(TravLDS &L, const double2 *__restrict__ pos, const i
             nwant += mw ? 1 : 0;
             const uint64_t U = __ballot(mw && mom_on);
             // same-query lanes of earlier records: the task order within a pass
-            const uint64_t qcol = 0x0001000100010001ull << (4 * q);
+            const uint64_t qcol = narrow_qcol0() << (4 * q);
             const int before = __popcll(U & qcol & lanemask_lt());
             const bool usem = mw && mom_on && ntask + before < MOM_TASKS;
             if (usem) nv.mtask[(h * 64 + part * NQ + q) * MOM_TASKS + ntask + before] = L.bref[w][kk];
@@ -1870,7 +1880,7 @@ __global__ __launch_bounds__(256) void bh_traverse_narrow(
     const int32_t *__restrict__ qlist, int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
     unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost, int32_t *__restrict__ tcost,
     const int32_t *__restrict__ cost_lab, NarrowView nv) {
-    __shared__ TravLDS L;
+    __shared__ NarrowLDS L;
     const int w = threadIdx.x >> 6;
     const int64_t slot = (int64_t)blockIdx.x * 4 + w;   // heavy slot x part
     const int64_t h = slot / NPARTS;
