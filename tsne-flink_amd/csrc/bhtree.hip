@@ -1562,7 +1562,7 @@ constexpr int NQ_LOG = 2;
 constexpr int NQ = 1 << NQ_LOG;    // queries per narrow wave
 constexpr int NKP = 16 / NQ;       // stack entries per narrow pass
 constexpr int NPARTS = 64 / NQ;    // narrow waves per 64-query group (NPARTS / 4 workgroups)
-static_assert(NKP * NQ * 4 == 64 && NPARTS % 4 == 0 && NKP <= 8, "narrow lane layout");
+static_assert(NKP * NQ * 4 == 64 && NPARTS % 4 == 0 && STACK / 2 + 4 * NKP + 3 * 32 <= STACK, "narrow lane layout, stack bound");
 
 // bits {4 i : i < NQ} of x (one query per 4 lanes) -> bits {i}
 __device__ __forceinline__ uint32_t narrow_compress(uint64_t x) {
