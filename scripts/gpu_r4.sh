@@ -87,13 +87,13 @@ if has snap3; then   # C4 snapshots in the transition, timed, counted and PMC-pr
     echo "# $v" >> $O/snap3.jsonl
     run 300 python scripts/bh_snap.py $files --reps 3 $opt >> $O/snap3.jsonl 2>> $O/snap3.err || exit $?
   done
-  TSNE_DEBUG_OCT=1 run 300 python scripts/bh_snap.py $files --reps 0 > $O/snap3_dbg.jsonl 2> $O/snap3_dbg.err || exit $?
+  TSNE_DEBUG_OCT=1 run 300 python scripts/bh_snap.py $files --reps 0 ${SNAP3_PMC_OPT:-} > $O/snap3_dbg.jsonl 2> $O/snap3_dbg.err || exit $?
   k=0
   for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
               "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"; do
     k=$((k+1))
     timeout -s KILL 180 rocprofv3 --pmc $pass --kernel-include-regex "oct_" -d $O/pmc3_$k -o pmc --output-format csv -- \
-      python scripts/bh_snap.py $files --reps 0 > $O/pmc3_$k.log 2>&1 || exit $?
+      python scripts/bh_snap.py $files --reps 0 ${SNAP3_PMC_OPT:-} > $O/pmc3_$k.log 2>&1 || exit $?
   done
 fi
 if has pmcsnap; then   # PMC passes over the 2-D BH kernels on the committed C3 snapshots
