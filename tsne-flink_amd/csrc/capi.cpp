@@ -117,7 +117,7 @@ static const OptionField k_options[] = {
     {"near_tol3_late", &Options::near_tol3_late, nullptr, 0.0, 1e-2},
     {"mom3_tol", &Options::mom3_tol, nullptr, 0.0, 1e-4},
     {"oct_moments", nullptr, &Options::oct_moments, 0, 1},
-    {"oct_records", nullptr, &Options::oct_records, 0, 3},
+    {"oct_records", nullptr, &Options::oct_records, 0, 2},
     {"coherent_sort", nullptr, &Options::coherent_sort, 0, 1},
     {"oct_layout_switch", &Options::oct_layout_switch, nullptr, 0, 1e6},
     {"root_tile", nullptr, &Options::root_tile, 0, 1},

@@ -1366,229 +1366,6 @@ __global__ __launch_bounds__(256) void oct_traverse64(
         atomicAdd(&mom_flag[1], ww);
 }
 
-
-// Record traversal, 32-query layout (oct_records 3): one wave = 32
-// Morton-consecutive queries, each on two lanes (half h = lane / 32); a
-// popped record's 8 children are evaluated in 4 sweeps, half h taking
-// children 2 sweep + h.  Between the two other layouts: lane masks over 32
-// neighbours are denser than over 64 (the 64-query layout uses ~30 % of its
-// child-evaluation lanes in the C4 transition), at half its record fetches
-// per query of the 8-query layout.  Same tests and decisions as both; the
-// two halves' sums are added by one fixed shuffle at the end.
-template <bool DBG>
-__global__ __launch_bounds__(256) void oct_traverse32(
-    const double4 *__restrict__ pos, const int32_t *__restrict__ dupc, const OctNode *__restrict__ nodes,
-    const ORec *__restrict__ orec, const int32_t *__restrict__ meta, double theta, int64_t g0, int64_t g1,
-    const int32_t *__restrict__ qlist, int32_t *__restrict__ mom_flag, int32_t *__restrict__ mtask,
-    int32_t *__restrict__ mtask_n, double *__restrict__ F, double *__restrict__ Z,
-    unsigned long long *__restrict__ dbg, double mom_tol, const double *__restrict__ Wp, double wthr, int regime) {
-    __shared__ int32_t sref[4][O64_STACK];
-    __shared__ uint32_t smask[4][O64_STACK];
-    __shared__ ORec srec[4][O64_KB];
-    __shared__ int32_t bref[4][O64_KB];
-    __shared__ uint32_t bmask[4][O64_KB];
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int q = lane & 31, h = lane >> 5;
-    const int64_t wid = (int64_t)blockIdx.x * 4 + w;
-    const int64_t kq = g0 + wid * 32 + q;
-    const bool valid = kq < g1;
-    if (__ballot(valid) == 0) return;
-    if (regime != 0 && (regime == 1) != (*Wp < wthr)) return;
-    const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
-    const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
-    double qx = 0.0, qy = 0.0, qz = 0.0;
-    if (valid) { const double4 p = pos[s]; qx = p.x; qy = p.y; qz = p.z; }
-    const double qmag = fabs(qx) + fabs(qy) + fabs(qz);
-    const int ndup = valid ? dupc[s] : 0;
-    const bool mom_on = mom_flag[0] != 0;
-    const bool h0 = h == 0;   // the query's first lane: its one-per-query terms and decisions
-    double fx = 0.0, fy = 0.0, fz = 0.0, zs = 0.0;
-    int ntask = 0, nwant = 0;
-    unsigned long long d_pops = 0, d_childs = 0, d_dense = 0, d_declined = 0;
-    int sp = 0;
-    const int root = meta[1];
-    if (root == ~0) {
-        if (valid && h0) { const double4 p = pos[0]; leaf3(qx, qy, qz, p.x, p.y, p.z, fx, fy, fz, zs); }
-    } else if (root >= 0) {
-        const OctNode &rt = nodes[root];
-        if (rt.delta >= 63) {
-            for (int p = rt.first; p <= rt.last; ++p) {
-                const double4 pp = pos[p];
-                if (valid && h0) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
-            }
-        } else {
-            bool open = false;
-            if (valid && h0) {
-                const double dx = qx - rt.cx, dy = qy - rt.cy, dz = qz - rt.cz;
-                if (summarise3(rt.h, dx, dy, dz, th_lo, th_hi, theta))
-                    cell3(dx, dy, dz, dx * dx + dy * dy + dz * dz, rt.cnt, fx, fy, fz, zs);
-                else
-                    open = true;
-            }
-            const uint32_t om = (uint32_t)__ballot(open);   // the first half's lanes
-            if (om) {
-                if (lane == 0) { sref[w][0] = root; smask[w][0] = om; }
-                sp = 1;
-            }
-        }
-    }
-    while (sp > 0) {
-        const int kb = sp > O64_BATCH ? 1 : (sp < O64_KB ? sp : O64_KB);
-        sp -= kb;
-        if (lane < kb) { bref[w][lane] = sref[w][sp + lane]; bmask[w][lane] = smask[w][sp + lane]; }
-        constexpr int V = sizeof(ORec) / 16;
-        if (lane < V * kb) {
-            const int rr = lane / V, part = lane - rr * V;
-            reinterpret_cast<uint4 *>(&srec[w][rr])[part] = reinterpret_cast<const uint4 *>(orec + sref[w][sp + rr])[part];
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: the batch is in LDS
-        __builtin_amdgcn_wave_barrier();
-        for (int r = 0; r < kb; ++r) {
-            if (DBG && lane == 0) ++d_pops;
-            const int ref = __builtin_amdgcn_readfirstlane(bref[w][r]);
-            const uint32_t msk = bmask[w][r];
-            bool act = valid && ((msk >> q) & 1u);
-            const ORec &nd = srec[w][r];
-            const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);
-            bool tile = false;
-            if ((nflags & ONCH_TILE) && act) {
-                const double cdx = qx - nd.cx, cdy = qy - nd.cy, cdz = qz - nd.cz;
-                tile = cdx * cdx + cdy * cdy + cdz * cdz <= nd.rball2;
-                if (!tile) {
-                    const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1) +
-                                               fabs(nd.bz0) + fabs(nd.bz1));
-                    const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
-                    const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-                    const double dzm = fmax(fabs(qz - nd.bz0), fabs(qz - nd.bz1)) + ex;
-                    tile = (dxm * dxm + dym * dym + dzm * dzm) * (1.0 + 1e-12) <= nd.thr;
-                }
-            }
-            if (__ballot(tile)) {
-                const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
-                const int cnt = __builtin_amdgcn_readfirstlane(nd.cnt);
-                // the moment decision and its task: the query's first lane
-                bool mw = false;
-                if (tile && h0 && cnt >= MOM3_MIN) {
-                    double bcx, bcy, bcz, R;
-                    box3(nodes[ref], bcx, bcy, bcz, R);
-                    mw = mom3_ok(qx - bcx, qy - bcy, qz - bcz, R, mom_tol);
-                }
-                bool usem0 = false;
-                if (mw) {
-                    ++nwant;
-                    if (mom_on && ntask < MOM3_TASKS) {
-                        usem0 = true;
-                        mtask[s * MOM3_TASKS + ntask] = ref;
-                    }
-                }
-                const uint64_t U = __ballot(usem0);
-                const bool usem = (U >> q) & 1ull;   // both halves of the query
-                if (usem) ++ntask;
-                const bool dense = tile && !usem && (b - a + 1) <= DENSE3_MAX;
-                if (DBG && h0 && tile && !usem && !dense) ++d_declined;
-                const bool taken = usem || dense;
-                if (taken && h0 && s >= a && s <= b) zs -= (double)ndup;   // the query's own copies add 1 each
-                if (__ballot(dense)) {
-                    if (DBG && dense && h0) d_dense += (unsigned long long)(b - a + 1);
-                    // the query's two lanes split the points (even / odd)
-                    double ux = 0.0, uy = 0.0, uz = 0.0, uq = 0.0;
-                    for (int p0 = a; p0 <= b; p0 += 2) {
-                        const int p = p0 + h;
-                        if (p <= b) {
-                            const double4 pp = pos[p];
-                            const double dx = qx - pp.x, dy = qy - pp.y, dz = qz - pp.z;
-                            const double rr = rcp2(__fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0))));
-                            const double sc = rr * rr;
-                            ux = __fma_rn(sc, dx, ux);
-                            uy = __fma_rn(sc, dy, uy);
-                            uz = __fma_rn(sc, dz, uz);
-                            uq += rr;
-                        }
-                    }
-                    if (dense) { fx += ux; fy += uy; fz += uz; zs += uq; }
-                }
-                act = act && !taken;
-            }
-            if (__ballot(act) == 0) continue;
-            const int nch = nflags & 0xff;
-            const int kinds = __builtin_amdgcn_readfirstlane(nd.kinds);
-            if (DBG && act && h0) d_childs += (unsigned long long)nch;
-            for (int c0 = 0; c0 < nch; c0 += 2) {
-                const int c = c0 + h;              // this half's child
-                const bool hasc = c < nch;
-                const int kind = hasc ? (kinds >> (2 * c)) & 3 : OK_TIE;   // per half (TIE: after the loop)
-                const int cc = hasc ? c : c0;
-                const double dx = qx - nd.ccx[cc], dy = qy - nd.ccy[cc], dz = qz - nd.ccz[cc];
-                const double D = __fma_rn(dx, dx, __fma_rn(dy, dy, dz * dz));
-                const bool isleaf = act && kind == OK_LEAF, iscell = act && kind == OK_CELL;
-                const double A = nd.ca[cc];
-                bool acc = D > A;
-                if (iscell && !acc && !(D < A * OACC_BAND))
-                    acc = nd.ch[cc] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
-                          theta;
-                const double wm = (isleaf && !(dx == 0.0 && dy == 0.0 && dz == 0.0)) ? 1.0
-                                  : ((iscell && acc) ? (double)nd.ccnt[cc] : 0.0);
-                const double Qv = rcp2(1.0 + D);
-                const double mult = wm * Qv;
-                const double sc = mult * Qv;
-                fx = __fma_rn(sc, dx, fx);
-                fy = __fma_rn(sc, dy, fy);
-                fz = __fma_rn(sc, dz, fz);
-                zs += mult;
-                // pushes in child order: c0 (first half's lanes), then c0 + 1 (second half's)
-                const uint64_t O = __ballot(iscell && !acc);
-                const uint32_t o0 = (uint32_t)O, o1 = (uint32_t)(O >> 32);
-                if (o0) {
-                    if (lane == 0) { sref[w][sp] = nd.cref[c0]; smask[w][sp] = o0; }
-                    ++sp;
-                }
-                if (o1) {
-                    if (lane == 0) { sref[w][sp] = nd.cref[c0 + 1]; smask[w][sp] = o1; }
-                    ++sp;
-                }
-            }
-            if (__builtin_expect(kinds & 0xAAAA, 0)) {   // key-tie groups: every point directly (first half)
-                for (int c = 0; c < nch; ++c) {
-                    if (((kinds >> (2 * c)) & 3) != OK_TIE) continue;
-                    const OctNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
-                    for (int p = tn.first; p <= tn.last; ++p) {
-                        const double4 pp = pos[p];
-                        if (act && h0) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the pushes landed before the next reads
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    // the query's two halves, one fixed shuffle (both lanes the same bits)
-    fx += __shfl_xor(fx, 32, 64); fy += __shfl_xor(fy, 32, 64);
-    fz += __shfl_xor(fz, 32, 64); zs += __shfl_xor(zs, 32, 64);
-    if (valid && h0) {
-        F[3 * s] = fx;
-        F[3 * s + 1] = fy;
-        F[3 * s + 2] = fz;
-        Z[s] = zs;
-        mtask_n[s] = ntask;
-    }
-    if (DBG) {
-        const unsigned long long a2 = wave_sum(d_childs), b2 = wave_sum(d_dense), c2 = wave_sum(d_declined),
-                                 e = wave_sum((unsigned long long)(h0 ? ntask : 0));
-        if (lane == 0) {
-            atomicAdd(dbg, d_pops * 2);   // in 64-query-wave units
-            atomicAdd(dbg + 1, a2);
-            atomicAdd(dbg + 2, b2);
-            atomicAdd(dbg + 3, c2);
-            atomicAdd(dbg + 4, e);
-        }
-    }
-    const int ww = wave_sum(h0 ? nwant : 0);
-    if (lane == 0 && ww && __hip_atomic_load(&mom_flag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mom_flag[2])
-        atomicAdd(&mom_flag[1], ww);
-}
-
 }  // namespace
 
 void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
@@ -1712,16 +1489,8 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
     // 8-query one while the root half-width is below oct_layout_switch x the
     // near-exact radius (its dense tiles have sparse lane masks there), the
     // 64-query one above (C4 transition, profiles/r04_s16_c4_probe_layouts.jsonl)
-    const bool swon = ctx->opts.oct_layout_switch > 0.0 && t.near_dmax > 0.0;
-    const bool sw = ctx->opts.oct_records == 2 && swon, sw3 = ctx->opts.oct_records == 3 && swon;
-    const double wthr = swon ? ctx->opts.oct_layout_switch * std::sqrt(t.near_dmax) : 0.0;
-    if (ctx->opts.oct_records == 3) {   // 32 queries per wave
-        const int64_t nw = ceil_div(s1 - s0, 32);
-        auto k32 = debug ? oct_traverse32<true> : oct_traverse32<false>;
-        hipLaunchKernelGGL(k32, dim3(ceil_div(nw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.orec,
-                           t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz, dbg,
-                           ctx->opts.mom3_tol, t.W, wthr, sw3 ? 2 : 0);
-    }
+    const bool sw = ctx->opts.oct_records == 2 && ctx->opts.oct_layout_switch > 0.0 && t.near_dmax > 0.0;
+    const double wthr = sw ? ctx->opts.oct_layout_switch * std::sqrt(t.near_dmax) : 0.0;
     if (ctx->opts.oct_records == 2) {
         const int64_t nw = ceil_div(s1 - s0, 64);
         auto k64 = debug ? oct_traverse64<true> : oct_traverse64<false>;
@@ -1729,12 +1498,12 @@ void oct_repulsion(tsne_ctx *ctx, const OctTree &t, double theta, int64_t s0, in
                            t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz, dbg,
                            ctx->opts.mom3_tol, t.W, wthr, sw ? 2 : 0);
     }
-    if (ctx->opts.oct_records == 1 || sw || sw3) {
+    if (ctx->opts.oct_records == 1 || sw) {
         const int64_t rw = ceil_div(s1 - s0, OQ);
         auto k8 = debug ? oct_traverse_rec<true> : oct_traverse_rec<false>;
         hipLaunchKernelGGL(k8, dim3(ceil_div(rw, 4)), dim3(256), 0, ctx->stream, t.pos, t.dupc, t.nodes, t.orec,
                            t.meta, theta, s0, s1, qlist, t.mom_flag, t.mtask, t.mtask_n, dF, dz, dbg,
-                           ctx->opts.mom3_tol, t.W, wthr, (sw || sw3) ? 1 : 0);
+                           ctx->opts.mom3_tol, t.W, wthr, sw ? 1 : 0);
     }
     if (ctx->opts.oct_records == 0) {   // the binary-node walk
         auto kb = debug ? oct_traverse<true> : oct_traverse<false>;
