@@ -12,7 +12,7 @@ from collections import defaultdict
 
 
 def family(name):
-    base = name.split("(")[0].replace("void ", "")
+    base = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
     base = base.split("::")[-1]
     return base.split("<")[0]
 

@@ -848,17 +848,54 @@ __global__ __launch_bounds__(1024) void moment_count(const BHNode *__restrict__ 
     }
 }
 
+// Fixed-order wave reduction of MOM_K per-lane partial sums to dst[0..MOM_K)
+// (LDSRED: 8 moments at a time transposed through a per-wave LDS tile -- 8
+// row sums per column + 3 shuffle stages, ~20 instructions per 8 moments --
+// instead of a 6-stage shuffle tree per moment).
+template <bool LDSRED>
+__device__ __forceinline__ void moments_wave_store(const double (&acc)[MOM_K], double *rw, int lane,
+                                                   double *__restrict__ dst) {
+    if (LDSRED) {
+        const int col = lane & 7, r0 = (lane >> 3) * 8;
+#pragma unroll
+        for (int k0 = 0; k0 < MOM_K; k0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rw[lane * 9 + j] = (k0 + j < MOM_K) ? acc[k0 + j] : 0.0;
+            // the other lanes' stores must have landed before the cross-lane
+            // loads (and those loads before the next round overwrites rw)
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+            __builtin_amdgcn_wave_barrier();
+            double v = 0.0;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v += rw[(r0 + r) * 9 + col];
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            v += __shfl_xor(v, 8, 64);
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (lane < 8 && k0 + lane < MOM_K) dst[k0 + lane] = v;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < MOM_K; ++k) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) dst[k] = v;
+        }
+    }
+}
+
 // One wave per item (<= MOM_CHUNK points of one node): lanes accumulate the
-// scaled moments u_x^a u_y^b / (a! b!) in registers, then a fixed reduction
-// order: LDSRED transposes 8 moments at a time through a per-wave LDS tile
-// (8 row sums per column + 3 shuffle stages, ~20 instructions per 8 moments)
-// instead of a 6-stage shuffle tree per moment.
+// scaled moments u_x^a u_y^b / (a! b!) in registers, then the fixed-order
+// wave reduction.  A node of one chunk (chunk counts cnt, when given) gets its
+// moments written directly to mom; moment_reduce sums the others' chunks.
 template <bool LDSRED>
 __global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ pos,
                                                     const BHNode *__restrict__ nodes,
                                                     const int32_t *__restrict__ off, int64_t n,
                                                     const int32_t *__restrict__ item,
-                                                    double *__restrict__ part) {
+                                                    double *__restrict__ part, const int32_t *__restrict__ cnt,
+                                                    double *__restrict__ mom) {
     __shared__ double red[4][64 * 9];
     double *rw = red[threadIdx.x >> 6];
     const int total = off[n];
@@ -891,52 +928,37 @@ __global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ 
                 for (int b = 0; b <= MOM_DEG; ++b)
                     if (a + b <= MOM_DEG) acc[midx(a, b)] = __fma_rn(X[a], Yv[b], acc[midx(a, b)]);
         }
-        if (LDSRED) {
-            const int col = lane & 7, r0 = (lane >> 3) * 8;
-#pragma unroll
-            for (int k0 = 0; k0 < MOM_K; k0 += 8) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) rw[lane * 9 + j] = (k0 + j < MOM_K) ? acc[k0 + j] : 0.0;
-                // the other lanes' stores must have landed before the cross-lane
-                // loads (and those loads before the next round overwrites rw)
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-                __builtin_amdgcn_wave_barrier();
-                double v = 0.0;
-#pragma unroll
-                for (int r = 0; r < 8; ++r) v += rw[(r0 + r) * 9 + col];
-                __builtin_amdgcn_s_waitcnt(0xc07f);
-                __builtin_amdgcn_wave_barrier();
-                v += __shfl_xor(v, 8, 64);
-                v += __shfl_xor(v, 16, 64);
-                v += __shfl_xor(v, 32, 64);
-                if (lane < 8 && k0 + lane < MOM_K) part[(int64_t)it * MOM_K + k0 + lane] = v;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < MOM_K; ++k) {
-                const double v = wave_sum(acc[k]);
-                if (lane == 0) part[(int64_t)it * MOM_K + k] = v;
-            }
-        }
+        const bool single = cnt && __builtin_amdgcn_readfirstlane(cnt[node]) == 1;
+        moments_wave_store<LDSRED>(acc, rw, lane, single ? mom + (int64_t)node * MOM_K : part + (int64_t)it * MOM_K);
     }
 }
 
-// One wave per moment-carrying node: lanes over moments, chunks summed in order.
-__global__ void moment_reduce(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
-                              const int32_t *__restrict__ cnt, const int32_t *__restrict__ off,
-                              const double *__restrict__ part, double *__restrict__ mom) {
+// One wave per moment node of several chunks: each lane sums its chunks'
+// partials (chunk j to lane j mod 64, in order), then the fixed-order wave
+// reduction -- the root's ~500 chunks are no longer one lane's serial chain.
+// Single-chunk nodes were written by moment_items.
+__global__ __launch_bounds__(256) void moment_reduce(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
+                                                     const int32_t *__restrict__ cnt, const int32_t *__restrict__ off,
+                                                     const double *__restrict__ part, double *__restrict__ mom) {
+    __shared__ double red[4][64 * 9];
+    double *rw = red[threadIdx.x >> 6];
     const int nl = meta[2];
     const int lane = lane_id();
     const int nw = gridDim.x * (blockDim.x >> 6);
     for (int e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < nl; e += nw) {
-        const int node = list[e];
-        const int o = off[node], c = cnt[node];
-        for (int k = lane; k < MOM_K; k += 64) {
-            double s = 0.0;
-            for (int j = 0; j < c; ++j) s += part[(int64_t)(o + j) * MOM_K + k];
-            mom[(int64_t)node * MOM_K + k] = s;
+        const int node = __builtin_amdgcn_readfirstlane(list[e]);
+        const int c = __builtin_amdgcn_readfirstlane(cnt[node]);
+        if (c <= 1) continue;
+        const int o = __builtin_amdgcn_readfirstlane(off[node]);
+        double acc[MOM_K];
+#pragma unroll
+        for (int k = 0; k < MOM_K; ++k) acc[k] = 0.0;
+        for (int j = lane; j < c; j += 64) {
+            const double *pp = part + (int64_t)(o + j) * MOM_K;
+#pragma unroll
+            for (int k = 0; k < MOM_K; ++k) acc[k] += pp[k];
         }
+        moments_wave_store<true>(acc, rw, lane, mom + (int64_t)node * MOM_K);
     }
 }
 
@@ -3009,7 +3031,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
                                t.mom_flag);
             const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
             hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, Y2, t.nodes, t.mom_off, n,
-                               t.mom_item, t.mom_part);
+                               t.mom_item, t.mom_part, nullptr, nullptr);
             hipLaunchKernelGGL(root_moment_reduce, dim3(MOM_K), dim3(256), 0, st, t.mom_off, n, t.mom_part, t.mom);
             hipLaunchKernelGGL(poly_coef, dim3(ceil_div(POLY_K, 128)), dim3(128), 0, st, t.mom, t.rcoef);
             t.root_pos = Y2;
@@ -3063,7 +3085,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
                        t.mom_cnt, t.mom_list, t.meta, t.mom_off, t.mom_item);
     const int mgrid = (int)std::min<int64_t>(2048, std::max<int64_t>(1, ceil_div(n, 256)));
     hipLaunchKernelGGL(moment_items<true>, dim3(mgrid), dim3(256), 0, st, t.pos, t.nodes, t.mom_off, n, t.mom_item,
-                       t.mom_part);
+                       t.mom_part, t.mom_cnt, t.mom);
     hipLaunchKernelGGL(moment_reduce, dim3(mgrid), dim3(256), 0, st, t.meta, t.mom_list, t.mom_cnt, t.mom_off,
                        t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
