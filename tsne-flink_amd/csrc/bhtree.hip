@@ -800,8 +800,8 @@ __device__ __forceinline__ void box_centre(const BHNode &nd, double &cx, double 
 }
 
 // Per binary node with >= MOM_MIN_POINTS points (when the gate is on, see
-// bbox_final): its chunk count, its place in the list of moment nodes (one
-// atomic per block) and its item range (one atomic per block on the item
+// bbox_final): its chunk count, its place in the list of moment nodes of
+// several chunks (one atomic per block; moment_reduce's work list) and its item range (one atomic per block on the item
 // counter off[n]; the placement of the ranges varies from run to run, a
 // node's chunks are summed in chunk order, so the moments do not), with the
 // item -> node map filled in.
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(1024) void moment_count(const BHNode *__restrict__ 
     if (i < n) cnt[i] = c;
     __shared__ int wcnt[16], wbase[16], wsum[16], wibase[16];
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const uint64_t bal = __ballot(c > 0);
+    const uint64_t bal = __ballot(c > 1);   // the list: nodes of several chunks (moment_reduce)
     int inc = c;   // inclusive scan of the chunk counts over the wave (item offsets)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -840,8 +840,8 @@ __global__ __launch_bounds__(1024) void moment_count(const BHNode *__restrict__ 
         for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { wbase[k] += base; wibase[k] += ibase; }
     }
     __syncthreads();
+    if (c > 1) list[wbase[w] + __popcll(bal & lanemask_lt())] = (int32_t)i;
     if (c > 0) {
-        list[wbase[w] + __popcll(bal & lanemask_lt())] = (int32_t)i;
         const int o = wibase[w] + inc - c;
         off[i] = o;
         for (int k = 0; k < c; ++k) item[o + k] = (int32_t)i;
@@ -933,10 +933,10 @@ __global__ __launch_bounds__(256) void moment_items(const double2 *__restrict__ 
     }
 }
 
-// One wave per moment node of several chunks: each lane sums its chunks'
-// partials (chunk j to lane j mod 64, in order), then the fixed-order wave
-// reduction -- the root's ~500 chunks are no longer one lane's serial chain.
-// Single-chunk nodes were written by moment_items.
+// One wave per moment node of several chunks (the list; single-chunk nodes
+// were written by moment_items): each lane sums its chunks' partials (chunk j
+// to lane j mod 64, in order), then the fixed-order wave reduction -- the
+// root's ~500 chunks are no longer one lane's serial chain.
 __global__ __launch_bounds__(256) void moment_reduce(const int32_t *__restrict__ meta, const int32_t *__restrict__ list,
                                                      const int32_t *__restrict__ cnt, const int32_t *__restrict__ off,
                                                      const double *__restrict__ part, double *__restrict__ mom) {
@@ -948,7 +948,6 @@ __global__ __launch_bounds__(256) void moment_reduce(const int32_t *__restrict__
     for (int e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < nl; e += nw) {
         const int node = __builtin_amdgcn_readfirstlane(list[e]);
         const int c = __builtin_amdgcn_readfirstlane(cnt[node]);
-        if (c <= 1) continue;
         const int o = __builtin_amdgcn_readfirstlane(off[node]);
         double acc[MOM_K];
 #pragma unroll
