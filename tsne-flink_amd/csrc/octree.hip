@@ -413,7 +413,6 @@ constexpr int MOM3_ORDER = 3;
 constexpr int MOM3_K = 70;          // (a, bx, by, bz) with a + bx + by + bz <= 4
 constexpr int MOM3_MIN = 64;        // nodes of >= 64 points carry moments
 constexpr int MOM3_CHUNK = 1024;    // points per moment item
-constexpr int MOM3_GROUP = 10;      // moments accumulated per pass over an item's points
 constexpr int MOM3_TASKS = 512;     // moment tiles recorded per query; more -> dense tiles
 constexpr int DENSE3_MAX = 2048;    // larger tiles only by moments (else traversed)
 
@@ -469,12 +468,16 @@ __device__ __forceinline__ double ipow(double x, int e) {
     for (int k = 0; k < e; ++k) r *= x;
     return r;
 }
-// One wave per item: lanes over the item's points, MOM3_GROUP moments per
-// pass (registers), a fixed-order wave reduction per moment.
+// One wave per item: lanes over the item's points, all MOM3_K moments in
+// registers in one pass (the powers from tables: the same products, in the
+// same order, as repeated multiplication), a fixed-order wave reduction per
+// moment.
 __global__ __launch_bounds__(256) void oct_mom_items(const double4 *__restrict__ pos, const OctNode *__restrict__ nodes,
                                                      const int32_t *__restrict__ mcnt, const int32_t *__restrict__ moff,
                                                      int64_t n, const int32_t *__restrict__ item_node, int64_t cap,
-                                                     double *__restrict__ part) {
+                                                     double *__restrict__ part, double *__restrict__ mom,
+                                                     int32_t *__restrict__ mlist, int32_t *__restrict__ mlist_n) {
+    constexpr M3Tab T = make_m3tab();
     const int64_t total = min((int64_t)moff[n - 1] + mcnt[n - 1], cap);
     const int lane = lane_id();
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -485,46 +488,55 @@ __global__ __launch_bounds__(256) void oct_mom_items(const double4 *__restrict__
         box3(nd, cx, cy, cz, R);
         const int c = (int)(it - moff[node]);
         const int p0 = nd.first + c * MOM3_CHUNK, p1 = min(nd.last + 1, p0 + MOM3_CHUNK);
-        for (int g0 = 0; g0 < MOM3_K; g0 += MOM3_GROUP) {
-            double acc[MOM3_GROUP];
+        double acc[MOM3_K];
 #pragma unroll
-            for (int g = 0; g < MOM3_GROUP; ++g) acc[g] = 0.0;
-            for (int p = p0 + lane; p < p1; p += 64) {
-                const double4 q = pos[p];
-                const double ux = q.x - cx, uy = q.y - cy, uz = q.z - cz;
-                const double s = ux * ux + uy * uy + uz * uz;
+        for (int k = 0; k < MOM3_K; ++k) acc[k] = 0.0;
+        for (int p = p0 + lane; p < p1; p += 64) {
+            const double4 q = pos[p];
+            const double ux = q.x - cx, uy = q.y - cy, uz = q.z - cz;
+            const double s = ux * ux + uy * uy + uz * uz;
+            double S[5], X[5], Yp[5], Zp[5];
+            S[0] = 1.0; X[0] = 1.0; Yp[0] = 1.0; Zp[0] = 1.0;
 #pragma unroll
-                for (int g = 0; g < MOM3_GROUP; ++g) {
-                    const int k = g0 + g;
-                    if (k < MOM3_K)
-                        acc[g] = __fma_rn(ipow(s, kM3.a[k]) * ipow(ux, kM3.bx[k]) * ipow(uy, kM3.by[k]),
-                                          ipow(uz, kM3.bz[k]), acc[g]);
-                }
+            for (int e = 1; e <= 4; ++e) {
+                S[e] = S[e - 1] * s; X[e] = X[e - 1] * ux; Yp[e] = Yp[e - 1] * uy; Zp[e] = Zp[e - 1] * uz;
             }
 #pragma unroll
-            for (int g = 0; g < MOM3_GROUP; ++g) {
-                const double v = wave_sum(acc[g]);
-                if (lane == 0 && g0 + g < MOM3_K) part[it * MOM3_K + g0 + g] = v;
-            }
+            for (int k = 0; k < MOM3_K; ++k)
+                acc[k] = __fma_rn(S[T.a[k]] * X[T.bx[k]] * Yp[T.by[k]], Zp[T.bz[k]], acc[k]);
+        }
+        // a node of one item: its moments directly; of several: listed once for oct_mom_reduce
+        const int nc = __builtin_amdgcn_readfirstlane(mcnt[node]);
+        double *dst = nc == 1 ? mom + (int64_t)node * MOM3_K : part + it * MOM3_K;
+        if (nc > 1 && c == 0 && lane == 0) mlist[atomicAdd(mlist_n, 1)] = node;
+#pragma unroll
+        for (int k = 0; k < MOM3_K; ++k) {
+            const double v = wave_sum(acc[k]);
+            if (lane == 0) dst[k] = v;
         }
     }
 }
-// node moments: its items' partials summed in item order (thread per (node, moment))
-__global__ void oct_mom_reduce(const int32_t *__restrict__ mcnt, const int32_t *__restrict__ moff, int64_t n,
-                               int64_t cap, const double *__restrict__ part, double *__restrict__ mom) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t i = e / MOM3_K;
-    const int k = (int)(e - i * MOM3_K);
-    if (i >= n || mcnt[i] == 0 || moff[i] + mcnt[i] > cap) return;
-    double s = 0.0;
-    for (int c = 0; c < mcnt[i]; ++c) s += part[(moff[i] + c) * MOM3_K + k];
-    mom[i * MOM3_K + k] = s;
+// moments of the nodes of several items (the list, any order): their items'
+// partials summed in item order (thread per (node, moment))
+__global__ void oct_mom_reduce(const int32_t *__restrict__ mcnt, const int32_t *__restrict__ moff,
+                               const int32_t *__restrict__ mlist, const int32_t *__restrict__ mlist_n, int64_t cap,
+                               const double *__restrict__ part, double *__restrict__ mom) {
+    const int64_t total = (int64_t)*mlist_n * MOM3_K;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = mlist[e / MOM3_K];
+        const int k = (int)(e % MOM3_K);
+        if (moff[i] + mcnt[i] > cap) continue;
+        double s = 0.0;
+        for (int c = 0; c < mcnt[i]; ++c) s += part[(moff[i] + c) * MOM3_K + k];
+        mom[i * MOM3_K + k] = s;
+    }
 }
 // the moments exist this iteration if the previous traversal had demand for
 // them (lanes whose tile could use them: >= n / 64), or at the first build
 __global__ void oct_mom_gate(int32_t *mom_flag) {
     mom_flag[0] = mom_flag[1] >= mom_flag[2];
     mom_flag[1] = 0;
+    mom_flag[3] = 0;   // oct_mom_items' list of nodes of several items
 }
 
 __device__ __forceinline__ bool mom3_ok(double vx, double vy, double vz, double R, double tol) {
@@ -1402,6 +1414,7 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
     t.item_node = ws.get<int32_t>("oct.item_node", t.item_cap);
     t.mom_part = ws.get<double>("oct.mom_part", (size_t)MOM3_K * t.item_cap);
     t.mom_flag = ws.get<int32_t>("oct.mom_flag", 4);
+    t.mlist = ws.get<int32_t>("oct.mlist", n / 256 + 64);   // nodes of > MOM3_CHUNK points: < 2 n / MOM3_CHUNK
     t.mtask = ws.get<int32_t>("oct.mtask", (size_t)MOM3_TASKS * n);
     t.mtask_n = ws.get<int32_t>("oct.mtask_n", n);
     size_t mb = 0;
@@ -1455,8 +1468,9 @@ void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta, bool l
     hipLaunchKernelGGL(oct_mom_fill, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.mcnt, t.moff, n, t.item_cap,
                        t.item_node);
     hipLaunchKernelGGL(oct_mom_items, dim3(std::max<int64_t>(1, std::min<int64_t>(4096, ceil_div(t.item_cap, 4)))),
-                       dim3(256), 0, st, t.pos, t.nodes, t.mcnt, t.moff, n, t.item_node, t.item_cap, t.mom_part);
-    hipLaunchKernelGGL(oct_mom_reduce, dim3(ceil_div(n * MOM3_K, 256)), dim3(256), 0, st, t.mcnt, t.moff, n, t.item_cap,
+                       dim3(256), 0, st, t.pos, t.nodes, t.mcnt, t.moff, n, t.item_node, t.item_cap, t.mom_part, t.mom,
+                       t.mlist, t.mom_flag + 3);
+    hipLaunchKernelGGL(oct_mom_reduce, dim3(256), dim3(256), 0, st, t.mcnt, t.moff, t.mlist, t.mom_flag + 3, t.item_cap,
                        t.mom_part, t.mom);
     TSNE_LAUNCH_CHECK();
 }

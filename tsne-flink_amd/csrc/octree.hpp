@@ -70,6 +70,7 @@ struct OctTree {
     // subtree moments (70 per node of >= MOM3_MIN points, about its box
     // centre), built in chunks; gated by the previous traversal's demand
     double *mom = nullptr, *mom_part = nullptr;
+    int32_t *mlist = nullptr;   // nodes whose moments sum several items (oct_mom_reduce)
     int32_t *mcnt = nullptr, *moff = nullptr, *item_node = nullptr, *mom_flag = nullptr;
     int32_t *mtask = nullptr, *mtask_n = nullptr;   // per query: nodes evaluated from their moments
     void *mscan_tmp = nullptr;
