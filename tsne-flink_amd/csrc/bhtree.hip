@@ -1218,6 +1218,27 @@ constexpr int PLAN_BUCKETS = 128;
 __device__ __forceinline__ int plan_bucket(int32_t c) {
     return c <= 0 ? 0 : min(PLAN_BUCKETS - 1, 1 + (int)(4.0f * __log2f((float)c)));
 }
+// hist[key] += 1 for every active lane of the wave, one LDS atomic per
+// distinct key (per-lane atomics serialise on the few cost buckets most
+// entries share -- late in the schedule nearly all in bucket 0); returns the
+// lane's slot (old value + its rank among the wave's lanes of that key).
+__device__ __forceinline__ int32_t wave_bucket_add(int32_t *hist, int key, bool act) {
+    const int lane = lane_id();
+    int32_t res = 0;
+    uint64_t rem = __ballot(act);
+    while (rem) {
+        const int leader = __builtin_ctzll(rem);
+        const int kb = __shfl(key, leader, 64);
+        const bool mine = act && key == kb;
+        const uint64_t m = __ballot(mine);
+        int32_t b0 = 0;
+        if (lane == leader) b0 = atomicAdd(&hist[kb], (int32_t)__popcll(m));
+        b0 = __shfl(b0, leader, 64);
+        if (mine) res = b0 + (int32_t)__popcll(m & lanemask_lt());
+        rem &= ~m;
+    }
+    return res;
+}
 __global__ __launch_bounds__(1024) void tile_plan(const int32_t *__restrict__ tcost, int64_t waves, int64_t slots_max,
                                                   int32_t *__restrict__ Cw, int32_t *__restrict__ slot0,
                                                   int32_t *__restrict__ slot_w, int32_t *__restrict__ slot_c,
@@ -1291,14 +1312,22 @@ __global__ __launch_bounds__(1024) void tile_plan(const int32_t *__restrict__ tc
     }
     if (!torder) return;
     __syncthreads();
-    for (int64_t b = t; b < tblocks; b += 1024) atomicAdd(&hist[plan_bucket(bc[b])], 1);
+    // the blocks' cost buckets (wave_bucket_add); the order within a bucket is free
+    for (int64_t b0 = (int64_t)w * 64; b0 < tblocks; b0 += 1024) {
+        const int64_t b = b0 + lane;
+        (void)wave_bucket_add(hist, b < tblocks ? plan_bucket(bc[b]) : 0, b < tblocks);
+    }
     __syncthreads();
     if (t == 0) {   // descending bucket starts
         int32_t r = 0;
         for (int k = PLAN_BUCKETS - 1; k >= 0; --k) { const int32_t c = hist[k]; hist[k] = r; r += c; }
     }
     __syncthreads();
-    for (int64_t b = t; b < tblocks; b += 1024) torder[atomicAdd(&hist[plan_bucket(bc[b])], 1)] = (int32_t)b;
+    for (int64_t b0 = (int64_t)w * 64; b0 < tblocks; b0 += 1024) {
+        const int64_t b = b0 + lane;
+        const int32_t pos = wave_bucket_add(hist, b < tblocks ? plan_bucket(bc[b]) : 0, b < tblocks);
+        if (b < tblocks) torder[pos] = (int32_t)b;
+    }
 }
 
 // F, Z of each query += its chunks' partial sums, in chunk order
@@ -2142,17 +2171,21 @@ __global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcos
     if (t < PLAN_BUCKETS) hist[t] = 0;
     __syncthreads();
     unsigned long long acc = 0;
-    for (int64_t g = t; g < waves; g += 1024) {
-        int32_t c = wcost[g];
-        const int32_t f = nflag[g];
-        if (f > 0) {
-            int32_t mx = 0;
-            for (int p = 0; p < NPARTS; ++p) mx = max(mx, ncost[(int64_t)(f - 1) * NPARTS + p]);
-            c = 2 * mx;
-            wcost[g] = c;
+    for (int64_t g0 = (int64_t)w * 64; g0 < waves; g0 += 1024) {
+        const int64_t g = g0 + lane;
+        int32_t c = 0;
+        if (g < waves) {
+            c = wcost[g];
+            const int32_t f = nflag[g];
+            if (f > 0) {
+                int32_t mx = 0;
+                for (int p = 0; p < NPARTS; ++p) mx = max(mx, ncost[(int64_t)(f - 1) * NPARTS + p]);
+                c = 2 * mx;
+                wcost[g] = c;
+            }
+            acc += (unsigned long long)max(c, 0);
         }
-        acc += (unsigned long long)max(c, 0);
-        if (hfill > 0) atomicAdd(&hist[plan_bucket(c)], 1);
+        if (hfill > 0) (void)wave_bucket_add(hist, plan_bucket(c), g < waves);
     }
     acc = wave_sum(acc);
     if (lane == 0) red[w] = acc;
