@@ -48,6 +48,7 @@ BF16_MFMA_PEAK_TF = 2500.0   # dense (MI355X_MICROARCH.md); the kNN filter's bf1
 HBM_PEAK_GBS = 8000.0
 PMC_ATTRACT = "r04_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
 PMC_BH = "r04_bh_valu.json"
+UPDATE_KERNELS = ("combine_update", "center_scatter")   # update + centre kernels in the PMC summary
 
 
 def parse():
@@ -80,6 +81,11 @@ def parse():
     ap.add_argument("--y0-seed", type=int, default=0, help="initWorkingSet seed (the reference is unseeded)")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="tsne_ctx_set_option on the bench's context (A/B of a tunable; repeatable)")
+    ap.add_argument("--detail-out", default="gpurun_out/bench_detail.json",
+                    help="side file for the per-iteration timeline, attraction launch log and PMC blobs "
+                         "(the stdout line stays < 8 KB; '' = none)")
+    ap.add_argument("--cpu-budget", type=float, default=1.0,
+                    help="CPU baseline: seconds of BH queries per snapshot (the build is timed apart)")
     ap.add_argument("--locality", action="store_true",
                     help="diagnostic: label-distance histogram of P's edges in the final Morton order (stderr)")
     return ap.parse_args()
@@ -320,8 +326,7 @@ def main():
     # profiled every --trace iterations (per-stage times, BH work counters),
     # plus the CPU baseline's trajectory snapshots and --dump-y
     window_profile, timeline, snaps = [], [], {}
-    snap_at = sorted({1, max(1, a.iterations // 10), max(1, a.iterations // 5), max(1, 2 * a.iterations // 5),
-                      a.iterations})
+    snap_at = sorted({max(1, a.iterations * f // 20) for f in (0, 2, 3, 4, 6, 8, 12)} | {a.iterations})
     want_snaps = rank == 0 and world == 1 and not a.no_cpu_baseline
     dumps = {int(v) for v in a.dump_y.split(",")} if a.dump_y else set()
     if a.trace > 0 or want_snaps or dumps:
@@ -356,17 +361,11 @@ def main():
     win_nl = [ms for (t, sa, ms) in alog if sa in (0, 3) and t <= win]
     attr_ms = float(np.mean(nonloss)) if nonloss else None
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
-    placement = {0: "side stream beside the tree build / BH", 3: "context stream, alone"}
     kinds = sorted({sa for (_, sa, _) in alog if sa in (0, 3)})
-    # the optimizer's tiled layout (attract_tiles) unless disabled or the rows
-    # are dense over a small embedding (the library's own rule, optimize.hip)
-    dense_small = nnz // max(n, 1) > 1024 and n * 16 <= (2 << 20)
-    tiles_on = os.environ.get("TSNE_ATTRACT_TILES", "1")[:1] != "0" and not dense_small
-    attr_kernel = "attract_tiles<LOSS=false>" if tiles_on else "attract_rows<64,4,LOSS=false>"
-    if C == 3:
-        attr_kernel = "attract3<LOSS=false>"
+    attr_kernel = {0: "attract_rows<64,4,LOSS=false>", 1: "attract_tiles<LOSS=false>",
+                   2: "attract3<LOSS=false>"}.get(ctx.counter("opt.attract_kernel"), "?")
     knn_flops = 2.0 * (r1 - r0) * n * d
-    knn_mode = "f32" if os.environ.get("TSNE_KNN_BF16", "1")[:1] == "0" else "bf16x3"
+    knn_mode = "bf16x3" if ctx.get_option("knn_bf16") else "f32"
     upd_bytes = 64 * C * rows   # N*C*(5 reads + 3 writes)*8 B
     upd_avg = float(np.mean(upd_ms)) if upd_ms else None
     prof = window_profile + timeline
@@ -375,94 +374,76 @@ def main():
     def bh_rate(key):
         return sum(e[key] for e in prof) / (bh_ms_sum * 1e-3) if bh_ms_sum > 0 else None
 
+    def r4(x):   # compact numbers for the one-line record
+        return None if x is None else float(f"{x:.4g}")
+
     workload = {"c3": f"C3: {n}x{d} GMM, sqeuclidean, k={k}, perplexity {a.perplexity}, theta {a.theta}",
-                "c4": f"C4: {n}x{d} sparse rows (30 nonzeros each), cosine, k={k}, perplexity {a.perplexity}, "
-                      f"theta {a.theta}, 3-D embedding (octree)",
-                "c5": f"C5: {n}-point precomputed distance matrix ({n}x{n - 1} entries), perplexity {a.perplexity}, "
-                      f"theta {a.theta}"}[a.config]
-    workload += (f"; timed region = the reference's whole schedule t=1..{a.iterations} (TsneHelpers.scala:396-430) "
-                 f"as {steps} steps of {a.iterations // steps} iterations, value = T / loop seconds; the "
-                 f"pre-expansion window t=1..{win} is reported apart as window_it_s")
+                "c4": f"C4: {n}x{d} sparse rows, cosine, k={k}, perplexity {a.perplexity}, theta {a.theta}, 3-D",
+                "c5": f"C5: {n}-point distance matrix, perplexity {a.perplexity}, theta {a.theta}"}[a.config]
+    workload += (f"; timed = the whole schedule t=1..{a.iterations} (TsneHelpers.scala:396-430) as {steps} steps; "
+                 f"value = T / loop s")
     e2e = t_knn + t_aff + t_setup + t_loop + t_out
+    detail_path = a.detail_out
 
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": r4(value),
         "unit": "iterations/s",
         "n_gpus": world,
         "steps": steps,
         "warmup": a.warmup,
-        "ms_per_step": 1e3 * t_loop / steps,
-        "ms_per_iteration": 1e3 * t_loop / a.iterations,
+        "ms_per_step": r4(1e3 * t_loop / steps),
+        "ms_per_iteration": r4(1e3 * t_loop / a.iterations),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": {"c3": "synthetic 10-blob Gaussian mixture (seed 2, fp32-rounded), seeded Y0 ~ N(0, 1e-4^2)",
-                 "c4": "synthetic 20-topic sparse count rows (tests/configs.py c4, seed 3), seeded Y0 ~ N(0, 1e-4^2)",
-                 "c5": "full sqeuclidean distance matrix (diagonal excluded) of a synthetic 10-blob 64-D Gaussian "
-                       "mixture (seed 4), seeded Y0 ~ N(0, 1e-4^2)"}[a.config],
+        "data": {"c3": "synthetic 10-blob GMM (seed 2), seeded Y0",
+                 "c4": "synthetic 20-topic sparse rows (seed 3), seeded Y0",
+                 "c5": "distance matrix of a synthetic 64-D GMM (seed 4), seeded Y0"}[a.config],
         "config": {"workload": workload, "n": n, "dim": d, "k": k, "theta": a.theta, "iterations": a.iterations,
                    "parallelism": f"rows{world}", "nnz_P": int(nnz),
-                   "step": f"{a.iterations // steps} iterations (ms_per_step is per step; ms_per_iteration apart)",
-                   "options": {kv.split("=", 1)[0]: float(kv.split("=", 1)[1]) for kv in a.option},
-                   "loop_full_s": t_loop, "full_schedule_it_s": value, "end_to_end_s": e2e,
-                   "window_it_s": (win / t_win) if t_win else None},
-        "loop_full_s": t_loop,
-        "full_schedule_it_s": value,
-        "window_it_s": (win / t_win) if t_win else None,
-        "window_note": f"t=1..{win}, timed inside the warmup from the same initial state: the root-tile phase, "
-                       "where the step is the attraction kernel's time; not the metric's workload",
-        "end_to_end_s": e2e,
-        "end_to_end_note": "kNN + affinities + joint + optimizer setup + the whole schedule + D2H of Y and losses; "
-                           "input already in HBM (synthetic), CSV/loss-file formatting not included",
-        "knn_s": t_knn,
-        "knn_pts_per_s": n / t_knn if t_knn > 0 else None,
-        "knn_filter_ms": knn_filter_ms,
-        "knn_mfma_tflops": knn_flops / (knn_filter_ms * 1e-3) / 1e12 if knn_filter_ms > 0 else None,
+                   "options": {kv.split("=", 1)[0]: float(kv.split("=", 1)[1]) for kv in a.option}},
+        "loop_full_s": r4(t_loop),
+        "window_it_s": r4(win / t_win) if t_win else None,
+        "end_to_end_s": r4(e2e),
+        "end_to_end_note": "kNN + affinities + joint + setup + schedule + D2H; input in HBM",
+        "knn_s": r4(t_knn),
+        "knn_pts_per_s": r4(n / t_knn) if t_knn > 0 else None,
+        "knn_filter_ms": r4(knn_filter_ms),
         "knn_filter_mode": knn_mode,
         # fraction of the MFMA pipe the filter runs on: f32-input MFMA (157.3 TF),
         # or bf16x3 = 3 bf16 MFMA products per dot-product term (2.5 PF dense)
-        "knn_mfma_frac_of_peak": ((knn_flops / (knn_filter_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF) if knn_mode == "f32"
-                                  else (3 * knn_flops / (knn_filter_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF))
+        "knn_mfma_frac_of_peak": r4((knn_flops / (knn_filter_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF) if knn_mode == "f32"
+                                    else (3 * knn_flops / (knn_filter_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF))
         if knn_filter_ms > 0 else None,
-        "knn_mfma_frac_whole_knn": ((knn_flops / t_knn / 1e12 / FP32_MFMA_PEAK_TF) if knn_mode == "f32"
-                                    else (3 * knn_flops / t_knn / 1e12 / BF16_MFMA_PEAK_TF)) if t_knn > 0 else None,
-        "affinities_joint_s": t_aff,
-        "opt_setup_s": t_setup,
+        "affinities_joint_s": r4(t_aff),
+        "opt_setup_s": r4(t_setup),
         "final_loss": losses.get(max(losses)) if losses else None,
-        "losses_sampled": {str(t): losses[t] for t in sorted(losses) if t in (10, 20, 100, 200, 500, 1000)},
-        "roofline": {"kernel": attr_kernel + " (CSR attraction, TsneHelpers.scala:269-306): mean HIP-event time of "
-                               "its non-loss launches over the timed region (the whole schedule), on the stream "
-                               "each ran on (" + "; ".join(placement[k_] for k_ in kinds) + ")",
-                     "bound": "hbm", "achieved": attr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
-                     "bytes_per_launch": attr_bytes, "avg_ms": attr_ms, "launches": len(nonloss),
-                     "avg_ms_window": float(np.mean(win_nl)) if win_nl else None,
+        "roofline": {"kernel": attr_kernel + ", mean HIP-event time of its non-loss launches over the timed "
+                               "schedule, on the stream each ran on (" +
+                               ", ".join({0: "side, beside BH", 3: "context, alone"}[k_] for k_ in kinds) + ")",
+                     "bound": "hbm", "achieved": r4(attr_gbs), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": r4(attr_gbs / HBM_PEAK_GBS) if attr_gbs else None, "traffic": None,
+                     "bytes_per_launch": attr_bytes, "avg_ms": r4(attr_ms), "launches": len(nonloss),
                      # the window's launches (root-tile phase: beside the short build kernels
                      # only); over the schedule the launches share the CUs with the BH kernels
-                     # (attract_tiles' 156 KB of LDS per CU time-slices them), so their event
-                     # time is the overlap's, not the kernel's own
-                     "frac_window": (attr_bytes / (float(np.mean(win_nl)) * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                     "frac_window": r4(attr_bytes / (float(np.mean(win_nl)) * 1e-3) / 1e9 / HBM_PEAK_GBS)
                      if win_nl else None,
-                     "loss_launch": {"kernel": attr_kernel.replace("LOSS=false", "LOSS=true") + " + KL terms",
-                                     "avg_ms": float(np.mean(loss_l)) if loss_l else None,
-                                     "launches": len(loss_l)}},
-        "update_centre": {"kernels": ("combine_update<1> (+ the centring mean's block partials) + mean2_final + "
-                                      "center_scatter") if C == 2 else
-                                     "combine_update3<1> (+ centring mean partials) + mean3_final + center3_scatter",
-                          "avg_ms": upd_avg, "bytes_per_iteration": upd_bytes,
-                          "achieved_GBs": upd_bytes / (upd_avg * 1e-3) / 1e9 if upd_avg else None,
-                          "frac": upd_bytes / (upd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if upd_avg else None},
-        "bh": {"note": "Barnes-Hut repulsion (QuadTree.scala:123-152): fp64 VALU / latency bound, no HBM roofline "
-                       "(SURVEY 8d); executed work per second of BH kernel time over the traced iterations of the "
-                       "trace pass (t=1..5 and every --trace-th)",
-               "kernel_ms_traced": bh_ms_sum,
-               "pops_per_s": bh_rate("pops"), "lane_child_evals_per_s": bh_rate("child_evals"),
-               "dense_pair_terms_per_s": bh_rate("dense_pairs"), "moment_evals_per_s": bh_rate("moment_evals")},
-        "window_profile": window_profile,
-        "timeline": timeline,
+                     "loss_launch_ms": r4(float(np.mean(loss_l))) if loss_l else None},
+        "update_centre": {"avg_ms": r4(upd_avg), "bytes_per_iteration": upd_bytes,
+                          "achieved_GBs": r4(upd_bytes / (upd_avg * 1e-3) / 1e9) if upd_avg else None,
+                          "frac": r4(upd_bytes / (upd_avg * 1e-3) / 1e9 / HBM_PEAK_GBS) if upd_avg else None},
+        "bh": {"kernel_ms_traced": r4(bh_ms_sum),
+               "pops_per_s": r4(bh_rate("pops")), "lane_child_evals_per_s": r4(bh_rate("child_evals")),
+               "dense_pair_terms_per_s": r4(bh_rate("dense_pairs")),
+               "moment_evals_per_s": r4(bh_rate("moment_evals"))},
+        "detail": detail_path,
     }
+    detail = {"window_profile": window_profile, "timeline": timeline,
+              "attract_log_note": "placement 0 side stream, 3 alone; loss launches apart",
+              "attract_ms_by_t": [[t, sa, ms] for (t, sa, ms) in alog],
+              "losses": {str(t): losses[t] for t in sorted(losses)}}
     # HBM bytes per non-loss attraction launch and BH VALU utilisation: PMC
     # counters cannot be collected by the process they count (rocprofv3 runs
     # the bench as its child), so these come from committed PMC passes over
@@ -475,31 +456,41 @@ def main():
             with open(tf) as fh:
                 tj = json.load(fh)
             out["roofline"]["traffic"] = tj.get("traffic_bytes_per_launch")
-            out["roofline"]["traffic_source"] = {"file": "profiles/" + PMC_ATTRACT, "commit": tj.get("commit"),
-                                                 "how": tj.get("source")}
+            out["roofline"]["traffic_source"] = "profiles/" + PMC_ATTRACT + " @" + str(tj.get("commit"))
+            upk = tj.get("kernels", {})
+            ub = sum(upk.get(kn, {}).get("traffic_bytes_per_launch", 0.0) for kn in UPDATE_KERNELS)
+            if ub:
+                out["update_centre"]["traffic"] = r4(ub)
+            detail["pmc_attract"] = tj
         pmc = os.path.join(here, "profiles", PMC_BH)
         if os.path.exists(pmc):
             with open(pmc) as fh:
-                out["bh"]["valu_pmc"] = json.load(fh)
+                bj = json.load(fh)
+            out["bh"]["valu_issue_pmc"] = {kn: r4(v.get("valu_issue_frac")) for kn, v in bj.get("kernels", {}).items()}
+            out["bh"]["valu_source"] = "profiles/" + PMC_BH + " @" + str(bj.get("commit"))
+            detail["pmc_bh"] = bj
     if a.config == "c4":
         out["metric"] = "t-SNE iterations/sec at C4 (500k x 300 sparse, cosine, 3-D embedding); end-to-end s"
-        out["window_note"] = (f"t=1..{win}, timed inside the warmup from the same initial state: the small-embedding "
-                              "phase (octree moments per query); not the metric's workload")
-        out["bh"]["note"] = ("octree Barnes-Hut repulsion (QuadTree.scala:123-152 generalised to 3-D, DESIGN 3b); "
-                             "the 2-D work counters do not apply")
         for key in ("pops_per_s", "lane_child_evals_per_s", "dense_pair_terms_per_s", "moment_evals_per_s"):
             out["bh"].pop(key, None)
     if a.config == "c5":
         out["metric"] = "t-SNE iterations/sec at the 50k precomputed-distance-matrix config (C5); affinities+joint s"
-        for key in ("knn_s", "knn_pts_per_s", "knn_filter_ms", "knn_mfma_tflops", "knn_mfma_frac_of_peak",
-                    "knn_mfma_frac_whole_knn"):
+        for key in ("knn_s", "knn_pts_per_s", "knn_filter_ms", "knn_filter_mode", "knn_mfma_frac_of_peak"):
             out.pop(key, None)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(snaps, a, n, X_host, (orp, oc, ov))
+        cb, cb_detail = cpu_baseline(snaps, a, n, X_host, (orp, oc, ov))
+        out["cpu_baseline"] = cb
+        detail["cpu_baseline"] = cb_detail
     if rank == 0 and a.locality:
         locality_report(Y[:n], orp, oc, n)
     if rank == 0:
-        print(json.dumps(out))
+        if detail_path:
+            os.makedirs(os.path.dirname(os.path.abspath(detail_path)), exist_ok=True)
+            with open(detail_path, "w") as fh:
+                json.dump(detail, fh)
+        line = json.dumps(out)
+        assert len(line) < 8192, f"bench line is {len(line)} bytes; the driver parses lines < 8 KB"
+        print(line, flush=True)
     ctx.close()
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -535,21 +526,23 @@ def cpu_threads():
 
 def cpu_baseline(snaps, a, n, X_host, P_dev):
     """The oracle (C fp64 restatement of the reference, OpenMP) timed on a
-    bounded sample of the same run.  Optimizer: at embedding snapshots taken
-    from the GPU trajectory (t in snaps), the reference quadtree build of all n
-    points + BH repulsion of `cpu_sample` random queries, extrapolated to n
-    queries, plus the attraction + update of a sample of rows extrapolated to
-    n; the per-iteration cost is held piecewise constant between snapshots and
-    integrated over the timed window (`value`) and over the whole schedule.
+    bounded sample of the same run.  Optimizer, at embedding snapshots taken
+    from the GPU trajectory (t in snaps): the reference's serial quadtree
+    build of all n points (TsneHelpers.scala:234-256, one Flink task) timed
+    once, then BH repulsion of random queries against that tree
+    (TsneHelpers.scala:258-264) in batches of growing size until --cpu-budget
+    seconds are spent (more queries where they are cheap: the late
+    snapshots), extrapolated to n queries; plus the attraction + update of a
+    sample of rows extrapolated to n.  The per-iteration cost is held
+    piecewise constant between snapshots and integrated over the schedule.
     kNN: the reference brute force (oracle_knn, all n candidates) for
-    `cpu_knn_sample` queries, extrapolated to n queries."""
+    `cpu_knn_sample` queries, extrapolated to n queries.  Returns the line's
+    block and the side file's detail."""
     import oracle_ctypes as O
     threads = cpu_threads()
-    q = min(a.cpu_sample, n)
     rng = np.random.default_rng(0)
-    sel = rng.choice(n, q, replace=False)
-    per_t = {}
-    # attraction + update of 20000 rows (one thread), extrapolated
+    per_t, detail = {}, {}
+    # attraction + update of ~20000 rows (one thread), extrapolated
     rp, col, val = (x.cpu().numpy() for x in P_dev)
     nr = int(min(n, 20000, max(16, 2e7 / max(1.0, len(val) / n))))   # ~2e7 entries at most
     r0 = int(rng.integers(0, n - nr + 1))
@@ -559,36 +552,58 @@ def cpu_baseline(snaps, a, n, X_host, P_dev):
     O.update(np.ascontiguousarray(g), Ys0[r0:r0 + nr].copy(), np.zeros((nr, 2)), np.ones((nr, 2)), 0.01, 0.8, 1000.0)
     t_attr = (time.perf_counter() - t0) / nr * n
     del rp, col, val
+    qmax = min(n, 1 << 16)
     for t, Ys in sorted(snaps.items()):
         print(f"[bench] cpu baseline sample at t={t}", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
-        O.repulsion_queries(Ys, a.theta, Ys[sel], threads=threads)
-        t_sample = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        O.repulsion_queries(Ys, a.theta, Ys[sel[:1]], threads=1)
+        tree = O.Tree(Ys)
         t_build = time.perf_counter() - t0
-        per_t[t] = t_build + max(t_sample - t_build, 1e-9) / q * n + t_attr
+        order = rng.permutation(n)
+        pos, q, spent, visits, batches = 0, max(threads, 16), 0.0, 0, []
+        while pos < qmax and (spent < a.cpu_budget or len(batches) < 2):
+            sel = order[pos:min(pos + q, qmax)]
+            pos += len(sel)
+            t0 = time.perf_counter()
+            _, _, v = tree.query(a.theta, Ys[sel], threads=threads)
+            dt = time.perf_counter() - t0
+            spent += dt
+            visits += v
+            batches.append(dt / len(sel))
+            q = min(2 * q, 1 << 14)
+        tree.close()
+        per_q = spent / pos     # wall seconds per query on `threads` threads
+        per_t[t] = t_build + per_q * n + t_attr
+        full = [b for b in batches[1:]] or batches   # the first batch warms the caches
+        detail[str(t)] = {"build_s": t_build, "queries": pos, "query_s": spent, "visits_per_query": visits / pos,
+                          "per_query_ms_batches": [1e3 * b for b in batches]}
+        detail[str(t)]["per_query_spread"] = (max(full) / min(full) - 1.0) if min(full) > 0 else None
     ts = sorted(per_t)
 
     def total(t_end):
         return sum(per_t[min(ts, key=lambda s: abs(s - it))] for it in range(1, t_end + 1))
 
-    out = {"value": a.iterations / total(a.iterations), "unit": "iterations/s", "cores": threads, "kind": "port",
-           "window_it_s": min(20, a.iterations) / total(min(20, a.iterations)),
-           "per_iteration_s_at": {str(t): per_t[t] for t in ts},
-           "sample": f"oracle (C fp64 reference restatement, OpenMP {threads} threads): at GPU-trajectory "
-                     f"snapshots t={ts}, reference quadtree build of all {n} points + BH repulsion of {q} "
-                     f"random queries extrapolated to {n}, + attraction/loss/update of {nr} rows (1 thread) "
-                     f"extrapolated; piecewise-constant over t=1..{a.iterations} (value)"}
+    def r4(x):
+        return float(f"{x:.4g}")
+
+    out = {"value": r4(a.iterations / total(a.iterations)), "unit": "iterations/s", "cores": threads, "kind": "port",
+           "per_iteration_s_at": {str(t): r4(per_t[t]) for t in ts},
+           "build_s_at": {str(t): r4(detail[str(t)]["build_s"]) for t in ts},
+           "queries_at": {str(t): detail[str(t)]["queries"] for t in ts},
+           "per_query_spread_at": {str(t): (r4(detail[str(t)]["per_query_spread"])
+                                            if detail[str(t)]["per_query_spread"] is not None else None) for t in ts},
+           "sample": f"oracle (C fp64 restatement, OpenMP {threads} threads) at GPU-trajectory snapshots: serial "
+                     f"reference quadtree build of all {n} points timed once, then BH queries against it "
+                     f"(random points, batches to ~{a.cpu_budget:g} s) extrapolated to {n}, + attraction/update "
+                     f"of {nr} rows extrapolated; piecewise-constant over t=1..{a.iterations}"}
     if X_host is not None:
         qk = min(a.cpu_knn_sample, n)
         t0 = time.perf_counter()
         O.knn(X_host, a.k, "sqeuclidean", q0=0, q1=qk, threads=threads)
         t_k = time.perf_counter() - t0
-        out["knn_pts_per_s"] = qk / t_k
-        out["knn_sample"] = (f"oracle_knn (exact fp64 brute force over all {n} points, {threads} threads) "
-                             f"for queries 0..{qk - 1}: {t_k:.2f} s -> points/s")
-    return out
+        out["knn_pts_per_s"] = r4(qk / t_k)
+        out["knn_sample"] = f"oracle_knn exact fp64 brute force over all {n} points, {qk} queries, {threads} threads"
+    detail["attraction_update_s_per_iteration"] = t_attr
+    return out, detail
 
 
 if __name__ == "__main__":

@@ -150,6 +150,11 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             selection reads the previous traversal's costs:
  *                             the optimizer's previous iteration, and for the
  *                             single-call operators only with
+ *   "comm_world1" 0           1: tsne_ctx_init_comm / tsne_ctx_init_comm_callbacks
+ *                             at world 1 still create the communicator (RCCL:
+ *                             a one-rank ncclCommInitRankConfig, id may be
+ *                             NULL), and the optimizer runs its sharded path
+ *                             through it -- the transport's own test;
  *   "reuse_costs" 0           1: tsne_gradient / tsne_repulsion select from the
  *                             previous call's costs (results then depend on
  *                             the call history at rounding level; 0 keeps
@@ -166,6 +171,10 @@ int tsne_ctx_get_option(tsne_ctx *ctx, const char *key, double *value_out);
  *   "bh.narrow_groups"   64-query groups the last single-call BH traversal
  *                        (tsne_gradient / tsne_repulsion) ran in the narrow layout;
  *   "opt.narrow_groups"  the same for the optimizer's last iteration;
+ *   "comm.kind"          the context's communicator: 0 none, 1 RCCL, 2 loopback,
+ *                        3 caller callbacks; "comm.calls" collectives it issued;
+ *   "opt.attract_kernel" the optimizer's attraction kernel: 0 attract_rows,
+ *                        1 attract_tiles, 2 attract3 (3-D), -1 no optimizer;
  *   "bh.csort_oversized", "opt.csort_oversized"  buckets of the last coherent
  *                        Morton sort (csort.hpp) beyond its LDS capacity. */
 int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);

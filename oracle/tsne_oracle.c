@@ -489,6 +489,44 @@ int oracle_repulsion_queries(const double *Y, int64_t n, double theta, const dou
     return 0;
 }
 
+/* The CPU baseline's two legs timed apart (bench.py cpu_baseline): the serial
+ * tree build of all n points (TsneHelpers.scala:234-256, one Flink task) once,
+ * then query batches against that tree (TsneHelpers.scala:258-264, the
+ * parallel map over points).  The handle is an opaque qtree_t. */
+void *oracle_tree_build(const double *Y, int64_t n) {
+    if (!Y || n < 1) return NULL;
+    qtree_t *t = (qtree_t *)malloc(sizeof(qtree_t));
+    build_tree(t, Y, n);
+    return t;
+}
+
+int oracle_tree_query(const void *handle, double theta, const double *Q, int64_t nq, double *rep, double *zi,
+                      int64_t *visits, int threads) {
+    const qtree_t *t = (const qtree_t *)handle;
+    if (!t || nq < 0) return -1;
+    int64_t vsum = 0;
+#ifdef _OPENMP
+    if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : vsum)
+#endif
+    for (int64_t i = 0; i < nq; ++i) {
+        double fx, fy, s;
+        int64_t v = 0;
+        qt_repulsive(t, 0, Q[2 * i], Q[2 * i + 1], theta, &fx, &fy, &s, &v);
+        rep[2 * i] = fx; rep[2 * i + 1] = fy; zi[i] = s;
+        vsum += v;
+    }
+    if (visits) *visits = vsum;
+    return 0;
+}
+
+void oracle_tree_free(void *handle) {
+    qtree_t *t = (qtree_t *)handle;
+    if (!t) return;
+    free(t->v);
+    free(t);
+}
+
 /* Attraction + combine for rows [r0, r1) given the full repulsion and Z
  * (TsneHelpers.scala:269-317).  grad is (r1-r0) x 2; loss (nullable) is the
  * partial KL sum of these rows. */

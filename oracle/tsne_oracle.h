@@ -79,6 +79,15 @@ int oracle_repulsion(const double *Y, int64_t n, double theta, int64_t q0, int64
 int oracle_repulsion_queries(const double *Y, int64_t n, double theta, const double *Q, int64_t nq,
                              double *rep, double *zi, int threads);
 
+/* The reference tree of all n points built once (serial, row order), then
+ * queried in batches: the CPU baseline times the build and the queries apart.
+ * visits (nullable) = nodes touched over the batch.  Free with
+ * oracle_tree_free. */
+void *oracle_tree_build(const double *Y, int64_t n);
+int oracle_tree_query(const void *tree, double theta, const double *Q, int64_t nq, double *rep, double *zi,
+                      int64_t *visits, int threads);
+void oracle_tree_free(void *tree);
+
 /* Attraction + combine for rows [r0, r1) given full rep (n x 2) and Z. */
 int oracle_attraction_rows(const int64_t *row_ptr, const int32_t *col, const double *val, int64_t n,
                            const double *Y, int metric, double exaggeration, const double *rep,

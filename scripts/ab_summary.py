@@ -1,4 +1,4 @@
-"""Summarise an A/B bench file of scripts/gpu_r4.sh (`# <variant>` lines, each
+"""Summarise an A/B bench file of scripts/gpu_session.sh (`# <variant>` lines, each
 followed by bench.py's JSON line): loop, end to end, and the timeline's
 tree / BH / attraction ms at a few iterations.
 

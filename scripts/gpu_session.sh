@@ -1,5 +1,7 @@
 # GPU session script: STEPS (space-separated) selects what runs, each GPU step
-# under its own time limit, outputs under gpurun_out/r4$TAG/:
+# under its own time limit, outputs under gpurun_out/r${ROUND:-5}$TAG/:
+#   driver      bench.py exactly as the driver runs it (--gpus 1 --steps 20 --warmup 5, CPU baseline included)
+#   mksnaps     bench.py --dump-y 250,450,650 into /tmp/snaps (the snapshots the snap steps read)
 #   snap        bh_snap.py on snaps/Y_t{250,450,650}.npy per SNAP_VARS entry ("-" = defaults, else KEY=VALUE)
 #   tests_narrow / tests3d / tests_all   GPU test subsets / the whole -m gpu suite
 #   bench / bench4   bench.py (C3 / C4) per BENCH_VARS / BENCH4_VARS entry
@@ -13,17 +15,25 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r4${TAG:-x}
+O=gpurun_out/r${ROUND:-5}${TAG:-x}
+SN=/tmp/snaps
 mkdir -p $O
 run() { local lim=$1; shift; timeout -k 10 $lim "$@"; }
 # a test step's failures do not stop the session; a time limit, abort or crash does
 tst() { run "$@"; local rc=$?; echo "tests rc=$rc" >> $O/status.txt; case $rc in 0|1) return 0;; *) return $rc;; esac; }
 has() { [[ " ${STEPS:-} " == *" $1 "* ]]; }
+if has driver; then
+  run 600 python bench.py --gpus 1 --steps 20 --warmup 5 --detail-out $O/bench_detail.json > $O/driver_bench.json 2> $O/driver_bench.err || exit $?
+fi
+if has mksnaps; then
+  mkdir -p $SN
+  run 300 python bench.py --no-cpu-baseline --trace 0 --dump-y 250,450,650 --dump-dir $SN --detail-out "" > $O/mksnaps.json 2> $O/mksnaps.err || exit $?
+fi
 if has snap; then
   for v in ${SNAP_VARS:--}; do
     opt=""; [ "$v" != "-" ] && opt="--option $v"
     echo "# $v" >> $O/snap.jsonl
-    run 300 python scripts/bh_snap.py snaps/Y_t250.npy snaps/Y_t450.npy snaps/Y_t650.npy $opt >> $O/snap.jsonl 2>> $O/snap.err || exit $?
+    run 300 python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t450.npy $SN/Y_t650.npy $opt >> $O/snap.jsonl 2>> $O/snap.err || exit $?
   done
 fi
 if has tests_narrow; then
@@ -102,7 +112,7 @@ if has pmcsnap; then   # PMC passes over the 2-D BH kernels on the committed C3 
               "SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
     k=$((k+1))
     timeout -s KILL 180 rocprofv3 --pmc $pass --kernel-include-regex "bh_traverse|tile_apply" -d $O/pmcs_$k -o pmc \
-      --output-format csv -- python scripts/bh_snap.py snaps/Y_t250.npy snaps/Y_t650.npy --reps 1 > $O/pmcs_$k.log 2>&1 || exit $?
+      --output-format csv -- python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t650.npy --reps 1 > $O/pmcs_$k.log 2>&1 || exit $?
   done
 fi
 if has proj; then

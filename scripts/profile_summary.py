@@ -1,4 +1,4 @@
-"""Summarise a `STEPS=ktrace bash scripts/gpu_r4.sh` run (rocprofv3 --kernel-trace
+"""Summarise a `STEPS=ktrace bash scripts/gpu_session.sh` run (rocprofv3 --kernel-trace
 --stats of the default bench) into profiles/:
 
   <tag>_rocprof_kernel_stats.csv   rocprofv3 --stats of `bench.py` (warmup + whole timed schedule)
@@ -57,7 +57,7 @@ def main():
             buckets[f"{b + 1}-{b + 100}"] = sum(v) / len(v)
     out = {
         "source": "rocprofv3 --kernel-trace --stats -- python bench.py --no-cpu-baseline --trace 0 "
-                  "(scripts/gpu_r4.sh ktrace); attract_tiles dispatches after the warmup's %d iterations" % W,
+                  "(scripts/gpu_session.sh ktrace); attract_tiles dispatches after the warmup's %d iterations" % W,
         "launches": len(pd),
         "avg_ms_schedule": sum(pd.values()) / len(pd) if pd else None,
         "avg_ms_per_100_iterations": buckets,

@@ -152,6 +152,41 @@ def repulsion_queries(Y, theta, Q, threads=1):
     return rep, zi
 
 
+class Tree:
+    """The reference quadtree of all points of Y (oracle_tree_build), kept for
+    several query batches: the CPU baseline times the build and the queries
+    apart."""
+
+    def __init__(self, Y):
+        self.Y = np.ascontiguousarray(Y, dtype=np.float64)
+        L = lib()
+        L.oracle_tree_build.restype = C.c_void_p
+        L.oracle_tree_build.argtypes = [C.POINTER(D), I64]
+        L.oracle_tree_free.argtypes = [C.c_void_p]
+        L.oracle_tree_query.argtypes = [C.c_void_p, D, C.POINTER(D), I64, C.POINTER(D), C.POINTER(D),
+                                        C.POINTER(I64), C.c_int]
+        self.h = L.oracle_tree_build(_p(self.Y, D), I64(self.Y.shape[0]))
+        assert self.h
+
+    def query(self, theta, Q, threads=1):
+        Q = np.ascontiguousarray(Q, dtype=np.float64)
+        rep = np.zeros((Q.shape[0], 2))
+        zi = np.zeros(Q.shape[0])
+        v = I64(0)
+        rc = lib().oracle_tree_query(self.h, D(theta), _p(Q, D), I64(Q.shape[0]), _p(rep, D), _p(zi, D),
+                                     C.byref(v), C.c_int(threads))
+        assert rc == 0
+        return rep, zi, v.value
+
+    def close(self):
+        if self.h:
+            lib().oracle_tree_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
 def attraction_rows(row_ptr, col, val, Y, rep, Z, r0, r1, metric="sqeuclidean", exaggeration=1.0,
                     want_loss=False):
     Y = np.ascontiguousarray(Y, dtype=np.float64)

@@ -231,3 +231,46 @@ def test_gloo_callbacks_world2_matches_single(tmp_path):
     for k, v in zip(res["keys"], res["vals"]):
         assert abs(v - ls[int(k)]) <= TOL * abs(ls[int(k)])
     assert close(res["Y"], Ys) and close(res["u"], us) and close(res["g"], gs)
+
+
+# ------------------------------------------------ RCCL transport at world 1
+def _world1_run(P, Y0, prm, transport):
+    """The sharded optimizer (query lists, collectives, centring from the
+    gathered embedding) at world 1 through a forced communicator
+    (Options::comm_world1): RCCL (a one-rank ncclCommInitRankConfig) or the
+    caller's callbacks (identity collectives)."""
+    ctx = T.Context(0)
+    try:
+        ctx.set_option("comm_world1", 1)
+        if transport == "rccl":
+            ctx.init_comm(0, 1, None)
+        else:
+            ctx.init_comm_callbacks(0, 1, lambda a: None, lambda buf, off: None)
+        assert ctx.rank_world() == (0, 1)
+        kind = ctx.counter("comm.kind")
+        Y, u, g = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+        loss = ctx.optimize(*P, Y, u, g, prm)
+        calls = ctx.counter("comm.calls")
+    finally:
+        ctx.close()
+    return Y, u, g, loss, kind, calls
+
+
+@pytest.mark.parametrize("c", [2, 3])
+def test_rccl_world1_sharded_path_matches_callbacks(c):
+    """RCCL's ncclAllReduce and the ncclBroadcast group of the ragged all-gather
+    execute in the optimizer's sharded path (one rank): bit-identical to the
+    same path through identity callbacks, and within the multi-rank tolerance
+    of the unsharded world-1 run (summation order of the query-list Z)."""
+    P, Y0 = problem(n=1200 if c == 2 else 800, c=c, seed=11)
+    prm = default_params(n_components=c, iterations=40, theta=0.5, learning_rate=200.0)
+    Yr, ur, gr, lr, kr, nr = _world1_run(P, Y0, prm, "rccl")
+    Yc, uc, gc, lc, kc, nc = _world1_run(P, Y0, prm, "callbacks")
+    assert (kr, kc) == (1, 3)
+    assert nr == nc and nr >= 40 + 40   # a Z all-reduce and a Y all-gather per iteration, at least
+    assert np.array_equal(Yr, Yc) and np.array_equal(ur, uc) and np.array_equal(gr, gc)
+    assert lr == lc
+    Ys, us, gs, ls = run_single(P, Y0, prm)
+    for t in ls:
+        assert abs(lr[t] - ls[t]) <= TOL * abs(ls[t]), t
+    assert close(Yr, Ys) and close(ur, us) and close(gr, gs)

@@ -129,6 +129,7 @@ static const OptionField k_options[] = {
     {"knn_bf16", nullptr, &Options::knn_bf16, 0, 1},
     {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
     {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
+    {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
 };
 static const OptionField &option_field(const char *key) {
     for (const OptionField &f : k_options)
@@ -383,6 +384,9 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         if (k == "bh.narrow_groups") *value_out = ctx->single_tree ? bh_narrow_groups(ctx, *ctx->single_tree) : 0;
         else if (k == "opt.narrow_groups") *value_out = opt_tree(ctx) ? bh_narrow_groups(ctx, *opt_tree(ctx)) : 0;
         else if (k == "bh.csort_oversized") *value_out = ctx->single_tree ? csort_oversized(ctx, ctx->single_tree->cs) : 0;
+        else if (k == "opt.attract_kernel") *value_out = opt_attract_kernel(ctx);
+        else if (k == "comm.kind") *value_out = comm_counter(ctx, false);
+        else if (k == "comm.calls") *value_out = comm_counter(ctx, true);
         else if (k == "opt.csort_oversized") *value_out = opt_tree(ctx) ? csort_oversized(ctx, opt_tree(ctx)->cs) : 0;
         else fail(TSNE_ERR_ARG, "unknown counter '" + k + "'");
     });

@@ -21,9 +21,12 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <functional>
 #include <map>
 #include <mutex>
+#include <thread>
 
+#include "comm_guard.hpp"
 #include "common.hpp"
 
 namespace tsne {
@@ -43,6 +46,8 @@ struct Comm {
     virtual void release(tsne_ctx *) {}
     // a phase boundary inside a rank's work (loopback serial mode: timed)
     virtual void mark(tsne_ctx *, const char *) {}
+    virtual int kind() const = 0;   // 1 RCCL, 2 loopback, 3 caller callbacks
+    int64_t calls = 0;              // collectives this rank has issued
 };
 
 namespace {
@@ -51,55 +56,79 @@ void nccl_check(ncclResult_t r, const char *what) {
     if (r != ncclSuccess) fail(TSNE_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-struct RcclComm : Comm {
-    ncclComm_t comm = nullptr;
-    // mu orders abort() against this rank's own collective calls: abort runs
-    // on a failing peer's thread (run_group), and ncclCommAbort frees the
-    // communicator, so no enqueue may be inside RCCL with it then.  The
-    // enqueues are asynchronous (the waiting happens later, in a stream
-    // synchronisation that the abort ends), so the lock is held briefly.
-    std::mutex mu;
-    bool aborted = false;
-    ~RcclComm() override {
-        if (comm && !aborted) (void)ncclCommDestroy(comm);
+// RCCL under the CommGuard protocol (comm_guard.hpp): communicators are
+// created non-blocking, so no RCCL call holds the rank's thread while a peer
+// is missing, and abort() from a failing peer's thread never waits for one.
+struct RcclBackend {
+    using Handle = ncclComm_t;
+    static int code(ncclResult_t r) { return r == ncclSuccess ? 0 : r == ncclInProgress ? 1 : -(int)r; }
+    template <class F> static int call(Handle h, F &&f) { return code(f(h)); }
+    static int poll(Handle h) {
+        ncclResult_t a = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(h, &a);
+        return r != ncclSuccess ? -(int)r : code(a);
     }
+    static void abort(Handle h) {
+        if (h) (void)ncclCommAbort(h);
+    }
+    static void destroy(Handle h) {
+        if (!h) return;
+        if (ncclCommFinalize(h) == ncclInProgress || poll(h) == 1)
+            while (poll(h) == 1) std::this_thread::yield();
+        (void)ncclCommDestroy(h);
+    }
+};
+
+// wait for a non-blocking communicator's initialisation
+void nccl_wait_init(ncclComm_t c, const char *what) {
+    for (;;) {
+        const int p = RcclBackend::poll(c);
+        if (p == 0) return;
+        if (p < 0) fail(TSNE_ERR_COMM, std::string(what) + ": " + ncclGetErrorString((ncclResult_t)-p));
+        std::this_thread::yield();
+    }
+}
+
+ncclConfig_t nonblocking_config() {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    return cfg;
+}
+
+struct RcclComm : Comm {
+    CommGuard<RcclBackend> g;
+    int kind() const override { return 1; }
+    ~RcclComm() override { g.destroy(); }
     // ncclCommAbort stops this rank's in-flight collective kernels and frees
     // the communicator: a peer blocked in a collective with it then fails
     // instead of hanging (run_group aborts every rank of a group once one
     // rank has thrown).  Later calls report TSNE_ERR_COMM.
-    void abort() override {
-        std::lock_guard<std::mutex> lk(mu);
-        if (comm && !aborted) {
-            aborted = true;
-            (void)ncclCommAbort(comm);
-        }
-    }
-    // caller holds mu
-    void live() {
-        if (aborted) fail(TSNE_ERR_COMM, "RCCL communicator aborted (another rank failed)");
+    void abort() override { g.abort(); }
+    void run(const char *what, const std::function<ncclResult_t(ncclComm_t)> &op) {
+        ncclResult_t last = ncclSuccess;
+        const int rc = g.run([&](ncclComm_t c) { return last = op(c); });
+        if (rc == -1) fail(TSNE_ERR_COMM, "RCCL communicator aborted (another rank failed)");
+        if (rc == -2) fail(TSNE_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(last == ncclSuccess ? ncclInternalError : last));
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override {
-        std::lock_guard<std::mutex> lk(mu);
-        live();
-        nccl_check(ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, comm, ctx->stream), "ncclAllReduce");
+        run("ncclAllReduce", [&](ncclComm_t c) { return ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, c, ctx->stream); });
     }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override {
-        std::lock_guard<std::mutex> lk(mu);
-        live();
-        nccl_check(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm, ctx->stream), "ncclAllReduce");
+        run("ncclAllReduce", [&](ncclComm_t c) { return ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, c, ctx->stream); });
     }
     // ragged all-gather: one in-place broadcast per root, fused into one group
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
-        std::lock_guard<std::mutex> lk(mu);
-        live();
         uint8_t *b = static_cast<uint8_t *>(buf);
-        nccl_check(ncclGroupStart(), "ncclGroupStart");
-        for (int r = 0; r < ctx->world; ++r) {
-            const size_t bytes = (size_t)(off[r + 1] - off[r]);
-            if (bytes == 0) continue;
-            nccl_check(ncclBroadcast(b + off[r], b + off[r], bytes, ncclUint8, r, comm, ctx->stream), "ncclBroadcast");
-        }
-        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+        run("ncclBroadcast group", [&](ncclComm_t c) {
+            ncclResult_t r = ncclGroupStart();
+            for (int q = 0; q < ctx->world && r == ncclSuccess; ++q) {
+                const size_t bytes = (size_t)(off[q + 1] - off[q]);
+                if (bytes == 0) continue;
+                r = ncclBroadcast(b + off[q], b + off[q], bytes, ncclUint8, q, c, ctx->stream);
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            return r != ncclSuccess ? r : e;
+        });
     }
 };
 
@@ -236,6 +265,7 @@ struct LoopGroup {
 
 struct LoopComm : Comm {
     std::shared_ptr<LoopGroup> g;
+    int kind() const override { return 2; }
     explicit LoopComm(std::shared_ptr<LoopGroup> grp) : g(std::move(grp)) {}
 
     // publish this rank's pointer once its stream has produced the data
@@ -282,6 +312,7 @@ struct LoopComm : Comm {
 // torch.distributed/gloo in the tests) carries the library's messages.  The
 // library stages each message through host memory.
 struct CallbackComm : Comm {
+    int kind() const override { return 3; }
     tsne_comm_ops ops{};
     void *user = nullptr;
     std::vector<uint8_t> host;
@@ -322,7 +353,7 @@ void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops
     TSNE_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
     TSNE_REQUIRE(ops && ops->allreduce_sum_f64 && ops->allreduce_sum_u64 && ops->allgatherv, "incomplete comm ops");
     comm_destroy(ctx);
-    if (world == 1) return;
+    if (world == 1 && !ctx->opts.comm_world1) return;
     CallbackComm *c = new CallbackComm();
     c->ops = *ops;
     c->user = user;
@@ -341,11 +372,15 @@ void comm_unique_id(uint8_t *out) {
 void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id) {
     TSNE_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
     comm_destroy(ctx);
-    if (world == 1) { ctx->rank = 0; ctx->world = 1; return; }
+    if (world == 1 && !ctx->opts.comm_world1) { ctx->rank = 0; ctx->world = 1; return; }
     ncclUniqueId uid;
-    std::memcpy(&uid, id, sizeof(uid));
+    if (id) std::memcpy(&uid, id, sizeof(uid));
+    else nccl_check(ncclGetUniqueId(&uid), "ncclGetUniqueId");   // world 1: our own id
     std::unique_ptr<RcclComm> c(new RcclComm());
-    nccl_check(ncclCommInitRank(&c->comm, world, uid, rank), "ncclCommInitRank");
+    ncclConfig_t cfg = nonblocking_config();
+    const ncclResult_t r = ncclCommInitRankConfig(&c->g.h, world, uid, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) nccl_check(r, "ncclCommInitRankConfig");
+    nccl_wait_init(c->g.h, "ncclCommInitRankConfig");
     ctx->comm = c.release();
     ctx->rank = rank;
     ctx->world = world;
@@ -367,14 +402,28 @@ void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback) {
         }
         return;
     }
-    std::vector<ncclComm_t> comms(world);
-    std::vector<int> devs(world);
-    for (int r = 0; r < world; ++r) devs[r] = subs[r]->device;
-    nccl_check(ncclCommInitAll(comms.data(), world, devs.data()), "ncclCommInitAll");
+    // one thread initialises every device's rank: a group of non-blocking
+    // ncclCommInitRankConfig calls (ncclCommInitAll has no config)
+    std::vector<ncclComm_t> comms(world, nullptr);
+    ncclUniqueId uid;
+    nccl_check(ncclGetUniqueId(&uid), "ncclGetUniqueId");
+    ncclConfig_t cfg = nonblocking_config();
+    int dev0 = 0;
+    TSNE_HIP(hipGetDevice(&dev0));
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int r = 0; r < world; ++r) {
+        TSNE_HIP(hipSetDevice(subs[r]->device));
+        const ncclResult_t e = ncclCommInitRankConfig(&comms[r], world, uid, r, &cfg);
+        if (e != ncclSuccess && e != ncclInProgress) nccl_check(e, "ncclCommInitRankConfig");
+    }
+    const ncclResult_t ge = ncclGroupEnd();
+    if (ge != ncclSuccess && ge != ncclInProgress) nccl_check(ge, "ncclGroupEnd");
+    TSNE_HIP(hipSetDevice(dev0));
+    for (int r = 0; r < world; ++r) nccl_wait_init(comms[r], "ncclCommInitRankConfig");
     for (int r = 0; r < world; ++r) {
         comm_destroy(subs[r]);
         RcclComm *c = new RcclComm();
-        c->comm = comms[r];
+        c->g.h = comms[r];
         subs[r]->comm = c;
         subs[r]->rank = r;
         subs[r]->world = world;
@@ -395,6 +444,11 @@ void comm_release(tsne_ctx *ctx) {
     if (ctx->comm) ctx->comm->release(ctx);
 }
 
+int64_t comm_counter(const tsne_ctx *ctx, bool calls) {
+    if (!ctx->comm) return 0;
+    return calls ? ctx->comm->calls : ctx->comm->kind();
+}
+
 void comm_destroy(tsne_ctx *ctx) {
     delete ctx->comm;
     ctx->comm = nullptr;
@@ -404,16 +458,19 @@ void comm_destroy(tsne_ctx *ctx) {
 
 void comm_allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off_bytes) {
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
+    ++ctx->comm->calls;
     ctx->comm->allgatherv(ctx, buf, off_bytes);
 }
 
 void comm_allreduce_sum_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) {
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
+    ++ctx->comm->calls;
     ctx->comm->allreduce_u64(ctx, buf, count);
 }
 
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count) {
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
+    ++ctx->comm->calls;
     ctx->comm->allreduce_f64(ctx, buf, count);
 }
 

@@ -180,6 +180,8 @@ struct Options {
     int recut = 0;            // several ranks on the tiled layout: re-cut by BH cost instead of relabels
     int knn_bf16 = 1;         // kNN threshold filter: bf16x3 MFMA (0: f32-input MFMA)
     double narrow = 3.0;      // BH: 64-query groups costing >= narrow x the mean run in the narrow layout (0: off)
+    int comm_world1 = 0;      // tsne_ctx_init_comm / _callbacks at world 1 still create the communicator, and
+                              // the optimizer runs its sharded code path through it (tests the transport)
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
                               // previous call's costs (results then depend on the call history at rounding level)
 };
@@ -262,6 +264,7 @@ void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits);
 double opt_last_z(tsne_ctx *ctx);
 int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap);
 void opt_destroy(tsne_ctx *ctx);
+int64_t opt_attract_kernel(tsne_ctx *ctx);   // the optimizer's attraction: 0 attract_rows, 1 attract_tiles, 2 attract3 (-1: none)
 BHTree *opt_tree(tsne_ctx *ctx);   // the optimizer's 2-D tree (nullptr without one)
 
 // comm.cpp
@@ -270,6 +273,8 @@ void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id);
 void comm_destroy(tsne_ctx *ctx);
 void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback);
 void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops *ops, void *user);
+// the context's communicator: kind (0 none, 1 RCCL, 2 loopback, 3 callbacks) or collectives issued
+int64_t comm_counter(const tsne_ctx *ctx, bool calls);
 void comm_abort(tsne_ctx *ctx);
 void comm_release(tsne_ctx *ctx);
 void comm_mark(tsne_ctx *ctx, const char *what);   // phase boundary (loopback serial timing)   // end of a rank's group call (loopback serial timing)

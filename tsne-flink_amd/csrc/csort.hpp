@@ -25,15 +25,19 @@ struct CoherentSort {
     int32_t *off = nullptr;         // P + 1 bucket offsets
     int32_t *cur = nullptr;         // P scatter cursors
     int32_t *bkt = nullptr;         // n: bucket of element j (the previous order's j-th point)
-    uint64_t *kb = nullptr;         // 2n: bucketed keys (the upper half: scratch of oversized buckets)
-    int32_t *vb = nullptr;          // 2n: bucketed point indices
+    uint64_t *kb = nullptr;         // 3n: bucketed keys [0, n), then the oversized buckets' scratch
+                                    // (bucket at offset o: [n + 2 o, n + 2 o + 2 m), power-of-two padded)
+    int32_t *vb = nullptr;          // 3n: bucketed point indices, the same layout
     int32_t *stat = nullptr;        // [0] oversized buckets of the last sort (diagnostics)
 };
 
 // Buffers for n points (ctx workspace, names pre + field).  n outside
 // [CSORT_MIN_N, CSORT_MAX_N]: nothing (the callers keep rocPRIM's sort).
 constexpr int64_t CSORT_MIN_N = 16384;
-constexpr int64_t CSORT_MAX_N = 2000000;   // <= 1024 buckets of ~2k points (LDS capacity 4k)
+// Above 1024 x 1.2k points the mean bucket outgrows the LDS sort's 4k capacity
+// at the measured 3.3x bucket skew (cs_split) and whole buckets would take the
+// slow global-memory bitonic path: rocPRIM's sort there.
+constexpr int64_t CSORT_MAX_N = 1250000;
 void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &pre);
 // keys[p] for points p < n -> keys_sorted / idx_sorted ascending by (key, p).
 // prev_idx_sorted: the previous sort's idx_sorted (a permutation of [0, n));

@@ -1380,47 +1380,47 @@ __global__ __launch_bounds__(256) void oct_traverse64(
 
 }  // namespace
 
-void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n) {
+void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n, const std::string &pre) {
     Workspace &ws = ctx->ws;
     t.n = n;
-    t.keys = ws.get<uint64_t>("oct.keys", n);
-    t.keys_sorted = ws.get<uint64_t>("oct.keys_sorted", n);
-    t.idx = ws.get<int32_t>("oct.idx", n);
-    t.idx_sorted = ws.get<int32_t>("oct.idx_sorted", n);
-    t.inv = ws.get<int32_t>("oct.inv", n);
-    t.dupc = ws.get<int32_t>("oct.dupc", n);
-    t.pos = ws.get<double4>("oct.pos", n);
-    t.nodes = ws.get<OctNode>("oct.nodes", n);
-    t.orec = ws.get<ORec>("oct.orec", n);
-    t.agg = ws.get<double>("oct.agg", AGG3 * (size_t)n);
-    t.parent_leaf = ws.get<int32_t>("oct.parent_leaf", n);
-    t.parent_node = ws.get<int32_t>("oct.parent_node", n);
-    t.arrive = ws.get<int32_t>("oct.arrive", n);
-    t.meta = ws.get<int32_t>("oct.meta", 4);
+    t.keys = ws.get<uint64_t>(pre + "keys", n);
+    t.keys_sorted = ws.get<uint64_t>(pre + "keys_sorted", n);
+    t.idx = ws.get<int32_t>(pre + "idx", n);
+    t.idx_sorted = ws.get<int32_t>(pre + "idx_sorted", n);
+    t.inv = ws.get<int32_t>(pre + "inv", n);
+    t.dupc = ws.get<int32_t>(pre + "dupc", n);
+    t.pos = ws.get<double4>(pre + "pos", n);
+    t.nodes = ws.get<OctNode>(pre + "nodes", n);
+    t.orec = ws.get<ORec>(pre + "orec", n);
+    t.agg = ws.get<double>(pre + "agg", AGG3 * (size_t)n);
+    t.parent_leaf = ws.get<int32_t>(pre + "parent_leaf", n);
+    t.parent_node = ws.get<int32_t>(pre + "parent_node", n);
+    t.arrive = ws.get<int32_t>(pre + "arrive", n);
+    t.meta = ws.get<int32_t>(pre + "meta", 4);
     t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
-    t.bbox_part = ws.get<double>("oct.bbox_part", 6 * (size_t)t.bbox_blocks);
+    t.bbox_part = ws.get<double>(pre + "bbox_part", 6 * (size_t)t.bbox_blocks);
     t.W = ws.get<double>("oct.W", 1);
     size_t tb = 0;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n, 0,
                                                64, ctx->stream));
     t.sort_tmp_bytes = tb;
-    t.sort_tmp = ws.get<uint8_t>("oct.sort_tmp", tb);
-    csort_alloc(ctx, t.cs, n, "oct.");
+    t.sort_tmp = ws.get<uint8_t>(pre + "sort_tmp", tb);
+    csort_alloc(ctx, t.cs, n, pre);
     t.cs_primed = false;
-    t.mom = ws.get<double>("oct.mom", (size_t)MOM3_K * n);
-    t.mcnt = ws.get<int32_t>("oct.mcnt", n);
-    t.moff = ws.get<int32_t>("oct.moff", n);
+    t.mom = ws.get<double>(pre + "mom", (size_t)MOM3_K * n);
+    t.mcnt = ws.get<int32_t>(pre + "mcnt", n);
+    t.moff = ws.get<int32_t>(pre + "moff", n);
     t.item_cap = n / 8 + 64;
-    t.item_node = ws.get<int32_t>("oct.item_node", t.item_cap);
-    t.mom_part = ws.get<double>("oct.mom_part", (size_t)MOM3_K * t.item_cap);
-    t.mom_flag = ws.get<int32_t>("oct.mom_flag", 4);
-    t.mlist = ws.get<int32_t>("oct.mlist", n / 256 + 64);   // nodes of > MOM3_CHUNK points: < 2 n / MOM3_CHUNK
-    t.mtask = ws.get<int32_t>("oct.mtask", (size_t)MOM3_TASKS * n);
-    t.mtask_n = ws.get<int32_t>("oct.mtask_n", n);
+    t.item_node = ws.get<int32_t>(pre + "item_node", t.item_cap);
+    t.mom_part = ws.get<double>(pre + "mom_part", (size_t)MOM3_K * t.item_cap);
+    t.mom_flag = ws.get<int32_t>(pre + "mom_flag", 4);
+    t.mlist = ws.get<int32_t>(pre + "mlist", n / 256 + 64);   // nodes of > MOM3_CHUNK points: < 2 n / MOM3_CHUNK
+    t.mtask = ws.get<int32_t>(pre + "mtask", (size_t)MOM3_TASKS * n);
+    t.mtask_n = ws.get<int32_t>(pre + "mtask_n", n);
     size_t mb = 0;
     TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, mb, t.mcnt, t.moff, (int)n, ctx->stream));
     t.mscan_tmp_bytes = mb;
-    t.mscan_tmp = ws.get<uint8_t>("oct.mscan_tmp", mb);
+    t.mscan_tmp = ws.get<uint8_t>(pre + "mscan_tmp", mb);
     // the first build computes moments (demand := threshold); threshold n / 64
     // lanes; Options::oct_moments = 0 turns the path off
     const bool on = ctx->opts.oct_moments != 0;

@@ -78,7 +78,10 @@ struct OctTree {
     int64_t item_cap = 0;
 };
 
-void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n);
+// Allocate (from ctx->ws, buffers named pre + field) for n points: the
+// optimizer's tree "oct.", the single-call operators' "oct1." (the coherent
+// sort reads the previous build's order, so two trees never share buffers).
+void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n, const std::string &pre = "oct.");
 // Octree of all n points of Y (n x 3, device); late: the optimizer after
 // early exaggeration (the near-exact tolerance the records are built for).
 void oct_build(tsne_ctx *ctx, OctTree &t, const double *dY, double theta, bool late = false);

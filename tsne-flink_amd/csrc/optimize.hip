@@ -129,6 +129,11 @@ struct OptState {
     int64_t last_visits[10] = {};
 };
 
+// The sharded code path (query lists, collectives, centring from the gathered
+// embedding) runs whenever the context has a communicator: world > 1, or a
+// world-1 communicator made with Options::comm_world1 (transport tests).
+static inline bool sharded(const tsne_ctx *ctx) { return ctx->comm != nullptr; }
+
 // TSNE_DEBUG_TILES=1: layout and per-iteration BH / tile diagnostics on stderr
 // (synchronises; a debug print, no effect on results)
 static bool debug_tiles() {
@@ -1295,7 +1300,7 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
         inv = t.inv;
     } else {
         OctTree t;
-        oct_alloc(ctx, t, n);
+        oct_alloc(ctx, t, n, "oct1.");
         oct_build(ctx, t, dY, theta);
         oct_repulsion(ctx, t, theta, 0, n, Fs, zs);
         inv = t.inv;
@@ -1311,7 +1316,7 @@ void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_
     TSNE_REQUIRE(n >= 1, "empty embedding");
     hipStream_t st = ctx->stream;
     OctTree t;
-    oct_alloc(ctx, t, n);
+    oct_alloc(ctx, t, n, "oct1.");
     oct_build(ctx, t, dY, theta);
     double *F = ctx->ws.get<double>("grad3.F", 3 * (size_t)n);
     double *z = ctx->ws.get<double>("grad.z", n);
@@ -1367,7 +1372,7 @@ static std::vector<int64_t> equal_cuts(int64_t n, int world) {
 // make every rank's upd / gains current for all labels (each rank updates
 // only its own labels between relabels): ragged all-gather of the slices
 static void gather_working_set(tsne_ctx *ctx, OptState *s) {
-    if (ctx->world == 1) return;
+    if (!sharded(ctx)) return;
     const int c = s->cur;
     std::vector<int64_t> off(ctx->world + 1);
     for (int r = 0; r <= ctx->world; ++r) off[r] = s->own[r] * s->C * (int64_t)sizeof(double);
@@ -1659,7 +1664,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
     s->visits = ws.get<unsigned long long>("opt.visits", 32);
-    if (world > 1) {
+    if (sharded(ctx)) {
         const int64_t nb = ceil_div(n, 256);
         s->qlist = ws.get<int32_t>("opt.qlist", n);
         s->qcnt = ws.get<int32_t>("opt.qcnt", nb);
@@ -1686,7 +1691,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         // initial labels in P's graph order (Options::graph_order = 0: the original order)
         const bool gorder = ctx->opts.graph_order != 0;
         const bool dense_small = s->nnz / n > 1024 && n * 16 <= (2 << 20);   // see maybe_relabel
-        if (gorder && n >= 2 && !(dense_small && world == 1)) {
+        if (gorder && n >= 2 && !(dense_small && !sharded(ctx))) {
             int32_t *order = ws.get<int32_t>("opt.g.order", n);
             graph_order(ctx, s, order);
             relabel(ctx, s, order, s->own);
@@ -1707,13 +1712,13 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
 // over its query list + an all-reduce of one double
 static void reduce_Z(tsne_ctx *ctx, OptState *s, const double *z) {
     hipStream_t st = ctx->stream;
-    if (ctx->world == 1) {
+    if (!sharded(ctx)) {
         hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, z, s->n, 1, 0, s->part2);
     } else {
         hipLaunchKernelGGL(reduce_list_partial, dim3(NPART), dim3(256), 0, st, z, s->qlist, s->L1 - s->L0, s->part2);
     }
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal, 0.0);
-    if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal, 1);
+    if (sharded(ctx)) comm_allreduce_sum_f64(ctx, s->scal, 1);
 }
 
 // loss of this iteration (all ranks' partial sums) into its slot
@@ -1723,7 +1728,7 @@ static void record_loss(tsne_ctx *ctx, OptState *s, int32_t t, int64_t blocks, b
     hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, s->part, blocks, 1, 0, s->part2);
     hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 1, 0.0);
     if (zfree) hipLaunchKernelGGL(loss_add_lnz, dim3(1), dim3(64), 0, st, s->scal, ex);
-    if (ctx->world > 1) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
+    if (sharded(ctx)) comm_allreduce_sum_f64(ctx, s->scal + 1, 1);
     const int slot = t / 10 - 1;
     if (slot >= 0 && slot < s->loss_slots) {
         TSNE_HIP(hipMemcpyAsync(s->loss + slot, s->scal + 1, sizeof(double), hipMemcpyDeviceToDevice, st));
@@ -1803,7 +1808,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
         ctx->timers.end("opt.attract", s->side);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     }
-    if (ctx->world > 1) {
+    if (sharded(ctx)) {
         build_qlist(ctx, s, s->otree.idx_sorted);
         oct_repulsion(ctx, s->otree, p.theta, 0, s->L1 - s->L0, s->F3, s->z, s->qlist);
     } else {
@@ -1820,12 +1825,12 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
                                  s->part, want_loss);
         ctx->timers.end("opt.attract", st);
     }
-    s->log_attract(t, want_loss ? 1 : 3);
+    s->log_attract(t, side ? 0 : 1);   // 0: beside the traversal (side stream); 1: loss launch alone after Z
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     ctx->timers.begin("opt.update", st);
     // one rank: the mean's block partials from combine_update3, one
     // workgroup for the mean, one pass for centre + the caller's copy
-    const bool fused_mean = ctx->world == 1;
+    const bool fused_mean = !sharded(ctx);
     if (s->L1 > s->L0)
         hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->L1 - s->L0, 256)), dim3(256), 0, st, s->L0, s->L1,
                            s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[0], s->gains[0],
@@ -1859,7 +1864,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
 // equal cost, applied (owned rows and their tiles rebuilt) when a cut moves
 // by more than 1/16 of a rank's share.
 static bool recut_mode(tsne_ctx *ctx, OptState *s) {
-    return ctx->opts.recut && ctx->opts.relabel == -1 && ctx->world > 1 && s->at_on && !s->morton_labels;
+    return ctx->opts.recut && ctx->opts.relabel == -1 && sharded(ctx) && s->at_on && !s->morton_labels;
 }
 static void recut(tsne_ctx *ctx, OptState *s, const std::vector<int64_t> &cuts) {
     gather_working_set(ctx, s);   // full upd / gains under the old cuts
@@ -1899,14 +1904,14 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     // dense rows over a small embedding (the distance-matrix mode, C5): every
     // row gathers all of Y, which sits in one XCD's L2 (n * 16 B <= 2 MiB)
     // whatever the labels, so a relabel (a copy of the whole P) buys nothing
-    if (ctx->world == 1 && s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
+    if (!sharded(ctx) && s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
     // Options::relabel: 0 never, 1 by the locality score, 2 always; -1: by the
     // score, except on one rank with the tiled layout, which keeps P's graph
     // order (attract_tiles reads Y in label windows; a Morton relabel hands
     // the attraction back to attract_rows: whole C3 schedule 7.23 -> 7.01 s
     // without relabels, A/B on one box)
     const int mode = ctx->opts.relabel;
-    if (mode == 0 || (mode == -1 && ctx->world == 1 && s->at_on)) return;
+    if (mode == 0 || (mode == -1 && !sharded(ctx) && s->at_on)) return;
     // a fixed sample of rows, ~1 << 22 entries at most (dense rows: fewer rows)
     const int64_t avg = std::max<int64_t>(1, s->nnz / std::max<int64_t>(1, n));
     const int64_t nsamp = std::max<int64_t>(1, std::min<int64_t>({n, 1 << 16, (1 << 22) / avg}));
@@ -1922,7 +1927,7 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     const bool go = mode == 2 || sc[1] > sc[0];
     if (!go) return;
     std::vector<int64_t> cuts = s->own;
-    if (ctx->world > 1) {
+    if (sharded(ctx)) {
         comm_allreduce_sum_u64(ctx, s->bcost, (size_t)ceil_div(n, 256));
         bh_balance(ctx, s->bcost, n, ctx->world, s->bounds);
         TSNE_HIP(hipMemcpyAsync(cuts.data(), s->bounds, sizeof(int64_t) * (ctx->world + 1), hipMemcpyDeviceToHost, st));
@@ -1991,7 +1996,6 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int want_loss = (t % 10 == 0);
     const bool check_relabel = t % RELABEL_EVERY == 0;
     const int64_t n = s->n;
-    const int world = ctx->world;
     double *Y = s->Y[s->cur];
     if (s->profile) {
         TSNE_HIP(hipMemsetAsync(s->visits, 0, 32 * sizeof(unsigned long long), st));
@@ -2028,15 +2032,15 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // the strict near-exact tolerance while P is exaggerated (the dynamics
     // amplify any difference fastest there), the late one after
     bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(ctx), bh_near_tol(ctx, ex == 1.0));
-    if (world > 1) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
+    if (sharded(ctx)) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
     if (!rt_phase) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
     // bucket costs only where a relabel may re-cut the ownership
-    unsigned long long *bcost = (world > 1 && check_relabel) ? s->bcost : nullptr;
+    unsigned long long *bcost = (sharded(ctx) && check_relabel) ? s->bcost : nullptr;
     if (bcost) TSNE_HIP(hipMemsetAsync(bcost, 0, sizeof(unsigned long long) * ceil_div(n, 256), st));
-    if (world > 1) {
+    if (sharded(ctx)) {
         build_qlist(ctx, s, s->tree.idx_sorted);
         bh_repulsion(ctx, s->tree, p.theta, 0, s->L1 - s->L0, s->F, s->z, s->profile ? s->visits : nullptr, s->qlist,
                      bcost, recut_mode(ctx, s));
@@ -2054,7 +2058,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // update + centre: combine_update (with the mean's block partials when one
     // rank holds every row), mean, centre + write-back of the caller's Y
     ctx->timers.begin("opt.update", st);
-    const bool fused_mean = world == 1;
+    const bool fused_mean = !sharded(ctx);
     const int c = s->cur;
     combine_launch<1>(st, s->L0, s->L1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
                       s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
@@ -2125,6 +2129,12 @@ int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, doub
         if (ms) ms[e] = v[e];
     }
     return k;
+}
+
+int64_t opt_attract_kernel(tsne_ctx *ctx) {
+    OptState *s = ctx->opt;
+    if (!s) return -1;
+    return s->C == 3 ? 2 : (s->at_on ? 1 : 0);
 }
 
 BHTree *opt_tree(tsne_ctx *ctx) {
