@@ -150,6 +150,12 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             selection reads the previous traversal's costs:
  *                             the optimizer's previous iteration, and for the
  *                             single-call operators only with
+ *   "bh_split" 0              several ranks (2-D), 1: partition the Barnes-Hut
+ *                             tree by ranges of its sorted points -- every rank
+ *                             walks every query over the cells holding its own
+ *                             points, each term taken by one rank, and the
+ *                             forces are summed by a reduce-scatter to the row
+ *                             owners (0: partition the queries, Z-only exchange);
  *   "comm_world1" 0           1: tsne_ctx_init_comm / tsne_ctx_init_comm_callbacks
  *                             at world 1 still create the communicator (RCCL:
  *                             a one-rank ncclCommInitRankConfig, id may be

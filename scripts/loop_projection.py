@@ -30,10 +30,13 @@ import tsne_amd as T  # noqa: E402
 from tsne_amd.api import default_params  # noqa: E402
 
 # collective model for W MI355X on xGMI (MI355X_MICROARCH.md: 7 links x ~153
-# GB/s per GPU, point to point): the per-iteration ragged all-gather of the
-# updated embedding (n x 2 doubles; every rank receives (W-1)/W of it) at an
-# assumed 100 GB/s effective per receiving GPU, plus ~25 us latency for each
-# small all-reduce (Z every iteration, the loss every 10th)
+# GB/s per GPU, point to point): each ragged all-gather of the updated
+# embedding (n x 2 doubles; every rank receives (W-1)/W of it) and each
+# ragged reduce-scatter of the tree partition's forces (n x 2 doubles; every
+# rank sends (W-1)/W of it) at an assumed 100 GB/s effective per GPU, plus
+# ~25 us latency for each small all-reduce (Z every iteration, the loss every
+# 10th, the tree partition's W costs); the counts are the run's own (the
+# serial summary's per-collective counts)
 AG_GBS = 100.0
 AR_US = 25.0
 
@@ -102,11 +105,14 @@ def main():
     with open(path) as fh:
         ser = json.load(fh)
     span_s = ser["span_ms"] * 1e-3
-    ag_s = a.iterations * (a.world - 1) / a.world * a.n * 16 / (AG_GBS * 1e9)
-    ar_s = (a.iterations + a.iterations // 10) * AR_US * 1e-6
+    cnt = {k_: v_["count"] for k_, v_ in ser["by_collective"].items()}
+    big = sum(v_ for k_, v_ in cnt.items() if k_ in ("allgatherv", "reduce_scatterv"))
+    small = sum(v_ for k_, v_ in cnt.items() if k_.startswith("allreduce_") and not k_.endswith(f"[{(a.n + 255) // 256}]"))
+    ag_s = big * (a.world - 1) / a.world * a.n * 16 / (AG_GBS * 1e9)
+    ar_s = small * AR_US * 1e-6
     proj = span_s + ag_s + ar_s
     out.update({"serial_call_s": t_w, "multi_final_loss": lossw[max(lossw)], "serial": ser,
-                "span_s": span_s, "modelled_allgather_s": ag_s, "modelled_allreduce_s": ar_s,
+                "span_s": span_s, "collective_counts": cnt, "modelled_allgather_s": ag_s, "modelled_allreduce_s": ar_s,
                 "projected_loop_s": proj,
                 "model": f"all-gather {AG_GBS} GB/s effective per GPU, {AR_US} us per small all-reduce"})
     if "single_loop_s" in out:

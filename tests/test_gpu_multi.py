@@ -274,3 +274,41 @@ def test_rccl_world1_sharded_path_matches_callbacks(c):
     for t in ls:
         assert abs(lr[t] - ls[t]) <= TOL * abs(ls[t]), t
     assert close(Yr, Ys) and close(ur, us) and close(gr, gs)
+
+
+# ------------------------------------------------------ tree partition (bh_split)
+def _run_opts(P, Y0, prm, world, opts):
+    h = T.Context(0) if world == 1 else T.Context.multi([0] * world)
+    try:
+        for k_, v_ in opts.items():
+            h.set_option(k_, v_)
+        Y, u, g = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+        loss = h.optimize(*P, Y, u, g, prm)
+    finally:
+        h.close()
+    return Y, u, g, loss
+
+
+@pytest.mark.parametrize("world,opts", [(3, {"bh_split": 1, "root_tile": 0}), (4, {"bh_split": 1}),
+                                        (5, {"bh_split": 1, "root_tile": 0, "relabel": 0}), (2, {"bh_split": 0})])
+def test_tree_partition_matches_single(world, opts):
+    """Options::bh_split = 1: every rank walks every query over the cells
+    holding its own sorted points; shared cells straddle the cuts, their terms
+    taken by the owner of their first point, and a shared cell that tiles for
+    a lane is summed exactly as the sum of its parts over the ranks
+    (REF_FORCED).  root_tile = 0 runs the full tree from t = 1, where the
+    tiny embedding makes the root a near-exact tile for every query: the
+    forced path from the root down.  Exact duplicate groups included (the
+    reference's multiplicities).  Within the multi-rank tolerance of world 1."""
+    P, Y0 = problem(n=2000, seed=12)
+    Y0 = Y0.copy()
+    Y0[100:110] = Y0[7]          # a duplicate group of 11
+    Y0[1500:1503] = Y0[900]      # and one of 4
+    prm = default_params(iterations=60, theta=0.5, learning_rate=200.0)
+    base = {k_: v_ for k_, v_ in opts.items() if k_ != "bh_split"}
+    Ys, us, gs, ls = _run_opts(P, Y0, prm, 1, base)
+    Y, u, g, lm = _run_opts(P, Y0, prm, world, opts)
+    assert sorted(lm) == sorted(ls)
+    for t in ls:
+        assert abs(lm[t] - ls[t]) <= TOL * abs(ls[t]), (t, lm[t], ls[t])
+    assert close(Y, Ys) and close(u, us) and close(g, gs)

@@ -1478,8 +1478,10 @@ __global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict_
             const BHNode &nd = nodes[i];
             QRec v;
             v.cx = dv.vcom[2 * i]; v.cy = dv.vcom[2 * i + 1]; v.rball = 0.0;
-            v.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax);
+            v.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
             v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
+            v.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+            v.pad_ = 0.0;
             v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
             v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.ch[0] = nd.h; v.cref[0] = i; v.ccnt[0] = nd.cnt;
             v.ca[0] = nd.h * inv_theta * (1.0 + QACC_MARGIN);
@@ -1504,8 +1506,10 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     if (nd.h < 0.0) return;                 // transparent or key tie: no record
     // the traversal's all-open thresholds, precomputed (see QRec)
     r.cx = nd.cx; r.cy = nd.cy; r.rball = nd.rball * nd.rball * (1.0 - 1e-9);
-    r.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax);
+    r.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
     r.bx0 = nd.bx0; r.bx1 = nd.bx1; r.by0 = nd.by0; r.by1 = nd.by1;
+    r.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+    r.pad_ = 0.0;
     r.first = nd.first; r.last = nd.last; r.cnt = nd.cnt;
     // <= 3 transparent nodes per quad level: a 2-deep descent covers them
     int32_t cand[4] = {nd.left, nd.right, 0, 0};
@@ -1638,6 +1642,24 @@ struct NarrowView {
     int32_t nbn = 0;                   // workgroups of the narrow part of the grid (hmax x NPARTS / 4)
 };
 
+// Tree partition (several ranks, bh_repulsion with `plim`): rank r owns the
+// sorted positions [lo, hi) and walks every query over the cells that hold
+// points of its own.  The cuts sit on boundaries of level-PART_LEVEL cells
+// (part_align), so at most PART_LEVEL levels of records straddle a cut.  A
+// record inside [lo, hi) takes the normal path; a straddling ("shared") one
+// the slow path of bh_traverse<., true>: a child without points of mine is
+// skipped, an opened one pushed, and a child's term (summarised cell, leaf,
+// duplicate leaf or key-tie group) is taken only by the rank owning the
+// child's first point -- so over the ranks every term of the reference's sum
+// is taken exactly once.  A shared record that passes the all-open /
+// near-exact test for a lane is an exact leaf sum for it: its children are
+// pushed with REF_FORCED (lanes in exact-sum mode); a forced record of mine
+// becomes one tile task (the exact leaf sum over its range), a forced shared
+// one is expanded again.  The sum over the ranks of these parts is the
+// record's exact leaf sum, up to rounding and the moments' 1e-12 truncation.
+constexpr int32_t REF_FORCED = 1 << 30;
+constexpr int PART_LEVEL = 10;
+
 // The traversal kernels' state (LDS per 4-wave block): KB records per batch
 // (4 in the 64-query layout, NKP in the narrow one).
 template <int KB>
@@ -1659,7 +1681,7 @@ __device__ __forceinline__ void stage_records(LDS &L, int w, int lane, int sp, i
     if (lane < k) { L.bref[w][lane] = L.sref[w][sp + lane]; L.bmask[w][lane] = L.smask[w][sp + lane]; }
     for (int e = lane; e < QREC_V4 * k; e += 64) {
         const int rr = e / QREC_V4, part = e - rr * QREC_V4;
-        const int rf = L.sref[w][sp + rr];
+        const int rf = L.sref[w][sp + rr] & ~REF_FORCED;
         reinterpret_cast<uint4 *>(&L.srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
     }
     __builtin_amdgcn_wave_barrier();
@@ -1669,16 +1691,17 @@ __device__ __forceinline__ void stage_records(LDS &L, int w, int lane, int sp, i
 
 // All-open / near-exact test of one (query, record) pair (see the comment above
 // bh_traverse): the subtree's exact leaf sum replaces its walk.
+// (The record carries the box's part of the rounding margin and the bound
+// with its 1 + 1e-12 factor folded in: 5 fp64 operations fewer per lane.)
 __device__ __forceinline__ bool tile_test(const QRec &nd, double qx, double qy, double qmag) {
     const double cdx = qx - nd.cx, cdy = qy - nd.cy;
     const double dc = cdx * cdx + cdy * cdy;
     bool tile = dc <= nd.rball;   // rball^2 (1 - 1e-9)
     if (!tile) {
-        const double ex = 1e-15 * (qmag + fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+        const double ex = __fma_rn(1e-15, qmag, nd.ex);   // 1e-15 (|q| + |box|)
         const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
         const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-        const double dmax = (dxm * dxm + dym * dym) * (1.0 + 1e-12);
-        tile = dmax <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax)
+        tile = dxm * dxm + dym * dym <= nd.hmin;   // max(hmin / theta (1 - 1e-12), near_dmax) / (1 + 1e-12), rounded down
     }
     return tile;
 }
@@ -1691,11 +1714,11 @@ __device__ __forceinline__ uint64_t root_step(const double2 *__restrict__ pos, c
                                               const QRec *__restrict__ qrec, const int32_t *__restrict__ meta,
                                               int32_t virt, bool eval, double qx, double qy, double theta,
                                               double th_lo, double th_hi, double &fx, double &fy, double &zs,
-                                              unsigned long long &nvis, int32_t &rpush) {
+                                              unsigned long long &nvis, int32_t &rpush, bool own0 = true) {
     const int root = meta[1];
     rpush = root;
     if (root == ~0) {
-        if (eval) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
+        if (eval && own0) { if (STATS) ++nvis; const double2 p = pos[0]; leaf_force(qx, qy, p.x, p.y, fx, fy, zs); }
         return 0;
     }
     if (root < 0) return 0;
@@ -1703,7 +1726,7 @@ __device__ __forceinline__ uint64_t root_step(const double2 *__restrict__ pos, c
     if (rt.delta >= 62) {
         for (int p = rt.first; p <= rt.last; ++p) {
             const double2 pp = pos[p];
-            if (eval) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+            if (eval && own0) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
         }
         return 0;
     }
@@ -1722,7 +1745,7 @@ __device__ __forceinline__ uint64_t root_step(const double2 *__restrict__ pos, c
         if (STATS) ++nvis;
         const double dx = qx - rcx, dy = qy - rcy;
         const double D = __fma_rn(dx, dx, dy * dy);
-        if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) cell_force(dx, dy, D, rcnt, fx, fy, zs);
+        if (summarise(rh, D, dx, dy, th_lo, th_hi, theta)) { if (own0) cell_force(dx, dy, D, rcnt, fx, fy, zs); }
         else open = true;
     }
     return __ballot(open);
@@ -1942,15 +1965,17 @@ __global__ __launch_bounds__(256) void bh_traverse_narrow(
 // Traversal kernel (see the comment above), one 64-query group per wave;
 // groups the narrow waves take (nv.nflag) return at once.  MODE 0 plain; 1
 // wave run times into the multi-GPU cost buckets; 2 every counter (profiling).
-template <int MODE>
+template <int MODE, bool PART>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0,
     int64_t g1, const int32_t *__restrict__ qlist, int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
     unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost, int32_t *__restrict__ wcost,
-    int32_t *__restrict__ tcost, const int32_t *__restrict__ cost_lab, NarrowView nv) {
+    int32_t *__restrict__ tcost, const int32_t *__restrict__ cost_lab, NarrowView nv, int32_t *__restrict__ plim) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
+    // tree partition: this rank's sorted positions [plo, phi) (plim[2]: stack overflow flag)
+    const int32_t plo = PART ? plim[0] : 0, phi = PART ? plim[1] : INT32_MAX;
     __shared__ TravLDS L;
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
@@ -1979,7 +2004,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     {
         int32_t rpush;
         const uint64_t om = root_step<STATS>(pos, nodes, qrec, meta, virt, valid, qx, qy, theta, th_lo, th_hi, fx, fy,
-                                             zs, nvis, rpush);
+                                             zs, nvis, rpush, plo <= 0 && phi > 0);
         if (om) {
             if (lane == 0) { L.sref[w][0] = rpush; L.smask[w][0] = om; }
             sp = 1;
@@ -2003,13 +2028,113 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
             if (STATS) ++wpops;
             const int ref = __builtin_amdgcn_readfirstlane(bref_c[r]);
             const uint64_t msk = bmask_c[r];
-            bool act = (msk >> lane) & 1ull;
+            const uint64_t msk_s = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(msk >> 32)) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)msk);   // the wave's (scalar)
+            bool act = (msk_s >> lane) & 1ull;
             const QRec &nd = brec[r];
-            // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum
+            if (PART) {   // a shared or forced record: the tree partition's slow path (see REF_FORCED)
+                const int rf = __builtin_amdgcn_readfirstlane(nd.first), rl = __builtin_amdgcn_readfirstlane(nd.last);
+                const bool forced = (ref & REF_FORCED) != 0, mine_rec = rf >= plo && rl < phi;
+                if (forced || !mine_rec) {
+                    auto push = [&](int32_t pref, uint64_t pm) {
+                        if (sp >= STACK) {   // the cut alignment bounds the depth: never expected
+                            if (lane == 0) plim[2] = 1;
+                            return;
+                        }
+                        if (lane == 0) { L.sref[w][sp] = pref; L.smask[w][sp] = pm; }
+                        ++sp;
+                    };
+                    const int rref = ref & ~REF_FORCED;
+                    const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);
+                    bool fm = forced && act, an = !forced && act;
+                    if (forced && mine_rec && ntt < TILE_CAP) {   // exact sum over a subtree of mine: one tile
+                        const uint64_t tm = __ballot(fm);
+                        if (lane == 0) {
+                            TileTask tt; tt.ref = rref; tt.first = rf; tt.last = rl; tt.pad = nd.cnt; tt.mask = tm;
+                            mytt[ntt] = tt;
+                        }
+                        ++ntt;
+                        ntilepts += rl - rf + 1;
+                        if (STATS) wtile += (unsigned long long)(rl - rf + 1);
+                        if (fm) {
+                            if (STATS) nvis += (unsigned long long)(rl - rf + 1);
+                            if (s >= rf && s <= rl) zs -= (double)ndup;
+                        }
+                        continue;
+                    }
+                    if (!forced && (nflags & QNCH_TILE) && an && tile_test(nd, qx, qy, qmag)) { fm = true; an = false; }
+                    if (__ballot(an || fm) == 0) continue;
+                    const int nch = nflags & 0xff;
+                    for (int c = 0; c < nch; ++c) {
+                        const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
+                        const int32_t cref = __builtin_amdgcn_readfirstlane(nd.cref[c]);
+                        int32_t c0, c1;   // the child's sorted range
+                        if (kind == QK_LEAF) {
+                            c0 = c1 = ~cref;
+                        } else {
+                            const BHNode &cn = nodes[cref >= virt ? cref - virt : cref];
+                            c0 = __builtin_amdgcn_readfirstlane(cn.first);
+                            c1 = __builtin_amdgcn_readfirstlane(cn.last);
+                        }
+                        if (c1 < plo || c0 >= phi) continue;         // no point of mine below
+                        const bool own = c0 >= plo && c0 < phi;      // the term's owner: its first point's rank
+                        const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
+                        const double D = __fma_rn(dx, dx, dy * dy);
+                        if (kind == QK_LEAF || kind == QK_CELL) {
+                            bool take, acc = false;
+                            if (kind == QK_LEAF) {
+                                take = own && (an || fm) && !(dx == 0.0 && dy == 0.0);
+                            } else {
+                                if (an) {
+                                    const double A = nd.ca[c];
+                                    acc = D > A;
+                                    if (!acc && !(D < A * QACC_BAND))
+                                        acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                                }
+                                take = own && an && acc;
+                                const uint64_t om = __ballot(an && !acc), fmm = __ballot(fm);
+                                if (om) push(cref, om);
+                                if (fmm) push(cref | REF_FORCED, fmm);
+                            }
+                            if (STATS && (an || fm)) ++nvis;
+                            const double wm = take ? (kind == QK_LEAF ? 1.0 : (double)nd.ccnt[c]) : 0.0;
+                            const double Q = recip_bh(1.0 + D);
+                            const double mult = wm * Q;
+                            const double sc = mult * Q;
+                            fx = __fma_rn(sc, dx, fx);
+                            fy = __fma_rn(sc, dy, fy);
+                            zs += mult;
+                        } else if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
+                            if (own && (an || fm) && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
+                                if (STATS) ++nvis;
+                                cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                            }
+                        } else if (own) {                // a key-tie group: every point directly
+                            for (int p = c0; p <= c1; ++p) {
+                                const double2 pp = pos[p];
+                                if (an || fm) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
+                            }
+                        }
+                    }
+                    continue;
+                }
+            }
+            // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum;
+            // both tests on every lane, their masks straight from the compares
+            // (tile_test's branch and a ballot of the combined bool cost more)
             bool tile = false;
+            uint64_t tm = 0;
+            uint64_t amask = msk_s;   // lanes that go on to the children
             const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
-            if ((nflags & QNCH_TILE) && act) tile = tile_test(nd, qx, qy, qmag);
-            const uint64_t tm = __ballot(tile);
+            if (nflags & QNCH_TILE) {
+                const double cdx = qx - nd.cx, cdy = qy - nd.cy;
+                const double ex = __fma_rn(1e-15, qmag, nd.ex);
+                const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
+                const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
+                const bool t1 = cdx * cdx + cdy * cdy <= nd.rball, t2 = dxm * dxm + dym * dym <= nd.hmin;
+                tm = msk_s & (__builtin_amdgcn_ballot_w64(t1) | __builtin_amdgcn_ballot_w64(t2));
+                tile = act && (t1 || t2);
+            }
             if (tm && ntt < TILE_CAP) {
                 // The wave records (subtree, lanes) for tile_apply, or, when its
                 // list is full, the lanes keep traversing (the reference's path).
@@ -2029,8 +2154,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                     if (s >= a && s <= b) zs -= (double)ndup;
                 }
                 act = act && !tile;
+                amask = msk_s & ~tm;
             }
-            if (__ballot(act) == 0) continue;
+            if (amask == 0) continue;
             // the opened cell's quad children, from its record
             const int nch = nflags & 0xff;
             if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
@@ -2055,16 +2181,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                         take = act && !(dx == 0.0 && dy == 0.0);
                         wm = take ? 1.0 : 0.0;
                     } else {
+                        // the masks straight from the compares (scalar: a
+                        // ballot of a combined bool costs two VALU per child)
                         const double A = nd.ca[c];
                         bool acc = D > A;
-                        if (act && !acc && !(D < A * QACC_BAND))
-                            acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                        uint64_t accm = __builtin_amdgcn_ballot_w64(D > A);
+                        const uint64_t band = amask & ~accm & ~__builtin_amdgcn_ballot_w64(D < A * QACC_BAND);
+                        if (band) {   // rare: inside the band the exact IEEE quotient decides
+                            const bool inb = (band >> lane) & 1ull;
+                            if (inb) acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                            accm |= __ballot(inb && acc);
+                        }
                         take = act && acc;
                         wm = (double)(take ? nd.ccnt[c] : 0);
-                        const uint64_t om = __ballot(act && !acc);
+                        const uint64_t om = amask & ~accm;
                         if (om) {
-                            if (lane == 0) { L.sref[w][sp] = nd.cref[c]; L.smask[w][sp] = om; }
-                            ++sp;
+                            if (PART && sp >= STACK) {
+                                if (lane == 0) plim[2] = 1;
+                            } else {
+                                if (lane == 0) { L.sref[w][sp] = nd.cref[c]; L.smask[w][sp] = om; }
+                                ++sp;
+                            }
                         }
                     }
                     const double Q = recip_bh(1.0 + D);
@@ -2998,6 +3135,75 @@ void bh_balance(tsne_ctx *ctx, const unsigned long long *bcost, int64_t n, int w
     TSNE_LAUNCH_CHECK();
 }
 
+// ---- tree partition (several ranks; see REF_FORCED)
+// One wave: cut r (1 <= r < world) moved forward to the first sorted position p
+// with p == m or a level-PART_LEVEL cell boundary between keys p - 1 and p.
+__global__ void part_align_kernel(const uint64_t *__restrict__ keys, const int32_t *__restrict__ meta,
+                                  const int64_t *__restrict__ cuts, int world, int rank, int32_t *__restrict__ plim) {
+    const int lane = lane_id();
+    const int64_t m = meta[0];
+    constexpr int SH = 62 - 2 * PART_LEVEL;
+    auto align = [&](int r) -> int64_t {
+        if (r <= 0) return 0;
+        if (r >= world) return INT32_MAX;
+        int64_t c = min(max(cuts[r], (int64_t)0), m);
+        if (c <= 0 || c >= m) return c;
+        for (int64_t b = c; b < m; b += 64) {
+            const int64_t p = b + lane;
+            const bool hit = p >= m || (keys[p - 1] >> SH) != (keys[p] >> SH);
+            const uint64_t bl = __ballot(hit);
+            if (bl) return b + __ffsll((long long)bl) - 1;
+        }
+        return m;
+    };
+    const int64_t lo = align(rank), hi = align(rank + 1);
+    if (lane == 0) {
+        plim[0] = (int32_t)lo;
+        plim[1] = (int32_t)max(lo, hi);
+    }
+}
+
+// One thread: equal-cost cuts of the cumulative cost, linear inside each
+// rank's current range, moved half way from the current cuts.
+__global__ void part_recut_kernel(const unsigned long long *__restrict__ cost, int world, int64_t n,
+                                  int64_t *__restrict__ cuts) {
+    if (threadIdx.x != 0) return;
+    double total = 0.0;
+    for (int r = 0; r < world; ++r) total += (double)cost[r];
+    if (!(total > 0.0)) return;
+    double nc[64];
+    int r = 0;
+    double cum = 0.0;
+    for (int k = 1; k < world && k < 64; ++k) {
+        const double T = total * k / world;
+        while (r < world - 1 && cum + (double)cost[r] <= T) cum += (double)cost[r++];
+        const double x0 = (double)cuts[r], x1 = (double)(r + 1 < world ? cuts[r + 1] : n);
+        const double f = cost[r] > 0 ? (T - cum) / (double)cost[r] : 0.5;
+        nc[k] = x0 + f * (x1 - x0);
+    }
+    for (int k = 1; k < world && k < 64; ++k) {
+        int64_t v = (int64_t)(0.5 * ((double)cuts[k] + nc[k]));
+        v = max(v, cuts[k - 1]);
+        cuts[k] = min(v, n);
+    }
+}
+
+// Sum of the traversal waves' costs (pops + tile points / 64).
+__global__ __launch_bounds__(1024) void part_cost_kernel(const int32_t *__restrict__ wcost, int64_t waves,
+                                                         unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long red[16];
+    unsigned long long a = 0;
+    for (int64_t i = threadIdx.x; i < waves; i += 1024) a += (unsigned long long)max(wcost[i], 0);
+    a = wave_sum(a);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int k = 0; k < 16; ++k) t += red[k];
+        *out = t;
+    }
+}
+
 // The near-exact tolerance of a build (Options::near_tol_early / near_tol_late;
 // 0 disables the test)
 double bh_near_tol(const tsne_ctx *ctx, bool late) { return late ? ctx->opts.near_tol_late : ctx->opts.near_tol_early; }
@@ -3125,7 +3331,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
 
 void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist,
-                  unsigned long long *bcost, bool cost_by_label) {
+                  unsigned long long *bcost, bool cost_by_label, int32_t *plim) {
     if (s1 <= s0) return;
     hipStream_t st = ctx->stream;
     const double mom_tol = ctx->opts.mom_tol;
@@ -3142,7 +3348,8 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the waves' run times
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    auto kern = mode == 2 ? bh_traverse<2> : mode == 1 ? bh_traverse<1> : bh_traverse<0>;
+    auto kern = plim ? (mode == 2 ? bh_traverse<2, true> : mode == 1 ? bh_traverse<1, true> : bh_traverse<0, true>)
+                     : (mode == 2 ? bh_traverse<2, false> : mode == 1 ? bh_traverse<1, false> : bh_traverse<0, false>);
     const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     // heavy groups: selected after the previous traversal of the same query
@@ -3151,7 +3358,8 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // none on a tree's first traversal or with Options::narrow = 0
     NarrowView nv;
     const double nfac = ctx->opts.narrow;
-    const bool narrow = nfac > 0.0 && t.sel_waves == waves;
+    // (not with a tree partition: every rank walks all queries, the 64-query grid fills the chip)
+    const bool narrow = nfac > 0.0 && t.sel_waves == waves && !plim;
     if (narrow) {
         nv.hlist = t.hlist; nv.hcount = t.hcount; nv.ncost = t.ncost; nv.mtask = t.nmtask; nv.mtask_n = t.nmtask_n;
         nv.nflag = t.nflag;
@@ -3170,7 +3378,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
                        t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
-                       t.tcost, clab, nv);
+                       t.tcost, clab, nv, plim);
     if (narrow) TSNE_HIP(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
     // tile chunks of heavy waves (ChunkView): the single-workgroup plan while
     // the per-wave costs fit its LDS, else the multi-launch plan and block sort
@@ -3205,7 +3413,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         TSNE_HIP(hipMemcpyAsync(t.hran, t.hcount, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     }
     // the next traversal's heavy groups (of the same query count) from this one's costs
-    if (nfac > 0.0) {
+    if (nfac > 0.0 && !plim) {
         if (!narrow) TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * waves, st));   // no stale slots
         hipLaunchKernelGGL(narrow_select, dim3(1), dim3(1024), 0, st, t.wcost, waves, t.nflag, t.ncost, t.hlist,
                            t.hcount, t.nar_hmax, nfac, std::min<int64_t>(t.nar_hmax, narrow_fill(ctx, waves)));
@@ -3213,6 +3421,24 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     } else {
         t.sel_waves = 0;
     }
+    TSNE_LAUNCH_CHECK();
+}
+
+void part_align(tsne_ctx *ctx, BHTree &t, const int64_t *cuts, int world, int rank, int32_t *plim) {
+    TSNE_REQUIRE(world <= 64, "tree partition: at most 64 ranks");
+    TSNE_REQUIRE(2 * t.n < (int64_t)REF_FORCED, "tree partition: too many points for the record flags");
+    hipLaunchKernelGGL(part_align_kernel, dim3(1), dim3(64), 0, ctx->stream, t.keys_sorted, t.meta, cuts, world, rank,
+                       plim);
+    TSNE_LAUNCH_CHECK();
+}
+
+void part_recut(tsne_ctx *ctx, const unsigned long long *cost, int world, int64_t n, int64_t *cuts) {
+    hipLaunchKernelGGL(part_recut_kernel, dim3(1), dim3(64), 0, ctx->stream, cost, world, n, cuts);
+    TSNE_LAUNCH_CHECK();
+}
+
+void part_cost(tsne_ctx *ctx, BHTree &t, int64_t waves, unsigned long long *out) {
+    hipLaunchKernelGGL(part_cost_kernel, dim3(1), dim3(1024), 0, ctx->stream, t.wcost, waves, out);
     TSNE_LAUNCH_CHECK();
 }
 

@@ -49,13 +49,15 @@ constexpr int QK_CELL = 0, QK_LEAF = 1, QK_TIE = 2, QK_MULTI = 3;
 struct __attribute__((aligned(16))) QRec {
     double cx, cy;              // centre of mass
     double rball, hmin;         // all-open tests, precomputed (build_qrec): rball^2 (1 - 1e-9) and
-                                // max(hmin / theta (1 - 1e-12), near_dmax) (see bottom_up)
+                                // max(hmin / theta (1 - 1e-12), near_dmax) (1 - 1.1e-12) (see bottom_up)
     double bx0, bx1, by0, by1;  // bounding box of the subtree's points
     int32_t first, last;        // leaf range in sorted order
     int32_t cnt, nch;           // cumSize, number of quad children | QNCH_TILE
     double ccx[4], ccy[4], ch[4];
     double ca[4];               // cells: the sure-accept bound on D, ch / theta (1 + 2.5e-14) (see QACC_BAND)
     int32_t cref[4], ccnt[4];
+    double ex;                  // the box test's rounding margin, record part: 1e-15 (|bx0| + |bx1| + |by0| + |by1|)
+    double pad_;
 };
 // A cell child is summarised for sure when D > ca, opened for sure when
 // D < ca * QACC_BAND (= ch / theta (1 - 2.5e-14)); in between, the exact
@@ -185,9 +187,24 @@ double bh_near_tol(const tsne_ctx *ctx, bool late);
 // position; visits (nullable) += node evaluations; bcost (nullable)
 // accumulates each wave's cost into the 256-position bucket of its first query
 // (cost_by_label: an equal share into each query's 256-label bucket).
+// plim (device, nullable): the tree partition -- plim[0..1] = this rank's
+// sorted positions [lo, hi) (part_cuts), plim[2] a stack-overflow flag; every
+// query then gets this rank's PART of its sums (the cells holding its points,
+// see bhtree.hip REF_FORCED), to be added over the ranks.
 void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1,
                   double2 *dF, double *dz, unsigned long long *visits, const int32_t *qlist = nullptr,
-                  unsigned long long *bcost = nullptr, bool cost_by_label = false);
+                  unsigned long long *bcost = nullptr, bool cost_by_label = false, int32_t *plim = nullptr);
+// Tree partition cuts: cuts[0..world] (device int64, sorted positions of the
+// previous build, refined by part_recut) -> this rank's [lo, hi) in plim,
+// each cut moved forward to the next boundary of level-10 cells of this
+// build's sorted keys (so no record below level 10 straddles a cut), within [0, m].
+void part_align(tsne_ctx *ctx, BHTree &t, const int64_t *cuts, int world, int rank, int32_t *plim);
+// New cuts from the ranks' traversal costs (cost[r], all-reduced): the
+// cumulative cost, linear inside each rank's current range, cut at equal
+// shares (moved half way: damped); identical on every rank.
+void part_recut(tsne_ctx *ctx, const unsigned long long *cost, int world, int64_t n, int64_t *cuts);
+// This traversal's cost (sum over its waves of pops + tile points / 64) into *out.
+void part_cost(tsne_ctx *ctx, BHTree &t, int64_t waves, unsigned long long *out);
 // Heavy groups the last traversal on t ran narrow (synchronises the stream).
 int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).

@@ -38,6 +38,12 @@ struct Comm {
     virtual void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) = 0;
     // in place: rank r's bytes [off[r], off[r+1]) of buf are copied to every rank
     virtual void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) = 0;
+    // in place: on rank r, elements [off[r], off[r+1]) of buf become their sum
+    // over the ranks (the rest of buf is unspecified afterwards).  Default: an
+    // all-reduce of the whole buffer (the caller-callback transport).
+    virtual void reduce_scatterv_f64(tsne_ctx *ctx, double *buf, const int64_t *off) {
+        allreduce_f64(ctx, buf, (size_t)off[ctx->world]);
+    }
     // a rank failed: make every pending and later collective of this rank
     // fail (TSNE_ERR_COMM) instead of waiting for it; callable from another thread
     virtual void abort() {}
@@ -115,6 +121,19 @@ struct RcclComm : Comm {
     }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override {
         run("ncclAllReduce", [&](ncclComm_t c) { return ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, c, ctx->stream); });
+    }
+    // ragged reduce-scatter: one in-place reduce per root, fused into one group
+    void reduce_scatterv_f64(tsne_ctx *ctx, double *buf, const int64_t *off) override {
+        run("ncclReduce group", [&](ncclComm_t c) {
+            ncclResult_t r = ncclGroupStart();
+            for (int q = 0; q < ctx->world && r == ncclSuccess; ++q) {
+                const size_t cnt = (size_t)(off[q + 1] - off[q]);
+                if (cnt == 0) continue;
+                r = ncclReduce(buf + off[q], buf + off[q], cnt, ncclFloat64, ncclSum, q, c, ctx->stream);
+            }
+            const ncclResult_t e = ncclGroupEnd();
+            return r != ncclSuccess ? r : e;
+        });
     }
     // ragged all-gather: one in-place broadcast per root, fused into one group
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
@@ -291,6 +310,20 @@ struct LoopComm : Comm {
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override { allreduce(ctx, buf, count); }
     void allreduce_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count) override { allreduce(ctx, buf, count); }
+    // this rank's slice summed over the ranks in fixed rank order
+    void reduce_scatterv_f64(tsne_ctx *ctx, double *buf, const int64_t *off) override {
+        publish(ctx, buf, "reduce_scatterv");
+        const int64_t a = off[ctx->rank], cnt = off[ctx->rank + 1] - a;
+        std::vector<double> acc(cnt, 0.0), tmp(cnt);
+        for (int r = 0; r < g->world && cnt > 0; ++r) {
+            TSNE_HIP(hipMemcpy(tmp.data(), static_cast<const double *>(g->ptr[r]) + a, sizeof(double) * cnt,
+                               hipMemcpyDeviceToHost));
+            for (int64_t e = 0; e < cnt; ++e) acc[e] += tmp[e];
+        }
+        g->barrier();   // every rank has read its slice of every buffer before any is overwritten
+        if (cnt > 0) TSNE_HIP(hipMemcpy(buf + a, acc.data(), sizeof(double) * cnt, hipMemcpyHostToDevice));
+        g->seg_begin(ctx);
+    }
     void abort() override { g->abort(); }
     void release(tsne_ctx *ctx) override { g->seg_release(ctx); }
     void mark(tsne_ctx *ctx, const char *what) override { g->seg_mark(ctx, what); }
@@ -466,6 +499,12 @@ void comm_allreduce_sum_u64(tsne_ctx *ctx, unsigned long long *buf, size_t count
     TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
     ++ctx->comm->calls;
     ctx->comm->allreduce_u64(ctx, buf, count);
+}
+
+void comm_reduce_scatterv_f64(tsne_ctx *ctx, double *buf, const int64_t *off_elems) {
+    TSNE_REQUIRE(ctx->comm != nullptr, "communicator not initialised");
+    ++ctx->comm->calls;
+    ctx->comm->reduce_scatterv_f64(ctx, buf, off_elems);
 }
 
 void comm_allreduce_sum_f64(tsne_ctx *ctx, double *buf, size_t count) {

@@ -180,6 +180,9 @@ struct Options {
     int recut = 0;            // several ranks on the tiled layout: re-cut by BH cost instead of relabels
     int knn_bf16 = 1;         // kNN threshold filter: bf16x3 MFMA (0: f32-input MFMA)
     double narrow = 3.0;      // BH: 64-query groups costing >= narrow x the mean run in the narrow layout (0: off)
+    int bh_split = 0;         // several ranks: 1 = partition the BH tree by sorted-position ranges (every rank walks
+                              // every query over its own cells; F summed by a reduce-scatter) instead of the queries
+                              // (0; measured faster at 8 projected ranks)
     int comm_world1 = 0;      // tsne_ctx_init_comm / _callbacks at world 1 still create the communicator, and
                               // the optimizer runs its sharded code path through it (tests the transport)
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
@@ -273,6 +276,8 @@ void comm_init(tsne_ctx *ctx, int rank, int world, const uint8_t *id);
 void comm_destroy(tsne_ctx *ctx);
 void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback);
 void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops *ops, void *user);
+// in place: on rank r, doubles [off[r], off[r+1]) of buf become their sum over the ranks
+void comm_reduce_scatterv_f64(tsne_ctx *ctx, double *buf, const int64_t *off_elems);
 // the context's communicator: kind (0 none, 1 RCCL, 2 loopback, 3 callbacks) or collectives issued
 int64_t comm_counter(const tsne_ctx *ctx, bool calls);
 void comm_abort(tsne_ctx *ctx);

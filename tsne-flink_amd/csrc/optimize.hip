@@ -127,6 +127,14 @@ struct OptState {
     double *at_pv = nullptr;
     double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits[10] = {};
+    // tree partition (Options::bh_split, several ranks, 2-D): cuts of the sorted
+    // points (world + 1), this rank's aligned [lo, hi) + overflow flag, the
+    // ranks' traversal costs (all-reduced), F in label order (reduce-scatter)
+    int64_t *pcuts = nullptr;
+    int32_t *plim = nullptr;
+    unsigned long long *pcost = nullptr;
+    double2 *Fl = nullptr;
+    bool split_last = false;   // the last iteration used the tree partition
 };
 
 // The sharded code path (query lists, collectives, centring from the gathered
@@ -683,7 +691,7 @@ __global__ __launch_bounds__(256) void combine_update(
     if (live) {
         const double Z = scal[0];
         const double2 at = attr[i - r0];
-        const double2 f = F[inv[i]];
+        const double2 f = F[inv ? inv[i] : i];   // sorted order, or already by label (inv = nullptr)
         const double gx = at.x - f.x / Z, gy = at.y - f.y / Z;  // attrForce - repForce / sumQ
         if (MODE == 0) {
             grad[2 * i] = gx;
@@ -865,6 +873,14 @@ __global__ void qlist_fill(const int32_t *__restrict__ idx_sorted, int64_t n, in
     int base = boff[blockIdx.x];
     for (int k = 0; k < w; ++k) base += wc[k];
     if (f) qlist[base + __popcll(bal & lanemask_lt())] = (int32_t)s;
+}
+
+// F in label order: Fl[l] = F[inv[l]] (the tree partition's reduce-scatter
+// buffer: each rank's partial sums of every point, summed at the row owners)
+__global__ void f_to_label(const int32_t *__restrict__ inv, int64_t n, const double2 *__restrict__ F,
+                           double2 *__restrict__ Fl) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l < n) Fl[l] = F[inv[l]];
 }
 
 // Z partial of a rank: sum of z over its query list (fixed order per block)
@@ -1666,6 +1682,17 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->visits = ws.get<unsigned long long>("opt.visits", 32);
     if (sharded(ctx)) {
         const int64_t nb = ceil_div(n, 256);
+        if (C == 2) {
+            s->pcuts = ws.get<int64_t>("opt.pcuts", world + 1);
+            s->plim = ws.get<int32_t>("opt.plim", 4);
+            s->pcost = ws.get<unsigned long long>("opt.pcost", world);
+            s->Fl = ws.get<double2>("opt.Fl", n);
+            std::vector<int64_t> c0(world + 1);
+            for (int r = 0; r <= world; ++r) c0[r] = n * r / world;
+            TSNE_HIP(hipMemcpyAsync(s->pcuts, c0.data(), sizeof(int64_t) * (world + 1), hipMemcpyHostToDevice, st));
+            TSNE_HIP(hipMemsetAsync(s->plim, 0, 4 * sizeof(int32_t), st));
+            TSNE_HIP(hipStreamSynchronize(st));
+        }
         s->qlist = ws.get<int32_t>("opt.qlist", n);
         s->qcnt = ws.get<int32_t>("opt.qcnt", nb);
         s->qoff = ws.get<int32_t>("opt.qoff", nb);
@@ -1710,9 +1737,9 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
 
 // Z = sum of z over all queries: locally (one rank) or this rank's partial
 // over its query list + an all-reduce of one double
-static void reduce_Z(tsne_ctx *ctx, OptState *s, const double *z) {
+static void reduce_Z(tsne_ctx *ctx, OptState *s, const double *z, bool all_points = false) {
     hipStream_t st = ctx->stream;
-    if (!sharded(ctx)) {
+    if (!sharded(ctx) || all_points) {   // every point (a tree partition: this rank's partial sums)
         hipLaunchKernelGGL(reduce_partial, dim3(NPART), dim3(256), 0, st, z, s->n, 1, 0, s->part2);
     } else {
         hipLaunchKernelGGL(reduce_list_partial, dim3(NPART), dim3(256), 0, st, z, s->qlist, s->L1 - s->L0, s->part2);
@@ -1863,7 +1890,13 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
 // (an equal share of its wave's time); the all-reduced buckets give cuts of
 // equal cost, applied (owned rows and their tiles rebuilt) when a cut moves
 // by more than 1/16 of a rank's share.
+// The tree partition (Options::bh_split): several ranks, 2-D.
+static bool split_mode(const tsne_ctx *ctx, const OptState *s) {
+    return sharded(ctx) && ctx->opts.bh_split && s->C == 2 && s->pcuts != nullptr;
+}
+
 static bool recut_mode(tsne_ctx *ctx, OptState *s) {
+    if (split_mode(ctx, s)) return false;   // BH cost does not follow the row ownership there
     return ctx->opts.recut && ctx->opts.relabel == -1 && sharded(ctx) && s->at_on && !s->morton_labels;
 }
 static void recut(tsne_ctx *ctx, OptState *s, const std::vector<int64_t> &cuts) {
@@ -1927,7 +1960,7 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
     const bool go = mode == 2 || sc[1] > sc[0];
     if (!go) return;
     std::vector<int64_t> cuts = s->own;
-    if (sharded(ctx)) {
+    if (sharded(ctx) && !split_mode(ctx, s)) {   // (tree partition: the rows keep equal label cuts)
         comm_allreduce_sum_u64(ctx, s->bcost, (size_t)ceil_div(n, 256));
         bh_balance(ctx, s->bcost, n, ctx->world, s->bounds);
         TSNE_HIP(hipMemcpyAsync(cuts.data(), s->bounds, sizeof(int64_t) * (ctx->world + 1), hipMemcpyDeviceToHost, st));
@@ -2038,9 +2071,18 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
     // bucket costs only where a relabel may re-cut the ownership
-    unsigned long long *bcost = (sharded(ctx) && check_relabel) ? s->bcost : nullptr;
+    // tree partition: every query over this rank's cells (sorted-position
+    // range, re-cut by the ranks' traversal costs every iteration)
+    const bool split = split_mode(ctx, s) && !s->tree.root_tile;
+    s->split_last = split;
+    unsigned long long *bcost = (sharded(ctx) && check_relabel && !split_mode(ctx, s)) ? s->bcost : nullptr;
     if (bcost) TSNE_HIP(hipMemsetAsync(bcost, 0, sizeof(unsigned long long) * ceil_div(n, 256), st));
-    if (sharded(ctx)) {
+    if (split) {
+        part_align(ctx, s->tree, s->pcuts, ctx->world, ctx->rank, s->plim);
+        bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr, nullptr, nullptr, false,
+                     s->plim);
+        comm_mark(ctx, "bh");
+    } else if (sharded(ctx)) {
         build_qlist(ctx, s, s->tree.idx_sorted);
         bh_repulsion(ctx, s->tree, p.theta, 0, s->L1 - s->L0, s->F, s->z, s->profile ? s->visits : nullptr, s->qlist,
                      bcost, recut_mode(ctx, s));
@@ -2050,7 +2092,24 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
-    reduce_Z(ctx, s, s->z);
+    reduce_Z(ctx, s, s->z, split);
+    const double2 *Fc = s->F;           // combine_update's forces: sorted order (inv) ...
+    const int32_t *Finv = s->tree.inv;
+    if (split) {
+        // the next iteration's cuts from this traversal's costs (identical on every rank)
+        TSNE_HIP(hipMemsetAsync(s->pcost, 0, sizeof(unsigned long long) * ctx->world, st));
+        part_cost(ctx, s->tree, ceil_div(n, 64), s->pcost + ctx->rank);
+        comm_allreduce_sum_u64(ctx, s->pcost, (size_t)ctx->world);
+        part_recut(ctx, s->pcost, ctx->world, n, s->pcuts);
+        // ... or, with the tree partition, by label after the reduce-scatter of
+        // every rank's partial sums to the row owners
+        hipLaunchKernelGGL(f_to_label, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->tree.inv, n, s->F, s->Fl);
+        std::vector<int64_t> off(ctx->world + 1);
+        for (int r = 0; r <= ctx->world; ++r) off[r] = 2 * s->own[r];
+        comm_reduce_scatterv_f64(ctx, reinterpret_cast<double *>(s->Fl), off.data());
+        Fc = s->Fl;
+        Finv = nullptr;
+    }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 4. the attraction's sums + update for owned rows
     TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
@@ -2060,7 +2119,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     ctx->timers.begin("opt.update", st);
     const bool fused_mean = !sharded(ctx);
     const int c = s->cur;
-    combine_launch<1>(st, s->L0, s->L1, s->attr, s->tree.inv, s->F, s->scal, Y, nullptr, s->Ynew, s->upd[c],
+    combine_launch<1>(st, s->L0, s->L1, s->attr, Finv, Fc, s->scal, Y, nullptr, s->Ynew, s->upd[c],
                       s->gains[c], p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
     if (want_loss) record_loss(ctx, s, t, blocks, true, ex);
     // 5. exchange (all-gather of the owned slices) + 6. centre
@@ -2082,10 +2141,21 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     if (s->profile) finish_profile(ctx, s, t);
 }
 
+// The tree partition's traversal stack guard (bh_traverse<., true>): never
+// expected to trip (the cut alignment bounds the shared depth); loud if it did.
+static void check_split_overflow(tsne_ctx *ctx, const OptState *s) {
+    if (!s->plim) return;
+    int32_t f = 0;
+    TSNE_HIP(hipMemcpyAsync(&f, s->plim + 2, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    if (f) fail(TSNE_ERR_HIP, "tree-partition traversal stack overflow (results invalid)");
+}
+
 // Write upd / gains (and Y) back to the caller's buffers in the original order.
 void opt_sync(tsne_ctx *ctx) {
     OptState *s = ctx->opt;
     TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    check_split_overflow(ctx, s);
     hipStream_t st = ctx->stream;
     gather_working_set(ctx, s);
     const int c = s->cur;
@@ -2102,6 +2172,7 @@ void opt_sync(tsne_ctx *ctx) {
 int32_t opt_losses(tsne_ctx *ctx, int32_t *keys, double *vals, int32_t cap) {
     OptState *s = ctx->opt;
     TSNE_REQUIRE(s != nullptr, "tsne_dev_opt_setup has not been called");
+    check_split_overflow(ctx, s);
     std::vector<double> h(s->loss_slots);
     TSNE_HIP(hipMemcpyAsync(h.data(), s->loss, sizeof(double) * s->loss_slots, hipMemcpyDeviceToHost, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
