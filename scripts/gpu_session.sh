@@ -49,8 +49,9 @@ if has bench; then
     # "-": defaults; "lib=PATH": another build of the library (TSNE_HIP_LIB); else KEY=VALUE options
     opt=""; lib=""
     case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option $v" ;; esac
+    bi=$((${bi:-0}+1))
     echo "# $v" >> $O/bench.jsonl
-    TSNE_HIP_LIB="$lib" run 400 python bench.py --no-cpu-baseline $opt >> $O/bench.jsonl 2>> $O/bench.err || exit $?
+    TSNE_HIP_LIB="$lib" run 400 python bench.py --no-cpu-baseline $opt --detail-out $O/bench_detail_$bi.json >> $O/bench.jsonl 2>> $O/bench.err || exit $?
   done
 fi
 if has tests3d; then

@@ -131,6 +131,7 @@ static const OptionField k_options[] = {
     {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
     {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
     {"bh_split", nullptr, &Options::bh_split, 0, 1},
+    {"attract_after", &Options::attract_after, nullptr, 0.0, 1e9},
 };
 static const OptionField &option_field(const char *key) {
     for (const OptionField &f : k_options)

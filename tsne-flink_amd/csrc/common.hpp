@@ -183,6 +183,8 @@ struct Options {
     int bh_split = 0;         // several ranks: 1 = partition the BH tree by sorted-position ranges (every rank walks
                               // every query over its own cells; F summed by a reduce-scatter) instead of the queries
                               // (0; measured faster at 8 projected ranks)
+    double attract_after = 0.0;   // 2-D optimizer: run the attraction after the BH kernels (not beside them) while
+                                  // the previous traversal's mean wave cost (pops + tile points / 64) is below this
     int comm_world1 = 0;      // tsne_ctx_init_comm / _callbacks at world 1 still create the communicator, and
                               // the optimizer runs its sharded code path through it (tests the transport)
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
