@@ -156,6 +156,16 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             points, each term taken by one rank, and the
  *                             forces are summed by a reduce-scatter to the row
  *                             owners (0: partition the queries, Z-only exchange);
+ *   "bu_acqrel" 0             1: the tree build's cross-workgroup bottom-up
+ *                             hand-off uses agent-scope acquire-release
+ *                             arrivals (the HIP memory model's ordering) instead
+ *                             of relaxed arrivals ordered by gfx950's in-order
+ *                             issue (the same trees; DESIGN.md 6 has the cost);
+ *   "loop_serial" 0           1 (a loopback tsne_ctx_create_multi group, set
+ *                             before tsne_optimize): the ranks take turns on the
+ *                             device and log their work between collectives --
+ *                             a one-GPU projection of N GPUs, read with
+ *                             tsne_ctx_loop_profile;
  *   "comm_world1" 0           1: tsne_ctx_init_comm / tsne_ctx_init_comm_callbacks
  *                             at world 1 still create the communicator (RCCL:
  *                             a one-rank ncclCommInitRankConfig, id may be
@@ -173,6 +183,11 @@ int tsne_ctx_set_option(tsne_ctx *ctx, const char *key, double value);
  * bindings refuse a different major version.  No device needed. */
 int tsne_hip_versions(int32_t *built_out, int32_t *runtime_out);
 int tsne_ctx_get_option(tsne_ctx *ctx, const char *key, double *value_out);
+/* The loopback group's "loop_serial" summary (JSON: the span of the ranks'
+ * work between collectives, per collective and per 100 occurrences) of the
+ * segments logged since the last read; *len_out = its length (buf may be NULL
+ * to ask), at most cap - 1 bytes + NUL written.  Empty for other handles. */
+int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_out);
 /* Diagnostic counters of the last call (synchronises the context's stream):
  *   "bh.narrow_groups"   64-query groups the last single-call BH traversal
  *                        (tsne_gradient / tsne_repulsion) ran in the narrow layout;

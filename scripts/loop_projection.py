@@ -1,6 +1,7 @@
 """Multi-GPU projection on ONE GPU: the library's own world > 1 optimizer run
-as W loopback ranks that take turns on the device (TSNE_LOOP_SERIAL, comm.cpp
-LoopGroup), against the world = 1 run of the same problem.
+as W loopback ranks that take turns on the device (option loop_serial,
+comm.cpp LoopGroup, read with tsne_ctx_loop_profile), against the world = 1
+run of the same problem.
 
 Each rank logs the wall time of every stretch of its own work between two
 collectives, alone on the device.  The sum over collectives of the slowest
@@ -14,9 +15,7 @@ Output: one JSON line.
 """
 import argparse
 import json
-import os
 import sys
-import tempfile
 import time
 from pathlib import Path
 
@@ -93,17 +92,15 @@ def main():
             t_full, loss1 = run(one, P, Y0, a.iterations)
         out.update({"single_call_s": t_full, "single_setup_s": t_setup, "single_loop_s": t_full - t_setup,
                     "single_final_loss": loss1[max(loss1)]})
-    path = os.path.join(tempfile.mkdtemp(), "serial.json")
-    os.environ["TSNE_LOOP_SERIAL"] = path
     m = T.Context.multi([0] * a.world)
     for k_, v_ in opts.items():
         m.set_option(k_, v_)
+    m.set_option("loop_serial", 1)
     try:
         t_w, lossw = run(m, P, Y0, a.iterations)
+        ser = m.loop_profile()
     finally:
         m.close()
-    with open(path) as fh:
-        ser = json.load(fh)
     span_s = ser["span_ms"] * 1e-3
     cnt = {k_: v_["count"] for k_, v_ in ser["by_collective"].items()}
     big = sum(v_ for k_, v_ in cnt.items() if k_ in ("allgatherv", "reduce_scatterv"))

@@ -93,27 +93,28 @@ def test_multi_optimize_loopback_matches_single(world):
     assert close(Y, Ys) and close(u, us) and close(g, gs)
 
 
-def test_multi_optimize_loopback_serial_timing(tmp_path, monkeypatch):
-    """TSNE_LOOP_SERIAL (comm.cpp LoopGroup): the ranks take turns on the
+def test_multi_optimize_loopback_serial_timing():
+    """Option loop_serial (comm.cpp LoopGroup): the ranks take turns on the
     device and log each stretch of work between collectives, with the tree /
-    BH phase marks -- the same results as world 1, and a summary whose
-    per-collective counts follow the schedule (scripts/loop_projection.py)."""
-    import json
+    BH phase marks -- the same results as world 1, and a summary
+    (tsne_ctx_loop_profile) whose per-collective counts follow the schedule
+    (scripts/loop_projection.py)."""
     P, Y0 = problem()
     prm = default_params(iterations=40, theta=0.5, learning_rate=200.0)
     Ys, _, _, ls = run_single(P, Y0, prm)
-    path = tmp_path / "serial.json"
-    monkeypatch.setenv("TSNE_LOOP_SERIAL", str(path))
     m = T.Context.multi([0, 0])
     try:
+        m.set_option("loop_serial", 1)
         Y, u, g = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
         lm = m.optimize(*P, Y, u, g, prm)
+        rep = m.loop_profile()
+        again = m.loop_profile()
     finally:
         m.close()
     for t in ls:
         assert abs(lm[t] - ls[t]) <= TOL * abs(ls[t]), t
     assert close(Y, Ys)
-    rep = json.loads(path.read_text())
+    assert again["segments"] == 0   # a read clears the log
     assert rep["world"] == 2 and len(rep["rank_total_ms"]) == 2 and rep["span_ms"] > 0
     lab = rep["by_collective"]
     # one Z all-reduce per iteration + the loss every 10th; one Y all-gather per iteration

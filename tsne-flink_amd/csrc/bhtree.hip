@@ -499,6 +499,11 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
 // combines it (agent-scope arrival counters, system-scope aggregates: the
 // hand-off described above st_sys) and climbs on.  Only the top ~log2(m / BU_FRONT) levels remain
 // for this cross-workgroup hand-off.
+// ACQREL (Options::bu_acqrel = 1): the arrival is an agent-scope acquire-
+// release RMW -- the HIP memory model's own ordering of the aggregates'
+// stores before it and the sibling's loads after it -- instead of relying on
+// gfx950's in-order issue (the measured cost is in DESIGN.md 6, round 5).
+template <bool ACQREL>
 __global__ __launch_bounds__(256) void bottom_up_top(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
                                                      const double *__restrict__ Wp, double inv_theta, BHNode *nodes,
                                                      double *agg, const int32_t *__restrict__ parent_node,
@@ -510,8 +515,12 @@ __global__ __launch_bounds__(256) void bottom_up_top(const double2 *__restrict__
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
         int p = top_list[e];
         while (p >= 0) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) break;
+            if (ACQREL) {
+                if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 0) break;
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (__hip_atomic_fetch_add(&arrive[p], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) break;
+            }
             __atomic_signal_fence(__ATOMIC_SEQ_CST);   // the sibling's aggregates are read after the arrival
             const int32_t ch[2] = {nodes[p].left, nodes[p].right};
             const int32_t dl = nodes[p].delta;
@@ -3303,7 +3312,8 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     const double inv_theta = theta > 0.0 ? 1.0 / theta : __builtin_inf();
     hipLaunchKernelGGL(bottom_up_intra, dim3(ceil_div(n, BU_NB)), dim3(BU_NB), 0, st, t.pos, t.meta, t.W, inv_theta,
                        t.nodes, t.agg, t.parent_leaf, t.parent_node, t.fstart, t.gen, t.top_list, t.top_cnt);
-    hipLaunchKernelGGL(bottom_up_top, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.meta, t.W,
+    hipLaunchKernelGGL(ctx->opts.bu_acqrel ? bottom_up_top<true> : bottom_up_top<false>,
+                       dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.meta, t.W,
                        inv_theta, t.nodes, t.agg, t.parent_node, t.arrive, t.top_list, t.top_cnt);
     // exact duplicates: the reference's multiplicities (each kernel returns
     // at once unless dup_count saw a duplicate)

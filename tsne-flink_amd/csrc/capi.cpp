@@ -130,8 +130,9 @@ static const OptionField k_options[] = {
     {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
     {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
     {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
+    {"loop_serial", nullptr, &Options::loop_serial, 0, 1},
+    {"bu_acqrel", nullptr, &Options::bu_acqrel, 0, 1},
     {"bh_split", nullptr, &Options::bh_split, 0, 1},
-    {"attract_after", &Options::attract_after, nullptr, 0.0, 1e9},
 };
 static const OptionField &option_field(const char *key) {
     for (const OptionField &f : k_options)
@@ -391,6 +392,20 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         else if (k == "comm.calls") *value_out = comm_counter(ctx, true);
         else if (k == "opt.csort_oversized") *value_out = opt_tree(ctx) ? csort_oversized(ctx, opt_tree(ctx)->cs) : 0;
         else fail(TSNE_ERR_ARG, "unknown counter '" + k + "'");
+    });
+}
+
+int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_out) {
+    return guard([&] {
+        check_ctx(ctx);
+        TSNE_REQUIRE(len_out != nullptr, "NULL argument");
+        const std::string js = comm_loop_profile(primary(ctx));
+        *len_out = (int64_t)js.size();
+        if (buf && cap > 0) {
+            const size_t k = std::min<size_t>(js.size(), (size_t)cap - 1);
+            std::memcpy(buf, js.data(), k);
+            buf[k] = 0;
+        }
     });
 }
 

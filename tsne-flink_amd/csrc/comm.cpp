@@ -53,6 +53,7 @@ struct Comm {
     // a phase boundary inside a rank's work (loopback serial mode: timed)
     virtual void mark(tsne_ctx *, const char *) {}
     virtual int kind() const = 0;   // 1 RCCL, 2 loopback, 3 caller callbacks
+    virtual std::string loop_profile() { return std::string(); }   // loopback serial-mode summary
     int64_t calls = 0;              // collectives this rank has issued
 };
 
@@ -153,14 +154,15 @@ struct RcclComm : Comm {
 
 // Shared state of the ranks of one loopback group (one device).
 //
-// TSNE_LOOP_SERIAL=<file>: the ranks take turns on the device.  A rank holds
-// the turn from the end of one collective to the start of the next, drains
-// the device before it lets go, and logs the wall time of that segment of its
-// own work.  With the segments of one collective aligned across ranks, the
-// sum over collectives of the slowest rank's segment is the compute span a
-// world-size group of devices would take (collectives excluded: they are the
-// loopback's host copies here).  The summary goes to <file> (JSON) when the
-// group ends: a projection tool for N GPUs measured on one.
+// Options::loop_serial (set on the group handle before tsne_optimize): the
+// ranks take turns on the device.  A rank holds the turn from the end of one
+// collective to the start of the next, drains the device before it lets go,
+// and logs the wall time of that segment of its own work.  With the segments
+// of one collective aligned across ranks, the sum over collectives of the
+// slowest rank's segment is the compute span a world-size group of devices
+// would take (collectives excluded: they are the loopback's host copies
+// here).  tsne_ctx_loop_profile returns the summary (JSON): a projection tool
+// for N GPUs measured on one (scripts/loop_projection.py).
 struct LoopGroup {
     int world;
     std::mutex mu;
@@ -170,65 +172,66 @@ struct LoopGroup {
     bool aborted = false;
     std::vector<void *> ptr;
     // serial timing mode
-    std::string serial_path;
     std::mutex turn;
     std::vector<char> holding;
     std::vector<std::chrono::steady_clock::time_point> t_acq;
     std::vector<std::vector<std::pair<std::string, double>>> segs;   // per rank: (collective, ms)
-    explicit LoopGroup(int w) : world(w), ptr(w, nullptr), holding(w, 0), t_acq(w), segs(w) {
-        const char *e = getenv("TSNE_LOOP_SERIAL");
-        if (e && e[0]) serial_path = e;
-    }
-    ~LoopGroup() {
-        if (serial_path.empty()) return;
-        if (FILE *f = fopen(serial_path.c_str(), "w")) {
-            // collectives are issued in the same sequence on every rank
-            size_t m = segs[0].size();
-            for (int r = 1; r < world; ++r) m = std::min(m, segs[r].size());
-            std::map<std::string, std::vector<double>> lab;   // [sum of max, sum of mean, count]
-            std::map<std::string, std::vector<double>> ser;   // per 100 occurrences of a label: sum of max
-            double span = 0.0;
-            std::vector<double> tot(world, 0.0);
-            for (size_t i = 0; i < m; ++i) {
-                double mx = 0.0, sm = 0.0;
-                for (int r = 0; r < world; ++r) {
-                    mx = std::max(mx, segs[r][i].second);
-                    sm += segs[r][i].second;
-                    tot[r] += segs[r][i].second;
-                }
-                auto &v = lab[segs[0][i].first];
-                if (v.empty()) v.assign(3, 0.0);
-                const size_t occ = (size_t)v[2];
-                v[0] += mx; v[1] += sm / world; v[2] += 1.0;
-                auto &sv = ser[segs[0][i].first];
-                if (sv.size() <= occ / 100) sv.resize(occ / 100 + 1, 0.0);
-                sv[occ / 100] += mx;
-                span += mx;
+    explicit LoopGroup(int w) : world(w), ptr(w, nullptr), holding(w, 0), t_acq(w), segs(w) {}
+    static bool serial(const tsne_ctx *ctx) { return ctx->opts.loop_serial != 0; }
+    // the summary of the segments logged so far (then cleared)
+    std::string summary() {
+        std::string out;
+        char b[256];
+        // collectives are issued in the same sequence on every rank
+        size_t m = segs[0].size();
+        for (int r = 1; r < world; ++r) m = std::min(m, segs[r].size());
+        std::map<std::string, std::vector<double>> lab;   // [sum of max, sum of mean, count]
+        std::map<std::string, std::vector<double>> ser;   // per 100 occurrences of a label: sum of max
+        double span = 0.0;
+        std::vector<double> tot(world, 0.0);
+        for (size_t i = 0; i < m; ++i) {
+            double mx = 0.0, sm = 0.0;
+            for (int r = 0; r < world; ++r) {
+                mx = std::max(mx, segs[r][i].second);
+                sm += segs[r][i].second;
+                tot[r] += segs[r][i].second;
             }
-            fprintf(f, "{\"world\": %d, \"segments\": %zu, \"span_ms\": %.6f, \"rank_total_ms\": [", world, m, span);
-            for (int r = 0; r < world; ++r) fprintf(f, "%s%.6f", r ? ", " : "", tot[r]);
-            fprintf(f, "], \"by_collective\": {");
-            bool first = true;
-            for (auto &kv : lab) {
-                fprintf(f, "%s\"%s\": {\"max_ms\": %.6f, \"mean_ms\": %.6f, \"count\": %.0f}", first ? "" : ", ",
-                        kv.first.c_str(), kv.second[0], kv.second[1], kv.second[2]);
-                first = false;
-            }
-            fprintf(f, "}, \"max_ms_per_100\": {");
-            first = true;
-            for (auto &kv : ser) {
-                fprintf(f, "%s\"%s\": [", first ? "" : ", ", kv.first.c_str());
-                for (size_t b = 0; b < kv.second.size(); ++b) fprintf(f, "%s%.3f", b ? ", " : "", kv.second[b]);
-                fprintf(f, "]");
-                first = false;
-            }
-            fprintf(f, "}}\n");
-            fclose(f);
+            auto &v = lab[segs[0][i].first];
+            if (v.empty()) v.assign(3, 0.0);
+            const size_t occ = (size_t)v[2];
+            v[0] += mx; v[1] += sm / world; v[2] += 1.0;
+            auto &sv = ser[segs[0][i].first];
+            if (sv.size() <= occ / 100) sv.resize(occ / 100 + 1, 0.0);
+            sv[occ / 100] += mx;
+            span += mx;
         }
+        snprintf(b, sizeof(b), "{\"world\": %d, \"segments\": %zu, \"span_ms\": %.6f, \"rank_total_ms\": [", world, m, span);
+        out += b;
+        for (int r = 0; r < world; ++r) { snprintf(b, sizeof(b), "%s%.6f", r ? ", " : "", tot[r]); out += b; }
+        out += "], \"by_collective\": {";
+        bool first = true;
+        for (auto &kv : lab) {
+            snprintf(b, sizeof(b), "%s\"%s\": {\"max_ms\": %.6f, \"mean_ms\": %.6f, \"count\": %.0f}", first ? "" : ", ",
+                     kv.first.c_str(), kv.second[0], kv.second[1], kv.second[2]);
+            out += b;
+            first = false;
+        }
+        out += "}, \"max_ms_per_100\": {";
+        first = true;
+        for (auto &kv : ser) {
+            snprintf(b, sizeof(b), "%s\"%s\": [", first ? "" : ", ", kv.first.c_str());
+            out += b;
+            for (size_t k = 0; k < kv.second.size(); ++k) { snprintf(b, sizeof(b), "%s%.3f", k ? ", " : "", kv.second[k]); out += b; }
+            out += "]";
+            first = false;
+        }
+        out += "}}";
+        for (auto &sg : segs) sg.clear();
+        return out;
     }
     // serial mode: the end of a segment of this rank's work (before a collective)
     void seg_end(tsne_ctx *ctx, const char *what) {
-        if (serial_path.empty()) return;
+        if (!serial(ctx)) return;
         TSNE_HIP(hipDeviceSynchronize());   // the side stream too
         const int r = ctx->rank;
         if (holding[r]) {
@@ -241,7 +244,7 @@ struct LoopGroup {
     // serial mode: a phase boundary -- the stretch so far is logged as `what`
     // and the next one starts (the turn is kept)
     void seg_mark(tsne_ctx *ctx, const char *what) {
-        if (serial_path.empty() || !holding[ctx->rank]) return;
+        if (!serial(ctx) || !holding[ctx->rank]) return;
         TSNE_HIP(hipDeviceSynchronize());
         const int r = ctx->rank;
         const auto now = std::chrono::steady_clock::now();
@@ -249,13 +252,13 @@ struct LoopGroup {
         t_acq[r] = now;
     }
     void seg_release(tsne_ctx *ctx) {
-        if (serial_path.empty() || !holding[ctx->rank]) return;
+        if (!holding[ctx->rank]) return;
         holding[ctx->rank] = 0;
         turn.unlock();
     }
     // serial mode: the start of the next segment (after a collective)
     void seg_begin(tsne_ctx *ctx) {
-        if (serial_path.empty()) return;
+        if (!serial(ctx)) return;
         const int r = ctx->rank;
         turn.lock();
         holding[r] = 1;
@@ -325,6 +328,7 @@ struct LoopComm : Comm {
         g->seg_begin(ctx);
     }
     void abort() override { g->abort(); }
+    std::string loop_profile() override { return g->summary(); }
     void release(tsne_ctx *ctx) override { g->seg_release(ctx); }
     void mark(tsne_ctx *ctx, const char *what) override { g->seg_mark(ctx, what); }
     void allgatherv(tsne_ctx *ctx, void *buf, const int64_t *off) override {
@@ -476,6 +480,8 @@ void comm_mark(tsne_ctx *ctx, const char *what) {
 void comm_release(tsne_ctx *ctx) {
     if (ctx->comm) ctx->comm->release(ctx);
 }
+
+std::string comm_loop_profile(tsne_ctx *ctx) { return ctx->comm ? ctx->comm->loop_profile() : std::string(); }
 
 int64_t comm_counter(const tsne_ctx *ctx, bool calls) {
     if (!ctx->comm) return 0;

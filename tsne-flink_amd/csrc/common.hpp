@@ -183,8 +183,10 @@ struct Options {
     int bh_split = 0;         // several ranks: 1 = partition the BH tree by sorted-position ranges (every rank walks
                               // every query over its own cells; F summed by a reduce-scatter) instead of the queries
                               // (0; measured faster at 8 projected ranks)
-    double attract_after = 0.0;   // 2-D optimizer: run the attraction after the BH kernels (not beside them) while
-                                  // the previous traversal's mean wave cost (pops + tile points / 64) is below this
+    int bu_acqrel = 0;        // bottom-up hand-off: 1 = agent-scope acquire-release arrivals (HIP memory model),
+                              // 0 = relaxed arrivals + gfx950 in-order issue (measured faster)
+    int loop_serial = 0;      // loopback groups: ranks take turns on the device and log their work between
+                              // collectives (tsne_ctx_loop_profile; a one-GPU projection of N GPUs)
     int comm_world1 = 0;      // tsne_ctx_init_comm / _callbacks at world 1 still create the communicator, and
                               // the optimizer runs its sharded code path through it (tests the transport)
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
@@ -282,6 +284,8 @@ void comm_init_callbacks(tsne_ctx *ctx, int rank, int world, const tsne_comm_ops
 void comm_reduce_scatterv_f64(tsne_ctx *ctx, double *buf, const int64_t *off_elems);
 // the context's communicator: kind (0 none, 1 RCCL, 2 loopback, 3 callbacks) or collectives issued
 int64_t comm_counter(const tsne_ctx *ctx, bool calls);
+// the loopback group's serial-mode summary (JSON; empty for other transports), then cleared
+std::string comm_loop_profile(tsne_ctx *ctx);
 void comm_abort(tsne_ctx *ctx);
 void comm_release(tsne_ctx *ctx);
 void comm_mark(tsne_ctx *ctx, const char *what);   // phase boundary (loopback serial timing)   // end of a rank's group call (loopback serial timing)

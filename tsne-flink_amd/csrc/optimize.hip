@@ -135,10 +135,6 @@ struct OptState {
     unsigned long long *pcost = nullptr;
     double2 *Fl = nullptr;
     bool split_last = false;   // the last iteration used the tree partition
-    // Options::attract_after: the traversal's wave-cost sum, copied to pinned
-    // host memory without a synchronisation (read one or more iterations later)
-    unsigned long long *wsum = nullptr;
-    volatile unsigned long long *wsum_h = nullptr;
 };
 
 // The sharded code path (query lists, collectives, centring from the gathered
@@ -390,6 +386,9 @@ using ATCfg0 = ATCfg<512, 5888, 1024>;    // 102 KB LDS
 using ATCfg1 = ATCfg<1024, 5888, 1024>;   // 110 KB
 using ATCfg2 = ATCfg<2048, 5888, 1024>;   // 126 KB
 using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
+#ifndef AT_DIAG
+#define AT_DIAG 0   // 1 / 2: diagnostic builds of attract_tiles (timing only)
+#endif
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
 
@@ -458,7 +457,11 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
                     const int k = k0 + u;
                     cu[u] = 0;
                     vu[u] = 0.0;
+#if AT_DIAG == 2   // diagnostic build: no entry loads
+                    if (k < len) { cu[u] = (uint32_t)((lane * 97 + k * 31) % W); vu[u] = 1e-9; }
+#else
                     if (k < len) { cu[u] = pk[off + lane]; vu[u] = pv[off + lane]; }
+#endif
                     off += __popcll(__ballot(len > k));   // the step's active lanes (a prefix)
                 }
                 if (k0 == 0 && sn < send) {
@@ -467,6 +470,10 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
                 }
 #pragma unroll
                 for (int u = 0; u < AT_U; ++u) {
+#if AT_DIAG == 1   // diagnostic build: loads only, no window reads or pair terms
+                    if (k0 + u < len) { fx += vu[u]; fy += (double)cu[u]; }
+                    continue;
+#endif
                     if (k0 + u < len) {
                         const double2 yj = win[cu[u]];
                         const double pij = __dmul_rn(vu[u], ex);
@@ -1730,9 +1737,6 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
             build_own_rows(ctx, s);
         }
     }
-    s->wsum = ws.get<unsigned long long>("opt.wsum", 1);
-    s->wsum_h = reinterpret_cast<volatile unsigned long long *>(ctx->pinned + 32);
-    *s->wsum_h = ~0ull;   // unknown: beside the BH kernels
     for (auto &e : s->ev) TSNE_HIP(hipEventCreate(&e));
     TSNE_HIP(hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking));   // the attraction's (stream priorities: no gain, round 1)
     TSNE_HIP(hipEventCreateWithFlags(&s->ev_y, hipEventDisableTiming));
@@ -2065,14 +2069,6 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         s->log_attract(t, want_loss ? 2 : 0);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
-    // Late phase (Options::attract_after): beside the BH kernels the
-    // attraction's 156 KB of LDS per CU keeps their workgroups off its CUs and
-    // both stretch; once a traversal is light (the previous one's mean wave
-    // cost, read back asynchronously: a phase decision, results identical)
-    // the attraction runs after them on the context stream.
-    const int64_t qrows = sharded(ctx) ? s->L1 - s->L0 : n;
-    const bool seq_attract = !rt_phase && ctx->opts.attract_after > 0.0 && !split_mode(ctx, s) &&
-                             (double)*s->wsum_h < ctx->opts.attract_after * (double)ceil_div(qrows, 64);
     if (rt_phase) side_attract();
     // 1. tree (identical on every rank)
     // insertion rows = original indices; the root-tile shortcut while the
@@ -2081,7 +2077,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // amplify any difference fastest there), the late one after
     bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(ctx), bh_near_tol(ctx, ex == 1.0));
     if (sharded(ctx)) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
-    if (!rt_phase && !seq_attract) side_attract();
+    if (!rt_phase) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
@@ -2105,18 +2101,6 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
-    if (ctx->opts.attract_after > 0.0 && !s->tree.root_tile && !split) {   // this traversal's cost, for the next decisions
-        part_cost(ctx, s->tree, ceil_div(qrows, 64), s->wsum);
-        TSNE_HIP(hipMemcpyAsync(const_cast<unsigned long long *>(s->wsum_h), s->wsum, sizeof(unsigned long long),
-                                hipMemcpyDeviceToHost, st));
-    }
-    if (seq_attract) {   // after the BH kernels, alone on the context stream
-        ctx->timers.begin("opt.attract", st);
-        blocks = attract_launch_opt(st, s, aa, want_loss != 0);
-        TSNE_LAUNCH_CHECK();
-        ctx->timers.end("opt.attract", st);
-        s->log_attract(t, want_loss ? 1 : 3);
-    }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
     reduce_Z(ctx, s, s->z, split);
@@ -2139,7 +2123,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     }
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[3], st));
     // 4. the attraction's sums + update for owned rows
-    if (!seq_attract) TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
+    TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     // update + centre: combine_update (with the mean's block partials when one
     // rank holds every row), mean, centre + write-back of the caller's Y

@@ -86,6 +86,18 @@ class Context:
         check(lib().tsne_ctx_counter(self._h, name.encode(), C.byref(out)))
         return out.value
 
+    def loop_profile(self):
+        """tsne_ctx_loop_profile: the loopback group's serial-mode summary (dict;
+        option loop_serial), or None."""
+        import json
+        n = C.c_int64()
+        check(lib().tsne_ctx_loop_profile(self._h, None, 0, C.byref(n)))
+        if n.value == 0:
+            return None
+        buf = C.create_string_buffer(n.value + 1)
+        check(lib().tsne_ctx_loop_profile(self._h, buf, n.value + 1, C.byref(n)))
+        return json.loads(buf.value.decode())
+
     def rank_world(self):
         r, w = C.c_int32(), C.c_int32()
         check(lib().tsne_ctx_rank(self._h, C.byref(r), C.byref(w)))
