@@ -156,11 +156,12 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             points, each term taken by one rank, and the
  *                             forces are summed by a reduce-scatter to the row
  *                             owners (0: partition the queries, Z-only exchange);
- *   "bu_acqrel" 0             1: the tree build's cross-workgroup bottom-up
+ *   "bu_acqrel" 1             the tree build's cross-workgroup bottom-up
  *                             hand-off uses agent-scope acquire-release
- *                             arrivals (the HIP memory model's ordering) instead
- *                             of relaxed arrivals ordered by gfx950's in-order
- *                             issue (the same trees; DESIGN.md 6 has the cost);
+ *                             arrivals (the HIP memory model's ordering); 0:
+ *                             relaxed arrivals ordered by gfx950's in-order
+ *                             issue (the same trees; no measurable cost
+ *                             difference);
  *   "loop_serial" 0           1 (a loopback tsne_ctx_create_multi group, set
  *                             before tsne_optimize): the ranks take turns on the
  *                             device and log their work between collectives --

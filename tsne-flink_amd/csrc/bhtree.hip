@@ -318,7 +318,11 @@ __global__ void karras_build(const uint64_t *__restrict__ k, int64_t n, const in
 // be hoisted above the relaxed atomic), and they bypass the non-coherent
 // caches (system scope).  This relies on gfx950's in-order issue and
 // write-through / bypassing system-scope accesses, not on the HIP memory
-// model's release / acquire; it is gfx950-only code like the rest.
+// model's release / acquire; it is gfx950-only code like the rest.  Since
+// round 5 the default arrival is an agent-scope acquire-release RMW instead
+// (bottom_up_top<true>, Options::bu_acqrel): the memory model's own ordering,
+// at no measurable cost in the two-phase scheme (the round-1 figure above was
+// for every level crossing workgroups); the relaxed form stays as option 0.
 __device__ __forceinline__ void st_sys(double *p, double v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -499,10 +503,12 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
 // combines it (agent-scope arrival counters, system-scope aggregates: the
 // hand-off described above st_sys) and climbs on.  Only the top ~log2(m / BU_FRONT) levels remain
 // for this cross-workgroup hand-off.
-// ACQREL (Options::bu_acqrel = 1): the arrival is an agent-scope acquire-
-// release RMW -- the HIP memory model's own ordering of the aggregates'
-// stores before it and the sibling's loads after it -- instead of relying on
-// gfx950's in-order issue (the measured cost is in DESIGN.md 6, round 5).
+// ACQREL (Options::bu_acqrel = 1, the default): the arrival is an agent-scope
+// acquire-release RMW -- the HIP memory model's own ordering of the
+// aggregates' stores before it and the sibling's loads after it -- instead of
+// relying on gfx950's in-order issue (0).  C3 whole schedule 5.46 / 5.45 s
+// (ABAB, round 5): no measurable cost with the two-phase bottom-up, where
+// only the top ~log2(m / 512) levels cross workgroups.
 template <bool ACQREL>
 __global__ __launch_bounds__(256) void bottom_up_top(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
                                                      const double *__restrict__ Wp, double inv_theta, BHNode *nodes,

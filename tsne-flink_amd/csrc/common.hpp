@@ -183,8 +183,8 @@ struct Options {
     int bh_split = 0;         // several ranks: 1 = partition the BH tree by sorted-position ranges (every rank walks
                               // every query over its own cells; F summed by a reduce-scatter) instead of the queries
                               // (0; measured faster at 8 projected ranks)
-    int bu_acqrel = 0;        // bottom-up hand-off: 1 = agent-scope acquire-release arrivals (HIP memory model),
-                              // 0 = relaxed arrivals + gfx950 in-order issue (measured faster)
+    int bu_acqrel = 1;        // bottom-up hand-off: 1 = agent-scope acquire-release arrivals (HIP memory model),
+                              // 0 = relaxed arrivals + gfx950 in-order issue (no measurable difference)
     int loop_serial = 0;      // loopback groups: ranks take turns on the device and log their work between
                               // collectives (tsne_ctx_loop_profile; a one-GPU projection of N GPUs)
     int comm_world1 = 0;      // tsne_ctx_init_comm / _callbacks at world 1 still create the communicator, and

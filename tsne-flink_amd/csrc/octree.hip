@@ -1307,7 +1307,8 @@ __global__ __launch_bounds__(256) void oct_traverse64(
                 }
                 act = act && !taken;
             }
-            if (__ballot(act) == 0) continue;
+            const uint64_t amask = __ballot(act);   // the lanes that go on to the children
+            if (amask == 0) continue;
             const int nch = nflags & 0xff;
             const int kinds = __builtin_amdgcn_readfirstlane(nd.kinds);
             if (DBG && act) d_childs += (unsigned long long)nch;
@@ -1320,13 +1321,21 @@ __global__ __launch_bounds__(256) void oct_traverse64(
                 if (kind == OK_LEAF) {
                     wm = (act && !(dx == 0.0 && dy == 0.0 && dz == 0.0)) ? 1.0 : 0.0;
                 } else {
+                    // the masks straight from the compares (scalar: a ballot of a
+                    // combined bool costs two VALU per child, as in bh_traverse)
                     const double A = nd.ca[c];
                     bool acc = D > A;
-                    if (act && !acc && !(D < A * OACC_BAND))
-                        acc = nd.ch[c] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
-                              theta;
+                    uint64_t accm = __builtin_amdgcn_ballot_w64(D > A);
+                    const uint64_t band = amask & ~accm & ~__builtin_amdgcn_ballot_w64(D < A * OACC_BAND);
+                    if (band) {   // rare: inside the band the exact IEEE quotient decides
+                        const bool inb = (band >> lane) & 1ull;
+                        if (inb)
+                            acc = nd.ch[c] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
+                                  theta;
+                        accm |= __ballot(inb && acc);
+                    }
                     wm = (act && acc) ? (double)nd.ccnt[c] : 0.0;
-                    const uint64_t om = __ballot(act && !acc);
+                    const uint64_t om = amask & ~accm;
                     if (om) {
                         if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
                         ++sp;
