@@ -172,6 +172,9 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             a one-rank ncclCommInitRankConfig, id may be
  *                             NULL), and the optimizer runs its sharded path
  *                             through it -- the transport's own test;
+ *   "rep_stats" 0             1: tsne_repulsion / tsne_dev_repulsion (2-D) run
+ *                             the traversal's counting variant, read with the
+ *                             "bh.*" counters below (diagnostics; the same sums);
  *   "reuse_costs" 0           1: tsne_gradient / tsne_repulsion select from the
  *                             previous call's costs (results then depend on
  *                             the call history at rounding level; 0 keeps
@@ -187,12 +190,18 @@ int tsne_ctx_get_option(tsne_ctx *ctx, const char *key, double *value_out);
 /* The loopback group's "loop_serial" summary (JSON: the span of the ranks'
  * work between collectives, per collective and per 100 occurrences) of the
  * segments logged since the last read; *len_out = its length (buf may be NULL
- * to ask), at most cap - 1 bytes + NUL written.  Empty for other handles. */
+ * to ask: the summary is then kept for the next call, which copies it out), at
+ * most cap - 1 bytes + NUL written.  Empty for other handles. */
 int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_out);
 /* Diagnostic counters of the last call (synchronises the context's stream):
  *   "bh.narrow_groups"   64-query groups the last single-call BH traversal
  *                        (tsne_gradient / tsne_repulsion) ran in the narrow layout;
  *   "opt.narrow_groups"  the same for the optimizer's last iteration;
+ *   "bh.pops", "bh.child_slots", "bh.tile_points", "bh.visits"  with option
+ *                        "rep_stats": the last 2-D single-call repulsion's
+ *                        traversal stack pops (wave level), child slots
+ *                        evaluated (wave level), tile points, and
+ *                        reference-equivalent node evaluations;
  *   "comm.kind"          the context's communicator: 0 none, 1 RCCL, 2 loopback,
  *                        3 caller callbacks; "comm.calls" collectives it issued;
  *   "opt.attract_kernel" the optimizer's attraction kernel: 0 attract_rows,

@@ -20,12 +20,24 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import tsne_amd as T  # noqa: E402
 
 
+def ctx_has_option(ctx, key):
+    """False for a library build without the option (A/B against older builds)."""
+    try:
+        ctx.get_option(key)
+        return True
+    except Exception:
+        return False
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("snaps", nargs="+")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--theta", type=float, default=0.5)
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE", help="tsne_ctx_set_option")
+    ap.add_argument("--stats", action="store_true",
+                    help="after the timed calls, one call of the counting traversal (option rep_stats): "
+                         "wave pops, child slots, tile points (2-D)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     with T.Context(0) as ctx:
@@ -47,9 +59,16 @@ def main():
                 times.append(time.perf_counter() - t0)
             narrow = ctx.counter("bh.narrow_groups")
             times = sorted(times[1:] if len(times) > 1 else times)   # --reps 0: the one (cold) call
-            print(json.dumps({"snapshot": os.path.basename(path), "n": n, "ms_median": 1e3 * times[len(times) // 2],
-                              "ms_min": 1e3 * times[0], "narrow_groups": narrow, "sum_abs_F": float(F.abs().sum()),
-                              "sum_z": float(z.sum())}), flush=True)
+            rec = {"snapshot": os.path.basename(path), "n": n, "ms_median": 1e3 * times[len(times) // 2],
+                   "ms_min": 1e3 * times[0], "narrow_groups": narrow, "sum_abs_F": float(F.abs().sum()),
+                   "sum_z": float(z.sum())}
+            if a.stats and Y.shape[1] == 2 and ctx_has_option(ctx, "rep_stats"):
+                ctx.set_option("rep_stats", 1)
+                ctx.dev_repulsion(Y, a.theta, F, z)
+                for k in ("pops", "child_slots", "tile_points", "visits"):
+                    rec[k] = ctx.counter("bh." + k)
+                ctx.set_option("rep_stats", 0)
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -12,6 +12,8 @@
 #   snap3       C4 snapshots (SNAP3_T) written by c4_probe, timed per SNAP3_VARS, debug counters, PMC
 #   pmcsnap     PMC passes (SQ waits / LDS / VALU) over the BH kernels on snaps/Y_t{250,650}.npy
 #   proj        scripts/loop_projection.py PROJ_ARGS per PROJ_VARS entry
+#   valusnap    VALU / SALU / LDS instructions per wave pop of bh_traverse on snapshots t = 250, 450,
+#               per VALU_LIBS library (scripts/valu_summary.py)
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -114,6 +116,21 @@ if has pmcsnap; then   # PMC passes over the 2-D BH kernels on the committed C3 
     k=$((k+1))
     timeout -s KILL 180 rocprofv3 --pmc $pass --kernel-include-regex "bh_traverse|tile_apply" -d $O/pmcs_$k -o pmc \
       --output-format csv -- python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t650.npy --reps 1 > $O/pmcs_$k.log 2>&1 || exit $?
+  done
+fi
+if has valusnap; then   # fp64/VALU instructions per wave pop of bh_traverse<0> on the C3 snapshots,
+  # per library build (VALU_LIBS, "-" = the in-tree one), narrow layout off so every group is a 64-query wave
+  k=0
+  for v in ${VALU_LIBS:--}; do
+    lib=""; [ "$v" != "-" ] && lib="$v"
+    k=$((k+1))
+    echo "# $v" >> $O/valusnap.jsonl
+    TSNE_HIP_LIB="$lib" run 300 python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t450.npy --reps 3 --stats \
+        --option narrow=0 >> $O/valusnap.jsonl 2>> $O/valusnap.err || exit $?
+    TSNE_HIP_LIB="$lib" timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
+        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex "bh_traverse" -d $O/valu_$k -o pmc \
+        --output-format csv -- python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t450.npy --reps 1 --option narrow=0 \
+        > $O/valu_$k.log 2>&1 || exit $?
   done
 fi
 if has proj; then

@@ -1496,12 +1496,13 @@ __global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict_
             v.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
             v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
             v.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-            v.pad_ = 0.0;
+            v.lmask = 0;
             v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
-            v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.ch[0] = nd.h; v.cref[0] = i; v.ccnt[0] = nd.cnt;
-            v.ca[0] = nd.h * inv_theta * (1.0 + QACC_MARGIN);
+            v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.cref[0] = i; v.ccnt[0] = nd.cnt;
+            v.ca[0] = qacc_accept(nd.h, inv_theta);
+            v.cb[0] = qacc_open(nd.h, inv_theta);
             for (int k = 1; k < 4; ++k) {
-                v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.ch[k] = QCH_LEAF; v.ca[k] = 0.0; v.cref[k] = 0; v.ccnt[k] = 0;
+                v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.cb[k] = 0.0; v.ca[k] = 0.0; v.cref[k] = 0; v.ccnt[k] = 0;
             }
             qrec[dv.virt + i] = v;
         }
@@ -1524,28 +1525,31 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     r.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
     r.bx0 = nd.bx0; r.bx1 = nd.bx1; r.by0 = nd.by0; r.by1 = nd.by1;
     r.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-    r.pad_ = 0.0;
+    r.lmask = 0;
     r.first = nd.first; r.last = nd.last; r.cnt = nd.cnt;
     // <= 3 transparent nodes per quad level: a 2-deep descent covers them
     int32_t cand[4] = {nd.left, nd.right, 0, 0};
     int ncand = 2;
     int nc = 0;
+    double ch[4];   // child half widths or kind codes (QCH_*): the kinds below; the traversal reads
+                    // a cell's width only in the rare exact-quotient band (qrec_child_h)
     auto put = [&](int32_t c) {
+        r.cb[nc] = 0.0; r.ca[nc] = 0.0;
         if (c < 0) {
             const double2 p = pos[~c];
-            r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ch[nc] = QCH_LEAF; r.ca[nc] = 0.0; r.cref[nc] = c; r.ccnt[nc] = 1;
+            r.ccx[nc] = p.x; r.ccy[nc] = p.y; ch[nc] = QCH_LEAF; r.cref[nc] = c; r.ccnt[nc] = 1;
         } else {
             const BHNode &cn = nodes[c];
-            r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; r.ch[nc] = cn.delta >= 62 ? QCH_TIE : cn.h;
+            r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; ch[nc] = cn.delta >= 62 ? QCH_TIE : cn.h;
             r.cref[nc] = c; r.ccnt[nc] = cn.cnt;
             if (cn.delta >= 62 && tiecnt && tiecnt[c] > 0) {   // pure duplicate group: one leaf, its multiplicity
                 const double2 p = pos[cn.first];
-                r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ch[nc] = QCH_MULTI; r.ccnt[nc] = tiecnt[c];
+                r.ccx[nc] = p.x; r.ccy[nc] = p.y; ch[nc] = QCH_MULTI; r.ccnt[nc] = tiecnt[c];
             } else if (cn.delta < 62 && dv.vflag && dv.vflag[c]) {   // the chain top C_1 of real node c
-                r.ccx[nc] = dv.vcom[2 * c]; r.ccy[nc] = dv.vcom[2 * c + 1]; r.ch[nc] = 0.5 * nd.h;
+                r.ccx[nc] = dv.vcom[2 * c]; r.ccy[nc] = dv.vcom[2 * c + 1]; ch[nc] = 0.5 * nd.h;
                 r.cref[nc] = dv.virt + c; r.ccnt[nc] = dv.vcntf[c];
             }
-            r.ca[nc] = r.ch[nc] > 0.0 ? r.ch[nc] * inv_theta * (1.0 + QACC_MARGIN) : 0.0;
+            if (ch[nc] >= 0.0) { r.ca[nc] = qacc_accept(ch[nc], inv_theta); r.cb[nc] = qacc_open(ch[nc], inv_theta); }
         }
         ++nc;
     };
@@ -1563,7 +1567,7 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
     }
     (void)ncand;
     for (int k = nc; k < 4; ++k) {
-        r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ch[k] = QCH_LEAF; r.ca[k] = 0.0; r.cref[k] = 0; r.ccnt[k] = 0;
+        r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.cb[k] = 0.0; r.ca[k] = 0.0; r.cref[k] = 0; r.ccnt[k] = 0;
     }
     // QNCH_TILE: some query could pass an all-open test here.  The box test's
     // max corner distance is at least the squared half-diagonal, so if that
@@ -1573,7 +1577,7 @@ __device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *
                                && !(notile && notile[i]);   // a duplicate group below: the reference's path
     int kinds = 0;
     for (int k = 0; k < nc; ++k) {
-        const double c = r.ch[k];
+        const double c = ch[k];
         kinds |= (c == QCH_LEAF ? QK_LEAF : c == QCH_TIE ? QK_TIE : c == QCH_MULTI ? QK_MULTI : QK_CELL) << (QNCH_KIND + 2 * k);
     }
     r.nch = nc | (tile_possible ? QNCH_TILE : 0) | kinds;
@@ -1679,29 +1683,55 @@ constexpr int PART_LEVEL = 10;
 // (4 in the 64-query layout, NKP in the narrow one).
 template <int KB>
 struct TravLDS_T {
+    QRec srec[4][KB];            // first: the record fields' LDS offsets fit the ds_read2 immediates
     int32_t sref[4][STACK];
     uint64_t smask[4][STACK];
-    QRec srec[4][KB];
-    int32_t bref[4][KB];
-    uint64_t bmask[4][KB];
+    int32_t bref[4][KB];         // the batch's refs (its masks ride in the records' lmask)
 };
 using TravLDS = TravLDS_T<4>;
 using NarrowLDS = TravLDS_T<(NKP > 4 ? NKP : 4)>;
 
 // Stage the records of stack entries [sp, sp + k) of wave w into LDS (one
-// round of coalesced 16-byte loads; their latencies overlap).
+// round of coalesced 16-byte loads; their latencies overlap), each with its
+// entry's lane mask in the copy's lmask slot (read with the record's other
+// fields from one LDS address).
 template <class LDS>
 __device__ __forceinline__ void stage_records(LDS &L, int w, int lane, int sp, int k,
                                               const QRec *__restrict__ qrec) {
-    if (lane < k) { L.bref[w][lane] = L.sref[w][sp + lane]; L.bmask[w][lane] = L.smask[w][sp + lane]; }
+    static_assert(offsetof(QRec, lmask) == 16 * (QREC_V4 - 1) + 8, "lmask: the upper half of the last 16 bytes");
+    if (lane < k) L.bref[w][lane] = L.sref[w][sp + lane];
     for (int e = lane; e < QREC_V4 * k; e += 64) {
         const int rr = e / QREC_V4, part = e - rr * QREC_V4;
         const int rf = L.sref[w][sp + rr] & ~REF_FORCED;
-        reinterpret_cast<uint4 *>(&L.srec[w][rr])[part] = reinterpret_cast<const uint4 *>(qrec + rf)[part];
+        uint4 v = reinterpret_cast<const uint4 *>(qrec + rf)[part];
+        if (part == QREC_V4 - 1) {
+            const uint64_t m = L.smask[w][sp + rr];
+            v.z = (uint32_t)m;
+            v.w = (uint32_t)(m >> 32);
+        }
+        reinterpret_cast<uint4 *>(&L.srec[w][rr])[part] = v;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_s_waitcnt(0);   // vmcnt = lgkmcnt = 0: batch staged in LDS
     __builtin_amdgcn_wave_barrier();
+}
+
+// The half width of cell child `cref` of record `ref` (flags stripped), for
+// the exact-quotient band (QACC_BAND): a real node's own h, or for the
+// virtual chain top of a duplicate group (cref >= virt) half its parent's
+// (build_qrec_one).  A virtual record's only child is a real node.
+__device__ __forceinline__ double qrec_child_h(const BHNode *__restrict__ nodes, int32_t ref, int32_t cref,
+                                               int32_t virt) {
+    return cref < virt ? nodes[cref].h : 0.5 * nodes[ref & ~REF_FORCED].h;
+}
+
+// The reference's summarise decision for a cell child from D1 = 1 + D (see
+// QACC_BAND): the two record bounds, the exact IEEE quotient in between.
+__device__ __forceinline__ bool qrec_accept(const QRec &nd, int c, double D1, double dx, double dy, double theta,
+                                            const BHNode *__restrict__ nodes, int32_t ref, int32_t virt) {
+    if (D1 > nd.ca[c]) return true;
+    if (D1 < nd.cb[c]) return false;
+    return qrec_child_h(nodes, ref, nd.cref[c], virt) / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
 }
 
 // All-open / near-exact test of one (query, record) pair (see the comment above
@@ -1814,7 +1844,7 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
         const bool kin = k < kn;
         const int kk = kin ? k : 0;
         const QRec &nd = L.srec[w][kk];
-        const uint32_t msk = (uint32_t)L.bmask[w][kk];
+        const uint32_t msk = (uint32_t)nd.lmask;
         bool act = kin && valid && ((msk >> q) & 1u);
         const int nflags = nd.nch;
         bool tile = false;
@@ -1860,17 +1890,17 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
         const int kind = (nflags >> (QNCH_KIND + 2 * c)) & 3;
         const bool has = act && c < nch;
         const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-        const double D = __fma_rn(dx, dx, dy * dy);
+        const double D1 = __fma_rn(dx, dx, __fma_rn(dy, dy, 1.0));   // 1 + D (QACC_BAND)
         const bool isleaf = has && kind == QK_LEAF, iscell = has && kind == QK_CELL;
-        const double A = nd.ca[c];
-        bool acc = D > A;
-        if (iscell && !acc && !(D < A * QACC_BAND))
-            acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+        bool acc = D1 > nd.ca[c];
+        if (iscell && !acc && !(D1 < nd.cb[c]))
+            acc = qrec_child_h(nodes, L.bref[w][kk], nd.cref[c], virt) / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) <
+                  theta;
         const bool takel = isleaf && !(dx == 0.0 && dy == 0.0);
         const bool takec = iscell && acc;
         const double wm = takel ? 1.0 : (takec ? (double)nd.ccnt[c] : 0.0);
         if (STATS && (isleaf || iscell)) ++nvis;
-        const double Qv = recip_bh(1.0 + D);
+        const double Qv = recip_bh(D1);
         const double mult = wm * Qv;
         const double sc = mult * Qv;
         fx = __fma_rn(sc, dx, fx);
@@ -1882,7 +1912,7 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
             if (dupk && kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
                 if (!(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
                     if (STATS) ++nvis;
-                    cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                    cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
                 }
             } else if (dupk) {                // a key-tie group: every point directly
                 const BHNode &tn = nodes[nd.cref[c]];
@@ -2037,15 +2067,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
         stage_records(L, w, lane, sp, kb, qrec);
         const QRec *brec = L.srec[w];
         const int32_t *bref_c = L.bref[w];
-        const uint64_t *bmask_c = L.bmask[w];
         npops += kb;
         for (int r = 0; r < kb; ++r) {
             if (STATS) ++wpops;
             const int ref = __builtin_amdgcn_readfirstlane(bref_c[r]);
-            const uint64_t msk = bmask_c[r];
+            const uint64_t msk = brec[r].lmask;
             const uint64_t msk_s = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(msk >> 32)) << 32) |
                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)msk);   // the wave's (scalar)
-            bool act = (msk_s >> lane) & 1ull;
+            bool act = __builtin_amdgcn_inverse_ballot_w64(msk_s);   // the mask's own SGPRs: no VALU
             const QRec &nd = brec[r];
             if (PART) {   // a shared or forced record: the tree partition's slow path (see REF_FORCED)
                 const int rf = __builtin_amdgcn_readfirstlane(nd.first), rl = __builtin_amdgcn_readfirstlane(nd.last);
@@ -2094,18 +2123,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                         if (c1 < plo || c0 >= phi) continue;         // no point of mine below
                         const bool own = c0 >= plo && c0 < phi;      // the term's owner: its first point's rank
                         const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                        const double D = __fma_rn(dx, dx, dy * dy);
+                        const double D1 = __fma_rn(dx, dx, __fma_rn(dy, dy, 1.0));   // 1 + D (QACC_BAND)
                         if (kind == QK_LEAF || kind == QK_CELL) {
                             bool take, acc = false;
                             if (kind == QK_LEAF) {
                                 take = own && (an || fm) && !(dx == 0.0 && dy == 0.0);
                             } else {
-                                if (an) {
-                                    const double A = nd.ca[c];
-                                    acc = D > A;
-                                    if (!acc && !(D < A * QACC_BAND))
-                                        acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
-                                }
+                                if (an) acc = qrec_accept(nd, c, D1, dx, dy, theta, nodes, rref, virt);
                                 take = own && an && acc;
                                 const uint64_t om = __ballot(an && !acc), fmm = __ballot(fm);
                                 if (om) push(cref, om);
@@ -2113,7 +2137,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                             }
                             if (STATS && (an || fm)) ++nvis;
                             const double wm = take ? (kind == QK_LEAF ? 1.0 : (double)nd.ccnt[c]) : 0.0;
-                            const double Q = recip_bh(1.0 + D);
+                            const double Q = recip_bh(D1);
                             const double mult = wm * Q;
                             const double sc = mult * Q;
                             fx = __fma_rn(sc, dx, fx);
@@ -2122,7 +2146,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                         } else if (kind == QK_MULTI) {   // a leaf of ccnt copies: 0 if it is the query's point
                             if (own && (an || fm) && !(nd.ccx[c] == qx && nd.ccy[c] == qy)) {
                                 if (STATS) ++nvis;
-                                cell_force(dx, dy, D, nd.ccnt[c], fx, fy, zs);
+                                cell_force(dx, dy, __fma_rn(dx, dx, dy * dy), nd.ccnt[c], fx, fy, zs);
                             }
                         } else if (own) {                // a key-tie group: every point directly
                             for (int p = c0; p <= c1; ++p) {
@@ -2136,19 +2160,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
             }
             // all-open / near-exact tests (per lane) -> the subtree's exact leaf sum;
             // both tests on every lane, their masks straight from the compares
-            // (tile_test's branch and a ballot of the combined bool cost more)
-            bool tile = false;
+            // (tile_test's branch and a ballot of the combined bool cost more).
+            // Lane state is kept as scalar masks (amask: lanes that go on to the
+            // children), turned into lane predicates by inverse ballots, which
+            // read the mask's SGPRs directly: no VALU per conversion.
             uint64_t tm = 0;
-            uint64_t amask = msk_s;   // lanes that go on to the children
+            uint64_t amask = msk_s;
             const int nflags = __builtin_amdgcn_readfirstlane(nd.nch);   // the record is the wave's
             if (nflags & QNCH_TILE) {
                 const double cdx = qx - nd.cx, cdy = qy - nd.cy;
                 const double ex = __fma_rn(1e-15, qmag, nd.ex);
                 const double dxm = fmax(fabs(qx - nd.bx0), fabs(qx - nd.bx1)) + ex;
                 const double dym = fmax(fabs(qy - nd.by0), fabs(qy - nd.by1)) + ex;
-                const bool t1 = cdx * cdx + cdy * cdy <= nd.rball, t2 = dxm * dxm + dym * dym <= nd.hmin;
-                tm = msk_s & (__builtin_amdgcn_ballot_w64(t1) | __builtin_amdgcn_ballot_w64(t2));
-                tile = act && (t1 || t2);
+                // (FMA forms: the bounds carry 1e-9 / 1.1e-12 relative margins)
+                tm = msk_s & (__builtin_amdgcn_ballot_w64(__fma_rn(cdx, cdx, cdy * cdy) <= nd.rball) |
+                              __builtin_amdgcn_ballot_w64(__fma_rn(dxm, dxm, dym * dym) <= nd.hmin));
             }
             if (tm && ntt < TILE_CAP) {
                 // The wave records (subtree, lanes) for tile_apply, or, when its
@@ -2164,14 +2190,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                 ++ntt;
                 ntilepts += b - a + 1;
                 if (STATS) wtile += (unsigned long long)(b - a + 1);
-                if (tile) {
+                if (__builtin_amdgcn_inverse_ballot_w64(tm)) {
                     if (STATS) nvis += (unsigned long long)(b - a + 1);
                     if (s >= a && s <= b) zs -= (double)ndup;
                 }
-                act = act && !tile;
                 amask = msk_s & ~tm;
             }
             if (amask == 0) continue;
+            act = __builtin_amdgcn_inverse_ballot_w64(amask);
             // the opened cell's quad children, from its record
             const int nch = nflags & 0xff;
             if (STATS) { wslots += (unsigned long long)nch; if (act) nevals += (unsigned long long)nch; }
@@ -2182,33 +2208,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                 if (kind == QK_CELL || kind == QK_LEAF) {
                     // A leaf (cumSize 1, com = the point) always interacts, zero if
                     // it is the query's own point (x - y == 0 iff x == y).  A cell is
-                    // summarised when ch / D < theta (QACC_BAND: two compares against
-                    // the record's bound, the exact quotient only inside the band;
-                    // at D = 0 never).  wm = the term's multiplicity where taken, else
-                    // 0: a zero term leaves the sums bit-equal.  Only wm is computed
-                    // per kind (uniform branch), so the accumulators stay in place.
+                    // summarised when ch / D < theta (QACC_BAND: two compares of
+                    // D1 = 1 + D against the record's bounds, the exact quotient only
+                    // inside the band; at D = 0 never).  wm = the term's multiplicity
+                    // where taken, else 0: a zero term leaves the sums bit-equal.
+                    // Only wm is computed per kind (uniform branch), so the
+                    // accumulators stay in place.
                     if (STATS && act) ++nvis;
                     const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c];
-                    const double D = __fma_rn(dx, dx, dy * dy);
-                    bool take;
+                    const double D1 = __fma_rn(dx, dx, __fma_rn(dy, dy, 1.0));   // 1 + D, the term's denominator
+                    uint64_t takem;
                     double wm;
                     if (kind == QK_LEAF) {
-                        take = act && !(dx == 0.0 && dy == 0.0);
-                        wm = take ? 1.0 : 0.0;
+                        takem = amask & ~(__builtin_amdgcn_ballot_w64(dx == 0.0) & __builtin_amdgcn_ballot_w64(dy == 0.0));
+                        wm = __builtin_amdgcn_inverse_ballot_w64(takem) ? 1.0 : 0.0;
                     } else {
                         // the masks straight from the compares (scalar: a
                         // ballot of a combined bool costs two VALU per child)
-                        const double A = nd.ca[c];
-                        bool acc = D > A;
-                        uint64_t accm = __builtin_amdgcn_ballot_w64(D > A);
-                        const uint64_t band = amask & ~accm & ~__builtin_amdgcn_ballot_w64(D < A * QACC_BAND);
+                        uint64_t accm = __builtin_amdgcn_ballot_w64(D1 > nd.ca[c]);
+                        const uint64_t band = amask & ~accm & ~__builtin_amdgcn_ballot_w64(D1 < nd.cb[c]);
                         if (band) {   // rare: inside the band the exact IEEE quotient decides
-                            const bool inb = (band >> lane) & 1ull;
-                            if (inb) acc = nd.ch[c] / __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
-                            accm |= __ballot(inb && acc);
+                            bool acc = false;
+                            if (__builtin_amdgcn_inverse_ballot_w64(band))
+                                acc = qrec_child_h(nodes, ref, nd.cref[c], virt) /
+                                          __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)) < theta;
+                            accm |= band & __builtin_amdgcn_ballot_w64(acc);
                         }
-                        take = act && acc;
-                        wm = (double)(take ? nd.ccnt[c] : 0);
+                        takem = amask & accm;
+                        wm = (double)(__builtin_amdgcn_inverse_ballot_w64(takem) ? nd.ccnt[c] : 0);
                         const uint64_t om = amask & ~accm;
                         if (om) {
                             if (PART && sp >= STACK) {
@@ -2219,16 +2246,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                             }
                         }
                     }
-                    const double Q = recip_bh(1.0 + D);
+                    const double Q = recip_bh(D1);
                     const double mult = wm * Q;
                     const double sc = mult * Q;
                     fx = __fma_rn(sc, dx, fx);
                     fy = __fma_rn(sc, dy, fy);
                     zs += mult;
                     if (STATS) {   // children every active lane takes (summarised cell or leaf), full wave or not
-                        const uint64_t am = __ballot(act), tk2 = __ballot(take);
-                        if (am && tk2 == am) {
-                            if (am == __ballot(valid)) ++wfull; else ++wpart;
+                        if (takem == amask) {
+                            if (amask == __ballot(valid)) ++wfull; else ++wpart;
                         }
                     }
                 }

@@ -53,17 +53,32 @@ struct __attribute__((aligned(16))) QRec {
     double bx0, bx1, by0, by1;  // bounding box of the subtree's points
     int32_t first, last;        // leaf range in sorted order
     int32_t cnt, nch;           // cumSize, number of quad children | QNCH_TILE
-    double ccx[4], ccy[4], ch[4];
-    double ca[4];               // cells: the sure-accept bound on D, ch / theta (1 + 2.5e-14) (see QACC_BAND)
+    double ccx[4], ccy[4];
+    double cb[4];               // cells: the sure-open bound on 1 + D (see QACC_BAND)
+    double ca[4];               // cells: the sure-accept bound on 1 + D
     int32_t cref[4], ccnt[4];
     double ex;                  // the box test's rounding margin, record part: 1e-15 (|bx0| + |bx1| + |by0| + |by1|)
-    double pad_;
+    uint64_t lmask;             // 0 in HBM; the LDS copy of a popped record: its stack entry's lane mask
 };
-// A cell child is summarised for sure when D > ca, opened for sure when
-// D < ca * QACC_BAND (= ch / theta (1 - 2.5e-14)); in between, the exact
-// IEEE quotient ch / D < theta decides (the reference's test, QuadTree.scala:134).
+// A cell child is tested on D1 = fma(dx, dx, fma(dy, dy, 1)) ~ 1 + D, the
+// denominator its term needs anyway (one fp64 add per child fewer than
+// testing D and forming 1 + D apart).  It is summarised for sure when
+// D1 > ca, opened for sure when D1 < cb, with
+//   ca = (1 + ch / theta (1 + 2.5e-14)) (1 + 1e-15)  (rounded: > the bound),
+//   cb = (1 + ch / theta (1 - 2.5e-14)) (1 - 1e-15)  (rounded: < the bound);
+// the 1e-15 factors cover D1's two roundings (<= 2^-52 relative), the
+// 2.5e-14 ones the distance between the reference's D and the exact one and
+// the quotient's rounding.  In between, the exact IEEE quotient ch / D < theta
+// decides (the reference's test, QuadTree.scala:134), with ch read from the
+// node (qrec_child_h: rare, so the record does not carry it).
 constexpr double QACC_MARGIN = 2.5e-14;
 constexpr double QACC_BAND = (1.0 - QACC_MARGIN) / (1.0 + QACC_MARGIN);
+__host__ __device__ inline double qacc_accept(double ch, double inv_theta) {
+    return (1.0 + ch * inv_theta * (1.0 + QACC_MARGIN)) * (1.0 + 1e-15);
+}
+__host__ __device__ inline double qacc_open(double ch, double inv_theta) {
+    return (1.0 + ch * inv_theta * (1.0 - QACC_MARGIN)) * (1.0 - 1e-15);
+}
 
 struct BHTree {
     int64_t n = 0;           // points (queries)

@@ -130,6 +130,7 @@ static const OptionField k_options[] = {
     {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
     {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
     {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
+    {"rep_stats", nullptr, &Options::rep_stats, 0, 1},
     {"loop_serial", nullptr, &Options::loop_serial, 0, 1},
     {"bu_acqrel", nullptr, &Options::bu_acqrel, 0, 1},
     {"bh_split", nullptr, &Options::bh_split, 0, 1},
@@ -388,6 +389,7 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         else if (k == "opt.narrow_groups") *value_out = opt_tree(ctx) ? bh_narrow_groups(ctx, *opt_tree(ctx)) : 0;
         else if (k == "bh.csort_oversized") *value_out = ctx->single_tree ? csort_oversized(ctx, ctx->single_tree->cs) : 0;
         else if (k == "opt.attract_kernel") *value_out = opt_attract_kernel(ctx);
+        else if (k.rfind("bh.", 0) == 0 && repulsion_stat(ctx, k, value_out)) {}
         else if (k == "comm.kind") *value_out = comm_counter(ctx, false);
         else if (k == "comm.calls") *value_out = comm_counter(ctx, true);
         else if (k == "opt.csort_oversized") *value_out = opt_tree(ctx) ? csort_oversized(ctx, opt_tree(ctx)->cs) : 0;
@@ -399,12 +401,17 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
     return guard([&] {
         check_ctx(ctx);
         TSNE_REQUIRE(len_out != nullptr, "NULL argument");
-        const std::string js = comm_loop_profile(primary(ctx));
+        // the summary is taken (and the log cleared) once; a length query
+        // (buf NULL) keeps it pending for the call that copies it out
+        tsne_ctx *p = primary(ctx);
+        if (p->loop_profile_pending.empty()) p->loop_profile_pending = comm_loop_profile(p);
+        const std::string &js = p->loop_profile_pending;
         *len_out = (int64_t)js.size();
         if (buf && cap > 0) {
             const size_t k = std::min<size_t>(js.size(), (size_t)cap - 1);
             std::memcpy(buf, js.data(), k);
             buf[k] = 0;
+            p->loop_profile_pending.clear();
         }
     });
 }

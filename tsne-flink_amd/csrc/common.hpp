@@ -75,6 +75,7 @@ struct Workspace {
         if (!b) b.reset(new DevBuf());
         return static_cast<T *>(b->ensure(count * sizeof(T)));
     }
+    bool has(const std::string &name) const { return bufs.count(name) != 0; }
     void clear() { bufs.clear(); }
     // free every buffer whose name starts with prefix (large one-time temporaries)
     void release_prefix(const std::string &prefix) {
@@ -187,6 +188,8 @@ struct Options {
                               // 0 = relaxed arrivals + gfx950 in-order issue (no measurable difference)
     int loop_serial = 0;      // loopback groups: ranks take turns on the device and log their work between
                               // collectives (tsne_ctx_loop_profile; a one-GPU projection of N GPUs)
+    int rep_stats = 0;        // tsne_repulsion / tsne_dev_repulsion (2-D): count the traversal's pops, child slots and
+                              // tile points (the counting kernel variant) for tsne_ctx_counter "bh.*"
     int comm_world1 = 0;      // tsne_ctx_init_comm / _callbacks at world 1 still create the communicator, and
                               // the optimizer runs its sharded code path through it (tests the transport)
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
@@ -207,6 +210,7 @@ struct tsne_ctx {
     tsne::OptState *opt = nullptr;
     tsne::Options opts;
     tsne::BHTree *single_tree = nullptr;   // bh_single_tree (owned; freed by tsne_ctx_destroy)
+    std::string loop_profile_pending;      // tsne_ctx_loop_profile: a summary read for its length, not yet copied out
     tsne::StageTimers timers;
     int32_t *pinned = nullptr;   // small pinned host scratch (per-iteration read-backs)
     int cu_count = 256;
@@ -255,6 +259,9 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
                      double theta, double exaggeration, double *d_grad, double *h_sumq,
                      double *h_loss);
 
+// "bh.pops" / "bh.child_slots" / "bh.tile_points" / "bh.visits" of the last 2-D
+// repulsion_device call with Options::rep_stats; false for other names.
+bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out);
 void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, double theta, double *dF,
                       double *dz);
 void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col, const double *d_P, int64_t n,

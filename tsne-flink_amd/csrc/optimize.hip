@@ -1323,7 +1323,12 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
     if (c == 2) {
         BHTree &t = bh_single_tree(ctx, n);
         bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled(ctx));
-        bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, nullptr);
+        unsigned long long *vis = nullptr;   // Options::rep_stats: the counting traversal
+        if (ctx->opts.rep_stats) {
+            vis = ctx->ws.get<unsigned long long>("rep.visits", 32);
+            TSNE_HIP(hipMemsetAsync(vis, 0, sizeof(unsigned long long) * 32, st));
+        }
+        bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, vis);
         inv = t.inv;
     } else {
         OctTree t;
@@ -1334,6 +1339,21 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
     }
     hipLaunchKernelGGL(unsort_fz, dim3(ceil_div(n, 256)), dim3(256), 0, st, inv, n, c, Fs, zs, dF, dz);
     TSNE_LAUNCH_CHECK();
+}
+
+bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) {
+    // indices of bh_traverse's counters (its STATS block): wave pops, tile
+    // points, wave child slots, reference-equivalent evaluations
+    const int at = name == "bh.pops" ? 3 : name == "bh.tile_points" ? 4 : name == "bh.child_slots" ? 6
+                 : name == "bh.visits" ? 0 : -1;
+    if (at < 0) return false;
+    TSNE_REQUIRE(ctx->opts.rep_stats && ctx->ws.has("rep.visits"), "counter '" + name + "' needs option rep_stats");
+    unsigned long long v[32];
+    TSNE_HIP(hipMemcpyAsync(v, ctx->ws.get<unsigned long long>("rep.visits", 32), sizeof(v), hipMemcpyDeviceToHost,
+                            ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    *value_out = (int64_t)v[at];
+    return true;
 }
 
 // 3-D gradient (octree): same contract as gradient_device, Y / grad n x 3.
