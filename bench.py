@@ -48,7 +48,7 @@ BF16_MFMA_PEAK_TF = 2500.0   # dense (MI355X_MICROARCH.md); the kNN filter's bf1
 HBM_PEAK_GBS = 8000.0
 PMC_ATTRACT = "r04_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
 PMC_BH = "r04_bh_valu.json"
-UPDATE_KERNELS = ("combine_update", "center_scatter")   # update + centre kernels in the PMC summary
+UPDATE_KERNELS = ("combine_update", "center2")   # update + centre kernels in the PMC summary
 
 
 def parse():
@@ -317,6 +317,7 @@ def main():
     t_loop = max_over_ranks(time.perf_counter() - t0, world)
     t0 = time.perf_counter()
     losses = ctx.dev_opt_losses()
+    ctx.dev_opt_sync()   # the working set back to the caller's buffers (collective), timed with the D2H
     Y_final = Y[:n].cpu().numpy() if rank == 0 else None   # noqa: F841 (the D2H of the result, timed)
     t_out = time.perf_counter() - t0
     alog = ctx.dev_opt_attract_log()
@@ -337,6 +338,8 @@ def main():
             if traced:
                 ctx.dev_opt_profile(1)
             ctx.dev_opt_step(t)
+            if traced or t in dumps or (world == 1 and t in snap_at):
+                ctx.dev_opt_sync()   # the caller's Y (every rank: a collective with several)
             if traced:
                 (window_profile if t <= 5 else timeline).append(trace_entry(ctx, t, r1 - r0, Y, n))
             if want_snaps and t in snap_at:

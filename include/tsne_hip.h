@@ -338,9 +338,11 @@ int tsne_dev_joint_distribution(tsne_ctx *ctx, const int64_t *d_row_ptr, const i
  * rank r computes the rows of its range of the optimizer's internal point
  * labels) and the working set (Y, upd, gains: n x n_components, original
  * point order) into its own state and allocates the workspace; step runs
- * global iteration t (1-based) with the reference phase schedule and
- * rewrites the caller's Y (original order) at the end of every step; sync
- * also writes back upd and gains.  Losses for t % 10 == 0 stay on the device
+ * global iteration t (1-based) with the reference phase schedule; sync
+ * writes the working set back to the caller's Y, upd and gains (original
+ * order; with several ranks a collective call).  The caller's buffers are
+ * not touched by a step (round 5: the per-step scatter of Y was a third of
+ * the update's HBM traffic).  Losses for t % 10 == 0 stay on the device
  * and are read by tsne_dev_opt_losses.  Internal labels (2-D): P's graph
  * order at setup (connected components, BFS level), then every 25
  * iterations the Morton order of the embedding when it keeps more of P's

@@ -70,6 +70,8 @@ for t in range(1, a.iterations + 1):
         ctx.dev_opt_profile(1)
     ts = time.perf_counter()
     ctx.dev_opt_step(t)
+    if trace or t in dumps:
+        ctx.dev_opt_sync()   # the caller's Y (written at sync)
     torch.cuda.synchronize()
     dt = time.perf_counter() - ts
     if trace:

@@ -30,7 +30,7 @@ def counters(kind):
 def label(name):
     if "attract_tiles" in name:
         return "attract_tiles<LOSS=false>" if ", false," in name else None
-    for k in ("combine_update", "center_scatter"):
+    for k in ("combine_update", "center2"):
         if k in name:
             return k
     return None

@@ -190,6 +190,7 @@ def run_schedule(ctx, Pd, n, c, params, snaps, seed=0, stop=None, steps=(), Y0=N
         if t in steps:
             st[t] = (before, state(), ctx.dev_opt_last_z())
         if t in snaps:
+            ctx.dev_opt_sync()   # the caller's Y is written at sync (not by a step)
             ctx.synchronize()
             out[t] = Y.cpu().numpy().copy()
     return out, ctx.dev_opt_losses(), st
@@ -435,6 +436,7 @@ def test_c5_distance_matrix_5k_matches_oracle(ctx):
     for t in range(1, T_ + 1):
         ctx.dev_opt_step(t)
         if t in snaps:   # per-iteration gradient parity at the trajectory's own states
+            ctx.dev_opt_sync()
             ctx.synchronize()
             Yt = Y.cpu().numpy()
             ex = exaggeration(t + 1, T_)

@@ -33,6 +33,7 @@ def run(n, C, coherent, seed, iterations=40, dups=False, scale=3.0):
             c.dev_opt_step(t)
             if coherent and C == 2:
                 over += c.counter("opt.csort_oversized")
+        c.dev_opt_sync()
         c.synchronize()
         return Y.cpu().numpy(), c.dev_opt_losses(), over
 

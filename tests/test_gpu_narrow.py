@@ -140,6 +140,7 @@ def test_optimizer_narrow_deterministic_and_equal():
                 c.dev_opt_step(t)
                 if t % 10 == 0:
                     used += c.counter("opt.narrow_groups")
+            c.dev_opt_sync()
             c.synchronize()
             return Y.cpu().numpy(), c.dev_opt_losses(), used
 

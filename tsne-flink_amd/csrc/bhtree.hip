@@ -411,13 +411,17 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
                                                         const int32_t *__restrict__ parent_node,
                                                         const int32_t *__restrict__ fstart, int32_t gen,
                                                         int32_t *__restrict__ top_list, int32_t *__restrict__ top_cnt) {
-    // aggregates (sx, sy, x0, x1, y0, y1, hmin, rball; the count is last - first + 1)
-    // and the topology of the range's nodes (ids [S0, S1), Karras: a node's id
-    // lies in its own leaf range), staged once so that the climb never waits
-    // on global memory
+    // aggregates (sx, sy, x0, x1, y0, y1, hmin, rball), the range's leaf
+    // positions, and the topology of its nodes (ids [S0, S1), Karras: a
+    // node's id lies in its own leaf range: count, children, delta, parent,
+    // whether the node lies inside the range), staged once so that the climb
+    // never waits on global memory (the leaf children's positions were
+    // dependent global loads at every level: the climb's latency)
     __shared__ double lagg[8][BU_CAP];
-    __shared__ int32_t lleft[BU_CAP], lright[BU_CAP], ldelta[BU_CAP], lfirst[BU_CAP], llast[BU_CAP], lpar[BU_CAP];
+    __shared__ double2 lpos[BU_CAP];
+    __shared__ int32_t lleft[BU_CAP], lright[BU_CAP], ldelta[BU_CAP], lcnt[BU_CAP], lpar[BU_CAP];
     __shared__ int32_t larr[BU_CAP];
+    __shared__ uint8_t lself[BU_CAP];
     __shared__ int32_t sS[2];
     const int m = meta[0];
     const int b = blockIdx.x;
@@ -437,17 +441,19 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
     for (int j = t; j < S1 - S0; j += BU_NB) {
         const int q = S0 + j;
         larr[j] = 0;
+        lpos[j] = pos[q];
         if (q < m - 1) {
             const BHNode &nd = nodes[q];
             lleft[j] = nd.left; lright[j] = nd.right; ldelta[j] = nd.delta;
-            lfirst[j] = nd.first; llast[j] = nd.last; lpar[j] = parent_node[q];
+            lcnt[j] = nd.last - nd.first + 1; lpar[j] = parent_node[q];
+            lself[j] = nd.first >= S0 && nd.last < S1;
         } else {
-            lfirst[j] = -1; llast[j] = INT32_MAX;   // not a node: never in range
+            lself[j] = 0;   // not a node: never in range
         }
     }
     __syncthreads();
     const double W = *Wp;
-    auto in_blk = [&](int q) { return q >= S0 && q < S1 && lfirst[q - S0] >= S0 && llast[q - S0] < S1; };
+    auto in_blk = [&](int q) { return q >= S0 && q < S1 && lself[q - S0]; };
     for (int s = S0 + t; s < S1; s += BU_NB) {
         int p = parent_leaf[s];
         if (p < 0) continue;
@@ -465,13 +471,17 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
             double a[2][7], c[2], rb[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
+                const int o = (ch[k] < 0 ? ~ch[k] : ch[k]) - S0;   // children of an in-range node are in range
                 if (ch[k] < 0) {
-                    bu_leaf(pos, ~ch[k], a[k], c[k], rb[k]);
-                } else {                                 // children of an in-range node are in range
-                    const int o = ch[k] - S0;
+                    const double2 q = lpos[o];
+                    a[k][0] = q.x; a[k][1] = q.y; a[k][2] = q.x; a[k][3] = q.x; a[k][4] = q.y; a[k][5] = q.y;
+                    a[k][6] = __builtin_inf();
+                    c[k] = 1.0;
+                    rb[k] = __builtin_inf();
+                } else {
 #pragma unroll
                     for (int f = 0; f < 7; ++f) a[k][f] = lagg[f][o];
-                    c[k] = (double)(llast[o] - lfirst[o] + 1);
+                    c[k] = (double)lcnt[o];
                     rb[k] = lagg[7][o];
                 }
             }
@@ -1868,15 +1878,20 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
             // included) add exactly 1 each to z in the leaf sum, taken off here
             if (tile && c == 0 && s >= a && s <= b) zs -= (double)dupc[s];
             if (STATS && tile && c == 0) nvis += (unsigned long long)(b - a + 1);
-            // dense: the query's 4 lanes split the subtree's points
-            int p = dense ? a + c : 1, last = dense ? b : 0;
-            while (__ballot(p <= last)) {
-                if (p <= last) {
+            // dense: the query's 4 lanes split the subtree's points, summed
+            // apart and added once (accumulating into fx / fy / zs inside the
+            // divergent loop made the compiler copy them at every merge)
+            // (a divergent do-while: lanes leave it one by one, no merge per point)
+            double ux = 0.0, uy = 0.0, uq = 0.0;
+            if (dense && a + c <= b) {
+                int p = a + c;
+                do {
                     const double2 pp = pos[p];
-                    pair_force(qx, qy, pp.x, pp.y, fx, fy, zs);
+                    pair_force(qx, qy, pp.x, pp.y, ux, uy, uq);
                     p += 4;
-                }
+                } while (p <= b);
             }
+            if (dense) { fx += ux; fy += uy; zs += uq; }
             const uint64_t tm = __ballot(tile && c == 0);
             for (uint64_t r = tm; r; r &= r - 1) {   // cost: points per (record, query), as the 64-query layout's
                 const int l = __ffsll((long long)r) - 1;

@@ -22,6 +22,7 @@
 // points staged through LDS), then evaluates the node's two binary children.
 #include <hipcub/hipcub.hpp>
 
+#include "bhtree.hpp"   // qacc_open / qacc_accept (the records' child bounds)
 #include "octree.hpp"
 
 namespace tsne {
@@ -838,8 +839,6 @@ __global__ __launch_bounds__(256) void oct_mom_apply(const double4 *__restrict__
 
 // ---- Octal records and the record traversal (the 2-D design of bhtree.hip:
 // quad records + batched record fetches, with the narrow lane layout).
-constexpr double OACC_MARGIN = 2.5e-14;   // sure-accept bound margin (bhtree.hpp QACC_MARGIN)
-constexpr double OACC_BAND = (1.0 - OACC_MARGIN) / (1.0 + OACC_MARGIN);
 
 // One thread per binary node: the record of every real cell (h >= 0, no key
 // tie); its children found through <= 2 levels of transparent nodes, in key
@@ -873,17 +872,17 @@ __global__ __launch_bounds__(OREC_BLK) void build_orec(const OctNode *__restrict
                 if (c < 0) {
                     const double4 p = pos[~c];
                     r.ccx[nc] = p.x; r.ccy[nc] = p.y; r.ccz[nc] = p.z;
-                    r.ch[nc] = 0.0; r.ca[nc] = 0.0; r.cref[nc] = c; r.ccnt[nc] = 1;
+                    r.cb[nc] = 0.0; r.ca[nc] = 0.0; r.cref[nc] = c; r.ccnt[nc] = 1;
                     kinds |= OK_LEAF << (2 * nc);
                 } else {
                     const OctNode &cn = nodes[c];
                     r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; r.ccz[nc] = cn.cz;
                     r.cref[nc] = c; r.ccnt[nc] = cn.cnt;
                     if (cn.delta >= 63) {
-                        r.ch[nc] = 0.0; r.ca[nc] = 0.0;
+                        r.cb[nc] = 0.0; r.ca[nc] = 0.0;
                         kinds |= OK_TIE << (2 * nc);
                     } else {
-                        r.ch[nc] = cn.h; r.ca[nc] = cn.h * inv_theta * (1.0 + OACC_MARGIN);
+                        r.cb[nc] = qacc_open(cn.h, inv_theta); r.ca[nc] = qacc_accept(cn.h, inv_theta);
                         kinds |= OK_CELL << (2 * nc);
                     }
                 }
@@ -907,7 +906,7 @@ __global__ __launch_bounds__(OREC_BLK) void build_orec(const OctNode *__restrict
                 }
             }
             for (int k = nc; k < 8; ++k) {
-                r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ccz[k] = 0.0; r.ch[k] = 0.0; r.ca[k] = 0.0;
+                r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.ccz[k] = 0.0; r.cb[k] = 0.0; r.ca[k] = 0.0;
                 r.cref[k] = 0; r.ccnt[k] = 0;
             }
             // a tile test can pass here unless the box's half-diagonal alone
@@ -1065,20 +1064,24 @@ __global__ __launch_bounds__(256) void oct_traverse_rec(
                 const bool taken = mq || dense;
                 if (taken && c == 0 && s >= a && s <= b) zs -= (double)ndup;   // the query's own copies add 1 each
                 if (DBG && dense && c == 0) d_dense += (unsigned long long)(b - a + 1);
-                int p = dense ? a + c : 1, last = dense ? b : 0;
-                while (__ballot(p <= last)) {
-                    if (p <= last) {
+                // the query's 8 lanes split the points; summed apart in a divergent
+                // do-while (no merge of the accumulators per point), added once
+                double ux = 0.0, uy = 0.0, uz = 0.0, uq = 0.0;
+                if (dense && a + c <= b) {
+                    int p = a + c;
+                    do {
                         const double4 pp = pos[p];
                         const double dx = qx - pp.x, dy = qy - pp.y, dz = qz - pp.z;
                         const double rr = rcp2(__fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0))));
                         const double sc = rr * rr;
-                        fx = __fma_rn(sc, dx, fx);
-                        fy = __fma_rn(sc, dy, fy);
-                        fz = __fma_rn(sc, dz, fz);
-                        zs += rr;
+                        ux = __fma_rn(sc, dx, ux);
+                        uy = __fma_rn(sc, dy, uy);
+                        uz = __fma_rn(sc, dz, uz);
+                        uq += rr;
                         p += 8;
-                    }
+                    } while (p <= b);
                 }
+                if (dense) { fx += ux; fy += uy; fz += uz; zs += uq; }
                 act = act && !taken;
             }
             if (__ballot(act) == 0) continue;
@@ -1088,16 +1091,16 @@ __global__ __launch_bounds__(256) void oct_traverse_rec(
             const bool has = act && c < nch;
             if (DBG && has) ++d_childs;
             const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c], dz = qz - nd.ccz[c];
-            const double D = __fma_rn(dx, dx, __fma_rn(dy, dy, dz * dz));
+            const double D1 = __fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0)));   // 1 + D (QACC_BAND)
             const bool isleaf = has && kind == OK_LEAF, iscell = has && kind == OK_CELL;
-            const double A = nd.ca[c];
-            bool acc = D > A;
-            if (iscell && !acc && !(D < A * OACC_BAND))
-                acc = nd.ch[c] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) < theta;
+            bool acc = D1 > nd.ca[c];
+            if (iscell && !acc && !(D1 < nd.cb[c]))
+                acc = nodes[nd.cref[c]].h / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
+                      theta;
             const bool takel = isleaf && !(dx == 0.0 && dy == 0.0 && dz == 0.0);
             const bool takec = iscell && acc;
             const double wm = takel ? 1.0 : (takec ? (double)nd.ccnt[c] : 0.0);
-            const double Qv = rcp2(1.0 + D);
+            const double Qv = rcp2(D1);
             const double mult = wm * Qv;
             const double sc = mult * Qv;
             fx = __fma_rn(sc, dx, fx);
@@ -1316,32 +1319,34 @@ __global__ __launch_bounds__(256) void oct_traverse64(
                 const int kind = (kinds >> (2 * c)) & 3;   // uniform: scalar branches
                 if (kind == OK_TIE) continue;                // after the loop (rare)
                 const double dx = qx - nd.ccx[c], dy = qy - nd.ccy[c], dz = qz - nd.ccz[c];
-                const double D = __fma_rn(dx, dx, __fma_rn(dy, dy, dz * dz));
+                const double D1 = __fma_rn(dx, dx, __fma_rn(dy, dy, __fma_rn(dz, dz, 1.0)));   // 1 + D (QACC_BAND)
+                // lane predicates from scalar masks (inverse ballots: no VALU),
+                // the masks straight from the compares, as in bh_traverse
                 double wm;
                 if (kind == OK_LEAF) {
-                    wm = (act && !(dx == 0.0 && dy == 0.0 && dz == 0.0)) ? 1.0 : 0.0;
+                    const uint64_t takem = amask & ~(__builtin_amdgcn_ballot_w64(dx == 0.0) &
+                                                     __builtin_amdgcn_ballot_w64(dy == 0.0) &
+                                                     __builtin_amdgcn_ballot_w64(dz == 0.0));
+                    wm = __builtin_amdgcn_inverse_ballot_w64(takem) ? 1.0 : 0.0;
                 } else {
-                    // the masks straight from the compares (scalar: a ballot of a
-                    // combined bool costs two VALU per child, as in bh_traverse)
-                    const double A = nd.ca[c];
-                    bool acc = D > A;
-                    uint64_t accm = __builtin_amdgcn_ballot_w64(D > A);
-                    const uint64_t band = amask & ~accm & ~__builtin_amdgcn_ballot_w64(D < A * OACC_BAND);
+                    uint64_t accm = __builtin_amdgcn_ballot_w64(D1 > nd.ca[c]);
+                    const uint64_t band = amask & ~accm & ~__builtin_amdgcn_ballot_w64(D1 < nd.cb[c]);
                     if (band) {   // rare: inside the band the exact IEEE quotient decides
-                        const bool inb = (band >> lane) & 1ull;
-                        if (inb)
-                            acc = nd.ch[c] / __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
+                        bool acc = false;
+                        if (__builtin_amdgcn_inverse_ballot_w64(band))
+                            acc = nodes[nd.cref[c]].h /
+                                      __dadd_rn(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)), __dmul_rn(dz, dz)) <
                                   theta;
-                        accm |= __ballot(inb && acc);
+                        accm |= band & __builtin_amdgcn_ballot_w64(acc);
                     }
-                    wm = (act && acc) ? (double)nd.ccnt[c] : 0.0;
+                    wm = (double)(__builtin_amdgcn_inverse_ballot_w64(amask & accm) ? nd.ccnt[c] : 0);
                     const uint64_t om = amask & ~accm;
                     if (om) {
                         if (lane == 0) { sref[w][sp] = nd.cref[c]; smask[w][sp] = om; }
                         ++sp;
                     }
                 }
-                const double Qv = rcp2(1.0 + D);
+                const double Qv = rcp2(D1);
                 const double mult = wm * Qv;
                 const double sc = mult * Qv;
                 fx = __fma_rn(sc, dx, fx);
@@ -1355,7 +1360,7 @@ __global__ __launch_bounds__(256) void oct_traverse64(
                     const OctNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
                     for (int p = tn.first; p <= tn.last; ++p) {
                         const double4 pp = pos[p];
-                        if (act) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
+                        if (__builtin_amdgcn_inverse_ballot_w64(amask)) leaf3(qx, qy, qz, pp.x, pp.y, pp.z, fx, fy, fz, zs);
                     }
                 }
             }

@@ -43,7 +43,8 @@ struct __attribute__((aligned(16))) ORec {
     int32_t first, last, cnt, nch;         // leaf range, cumSize, children | ONCH_TILE
     int32_t kinds, pad;
     double ccx[8], ccy[8], ccz[8];         // child centres of mass (leaf: the point)
-    double ch[8], ca[8];                   // child half widths, sure-accept bounds ch / theta (1 + 2.5e-14)
+    double cb[8], ca[8];                   // cells: sure-open / sure-accept bounds on 1 + D (bhtree.hpp QACC_BAND:
+                                           // qacc_open / qacc_accept; the band's exact quotient reads h from the node)
     int32_t cref[8], ccnt[8];
 };
 static_assert(sizeof(ORec) % 16 == 0, "records are fetched in 16-byte pieces");

@@ -21,8 +21,8 @@
 // iterations the current Morton order of the embedding when that keeps more
 // of P's edges local -- rows consecutive in memory gather Y_j from nearby
 // labels, so the CSR attraction's gathers hit the L2.  Rank r owns a range of
-// labels (cost-balanced cuts at relabels).  The caller's Y is rewritten in
-// the original order after every step; upd / gains on tsne_dev_opt_sync.
+// labels (cost-balanced cuts at relabels).  The caller's Y, upd and gains
+// are written back in the original order by tsne_dev_opt_sync.
 #include <hipcub/hipcub.hpp>
 
 #include "bhtree.hpp"
@@ -686,7 +686,7 @@ __global__ void at_ranges(const ATile *__restrict__ tiles, int32_t nt, int64_t n
 // per row, all accesses coalesced except F[inv[i]] (near-identity gather).
 // With `mpart` (MODE 1) each block also writes the sum of its rows' Ynew
 // (x, y) to mpart[2 * block]: the centring mean's partials, fused into the
-// update so that centerEmbedding costs one more pass (center_scatter); the
+// update so that centerEmbedding costs one more pass (center2); the
 // mean itself is mean2_final (finalising it in the last block instead saved a
 // launch but cost 3,907 same-address arrival atomics: 0.062 -> 0.085 ms).
 template <int MODE>
@@ -751,20 +751,16 @@ __global__ __launch_bounds__(256) void mean2_final(const double *__restrict__ mp
     if (threadIdx.x < 2) mean[threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3])) / n;
 }
 
-// centerEmbedding (TsneHelpers.scala:320-329) fused with the write-back of
-// the caller's embedding in the original point order: Y = Ynew - mean,
-// Yu[orig[i]] = Y[i].
-__global__ __launch_bounds__(256) void center_scatter(const double *__restrict__ Ynew, const int32_t *__restrict__ orig,
-                                                      int64_t n, const double *__restrict__ mean,
-                                                      double *__restrict__ Y, double *__restrict__ Yu) {
+// centerEmbedding (TsneHelpers.scala:320-329): Y = Ynew - mean, label order.
+// The caller's copy (original point order) is written by tsne_dev_opt_sync
+// (opt_sync), not here: its scattered 16-byte writes were a third of the
+// update's HBM traffic per iteration (round 4: 69 of 250 MB).
+__global__ __launch_bounds__(256) void center2(const double *__restrict__ Ynew, int64_t n,
+                                               const double *__restrict__ mean, double *__restrict__ Y) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double2 v = *reinterpret_cast<const double2 *>(Ynew + 2 * i);
-    const double2 y = make_double2(v.x - mean[0], v.y - mean[1]);
-    *reinterpret_cast<double2 *>(Y + 2 * i) = y;
-    const int64_t o = orig[i];   // the caller's buffer: 8-byte alignment only
-    Yu[2 * o] = y.x;
-    Yu[2 * o + 1] = y.y;
+    *reinterpret_cast<double2 *>(Y + 2 * i) = make_double2(v.x - mean[0], v.y - mean[1]);
 }
 
 __global__ void center_apply(const double *__restrict__ src, int64_t n, int32_t c,
@@ -1131,16 +1127,13 @@ __global__ __launch_bounds__(256) void mean3_final(const double *__restrict__ mp
         mean[threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + (sm[threadIdx.x][2] + sm[threadIdx.x][3])) / n;
 }
 
-// centerEmbedding (TsneHelpers.scala:320-329) + the caller's copy (3-D: the
-// labels are the original indices): Y = Yu = Ynew - mean
-__global__ __launch_bounds__(256) void center3_scatter(const double *__restrict__ Ynew, int64_t n,
-                                                       const double *__restrict__ mean, double *__restrict__ Y,
-                                                       double *__restrict__ Yu) {
+// centerEmbedding (TsneHelpers.scala:320-329), 3-D: Y = Ynew - mean (the
+// caller's copy at tsne_dev_opt_sync, as in 2-D)
+__global__ __launch_bounds__(256) void center3(const double *__restrict__ Ynew, int64_t n,
+                                               const double *__restrict__ mean, double *__restrict__ Y) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= 3 * n) return;
-    const double v = Ynew[e] - mean[e % 3];
-    Y[e] = v;
-    Yu[e] = v;
+    Y[e] = Ynew[e] - mean[e % 3];
 }
 
 static int64_t attract3_blocks(int64_t rows) { return std::max<int64_t>(1, std::min<int64_t>(8192, ceil_div(rows, 4))); }
@@ -1887,7 +1880,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[4], st));
     ctx->timers.begin("opt.update", st);
     // one rank: the mean's block partials from combine_update3, one
-    // workgroup for the mean, one pass for centre + the caller's copy
+    // workgroup for the mean, one pass for the centring
     const bool fused_mean = !sharded(ctx);
     if (s->L1 > s->L0)
         hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->L1 - s->L0, 256)), dim3(256), 0, st, s->L0, s->L1,
@@ -1898,8 +1891,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     if (fused_mean) {
         hipLaunchKernelGGL(mean3_final, dim3(1), dim3(256), 0, st, s->mpart, ceil_div(s->L1 - s->L0, 256), (double)n,
                            s->scal + 2);
-        hipLaunchKernelGGL(center3_scatter, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, s->scal + 2, Y,
-                           s->Yu);
+        hipLaunchKernelGGL(center3, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, s->scal + 2, Y);
     } else {
         gather_Ynew(ctx, s);
         for (int k = 0; k < 3; ++k) {
@@ -1907,7 +1899,6 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
             hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 2 + k, (double)n);
         }
         hipLaunchKernelGGL(center_apply, dim3(ceil_div(n * 3, 256)), dim3(256), 0, st, s->Ynew, n, 3, s->scal + 2, Y);
-        TSNE_HIP(hipMemcpyAsync(s->Yu, Y, sizeof(double) * 3 * n, hipMemcpyDeviceToDevice, st));
     }
     ctx->timers.end("opt.update", st);
     TSNE_LAUNCH_CHECK();
@@ -2164,8 +2155,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
             hipLaunchKernelGGL(reduce_final, dim3(1), dim3(256), 0, st, s->part2, NPART, s->scal + 2 + k, (double)n);
         }
     }
-    hipLaunchKernelGGL(center_scatter, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Ynew, s->orig[c], n, s->scal + 2,
-                       Y, s->Yu);
+    hipLaunchKernelGGL(center2, dim3(ceil_div(n, 256)), dim3(256), 0, st, s->Ynew, n, s->scal + 2, Y);
     ctx->timers.end("opt.update", st);
     TSNE_LAUNCH_CHECK();
     if (check_relabel) maybe_relabel(ctx, s);
