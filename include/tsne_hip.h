@@ -202,6 +202,9 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *                        traversal stack pops (wave level), child slots
  *                        evaluated (wave level), tile points, and
  *                        reference-equivalent node evaluations;
+ *   "bh.wave_ticks_max", "bh.wave_ticks_sum", "bh.span_ticks"  (rep_stats) the
+ *                        traversal waves' longest and summed run time and
+ *                        the grid's span, in 100 MHz ticks (both layouts);
  *   "comm.kind"          the context's communicator: 0 none, 1 RCCL, 2 loopback,
  *                        3 caller callbacks; "comm.calls" collectives it issued;
  *   "opt.attract_kernel" the optimizer's attraction kernel: 0 attract_rows,

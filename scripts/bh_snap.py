@@ -65,7 +65,8 @@ def main():
             if a.stats and Y.shape[1] == 2 and ctx_has_option(ctx, "rep_stats"):
                 ctx.set_option("rep_stats", 1)
                 ctx.dev_repulsion(Y, a.theta, F, z)
-                for k in ("pops", "child_slots", "tile_points", "visits"):
+                for k in ("pops", "child_slots", "tile_points", "visits", "wave_ticks_max", "wave_ticks_sum",
+                          "span_ticks"):
                     rec[k] = ctx.counter("bh." + k)
                 ctx.set_option("rep_stats", 0)
             print(json.dumps(rec), flush=True)

@@ -1338,14 +1338,16 @@ bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) 
     // indices of bh_traverse's counters (its STATS block): wave pops, tile
     // points, wave child slots, reference-equivalent evaluations
     const int at = name == "bh.pops" ? 3 : name == "bh.tile_points" ? 4 : name == "bh.child_slots" ? 6
-                 : name == "bh.visits" ? 0 : -1;
+                 : name == "bh.visits" ? 0 : name == "bh.wave_ticks_max" ? 15 : name == "bh.wave_ticks_sum" ? 18
+                 : name == "bh.span_ticks" ? 17 : -1;
     if (at < 0) return false;
     TSNE_REQUIRE(ctx->opts.rep_stats && ctx->ws.has("rep.visits"), "counter '" + name + "' needs option rep_stats");
     unsigned long long v[32];
     TSNE_HIP(hipMemcpyAsync(v, ctx->ws.get<unsigned long long>("rep.visits", 32), sizeof(v), hipMemcpyDeviceToHost,
                             ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
-    *value_out = (int64_t)v[at];
+    // span: last wave end - first wave start ([16] holds ~first start), 100 MHz ticks
+    *value_out = at == 17 ? (int64_t)(v[17] - (~0ull - v[16])) : (int64_t)v[at];
     return true;
 }
 
