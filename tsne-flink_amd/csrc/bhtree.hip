@@ -563,7 +563,6 @@ __global__ __launch_bounds__(256) void bottom_up_top(const double2 *__restrict__
     }
 }
 
-
 // 1/x for the BH terms: v_rcp_f64 + one Newton step, within 11 ulp of the
 // IEEE quotient over the whole range (scripts/rcp_accuracy.hip: rcp alone
 // 2.5e8 ulp, one step 11, two steps 0) -- ~2e-15 relative per term, far
