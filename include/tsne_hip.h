@@ -205,6 +205,11 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *   "bh.wave_ticks_max", "bh.wave_ticks_sum", "bh.span_ticks"  (rep_stats) the
  *                        traversal waves' longest and summed run time and
  *                        the grid's span, in 100 MHz ticks (both layouts);
+ *   "bh.dense_pairs", "bh.moment_evals", "bh.tile_steps0".."bh.tile_steps3",
+ *   "bh.tile_pairs0".."bh.tile_pairs3"  (rep_stats) exact-sum work: pair terms,
+ *                        moment evaluations, and per dense path of tile_apply
+ *                        (lane-wise, packed, query-major, staged sweep) the
+ *                        wave steps issued and the useful lane pairs;
  *   "comm.kind"          the context's communicator: 0 none, 1 RCCL, 2 loopback,
  *                        3 caller callbacks; "comm.calls" collectives it issued;
  *   "opt.attract_kernel" the optimizer's attraction kernel: 0 attract_rows,

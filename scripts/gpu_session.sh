@@ -2,7 +2,8 @@
 # under its own time limit, outputs under gpurun_out/r${ROUND:-5}$TAG/:
 #   driver      bench.py exactly as the driver runs it (--gpus 1 --steps 20 --warmup 5, CPU baseline included)
 #   mksnaps     bench.py --dump-y 250,450,650 into /tmp/snaps (the snapshots the snap steps read)
-#   snap        bh_snap.py on snaps/Y_t{250,450,650}.npy per SNAP_VARS entry ("-" = defaults, else KEY=VALUE)
+#   snap        bh_snap.py on snaps/Y_t{250,450,650}.npy per SNAP_VARS entry ("-" = defaults, else KEY=VALUE;
+#               SNAP_ARGS: more bh_snap arguments, e.g. --stats)
 #   tests_narrow / tests3d / tests_all   GPU test subsets / the whole -m gpu suite
 #   bench / bench4   bench.py (C3 / C4) per BENCH_VARS / BENCH4_VARS entry
 #   ktrace      rocprofv3 --kernel-trace --stats of the default bench (KTRACE_ARGS)
@@ -35,7 +36,7 @@ if has snap; then
   for v in ${SNAP_VARS:--}; do
     opt=""; [ "$v" != "-" ] && opt="--option $v"
     echo "# $v" >> $O/snap.jsonl
-    run 300 python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t450.npy $SN/Y_t650.npy $opt >> $O/snap.jsonl 2>> $O/snap.err || exit $?
+    run 300 python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t450.npy $SN/Y_t650.npy $opt ${SNAP_ARGS:-} >> $O/snap.jsonl 2>> $O/snap.err || exit $?
   done
 fi
 if has tests_narrow; then

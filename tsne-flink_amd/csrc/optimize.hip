@@ -1339,15 +1339,20 @@ bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) 
     // points, wave child slots, reference-equivalent evaluations
     const int at = name == "bh.pops" ? 3 : name == "bh.tile_points" ? 4 : name == "bh.child_slots" ? 6
                  : name == "bh.visits" ? 0 : name == "bh.wave_ticks_max" ? 15 : name == "bh.wave_ticks_sum" ? 18
-                 : name == "bh.span_ticks" ? 17 : -1;
-    if (at < 0) return false;
+                 : name == "bh.span_ticks" ? 17 : name == "bh.dense_pairs" ? 2 : name == "bh.moment_evals" ? 1 : -1;
+    // tile_apply's dense paths k = 0..3 (lane-wise, packed, query-major, staged
+    // sweep): "bh.tile_steps<k>" wave steps issued, "bh.tile_pairs<k>" useful lane pairs
+    int atk = at;
+    if (at < 0 && name.size() == 14 && name.compare(0, 13, "bh.tile_steps") == 0) atk = 24 + 2 * (name[13] - '0');
+    if (at < 0 && name.size() == 14 && name.compare(0, 13, "bh.tile_pairs") == 0) atk = 25 + 2 * (name[13] - '0');
+    if (atk < 0 || atk > 31) return false;
     TSNE_REQUIRE(ctx->opts.rep_stats && ctx->ws.has("rep.visits"), "counter '" + name + "' needs option rep_stats");
     unsigned long long v[32];
     TSNE_HIP(hipMemcpyAsync(v, ctx->ws.get<unsigned long long>("rep.visits", 32), sizeof(v), hipMemcpyDeviceToHost,
                             ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     // span: last wave end - first wave start ([16] holds ~first start), 100 MHz ticks
-    *value_out = at == 17 ? (int64_t)(v[17] - (~0ull - v[16])) : (int64_t)v[at];
+    *value_out = atk == 17 ? (int64_t)(v[17] - (~0ull - v[16])) : (int64_t)v[atk];
     return true;
 }
 
