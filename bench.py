@@ -317,6 +317,7 @@ def main():
     t_loop = max_over_ranks(time.perf_counter() - t0, world)
     t0 = time.perf_counter()
     losses = ctx.dev_opt_losses()
+    csort_over = ctx.counter("opt.csort_oversized_total") if C == 2 else None   # the timed run's sorts
     ctx.dev_opt_sync()   # the working set back to the caller's buffers (collective), timed with the D2H
     Y_final = Y[:n].cpu().numpy() if rank == 0 else None   # noqa: F841 (the D2H of the result, timed)
     t_out = time.perf_counter() - t0
@@ -440,7 +441,8 @@ def main():
         "bh": {"kernel_ms_traced": r4(bh_ms_sum),
                "pops_per_s": r4(bh_rate("pops")), "lane_child_evals_per_s": r4(bh_rate("child_evals")),
                "dense_pair_terms_per_s": r4(bh_rate("dense_pairs")),
-               "moment_evals_per_s": r4(bh_rate("moment_evals"))},
+               "moment_evals_per_s": r4(bh_rate("moment_evals")),
+               "csort_oversized_total": csort_over},
         "detail": detail_path,
     }
     detail = {"window_profile": window_profile, "timeline": timeline,

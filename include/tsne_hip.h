@@ -214,6 +214,7 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *                        3 caller callbacks; "comm.calls" collectives it issued;
  *   "opt.attract_kernel" the optimizer's attraction kernel: 0 attract_rows,
  *                        1 attract_tiles, 2 attract3 (3-D), -1 no optimizer;
+ *   "opt.csort_oversized_total"  the same summed over every build of the optimizer's tree;
  *   "bh.csort_oversized", "opt.csort_oversized"  buckets of the last coherent
  *                        Morton sort (csort.hpp) beyond its LDS capacity. */
 int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);

@@ -393,6 +393,8 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         else if (k == "comm.kind") *value_out = comm_counter(ctx, false);
         else if (k == "comm.calls") *value_out = comm_counter(ctx, true);
         else if (k == "opt.csort_oversized") *value_out = opt_tree(ctx) ? csort_oversized(ctx, opt_tree(ctx)->cs) : 0;
+        else if (k == "opt.csort_oversized_total")
+            *value_out = opt_tree(ctx) ? csort_oversized(ctx, opt_tree(ctx)->cs, true) : 0;
         else fail(TSNE_ERR_ARG, "unknown counter '" + k + "'");
     });
 }

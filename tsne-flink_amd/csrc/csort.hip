@@ -172,7 +172,7 @@ __global__ __launch_bounds__(1024) void cs_scan(const int32_t *__restrict__ cnt,
     }
     if (t == 1023) off[P] = s[1023];
     __syncthreads();
-    if (t == 0) stat[0] = nover;
+    if (t == 0) { stat[0] = nover; stat[1] += nover; }   // the last sort's, and the running total
 }
 
 __global__ __launch_bounds__(CS_BLK) void cs_scatter(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
@@ -256,14 +256,14 @@ void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &
     cs.bkt = ws.get<int32_t>(pre + "cs.bkt", n);
     cs.kb = ws.get<uint64_t>(pre + "cs.kb", 3 * (size_t)n);
     cs.vb = ws.get<int32_t>(pre + "cs.vb", 3 * (size_t)n);
-    cs.stat = ws.get<int32_t>(pre + "cs.stat", 1);
-    TSNE_HIP(hipMemsetAsync(cs.stat, 0, sizeof(int32_t), ctx->stream));
+    cs.stat = ws.get<int32_t>(pre + "cs.stat", 2);
+    TSNE_HIP(hipMemsetAsync(cs.stat, 0, 2 * sizeof(int32_t), ctx->stream));
 }
 
-int64_t csort_oversized(tsne_ctx *ctx, const CoherentSort &cs) {
+int64_t csort_oversized(tsne_ctx *ctx, const CoherentSort &cs, bool total) {
     if (cs.P <= 0 || !cs.stat) return 0;
     int32_t h = 0;
-    TSNE_HIP(hipMemcpyAsync(&h, cs.stat, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipMemcpyAsync(&h, cs.stat + (total ? 1 : 0), sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     return h;
 }

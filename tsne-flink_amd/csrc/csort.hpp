@@ -28,7 +28,7 @@ struct CoherentSort {
     uint64_t *kb = nullptr;         // 3n: bucketed keys [0, n), then the oversized buckets' scratch
                                     // (bucket at offset o: [n + 2 o, n + 2 o + 2 m), power-of-two padded)
     int32_t *vb = nullptr;          // 3n: bucketed point indices, the same layout
-    int32_t *stat = nullptr;        // [0] oversized buckets of the last sort (diagnostics)
+    int32_t *stat = nullptr;        // [0] oversized buckets of the last sort, [1] their running total (diagnostics)
 };
 
 // Buffers for n points (ctx workspace, names pre + field).  n outside
@@ -44,7 +44,8 @@ void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &
 // it may be the same buffer as idx_sorted (read before it is written).
 void csort_run(tsne_ctx *ctx, CoherentSort &cs, const uint64_t *keys, const int32_t *prev_idx_sorted,
                uint64_t *keys_sorted, int32_t *idx_sorted, hipStream_t st);
-// Oversized buckets of the last csort_run (synchronises the context's stream; 0 if none ran).
-int64_t csort_oversized(tsne_ctx *ctx, const CoherentSort &cs);
+// Oversized buckets of the last csort_run, or (total) of every run since the
+// allocation (synchronises the context's stream; 0 if none ran).
+int64_t csort_oversized(tsne_ctx *ctx, const CoherentSort &cs, bool total = false);
 
 }  // namespace tsne
