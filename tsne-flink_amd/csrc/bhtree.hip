@@ -1467,128 +1467,122 @@ __device__ __forceinline__ void cell_force(double dx, double dy, double D, int32
     zs += mult;
 }
 
-// Quad records: one per real node, children found through transparent nodes.
-// Records are assembled in LDS and written out as one contiguous, coalesced
-// 16-byte-per-lane copy of the workgroup's 256 slots (208-byte records
-// written field by field from each lane touched 64 cache lines per store).
-// Slots of transparent nodes receive don't-care bytes: only real cells are
-// ever pushed (and their records read) by the traversal.
-constexpr int QREC_BLK = 64;   // one wave: 15 KB of LDS staging, many workgroups per CU to overlap the node loads
+// Quad records: one per real node, children found through transparent nodes
+// (build_qrec below).  Slots of transparent nodes are never written: only
+// real cells are ever pushed (and their records read) by the traversal.
 struct DupView {   // duplicate-multiplicity data for build_qrec (nullptr members when there is none)
     const int32_t *tiecnt, *notile, *vflag, *vcntf;
     const double *vcom;
     int32_t virt;   // record index offset of the virtual chain tops (= n)
 };
-__device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos, int i,
-                               double inv_theta, double near_dmax, const DupView &dv, QRec &r);
-__global__ __launch_bounds__(QREC_BLK) void build_qrec(const BHNode *__restrict__ nodes,
-                                                       const double2 *__restrict__ pos,
-                                                       const int32_t *__restrict__ meta, double inv_theta,
-                                                       double near_dmax, const int32_t *__restrict__ dflag,
-                                                       DupView dv, QRec *__restrict__ qrec) {
-    __shared__ QRec srec_out[QREC_BLK];
-    __shared__ int32_t sreal[QREC_BLK];
+__device__ __forceinline__ void build_qrec_reg(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos, int i,
+                                               double inv_theta, double near_dmax, const DupView &dv, QRec &r);
+// One thread per binary node: it builds its record in registers
+// (build_qrec_reg) and writes it as 16 contiguous 16-byte stores (the partial
+// lines of a wave's stores merge in the L2), so the occupancy is set by
+// registers -- an LDS-staged version (coalesced copies of 64 records per
+// workgroup, 16 KB of LDS each) took 103 us at C3, this one 87 us (round 5).
+__global__ __launch_bounds__(256) void build_qrec(const BHNode *__restrict__ nodes,
+                                                         const double2 *__restrict__ pos,
+                                                         const int32_t *__restrict__ meta, double inv_theta,
+                                                         double near_dmax, const int32_t *__restrict__ dflag,
+                                                         DupView dv, QRec *__restrict__ qrec) {
     const int m = meta[0];
-    const int b0 = blockIdx.x * QREC_BLK;
-    const int nrec = min(QREC_BLK, m - 1 - b0);   // uniform over the workgroup
-    if (nrec <= 0) return;
-    const int i = b0 + threadIdx.x;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m - 1) return;
     const bool dups = dflag[0] != 0;
     if (!dups) dv = DupView{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
-    if (threadIdx.x < nrec) {
-        sreal[threadIdx.x] = nodes[i].h >= 0.0;   // transparent / key-tie nodes get no record
-        build_qrec_one(nodes, pos, i, inv_theta, near_dmax, dv, srec_out[threadIdx.x]);
-        if (dups && dv.vflag[i]) {   // node i's chain top C_1: one child, node i itself (cells C_2..C_k)
-            const BHNode &nd = nodes[i];
-            QRec v;
-            v.cx = dv.vcom[2 * i]; v.cy = dv.vcom[2 * i + 1]; v.rball = 0.0;
-            v.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
-            v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
-            v.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
-            v.lmask = 0;
-            v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
-            v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.cref[0] = i; v.ccnt[0] = nd.cnt;
-            v.ca[0] = qacc_accept(nd.h, inv_theta);
-            v.cb[0] = qacc_open(nd.h, inv_theta);
-            for (int k = 1; k < 4; ++k) {
-                v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.cb[k] = 0.0; v.ca[k] = 0.0; v.cref[k] = 0; v.ccnt[k] = 0;
-            }
-            qrec[dv.virt + i] = v;
-        }
+    if (nodes[i].h >= 0.0) {   // transparent / key-tie nodes get no record
+        QRec r;
+        build_qrec_reg(nodes, pos, i, inv_theta, near_dmax, dv, r);
+        const uint4 *src = reinterpret_cast<const uint4 *>(&r);
+        uint4 *dst = reinterpret_cast<uint4 *>(qrec + i);
+#pragma unroll
+        for (int k = 0; k < (int)(sizeof(QRec) / 16); ++k) dst[k] = src[k];
     }
-    __syncthreads();
-    constexpr int V = sizeof(QRec) / 16;
-    const uint4 *src = reinterpret_cast<const uint4 *>(srec_out);
-    uint4 *dst = reinterpret_cast<uint4 *>(qrec + b0);
-    for (int k = threadIdx.x; k < nrec * V; k += QREC_BLK)
-        if (sreal[k / V]) dst[k] = src[k];
+    if (dups && dv.vflag[i]) {   // node i's chain top C_1 (as build_qrec)
+        const BHNode &nd = nodes[i];
+        QRec v;
+        v.cx = dv.vcom[2 * i]; v.cy = dv.vcom[2 * i + 1]; v.rball = 0.0;
+        v.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
+        v.bx0 = nd.bx0; v.bx1 = nd.bx1; v.by0 = nd.by0; v.by1 = nd.by1;
+        v.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
+        v.lmask = 0;
+        v.first = nd.first; v.last = nd.last; v.cnt = dv.vcntf[i]; v.nch = 1;
+        v.ccx[0] = nd.cx; v.ccy[0] = nd.cy; v.cref[0] = i; v.ccnt[0] = nd.cnt;
+        v.ca[0] = qacc_accept(nd.h, inv_theta);
+        v.cb[0] = qacc_open(nd.h, inv_theta);
+        for (int k = 1; k < 4; ++k) {
+            v.ccx[k] = 0.0; v.ccy[k] = 0.0; v.cb[k] = 0.0; v.ca[k] = 0.0; v.cref[k] = 0; v.ccnt[k] = 0;
+        }
+        qrec[dv.virt + i] = v;
+    }
 }
 
-__device__ void build_qrec_one(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos, int i,
-                               double inv_theta, double near_dmax, const DupView &dv, QRec &r) {
+// One quad record, every array of it indexed by compile-time constants (the
+// children's refs collected first, then one unrolled slot per child), so that
+// the record stays in registers (build_qrec).
+__device__ __forceinline__ void build_qrec_reg(const BHNode *__restrict__ nodes, const double2 *__restrict__ pos, int i,
+                                               double inv_theta, double near_dmax, const DupView &dv, QRec &r) {
     const int32_t *tiecnt = dv.tiecnt, *notile = dv.notile;
     const BHNode &nd = nodes[i];
-    if (nd.h < 0.0) return;                 // transparent or key tie: no record
-    // the traversal's all-open thresholds, precomputed (see QRec)
     r.cx = nd.cx; r.cy = nd.cy; r.rball = nd.rball * nd.rball * (1.0 - 1e-9);
     r.hmin = fmax(nd.hmin * inv_theta * (1.0 - 1e-12), near_dmax) * (1.0 - 1.1e-12);
     r.bx0 = nd.bx0; r.bx1 = nd.bx1; r.by0 = nd.by0; r.by1 = nd.by1;
     r.ex = 1e-15 * (fabs(nd.bx0) + fabs(nd.bx1) + fabs(nd.by0) + fabs(nd.by1));
     r.lmask = 0;
     r.first = nd.first; r.last = nd.last; r.cnt = nd.cnt;
-    // <= 3 transparent nodes per quad level: a 2-deep descent covers them
-    int32_t cand[4] = {nd.left, nd.right, 0, 0};
-    int ncand = 2;
+    auto transparent = [&](int32_t c) { return c >= 0 && nodes[c].delta < 62 && nodes[c].h < 0.0; };
+    // the quad children in key order (<= 4: a 2-deep descent through transparent nodes)
+    int32_t l0 = 0, l1 = 0, l2 = 0, l3 = 0;
     int nc = 0;
-    double ch[4];   // child half widths or kind codes (QCH_*): the kinds below; the traversal reads
-                    // a cell's width only in the rare exact-quotient band (qrec_child_h)
-    auto put = [&](int32_t c) {
-        r.cb[nc] = 0.0; r.ca[nc] = 0.0;
-        if (c < 0) {
-            const double2 p = pos[~c];
-            r.ccx[nc] = p.x; r.ccy[nc] = p.y; ch[nc] = QCH_LEAF; r.cref[nc] = c; r.ccnt[nc] = 1;
-        } else {
-            const BHNode &cn = nodes[c];
-            r.ccx[nc] = cn.cx; r.ccy[nc] = cn.cy; ch[nc] = cn.delta >= 62 ? QCH_TIE : cn.h;
-            r.cref[nc] = c; r.ccnt[nc] = cn.cnt;
-            if (cn.delta >= 62 && tiecnt && tiecnt[c] > 0) {   // pure duplicate group: one leaf, its multiplicity
-                const double2 p = pos[cn.first];
-                r.ccx[nc] = p.x; r.ccy[nc] = p.y; ch[nc] = QCH_MULTI; r.ccnt[nc] = tiecnt[c];
-            } else if (cn.delta < 62 && dv.vflag && dv.vflag[c]) {   // the chain top C_1 of real node c
-                r.ccx[nc] = dv.vcom[2 * c]; r.ccy[nc] = dv.vcom[2 * c + 1]; ch[nc] = 0.5 * nd.h;
-                r.cref[nc] = dv.virt + c; r.ccnt[nc] = dv.vcntf[c];
-            }
-            if (ch[nc] >= 0.0) { r.ca[nc] = qacc_accept(ch[nc], inv_theta); r.cb[nc] = qacc_open(ch[nc], inv_theta); }
-        }
+    auto add = [&](int32_t c) {
+        l3 = nc == 3 ? c : l3; l2 = nc == 2 ? c : l2; l1 = nc == 1 ? c : l1; l0 = nc == 0 ? c : l0;
         ++nc;
     };
-    auto transparent = [&](int32_t c) { return c >= 0 && nodes[c].delta < 62 && nodes[c].h < 0.0; };
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const int32_t c = cand[k];
+        const int32_t c = k == 0 ? nd.left : nd.right;
         if (transparent(c)) {
             const int32_t l = nodes[c].left, rr = nodes[c].right;
-            if (transparent(l)) { put(nodes[l].left); put(nodes[l].right); } else put(l);
-            if (transparent(rr)) { put(nodes[rr].left); put(nodes[rr].right); } else put(rr);
+            if (transparent(l)) { add(nodes[l].left); add(nodes[l].right); } else add(l);
+            if (transparent(rr)) { add(nodes[rr].left); add(nodes[rr].right); } else add(rr);
         } else {
-            put(c);
+            add(c);
         }
     }
-    (void)ncand;
-    for (int k = nc; k < 4; ++k) {
-        r.ccx[k] = 0.0; r.ccy[k] = 0.0; r.cb[k] = 0.0; r.ca[k] = 0.0; r.cref[k] = 0; r.ccnt[k] = 0;
+    int kinds = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int32_t c = k == 0 ? l0 : k == 1 ? l1 : k == 2 ? l2 : l3;
+        double x = 0.0, y = 0.0, cb = 0.0, ca = 0.0;
+        int32_t cref = 0, ccnt = 0;
+        if (k < nc) {
+            double chv;
+            if (c < 0) {
+                const double2 p = pos[~c];
+                x = p.x; y = p.y; chv = QCH_LEAF; cref = c; ccnt = 1;
+            } else {
+                const BHNode &cn = nodes[c];
+                x = cn.cx; y = cn.cy; chv = cn.delta >= 62 ? QCH_TIE : cn.h;
+                cref = c; ccnt = cn.cnt;
+                if (cn.delta >= 62 && tiecnt && tiecnt[c] > 0) {   // pure duplicate group: one leaf, its multiplicity
+                    const double2 p = pos[cn.first];
+                    x = p.x; y = p.y; chv = QCH_MULTI; ccnt = tiecnt[c];
+                } else if (cn.delta < 62 && dv.vflag && dv.vflag[c]) {   // the chain top C_1 of real node c
+                    x = dv.vcom[2 * c]; y = dv.vcom[2 * c + 1]; chv = 0.5 * nd.h;
+                    cref = dv.virt + c; ccnt = dv.vcntf[c];
+                }
+                if (chv >= 0.0) { ca = qacc_accept(chv, inv_theta); cb = qacc_open(chv, inv_theta); }
+            }
+            kinds |= (chv == QCH_LEAF ? QK_LEAF : chv == QCH_TIE ? QK_TIE : chv == QCH_MULTI ? QK_MULTI : QK_CELL)
+                     << (QNCH_KIND + 2 * k);
+        }
+        r.ccx[k] = x; r.ccy[k] = y; r.cb[k] = cb; r.ca[k] = ca; r.cref[k] = cref; r.ccnt[k] = ccnt;
     }
-    // QNCH_TILE: some query could pass an all-open test here.  The box test's
-    // max corner distance is at least the squared half-diagonal, so if that
-    // exceeds both hmin / theta and near_dmax (and rball = 0) no query can.
     const double hx = 0.5 * (nd.bx1 - nd.bx0), hy = 0.5 * (nd.by1 - nd.by0);
     const bool tile_possible = (nd.rball > 0.0 || (hx * hx + hy * hy) * (1.0 - 1e-9) <= fmax(nd.hmin * inv_theta, near_dmax))
-                               && !(notile && notile[i]);   // a duplicate group below: the reference's path
-    int kinds = 0;
-    for (int k = 0; k < nc; ++k) {
-        const double c = ch[k];
-        kinds |= (c == QCH_LEAF ? QK_LEAF : c == QCH_TIE ? QK_TIE : c == QCH_MULTI ? QK_MULTI : QK_CELL) << (QNCH_KIND + 2 * k);
-    }
+                               && !(notile && notile[i]);
     r.nch = nc | (tile_possible ? QNCH_TILE : 0) | kinds;
 }
 
@@ -1728,7 +1722,7 @@ __device__ __forceinline__ void stage_records(LDS &L, int w, int lane, int sp, i
 // The half width of cell child `cref` of record `ref` (flags stripped), for
 // the exact-quotient band (QACC_BAND): a real node's own h, or for the
 // virtual chain top of a duplicate group (cref >= virt) half its parent's
-// (build_qrec_one).  A virtual record's only child is a real node.
+// (build_qrec_reg).  A virtual record's only child is a real node.
 __device__ __forceinline__ double qrec_child_h(const BHNode *__restrict__ nodes, int32_t ref, int32_t cref,
                                                int32_t virt) {
     return cref < virt ? nodes[cref].h : 0.5 * nodes[ref & ~REF_FORCED].h;
@@ -3372,7 +3366,7 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     hipLaunchKernelGGL(dup_apply, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.meta, t.dflag, t.cntcorr, t.sumcorr,
                        t.vflag, t.vcnt, t.vsum, t.vcntf, t.vcom, t.nodes);
     const DupView dv{t.tiecnt, t.notile, t.vflag, t.vcntf, t.vcom, (int32_t)n};
-    hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, QREC_BLK)), dim3(QREC_BLK), 0, st, t.nodes, t.pos, t.meta, inv_theta,
+    hipLaunchKernelGGL(build_qrec, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.nodes, t.pos, t.meta, inv_theta,
                        t.near_dmax, t.dflag, dv, t.qrec);
     // subtree moments for the all-open fast path
     hipLaunchKernelGGL(moment_count, dim3(ceil_div(n + 1, 1024)), dim3(1024), 0, st, t.nodes, n, t.meta, t.mom_flag,
