@@ -405,29 +405,34 @@ __device__ __forceinline__ void bu_leaf(const double2 *__restrict__ pos, int s, 
 // them) and appends the parent to the arrival list of phase 2, as does a leaf
 // whose parent lies outside.  Nothing waits on another workgroup, so a
 // workgroup's run is its own short climb.
+// The climbs run in steps over an LDS queue of arrivals: each step every
+// queued arrival is taken by one thread (the first arriver at a node stops,
+// the second combines it and queues the parent for the next step), so the
+// live climbers are packed into the first waves -- a climb per thread kept
+// all 16 waves issuing every step for their one or two live lanes (round 5:
+// 136 us at C3).  The sums are the same: each node is combined from its two
+// children in a fixed order, whichever thread does it.
 __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restrict__ pos, const int32_t *__restrict__ meta,
                                                         const double *__restrict__ Wp, double inv_theta, BHNode *nodes,
                                                         double *__restrict__ agg, const int32_t *__restrict__ parent_leaf,
                                                         const int32_t *__restrict__ parent_node,
                                                         const int32_t *__restrict__ fstart, int32_t gen,
                                                         int32_t *__restrict__ top_list, int32_t *__restrict__ top_cnt) {
-    // aggregates (sx, sy, x0, x1, y0, y1, hmin, rball), the range's leaf
-    // positions, and the topology of its nodes (ids [S0, S1), Karras: a
-    // node's id lies in its own leaf range: count, children, delta, parent,
-    // whether the node lies inside the range), staged once so that the climb
-    // never waits on global memory (the leaf children's positions were
-    // dependent global loads at every level: the climb's latency)
+    // aggregates (sx, sy, x0, x1, y0, y1, hmin, rball) and the topology of the
+    // range's nodes (ids [S0, S1), Karras: a node's id lies in its own leaf
+    // range: count, children, delta, parent, whether the node lies inside the
+    // range), staged once so that the climb never waits on global memory
     __shared__ double lagg[8][BU_CAP];
-    __shared__ double2 lpos[BU_CAP];
     __shared__ int32_t lleft[BU_CAP], lright[BU_CAP], ldelta[BU_CAP], lcnt[BU_CAP], lpar[BU_CAP];
     __shared__ int32_t larr[BU_CAP];
+    __shared__ int32_t queue[2][BU_CAP];
     __shared__ uint8_t lself[BU_CAP];
-    __shared__ int32_t sS[2];
+    __shared__ int32_t sS[2], qn[2];
     const int m = meta[0];
     const int b = blockIdx.x;
     if (m < 2 || b * BU_NB >= m) return;
     const int t = threadIdx.x;
-    if (t < 2) sS[t] = INT32_MAX;
+    if (t < 2) { sS[t] = INT32_MAX; qn[t] = 0; }
     __syncthreads();
     // a frontier subtree starts within any BU_FRONT + 1 consecutive leaves
     for (int j = t; j < 2 * (BU_FRONT + 1); j += BU_NB) {
@@ -441,7 +446,6 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
     for (int j = t; j < S1 - S0; j += BU_NB) {
         const int q = S0 + j;
         larr[j] = 0;
-        lpos[j] = pos[q];
         if (q < m - 1) {
             const BHNode &nd = nodes[q];
             lleft[j] = nd.left; lright[j] = nd.right; ldelta[j] = nd.delta;
@@ -454,31 +458,34 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
     __syncthreads();
     const double W = *Wp;
     auto in_blk = [&](int q) { return q >= S0 && q < S1 && lself[q - S0]; };
+    // the leaves' arrivals: at a parent in the range (queue 0), or phase 2's
     for (int s = S0 + t; s < S1; s += BU_NB) {
-        int p = parent_leaf[s];
+        const int p = parent_leaf[s];
         if (p < 0) continue;
-        if (!in_blk(p)) {   // a leaf hanging off a node above the frontier
-            top_list[atomicAdd(top_cnt, 1)] = p;
-            continue;
-        }
-        while (true) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (!in_blk(p)) top_list[atomicAdd(top_cnt, 1)] = p;   // a leaf hanging off a node above the frontier
+        else queue[0][atomicAdd(&qn[0], 1)] = p;
+    }
+    int cur = 0;
+    while (true) {
+        __syncthreads();   // the step's queue complete; the other queue empty
+        const int na = qn[cur];
+        if (na == 0) break;
+        const int nxt = cur ^ 1;
+        for (int e = t; e < na; e += BU_NB) {
+            const int p = queue[cur][e];
             const int op = p - S0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (__hip_atomic_fetch_add(&larr[op], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-                break;                                   // first arriver stops
+                continue;                                // first arriver stops
             const int32_t ch[2] = {lleft[op], lright[op]};
             const int32_t dl = ldelta[op];
             double a[2][7], c[2], rb[2];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
-                const int o = (ch[k] < 0 ? ~ch[k] : ch[k]) - S0;   // children of an in-range node are in range
                 if (ch[k] < 0) {
-                    const double2 q = lpos[o];
-                    a[k][0] = q.x; a[k][1] = q.y; a[k][2] = q.x; a[k][3] = q.x; a[k][4] = q.y; a[k][5] = q.y;
-                    a[k][6] = __builtin_inf();
-                    c[k] = 1.0;
-                    rb[k] = __builtin_inf();
-                } else {
+                    bu_leaf(pos, ~ch[k], a[k], c[k], rb[k]);
+                } else {                                 // children of an in-range node are in range
+                    const int o = ch[k] - S0;
 #pragma unroll
                     for (int f = 0; f < 7; ++f) a[k][f] = lagg[f][o];
                     c[k] = (double)lcnt[o];
@@ -492,19 +499,21 @@ __global__ __launch_bounds__(BU_NB) void bottom_up_intra(const double2 *__restri
             double o9[9];
             bu_combine_d(p, a, c, rb, ch, dl, par, pdelta, W, inv_theta, nodes, o9);
             if (pin) {
-                const int o = op;
 #pragma unroll
-                for (int f = 0; f < 7; ++f) lagg[f][o] = o9[f];
-                lagg[7][o] = o9[8];
-                p = par;
+                for (int f = 0; f < 7; ++f) lagg[f][op] = o9[f];
+                lagg[7][op] = o9[8];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                queue[nxt][atomicAdd(&qn[nxt], 1)] = par;
             } else {
                 double *g = agg + AGG * (int64_t)p;
 #pragma unroll
                 for (int f = 0; f < 9; ++f) g[f] = o9[f];
                 if (par >= 0) top_list[atomicAdd(top_cnt, 1)] = par;
-                break;
             }
         }
+        __syncthreads();   // every push of the step done
+        if (t == 0) qn[cur] = 0;   // consumed: the next step's push queue
+        cur = nxt;
     }
 }
 
