@@ -85,26 +85,69 @@ __device__ __forceinline__ void bitonic_k(uint64_t *a, int N) {
 // (the box moves its deep cell boundaries), so the samples there are random
 // ones: 4x oversampling keeps the buckets within ~3.3x of their mean on the
 // C3 snapshots (max 3290 of 1024 at t = 650, CS_CAP 4096).
-__global__ __launch_bounds__(1024) void cs_split(const uint64_t *__restrict__ keys, const int32_t *__restrict__ prev,
-                                                 int64_t n, int32_t P, uint64_t *__restrict__ split) {
-    __shared__ uint64_t s[CS_OVS * CS_PMAX];
-    const int S = CS_OVS * P;
+//
+// Two launches over CS_RUNS compute units instead of one workgroup's 4096-entry
+// network (LDS-bound on one CU, 47 us at n = 1M): cs_split_runs sorts CS_RUNS
+// runs of <= CS_RUN samples, one workgroup each (at n = 1M: 488); cs_split_rank places every
+// sample at its rank in the merged order (its index in its run + the entries
+// before it in every other run: binary searches, equal keys ordered by run)
+// and keeps the ranks that are multiples of CS_OVS -- the same splitters as
+// sorting all samples.
+constexpr int CS_RUNS = 8;
+constexpr int CS_RUN = CS_OVS * CS_PMAX / CS_RUNS;   // 512 samples per run at most
+constexpr int CS_RANK_T = 256;
+
+__global__ __launch_bounds__(CS_RUN / 2) void cs_split_runs(const uint64_t *__restrict__ keys,
+                                                            const int32_t *__restrict__ prev, int64_t n, int32_t P,
+                                                            uint64_t *__restrict__ runs) {
+    __shared__ uint64_t s[CS_RUN];
+    const int S = CS_OVS * P, L = (S + CS_RUNS - 1) / CS_RUNS;
+    const int j0 = blockIdx.x * L, m = max(0, min(S, j0 + L) - j0);
     int N = 2;
-    while (N < S) N <<= 1;
-    int32_t pi[CS_OVS];   // every thread's gathers in flight together
+    while (N < L) N <<= 1;
+    int32_t pi[2];
 #pragma unroll
-    for (int e = 0; e < CS_OVS; ++e) {
-        const int j = threadIdx.x + 1024 * e;
-        pi[e] = j < S ? prev[(int64_t)j * n / S] : 0;
+    for (int e = 0; e < 2; ++e) {
+        const int i = threadIdx.x + (CS_RUN / 2) * e;
+        pi[e] = i < m ? prev[(int64_t)(j0 + i) * n / S] : 0;
     }
 #pragma unroll
-    for (int e = 0; e < CS_OVS; ++e) {
-        const int j = threadIdx.x + 1024 * e;
-        if (j < N) s[j] = j < S ? keys[pi[e]] : ~0ull;
+    for (int e = 0; e < 2; ++e) {
+        const int i = threadIdx.x + (CS_RUN / 2) * e;
+        if (i < N) s[i] = i < m ? keys[pi[e]] : ~0ull;
     }
     __syncthreads();
-    bitonic_k<1024>(s, N);
-    for (int j = threadIdx.x; j < P; j += 1024) split[j] = s[j * CS_OVS];
+    bitonic_k<CS_RUN / 2>(s, N);
+    for (int i = threadIdx.x; i < m; i += CS_RUN / 2) runs[blockIdx.x * CS_RUN + i] = s[i];
+}
+
+__global__ __launch_bounds__(CS_RANK_T) void cs_split_rank(const uint64_t *__restrict__ runs, int32_t P,
+                                                           uint64_t *__restrict__ split) {
+    __shared__ uint64_t s[CS_RUNS * CS_RUN];
+    const int S = CS_OVS * P, L = (S + CS_RUNS - 1) / CS_RUNS;
+    for (int i = threadIdx.x; i < CS_RUNS * CS_RUN; i += CS_RANK_T) {
+        const int r = i / CS_RUN, k = i - r * CS_RUN;
+        if (r * L + k < S && k < L) s[i] = runs[i];
+    }
+    __syncthreads();
+    const int j = blockIdx.x * CS_RANK_T + threadIdx.x;
+    if (j >= S) return;
+    const int r = j / L, i = j - r * L;
+    const uint64_t x = s[r * CS_RUN + i];
+    int rank = i;
+    for (int q = 0; q < CS_RUNS; ++q) {
+        if (q == r) continue;
+        const int m = max(0, min(S, q * L + L) - q * L);
+        const uint64_t *a = s + q * CS_RUN;
+        int lo = 0, hi = m;   // entries of run q before x: keys < x, or <= x for an earlier run
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (q < r ? a[mid] <= x : a[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        rank += lo;
+    }
+    if (rank % CS_OVS == 0) split[rank / CS_OVS] = x;
 }
 
 // bucket of key k: the number of splitters split[1..P-1] <= k; guess g first
@@ -250,6 +293,7 @@ void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &
     cs.P = (int32_t)std::min<int64_t>(CS_PMAX, std::max<int64_t>(2, n / CS_TARGET));
     Workspace &ws = ctx->ws;
     cs.split = ws.get<uint64_t>(pre + "cs.split", cs.P);
+    cs.runs = ws.get<uint64_t>(pre + "cs.runs", CS_RUNS * CS_RUN);
     cs.cnt = ws.get<int32_t>(pre + "cs.cnt", cs.P);
     cs.off = ws.get<int32_t>(pre + "cs.off", cs.P + 1);
     cs.cur = ws.get<int32_t>(pre + "cs.cur", cs.P);
@@ -274,7 +318,9 @@ void csort_run(tsne_ctx *ctx, CoherentSort &cs, const uint64_t *keys, const int3
     TSNE_REQUIRE(cs.P > 0, "coherent sort not allocated");
     const int64_t n = cs.n;
     const int64_t nb = ceil_div(n, CS_BLK);
-    hipLaunchKernelGGL(cs_split, dim3(1), dim3(1024), 0, st, keys, prev, n, cs.P, cs.split);
+    hipLaunchKernelGGL(cs_split_runs, dim3(CS_RUNS), dim3(CS_RUN / 2), 0, st, keys, prev, n, cs.P, cs.runs);
+    hipLaunchKernelGGL(cs_split_rank, dim3(ceil_div(CS_OVS * cs.P, CS_RANK_T)), dim3(CS_RANK_T), 0, st, cs.runs, cs.P,
+                       cs.split);
     TSNE_HIP(hipMemsetAsync(cs.cnt, 0, sizeof(int32_t) * cs.P, st));
     hipLaunchKernelGGL(cs_count, dim3(nb), dim3(CS_BLK), 0, st, keys, prev, n, cs.P, cs.split, cs.bkt, cs.cnt);
     hipLaunchKernelGGL(cs_scan, dim3(1), dim3(1024), 0, st, cs.cnt, cs.P, cs.off, cs.cur, cs.stat);

@@ -21,6 +21,7 @@ struct CoherentSort {
     int64_t n = 0;
     int32_t P = 0;                  // buckets
     uint64_t *split = nullptr;      // P sorted splitters (bucket b holds keys in [split[b], split[b + 1]))
+    uint64_t *runs = nullptr;       // the sorted sample runs the splitters are merged from
     int32_t *cnt = nullptr;         // P bucket sizes
     int32_t *off = nullptr;         // P + 1 bucket offsets
     int32_t *cur = nullptr;         // P scatter cursors
@@ -35,7 +36,7 @@ struct CoherentSort {
 // [CSORT_MIN_N, CSORT_MAX_N]: nothing (the callers keep rocPRIM's sort).
 constexpr int64_t CSORT_MIN_N = 16384;
 // Above 1024 x 1.2k points the mean bucket outgrows the LDS sort's 4k capacity
-// at the measured 3.3x bucket skew (cs_split) and whole buckets would take the
+// at the measured 3.3x bucket skew (cs_split_runs) and whole buckets would take the
 // slow global-memory bitonic path: rocPRIM's sort there.
 constexpr int64_t CSORT_MAX_N = 1250000;
 void csort_alloc(tsne_ctx *ctx, CoherentSort &cs, int64_t n, const std::string &pre);
