@@ -623,6 +623,16 @@ __device__ __forceinline__ void pair_force(double qx, double qy, double px, doub
     fy = __fma_rn(sc, dy, fy);
     zs += r;
 }
+// pair_force's term added only with `take` (else + 0: the sums bit-equal)
+__device__ __forceinline__ void pair_force_m(bool take, double qx, double qy, double px, double py, double &fx,
+                                             double &fy, double &zs) {
+    const double dx = qx - px, dy = qy - py;
+    const double r = recip_bh(__fma_rn(dx, dx, __fma_rn(dy, dy, 1.0)));
+    const double sc = r * r;
+    fx = __fma_rn(take ? sc : 0.0, dx, fx);
+    fy = __fma_rn(take ? sc : 0.0, dy, fy);
+    zs += take ? r : 0.0;
+}
 
 // Number of points whose coordinates equal pos[s] exactly (itself included);
 // they sit in the same equal-key run of the sorted order.
@@ -2541,27 +2551,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 goto masked;
             }
             double ux = 0.0, uy = 0.0, uz = 0.0;
-            int p = 0, last = -1, nmine = 0;
-            while (true) {
-                if (p > last && W) {
-                    const int i = __ffsll((long long)W) - 1;
-                    W &= W - 1;
-                    const int2 r = srng[w][i];
-                    p = r.x; last = r.y;
-                }
-                const bool on = p <= last;
-                if (__ballot(on) == 0) break;
-                if (visits) ps_steps[0] += 2;
-                if (on) {
-                    const bool two = p + 1 <= last;
+            int nmine = 0, nit = 0;
+            // a divergent do-while per lane (two points of one tile per step,
+            // the second masked at a tile's odd end): the accumulators are
+            // updated in place, not copied at the merges of a wave-uniform loop
+            if (W) {
+                int i = __ffsll((long long)W) - 1;
+                W &= W - 1;
+                int2 r = srng[w][i];
+                int p = r.x, last = r.y;
+                bool more;
+                do {
+                    const bool two = p < last;
                     const double2 p0 = pos[p];
                     const double2 p1 = pos[two ? p + 1 : p];
                     pair_force(qx, qy, p0.x, p0.y, ux, uy, uz);
-                    if (two) pair_force(qx, qy, p1.x, p1.y, ux, uy, uz);
-                    p += 2;
+                    pair_force_m(two, qx, qy, p1.x, p1.y, ux, uy, uz);
                     nmine += two ? 2 : 1;
-                }
+                    ++nit;
+                    p += 2;
+                    if (p > last && W) {
+                        i = __ffsll((long long)W) - 1;
+                        W &= W - 1;
+                        r = srng[w][i];
+                        p = r.x; last = r.y;
+                    }
+                    more = p <= last;
+                } while (more);
             }
+            if (visits) ps_steps[0] += 2ull * (unsigned long long)wave_max(nit);
             __builtin_amdgcn_wave_barrier();
             fx += ux; fy += uy; zs += uz;
             ndense += (unsigned long long)nmine;
@@ -2633,20 +2651,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
                 const uint64_t y = ((uint64_t)yhi << 32) | ylo;
                 M = (lane & j) ? ((M & ~lo) | ((y & ~lo) >> j)) : ((M & lo) | ((y & lo) << j));
             }
-            while (__ballot(M != 0ull)) {
-                if (M) {
-                    const int j0 = __ffsll((long long)M) - 1;
+            // a divergent do-while per lane, the next slot's point read before
+            // the current one is summed: the accumulators are updated in place
+            // (a wave-uniform loop with an `if (M)` body made the compiler copy
+            // them at every merge -- ~20 moves per two pairs)
+            if (M) {
+                int j = __ffsll((long long)M) - 1;
+                M &= M - 1;
+                double2 pp = buf[j];
+                bool more;
+                do {
+                    more = M != 0ull;
+                    j = more ? __ffsll((long long)M) - 1 : j;
                     M &= M - 1;
-                    const int j1 = M ? __ffsll((long long)M) - 1 : -1;
-                    if (M) M &= M - 1;
-                    const double2 p0 = buf[j0];
-                    const double2 p1 = buf[j1 < 0 ? j0 : j1];
-                    pair_force(qx, qy, p0.x, p0.y, ux, uy, uz);
-                    if (j1 >= 0) pair_force(qx, qy, p1.x, p1.y, ux, uy, uz);
-                    if (visits) nmine += j1 >= 0 ? 2 : 1;
-                }
-                if (visits) ps_steps[1] += 2;
+                    const double2 pn = buf[j];
+                    pair_force(qx, qy, pp.x, pp.y, ux, uy, uz);
+                    if (visits) ++nmine;
+                    pp = pn;
+                } while (more);
             }
+            if (visits) ps_steps[1] += (unsigned long long)wave_max(nmine);
             __builtin_amdgcn_wave_barrier();
             fx += ux; fy += uy; zs += uz;
             ndense += (unsigned long long)nmine;
