@@ -234,6 +234,25 @@ __device__ __forceinline__ double qterm_t(double ax, double ay, double bx, doubl
     r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
     return r;
 }
+// The tiled attraction's q (attract_tiles), given d = a - b: the sqeuclidean
+// 1 + |d|^2 as an FMA chain and v_rcp_f64 + one Newton step (within 11 ulp,
+// as recip_bh) -- 4 fp64 operations fewer per entry than qterm_t; x = 1 + metric.
+template <int MET>
+__device__ __forceinline__ double qforce_t(double ax, double ay, double bx, double by, double dx, double dy,
+                                           double &x) {
+    if (MET == TSNE_METRIC_COSINE) {
+        const double dt = __dadd_rn(__dmul_rn(ax, bx), __dmul_rn(ay, by));
+        const double na = sqrt(__dadd_rn(__dmul_rn(ax, ax), __dmul_rn(ay, ay)));
+        const double nb = sqrt(__dadd_rn(__dmul_rn(bx, bx), __dmul_rn(by, by)));
+        x = 1.0 + (1.0 - dt / (na * nb));
+    } else if (MET == TSNE_METRIC_EUCLIDEAN) {
+        x = 1.0 + sqrt(__fma_rn(dx, dx, dy * dy));
+    } else {
+        x = __fma_rn(dx, dx, __fma_rn(dy, dy, 1.0));
+    }
+    const double r = __builtin_amdgcn_rcp(x);
+    return __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+}
 template <int MET>
 __device__ __forceinline__ double qterm_t(double ax, double ay, double bx, double by) {
     double x;
@@ -475,16 +494,21 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
                     continue;
 #endif
                     if (k0 + u < len) {
+                        // P q d with P's exaggeration applied to the row's total
+                        // (attr below), the q d terms accumulated by FMA
                         const double2 yj = win[cu[u]];
-                        const double pij = __dmul_rn(vu[u], ex);
+                        const double dx = __dsub_rn(yi.x, yj.x), dy = __dsub_rn(yi.y, yj.y);
                         double x1m;   // 1 + metric = 1 / q
-                        const double q = qterm_t<MET>(yi.x, yi.y, yj.x, yj.y, x1m);
-                        const double sc = __dmul_rn(pij, q);
-                        fx = __dadd_rn(fx, __dmul_rn(sc, __dsub_rn(yi.x, yj.x)));
-                        fy = __dadd_rn(fy, __dmul_rn(sc, __dsub_rn(yi.y, yj.y)));
+                        const double q = qforce_t<MET>(yi.x, yi.y, yj.x, yj.y, dx, dy, x1m);
+                        const double sc = __dmul_rn(vu[u], q);
+                        fx = __fma_rn(sc, dx, fx);
+                        fy = __fma_rn(sc, dy, fy);
                         // P ln(P / (q / Z)) = P ln(P Z (1 + metric)): no divisions
                         // (0 ln 0 = NaN for an underflowed P, as the reference)
-                        if (LOSS) lsum += pij * log_kl(pij * Z * x1m);
+                        if (LOSS) {
+                            const double pij = __dmul_rn(vu[u], ex);
+                            lsum += pij * log_kl(pij * Z * x1m);
+                        }
                     }
                 }
             }
@@ -505,7 +529,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
         }
         __syncthreads();
     }
-    for (int i = tid; i < nr; i += NT) attr[b0 + i] = acc[i];
+    for (int i = tid; i < nr; i += NT) attr[b0 + i] = make_double2(acc[i].x * ex, acc[i].y * ex);
     if (LOSS) {
         lsum = wave_sum(lsum);
         if (lane == 0) sl[w] = lsum;
