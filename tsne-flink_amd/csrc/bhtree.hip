@@ -2455,7 +2455,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     __shared__ double2 tbuf[4][64];
     __shared__ int smark[4][64];
     __shared__ int2 srng[4][64];
-    constexpr float LW_COST = 1.6f;   // lane-wise cost per point relative to a sweep slot (gathers, refills)
+    constexpr float LW_COST = 1.0f;   // lane-wise cost per point relative to a sweep slot (gathers, refills;
+                                      // 1.6 before the lane-wise loop lost its accumulator copies, round 5)
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const int64_t blk = torder ? (int64_t)torder[blockIdx.x] : (int64_t)blockIdx.x;
     const int64_t wid = blk * 4 + w;
