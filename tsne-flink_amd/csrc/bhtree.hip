@@ -1839,7 +1839,8 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
     const int64_t kq = g0 + grp * 64 + part * NQ + q;
     const bool valid = kq < g1;
     const int32_t s = valid ? (qlist ? qlist[kq] : (int32_t)kq) : -1;   // sorted position (< 2^31)
-    if (part == 0 && lane == 0) { ttask_n[grp] = 0; tcost[grp] = 0; }   // tile_apply: nothing for this group
+    // (the group's empty tile list and cost are the 64-query kernel's: tile_apply
+    // need not wait for this kernel)
     const long long t_start = COST ? clock64() : 0;
     const unsigned long long w_start = STATS ? wall_clock64() : 0;
     double qx = 0.0, qy = 0.0;
@@ -2058,8 +2059,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     const bool valid = k < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
     if (__ballot(valid) == 0) return;
-    if (nv.nflag && nv.nflag[wid]) return;   // a heavy group: the narrow waves take it
     if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
+    if (nv.nflag && nv.nflag[wid]) return;   // a heavy group: the narrow waves take it (no tiles here)
     const long long t_start = COST ? clock64() : 0;
     const unsigned long long w_start = STATS ? wall_clock64() : 0;
     int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next selection
@@ -3463,7 +3464,6 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
                        t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
                        t.tcost, clab, nv, plim);
-    if (narrow) TSNE_HIP(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
     // tile chunks of heavy waves (ChunkView): the single-workgroup plan while
     // the per-wave costs fit its LDS, else the multi-launch plan and block sort
     ChunkView cv;
@@ -3491,7 +3491,10 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
     hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.ch_Fp, t.ch_Zp, t.ch_C,
                        t.ch_slot0, s0, s1, qlist, dF, dz);
+    // the narrow waves' own queries from here on (their F / Z entries are
+    // disjoint from the 64-query waves' above, so the tiles did not wait for them)
     if (narrow) {
+        TSNE_HIP(hipStreamWaitEvent(st, ctx->aux_ev[1], 0));
         hipLaunchKernelGGL(narrow_moment_apply, dim3(ceil_div(t.nar_hmax * 64, 256)), dim3(256), 0, st, t.pos,
                            t.nodes, t.mom, t.hlist, t.hcount, t.nmtask, t.nmtask_n, s0, s1, qlist, dF, dz);
         TSNE_HIP(hipMemcpyAsync(t.hran, t.hcount, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
