@@ -14,8 +14,19 @@ from test_gpu_parity import random_problem
 pytestmark = pytest.mark.gpu
 
 
-def run(n, C, coherent, seed, iterations=40, dups=False, scale=3.0):
-    rp, col, val = random_problem(n, 20, seed=seed)
+def ring_problem(n, half=5):
+    """A symmetric P without a kNN (sizes the oracle's O(n^2) kNN cannot reach):
+    point i joined to i +- 1 .. i +- half (mod n), every entry 1 / (2 half n).
+    (A ring's diameter is n / (2 half): run it with graph_order 0.)"""
+    off = np.concatenate([np.arange(-half, 0), np.arange(1, half + 1)])
+    col = np.sort((np.arange(n)[:, None] + off[None, :]) % n, axis=1).astype(np.int32).ravel()
+    rp = np.arange(0, n * 2 * half + 1, 2 * half, dtype=np.int64)
+    val = np.full(col.size, 1.0 / (2 * half * n))
+    return rp, col, val
+
+
+def run(n, C, coherent, seed, iterations=40, dups=False, scale=3.0, problem=None, options=()):
+    rp, col, val = problem if problem is not None else random_problem(n, 20, seed=seed)
     Y0 = np.random.default_rng(seed).normal(size=(n, C)) * scale
     if dups:   # exact duplicates (the reference's multiplicities) and a key-tie run
         Y0[[3, 500, n - 7]] = Y0[3]
@@ -25,6 +36,8 @@ def run(n, C, coherent, seed, iterations=40, dups=False, scale=3.0):
     Pd = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (rp, col, val))
     with T.Context(0) as c:
         c.set_option("coherent_sort", coherent)
+        for k, v in options:
+            c.set_option(k, v)
         Y = torch.from_numpy(Y0.copy()).to(dev)
         u, g = torch.zeros_like(Y), torch.ones_like(Y)
         c.dev_opt_setup(p, *Pd, n, Y, u, g)
@@ -43,6 +56,18 @@ def test_coherent_sort_bit_identical(n, C, dups):
     Ya, la, over = run(n, C, 1, 31, dups=dups)
     Yb, lb, _ = run(n, C, 0, 31, dups=dups)
     assert over == 0   # oversampled splitters: every bucket within the LDS capacity
+    assert la == lb
+    assert np.array_equal(Ya, Yb)
+
+
+def test_coherent_sort_at_the_largest_bucket_count():
+    """n = 1.2M: 1024 buckets, 4096 splitter samples merged from 8 sorted runs
+    of 512 (the run capacity exactly) -- rocPRIM's permutation every iteration."""
+    n = 1_200_000
+    prob = ring_problem(n)
+    opts = (("graph_order", 0),)
+    Ya, la, over = run(n, 2, 1, 5, iterations=4, problem=prob, options=opts)
+    Yb, lb, _ = run(n, 2, 0, 5, iterations=4, problem=prob, options=opts)
     assert la == lb
     assert np.array_equal(Ya, Yb)
 
