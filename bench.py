@@ -27,6 +27,7 @@ queries are sharded, so N GPUs share one problem (strong scaling).
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -71,6 +72,8 @@ def parse():
     ap.add_argument("--trace", type=int, default=50,
                     help="trace pass after the timed region: profile t=1..5 and every N-th iteration (0 = no pass)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cli-e2e", action="store_true",
+                    help="skip the end-to-end leg through the native CLI from the reference's COO input (C3, N=1)")
     ap.add_argument("--cpu-sample", type=int, default=64, help="queries in the CPU baseline sample")
     ap.add_argument("--cpu-knn-sample", type=int, default=32, help="queries in the CPU baseline kNN sample")
     ap.add_argument("--dump-y", default="", help="comma-separated iterations t: save Y as <dump-dir>/Y_t<t>.npy")
@@ -486,6 +489,8 @@ def main():
         cb, cb_detail = cpu_baseline(snaps, a, n, X_host, (orp, oc, ov))
         out["cpu_baseline"] = cb
         detail["cpu_baseline"] = cb_detail
+    if rank == 0 and world == 1 and a.config == "c3" and not a.no_cli_e2e:
+        out["end_to_end_cli"] = cli_end_to_end(a, X_host, dev)
     if rank == 0 and a.locality:
         locality_report(Y[:n], orp, oc, n)
     if rank == 0:
@@ -499,6 +504,65 @@ def main():
     ctx.close()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def cli_end_to_end(a, X_host, dev):
+    """The native CLI (tsne-flink_amd/tsne_hip: Tsne.main's flags and file
+    formats, Tsne.scala:54-101) end to end on this workload written as the
+    reference's input: one "i,j,v" COO line per entry (Tsne.readInput,
+    Tsne.scala:138-153; 3.7 GB at 1M x 128), produced untimed on local disk by
+    scripts/coo_write.  The timed child process reads the file, runs kNN,
+    affinities + joint and the whole schedule, and writes the embedding CSV and
+    the loss file (Tsne.scala:86, 99-101); its own phase times come from its
+    log.  Returns the line's block (wall time and phases, seconds)."""
+    import shutil
+    import subprocess
+    import tempfile
+    here = os.path.dirname(os.path.abspath(__file__))
+    exe, writer = os.path.join(here, "tsne-flink_amd", "tsne_hip"), os.path.join(here, "scripts", "coo_write")
+    if not (os.path.exists(exe) and os.path.exists(writer)):
+        return {"skipped": "tsne_hip / scripts/coo_write not built (__graft_entry__.build)"}
+    n, d = a.n, a.dim
+    wd = tempfile.mkdtemp(prefix="tsne_cli_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        X = X_host if X_host is not None else gmm(n, d, 2, dev).cpu().numpy()
+        xbin, csv = os.path.join(wd, "x.bin"), os.path.join(wd, "input.csv")
+        np.ascontiguousarray(X, dtype="<f8").tofile(xbin)
+        del X
+        t0 = time.perf_counter()
+        subprocess.run([writer, xbin, str(n), str(d), csv], check=True, timeout=900)
+        t_gen = time.perf_counter() - t0
+        os.remove(xbin)
+        in_bytes = os.path.getsize(csv)
+        cmd = [exe, "--input", csv, "--output", os.path.join(wd, "y.csv"), "--dimension", str(d),
+               "--knnMethod", "bruteforce", "--metric", "sqeuclidean", "--perplexity", str(a.perplexity),
+               "--iterations", str(a.iterations), "--theta", str(a.theta), "--loss", os.path.join(wd, "loss.txt")]
+        print("[bench] CLI end to end: " + " ".join(os.path.basename(c) for c in cmd[:1]) + f" on {in_bytes} B",
+              file=sys.stderr, flush=True)
+        t0 = time.perf_counter()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        wall = time.perf_counter() - t0
+        if r.returncode != 0:
+            return {"failed": r.returncode, "log": r.stderr[-400:]}
+        ph = {}
+        for line in r.stderr.splitlines():
+            m = re.search(r"\[tsne_hip\] (read|kNN|affinities \+ joint|\d+ iterations|end-to-end)\D.*?([0-9.]+) s", line)
+            if m:
+                key = {"read": "read_s", "kNN": "knn_s", "affinities + joint": "affinities_joint_s",
+                       "end-to-end": "inside_s"}.get(m.group(1), "loop_s")
+                ph[key] = float(m.group(2))
+        out = {"wall_s": round(wall, 3), "input_bytes": in_bytes, "input_write_s_untimed": round(t_gen, 1)}
+        out.update({k: round(v, 3) for k, v in ph.items()})
+        if "inside_s" in ph:
+            known = sum(ph.get(k, 0.0) for k in ("read_s", "knn_s", "affinities_joint_s", "loop_s"))
+            out["setup_and_write_s"] = round(ph["inside_s"] - known, 3)
+            out["process_start_s"] = round(wall - ph["inside_s"], 3)
+        out["note"] = ("tsne_hip --knnMethod bruteforce --perplexity %g --iterations %d --theta %g from the "
+                       "reference's COO text input on local disk to the embedding CSV + loss file" %
+                       (a.perplexity, a.iterations, a.theta))
+        return out
+    finally:
+        shutil.rmtree(wd, ignore_errors=True)
 
 
 def locality_report(Y, rp, col, n):

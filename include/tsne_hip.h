@@ -216,7 +216,12 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *                        1 attract_tiles, 2 attract3 (3-D), -1 no optimizer;
  *   "opt.csort_oversized_total"  the same summed over every build of the optimizer's tree;
  *   "bh.csort_oversized", "opt.csort_oversized"  buckets of the last coherent
- *                        Morton sort (csort.hpp) beyond its LDS capacity. */
+ *                        Morton sort (csort.hpp) beyond its LDS capacity;
+ *   "bh.spill_tasks", "opt.spill_tasks"  BH walks split off as tasks (option
+ *                        "spill"), summed over every traversal of the tree;
+ *   "bh.spill_flags", "opt.spill_flags"  1 a task list full, 2 task tile pages
+ *                        exhausted (those walks went on unsplit / untiled: the
+ *                        same sums, but their split points then depend on timing). */
 int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);
 
 /* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls

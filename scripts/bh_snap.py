@@ -62,6 +62,9 @@ def main():
             rec = {"snapshot": os.path.basename(path), "n": n, "ms_median": 1e3 * times[len(times) // 2],
                    "ms_min": 1e3 * times[0], "narrow_groups": narrow, "sum_abs_F": float(F.abs().sum()),
                    "sum_z": float(z.sum())}
+            if ctx_has_option(ctx, "spill"):
+                rec["spill_tasks"] = ctx.counter("bh.spill_tasks")
+                rec["spill_flags"] = ctx.counter("bh.spill_flags")
             if a.stats and Y.shape[1] == 2 and ctx_has_option(ctx, "rep_stats"):
                 ctx.set_option("rep_stats", 1)
                 ctx.dev_repulsion(Y, a.theta, F, z)

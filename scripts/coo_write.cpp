@@ -27,11 +27,11 @@ int main(int argc, char **argv) {
             char buf[128];
             for (long i = r0; i < r1; ++i)
                 for (long j = 0; j < d; ++j) {
-                    auto r = std::to_chars(buf, buf + 128, i);
+                    auto r = std::to_chars(buf, buf + 96, i);
                     *r.ptr++ = ',';
-                    r = std::to_chars(r.ptr, buf + 128, j);
+                    r = std::to_chars(r.ptr, buf + 96, j);
                     *r.ptr++ = ',';
-                    r = std::to_chars(r.ptr, buf + 128, x[(size_t)i * d + j]);
+                    r = std::to_chars(r.ptr, buf + 96, x[(size_t)i * d + j]);
                     *r.ptr++ = '\n';
                     s.append(buf, r.ptr);
                 }

@@ -4,8 +4,8 @@
 #   mksnaps     bench.py --dump-y 250,450,650 into /tmp/snaps (the snapshots the snap steps read)
 #   snap        bh_snap.py on snaps/Y_t{250,450,650}.npy per SNAP_VARS entry ("-" = defaults, else KEY=VALUE;
 #               SNAP_ARGS: more bh_snap arguments, e.g. --stats)
-#   tests_narrow / tests3d / tests_all   GPU test subsets / the whole -m gpu suite
-#   bench / bench4   bench.py (C3 / C4) per BENCH_VARS / BENCH4_VARS entry
+#   tests_narrow / tests_spill / tests3d / tests_all   GPU test subsets / the whole -m gpu suite
+#   bench / bench4   bench.py (C3 / C4) per BENCH_VARS / BENCH4_VARS entry ("K1=V1+K2=V2": two options)
 #   ktrace      rocprofv3 --kernel-trace --stats of the default bench (KTRACE_ARGS)
 #   smoke       __graft_entry__.smoke()
 #   pmc         scripts/gpu_pmc.sh (summarise with scripts/pmc_summary.py <tag>)
@@ -34,7 +34,7 @@ if has mksnaps; then
 fi
 if has snap; then
   for v in ${SNAP_VARS:--}; do
-    opt=""; [ "$v" != "-" ] && opt="--option $v"
+    opt=""; [ "$v" != "-" ] && opt="--option ${v//+/ --option }"
     echo "# $v" >> $O/snap.jsonl
     run 300 python scripts/bh_snap.py $SN/Y_t250.npy $SN/Y_t450.npy $SN/Y_t650.npy $opt ${SNAP_ARGS:-} >> $O/snap.jsonl 2>> $O/snap.err || exit $?
   done
@@ -42,6 +42,10 @@ fi
 if has tests_narrow; then
   TSNE_HIP_LIB="${TESTS_LIB:-}" tst 900 python -u -m pytest tests/test_gpu_csort.py tests/test_gpu_narrow.py tests/test_gpu_parity.py -v -p no:cacheprovider \
       --timeout 300 --timeout-method thread > $O/tests_narrow.log 2>&1 || exit $?
+fi
+if has tests_spill; then
+  tst 900 python -u -m pytest tests/test_gpu_spill.py -v -p no:cacheprovider \
+      --timeout 300 --timeout-method thread > $O/tests_spill.log 2>&1 || exit $?
 fi
 if has tests_multi; then
   tst 900 python -u -m pytest tests/test_gpu_multi.py -v -p no:cacheprovider \
@@ -51,7 +55,7 @@ if has bench; then
   for v in ${BENCH_VARS:--}; do
     # "-": defaults; "lib=PATH": another build of the library (TSNE_HIP_LIB); else KEY=VALUE options
     opt=""; lib=""
-    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option $v" ;; esac
+    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option ${v//+/ --option }" ;; esac
     bi=$((${bi:-0}+1))
     echo "# $v" >> $O/bench.jsonl
     TSNE_HIP_LIB="$lib" run 400 python bench.py --no-cpu-baseline $opt --detail-out $O/bench_detail_$bi.json >> $O/bench.jsonl 2>> $O/bench.err || exit $?
@@ -137,7 +141,7 @@ fi
 if has proj; then
   for v in ${PROJ_VARS:--}; do
     opt=""; lib=""
-    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option $v" ;; esac
+    case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option ${v//+/ --option }" ;; esac
     echo "# $v" >> $O/proj.jsonl
     TSNE_HIP_LIB="$lib" run 600 python scripts/loop_projection.py ${PROJ_ARGS:-} $opt >> $O/proj.jsonl 2>> $O/proj.err || exit $?
   done

@@ -11,7 +11,9 @@
 
 struct Fake {
     std::atomic<bool> peer{false};      // the collective's peer has arrived
+    std::atomic<int> async_err{0};      // > 0: the next poll reports this library error
     std::atomic<bool> freed{false};
+    std::atomic<int> aborts{0}, destroys{0};
     std::atomic<int> after_free{0};     // library calls on a freed communicator (must stay 0)
     std::atomic<int> calls{0};
 };
@@ -24,10 +26,11 @@ struct FakeBackend {
     }
     static int poll(Handle h) {
         if (h->freed) ++h->after_free;
+        if (h->async_err) return -h->async_err;
         return h->peer ? 0 : 1;
     }
-    static void abort(Handle h) { h->freed = true; }
-    static void destroy(Handle h) { h->freed = true; }
+    static void abort(Handle h) { h->freed = true; ++h->aborts; }
+    static void destroy(Handle h) { h->freed = true; ++h->destroys; }
 };
 
 static int fail(const char *m) {
@@ -70,6 +73,31 @@ int main() {
         if (rc != 0) return fail("completed collective reported an error");
         g.destroy();
         if (!f.freed) return fail("destroy");
+    }
+    {   // the library reports an async error while the collective is in flight:
+        // run() fails with it, and destroy() then aborts the errored communicator
+        Fake f;
+        tsne::CommGuard<FakeBackend> g;
+        g.h = &f;
+        std::atomic<int> rc{99};
+        std::thread owner([&] { rc = g.run([](Fake *h) { return h->peer ? 0 : 1; }); });
+        std::this_thread::sleep_for(milliseconds(20));
+        f.async_err = 7;
+        owner.join();
+        if (rc != -2) return fail("async error not reported");
+        if (g.error() != 7) return fail("the async error's own code not kept");
+        g.destroy();
+        if (f.aborts != 1 || f.destroys != 0) return fail("errored communicator not aborted at destroy");
+        if (f.after_free != 0) return fail("library call after free");
+    }
+    {   // a clean run is destroyed in order (finalize + destroy), not aborted
+        Fake f;
+        f.peer = true;
+        tsne::CommGuard<FakeBackend> g;
+        g.h = &f;
+        if (g.run([](Fake *) { return 0; }) != 0 || g.error() != 0) return fail("clean run");
+        g.destroy();
+        if (f.aborts != 0 || f.destroys != 1) return fail("clean communicator not destroyed in order");
     }
     {   // many concurrent aborts against a rank issuing collectives in a loop
         for (int rep = 0; rep < 200; ++rep) {

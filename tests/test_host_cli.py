@@ -203,3 +203,62 @@ def test_cli_end_to_end_on_gpu(tmp_path, method, nc, extra):
     assert np.isfinite(Y).all()
     loss = (tmp_path / "loss.txt").read_text()
     assert loss.startswith("{") and "10=" in loss and "50=" in loss
+
+
+DENSE_HARNESS = r'''
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include "coo_reader.hpp"
+using namespace tsne_flink;
+// argv: file dimension threads -> 0 when readInputDense equals cooToVectors'
+// rows sorted by id, bit for bit (and prints the row count)
+int main(int argc, char **argv) {
+    const int dim = std::atoi(argv[2]), th = std::atoi(argv[3]);
+    auto rows = cooToVectors(readCooFile(argv[1], 1), dim);
+    std::sort(rows.begin(), rows.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::vector<int32_t> ids;
+    std::vector<double> X;
+    readInputDense(argv[1], dim, ids, X, th);
+    if (ids.size() != rows.size() || X.size() != rows.size() * (size_t)dim) return 1;
+    for (size_t r = 0; r < rows.size(); ++r) {
+        if (ids[r] != rows[r].first) return 2;
+        if (std::memcmp(&X[r * dim], rows[r].second.data(), sizeof(double) * dim) != 0) return 3;
+    }
+    std::printf("%zu\n", ids.size());
+    return 0;
+}
+'''
+
+
+@pytest.mark.parametrize("case", ["plain", "dups", "sparse_ids"])
+def test_read_input_dense_equals_reference_rows(tmp_path, case):
+    """Tsne.readInput (Tsne.scala:138-153) straight into the kNN's dense form
+    (coo_reader.cpp readInputDense, 4 threads over a > 1 MB file): the same
+    rows and bits as the per-row VectorBuilder restatement (cooToVectors)
+    ordered by id -- with cells given several times (summed in file order,
+    across the threads' ranges), shuffled lines, -0.0 values, and ids too
+    sparse for the dense id table."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    n, d = 6000, 24
+    ids = np.arange(n) * (100_003 if case == "sparse_ids" else 1) + 5
+    i = np.repeat(ids, d)
+    j = np.tile(np.arange(d), n)
+    v = rng.normal(size=n * d)
+    v[::97] = -0.0
+    if case == "dups":
+        k = rng.integers(0, n * d, 5000)
+        i, j, v = np.concatenate([i, i[k]]), np.concatenate([j, j[k]]), np.concatenate([v, rng.normal(size=5000)])
+    p = rng.permutation(len(i))
+    lines = "\n".join(f"{int(a)},{int(b)},{float(c)!r}" for a, b, c in zip(i[p], j[p], v[p]))
+    f = tmp_path / "in.csv"
+    f.write_text(lines + "\n")
+    assert f.stat().st_size > (1 << 20)
+    src = tmp_path / "h.cpp"
+    src.write_text(DENSE_HARNESS)
+    exe = tmp_path / "h"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-pthread", f"-I{PKG / 'host'}", str(src),
+                           str(PKG / "host" / "coo_reader.cpp"), "-o", str(exe)])
+    r = subprocess.run([str(exe), str(f), str(d), "4"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == str(n), (r.returncode, r.stdout, r.stderr)

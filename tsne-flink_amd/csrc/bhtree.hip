@@ -2035,17 +2035,176 @@ __global__ __launch_bounds__(256) void bh_traverse_narrow(
                       F, Z, visits, bcost, cost_lab, ttask_n, tcost, mom_flag, nv, h, (int)(slot % NPARTS), w);
 }
 
+// ---- Spill: splitting long walks over the chip (Options::spill; round 6).
+// A walk -- a wave's own 64-query group, or a task -- that has popped its
+// budget of records stops at the next batch boundary and hands its LDS stack
+// (the rest of the walk: (cell record, lane mask) entries) to the task list of
+// the next level, cut into tasks of consecutive entries (1, 1, 2, 4, 8, 16, 16,
+// ... from the bottom of the stack, whose entries are the largest subtrees).
+// Level l's tasks are taken by the l-th drain launch after the traversal: one
+// atomic add per claim on the level's head, no waiting (the list is complete
+// when the launch starts, as its producers ran in the previous launch); the
+// task's entries become the wave's stack, the walk is the same loop -- the
+// reference's opened / summarised cells (QuadTree.scala:123-152: a cell's
+// decision depends on the query and the cell only, not on who walks it) --
+// and splits again into level l + 1 (the last level never splits).  The split
+// points depend on the pop counts of the walks alone (the tree and the
+// queries), not on timing; the tasks' sums go to per-query fixed-point
+// accumulators (2^-64 units in two carry-free words, fxp_add), whose integer
+// adds are associative, so the result does not depend on which wave took which
+// task.
+// Tiles a task records go to 64-tile pages (tile_apply<true>), added the same
+// way.  The heavy waves of the mid phase are one LDS stack walked serially
+// (DESIGN 5, 6): this spreads their walks over the chip.
+constexpr int SP_LMAX = 4;     // task levels (drain launches) at most
+constexpr int SP_PAGES = 0, SP_B0 = 1, SP_B1 = 2, SP_OVF = 3, SP_TASKS = 4;
+__host__ __device__ constexpr int sp_head(int l) { return 8 + 3 * (l - 1); }    // level l's next task to take
+__host__ __device__ constexpr int sp_ttail(int l) { return 9 + 3 * (l - 1); }   // level l's tasks
+__host__ __device__ constexpr int sp_etail(int l) { return 10 + 3 * (l - 1); }  // level l's stack entries
+constexpr int SP_NCTL = 8 + 3 * SP_LMAX;
+constexpr int SP_FRAC = 64;    // fixed-point fraction bits: |value| < 2^31, resolution 2^-64
+constexpr int SP_PAGE = 64;    // tiles per task tile page
+constexpr int SP_CHUNK = 16;   // stack entries per task at most (<= 64: one lane each)
+struct SpillView {
+    int32_t *ctl = nullptr;               // SP_* / sp_*(l) words
+    int4 *task = nullptr;                 // level l's at [(l - 1) cap, l cap): {group, first entry, entries, 0}
+    uint4 *ent = nullptr;                 // level l's at [(l - 1) cap, l cap): {ref, 0, mask lo, mask hi}
+    int32_t *gflag = nullptr;             // group -> gen when it spilled
+    unsigned long long *acc = nullptr;    // sorted position -> fx, fy, z as (lo, hi)
+    TileTask *pg_tiles = nullptr;
+    int32_t *pg_grp = nullptr, *pg_n = nullptr;
+    int32_t cap = 0, pg_cap = 0, gen = 0;
+    int32_t lin = 0;    // TASK launches: the level whose tasks they take
+    int32_t lout = 0;   // the level a walk past its budget splits into (0: none, the last level)
+    int32_t force = 0;  // > 0: both budgets this many pops
+};
+
+// a += v as fixed point: X = v 2^64 truncated toward zero (|v| < 2^31), kept
+// as two words that add without carries, so both atomics are independent
+// (no returned value to wait for): a[0] += the low 32 bits of X (unsigned,
+// < 2^32 per add), a[1] += X >> 32 (signed).  The value is a[1] 2^-32 +
+// a[0] 2^-64, exact as a 128-bit integer; resolution 2^-64 absolute.
+__device__ __forceinline__ void fxp_add(unsigned long long *a, double v) {
+    if (v == 0.0) return;
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+    const int ex = (int)((bits >> 52) & 0x7ff);
+    const unsigned long long M = (bits & 0xFFFFFFFFFFFFFull) | (ex ? (1ull << 52) : 0ull);
+    const int sh = (ex ? ex : 1) - 1075 + SP_FRAC;   // |v| 2^64 = M 2^sh
+    unsigned long long lo, hi;                       // |X| = hi 2^32 + lo, lo < 2^32
+    if (sh >= 32) { lo = (M << sh) & 0xFFFFFFFFull; hi = M << (sh - 32); }
+    else if (sh >= 0) { const unsigned long long m = M << sh; lo = m & 0xFFFFFFFFull; hi = sh ? (M >> (32 - sh)) : (M >> 32); }
+    else if (sh > -64) { const unsigned long long m = M >> (-sh); lo = m & 0xFFFFFFFFull; hi = m >> 32; }
+    else { lo = 0; hi = 0; }
+    if (bits >> 63) {   // X = -|X|: lo' = (2^32 - lo) mod 2^32, hi' = -hi - (lo != 0)
+        hi = ~hi + (lo ? 0ull : 1ull);
+        lo = (0x100000000ull - lo) & 0xFFFFFFFFull;
+    }
+    atomicAdd(a, lo);
+    atomicAdd(a + 1, hi);
+}
+__device__ __forceinline__ double fxp_value(unsigned long long lo, unsigned long long hi) {
+    return ldexp((double)(long long)hi, 32 - SP_FRAC) + ldexp((double)lo, -SP_FRAC);
+}
+
+// task k of a split: its first entry and size (1, 1, 2, 4, 8, 16, 16, ...)
+__device__ __forceinline__ int sp_size(int k) { return k < 2 ? 1 : min(1 << (k - 1), SP_CHUNK); }
+__device__ __forceinline__ int sp_start(int k) {
+    int s = 0;
+    for (int j = 0; j < k; ++j) s += sp_size(j);
+    return s;
+}
+__device__ __forceinline__ int sp_ntasks(int n) {
+    int k = 0;
+    for (int c = 0; c < n; ++k) c += sp_size(k);
+    return k;
+}
+
+// The next task of level sv.lin (wave-uniform; false when the level's list is
+// taken): its group, and its entries pushed onto wave w's stack (sp).
+template <class LDS>
+__device__ __forceinline__ bool sp_next(const SpillView &sv, LDS &L, int w, int64_t &grp, int &sp) {
+    int h = -1;
+    if (lane_id() == 0) {
+        h = atomicAdd(&sv.ctl[sp_head(sv.lin)], 1);
+        if (h >= sv.ctl[sp_ttail(sv.lin)]) h = -1;
+    }
+    h = __builtin_amdgcn_readfirstlane(h);
+    if (h < 0) return false;
+    const int4 tk = sv.task[(int64_t)(sv.lin - 1) * sv.cap + h];
+    grp = __builtin_amdgcn_readfirstlane(tk.x);
+    const int e0 = __builtin_amdgcn_readfirstlane(tk.y), n = __builtin_amdgcn_readfirstlane(tk.z);
+    if (lane_id() < n) {
+        const uint4 v = sv.ent[(int64_t)(sv.lin - 1) * sv.cap + e0 + lane_id()];
+        L.sref[w][lane_id()] = (int32_t)v.x;
+        L.smask[w][lane_id()] = ((uint64_t)v.w << 32) | v.z;
+    }
+    sp = n;
+    return true;
+}
+
+// Room for n stack entries (and their tasks) in level sv.lout's lists: the
+// first entry and the first task (wave-uniform), or e = -1 when the entries
+// do not fit (the walk goes on: nothing is lost).  Only the allocation runs
+// inside the walk's loop (few registers); sp_write fills the slots after it.
+__device__ __forceinline__ int sp_alloc(const SpillView &sv, int n, int &t) {
+    int e = -1, tt = 0;
+    if (lane_id() == 0) {
+        int c = __hip_atomic_load(&sv.ctl[sp_etail(sv.lout)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int tries = 0; tries < 100000; ++tries) {
+            if (c + n > sv.cap) break;
+            if (__hip_atomic_compare_exchange_strong(&sv.ctl[sp_etail(sv.lout)], &c, c + n, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                e = c;
+                break;
+            }
+        }
+        if (e < 0) {
+            atomicOr(&sv.ctl[SP_OVF], 1);
+        } else {   // tasks <= entries <= cap: always room
+            const int nt = sp_ntasks(n);
+            tt = atomicAdd(&sv.ctl[sp_ttail(sv.lout)], nt);
+            atomicAdd(&sv.ctl[SP_TASKS], nt);
+        }
+    }
+    t = __builtin_amdgcn_readfirstlane(tt);
+    return __builtin_amdgcn_readfirstlane(e);
+}
+// Stack entries [0, n) of wave w -> level sv.lout's entries [e, e + n) and
+// tasks [t, t + ntasks(n)) of group grp (read by the next launch).
+template <class LDS>
+__device__ __forceinline__ void sp_write(const SpillView &sv, LDS &L, int w, int e, int t, int n, int32_t grp) {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the stack's last pushes landed
+    __builtin_amdgcn_wave_barrier();
+    if (lane_id() == 0) sv.gflag[grp] = sv.gen;
+    const int64_t lb = (int64_t)(sv.lout - 1) * sv.cap;
+    for (int i = lane_id(); i < n; i += 64) {
+        const uint64_t m = L.smask[w][i];
+        sv.ent[lb + e + i] = make_uint4((uint32_t)L.sref[w][i], 0u, (uint32_t)m, (uint32_t)(m >> 32));
+    }
+    const int nt = sp_ntasks(n);
+    for (int k = lane_id(); k < nt; k += 64) {
+        const int a = sp_start(k);
+        sv.task[lb + t + k] = make_int4(grp, e + a, min(sp_size(k), n - a), 0);
+    }
+}
+
 // Traversal kernel (see the comment above), one 64-query group per wave;
 // groups the narrow waves take (nv.nflag) return at once.  MODE 0 plain; 1
 // wave run times into the multi-GPU cost buckets; 2 every counter (profiling).
-template <int MODE, bool PART>
+// With spill (sv.mode, never with a tree partition) a walk past its budget
+// hands the rest to the task queue; TASK: the drain launches' instantiation,
+// whose waves take tasks while the queue has any (see "Spill" above) -- a
+// kernel of its own, so that the 64-query walk keeps its registers.
+template <int MODE, bool PART, bool TASK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0,
     int64_t g1, const int32_t *__restrict__ qlist, int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
     unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost, int32_t *__restrict__ wcost,
-    int32_t *__restrict__ tcost, const int32_t *__restrict__ cost_lab, NarrowView nv, int32_t *__restrict__ plim) {
+    int32_t *__restrict__ tcost, const int32_t *__restrict__ cost_lab, NarrowView nv, int32_t *__restrict__ plim,
+    SpillView sv) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
     // tree partition: this rank's sorted positions [plo, phi) (plim[2]: stack overflow flag)
     const int32_t plo = PART ? plim[0] : 0, phi = PART ? plim[1] : INT32_MAX;
@@ -2053,17 +2212,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
     const int64_t wid = (int64_t)blockIdx.x * 4 + w;   // query slots g0 + 64 wid .. + 63, tile list wid
+    const bool spill_on = !PART && sv.lout != 0;
+    int32_t bud = 0;   // pops after which a walk splits (0: never)
+    if (spill_on) bud = sv.force > 0 ? sv.force : sv.ctl[TASK ? SP_B1 : SP_B0];
+    // the wave's first item: its own group, or (TASK) a task
+    int64_t grp = wid;
+    constexpr bool task = TASK;
+    int tsp = 0;   // TASK: the task's entries on the stack
+    if (TASK) {
+        if (!sp_next(sv, L, w, grp, tsp)) return;
+    } else {
+        if (g0 + wid * 64 >= g1) return;
+        if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
+        if (nv.nflag && nv.nflag[wid]) return;   // a heavy group: the narrow waves take it (no tiles here)
+    }
+    for (;;) {
     // query slot k -> sorted position s (the identity, or this rank's list of
     // its own queries in sorted order: the waves stay Morton-coherent)
-    const int64_t k = g0 + wid * 64 + lane;
+    const int64_t k = g0 + grp * 64 + lane;
     const bool valid = k < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[k] : k) : -1;
-    if (__ballot(valid) == 0) return;
-    if (lane == 0) { ttask_n[wid] = 0; wcost[wid] = 0; tcost[wid] = 0; }
-    if (nv.nflag && nv.nflag[wid]) return;   // a heavy group: the narrow waves take it (no tiles here)
     const long long t_start = COST ? clock64() : 0;
     const unsigned long long w_start = STATS ? wall_clock64() : 0;
-    int32_t npops = 0, ntilepts = 0;   // wave-uniform: this wave's cost for the next selection
+    int32_t npops = 0, ntilepts = 0;   // wave-uniform: this walk's cost for the next selection
     double qx = 0.0, qy = 0.0;
     if (valid) { double2 q = pos[s]; qx = q.x; qy = q.y; }
     const double qmag = fabs(qx) + fabs(qy);
@@ -2073,8 +2244,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     unsigned long long wfull = 0, wpart = 0;                                   // STATS only
     int sp = 0;
     int ntt = 0;
-    TileTask *mytt = ttask + wid * TILE_CAP;
-    {
+    // tile sink: a group's own list (TILE_CAP), or a task's current page
+    TileTask *const mytt = ttask + wid * TILE_CAP;
+    TileTask *tdst = task ? nullptr : mytt;
+    int tcap = task ? 0 : TILE_CAP;
+    int32_t page = -1;
+    if (!task) {
         int32_t rpush;
         const uint64_t om = root_step<STATS>(pos, nodes, qrec, meta, virt, valid, qx, qy, theta, th_lo, th_hi, fx, fy,
                                              zs, nvis, rpush, plo <= 0 && phi > 0);
@@ -2082,6 +2257,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
             if (lane == 0) { L.sref[w][0] = rpush; L.smask[w][0] = om; }
             sp = 1;
         }
+    } else {
+        sp = tsp;   // (sp_next staged its entries)
     }
     // Pop up to 4 cells at a time (one while the stack is over half full: the
     // depth stays bounded): their records are fetched with one round of
@@ -2089,7 +2266,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     // broadcasts.  (A software pipeline -- the next batch's records in flight
     // in registers while one is processed -- measured no gain: C3 loop 5.645
     // vs 5.643 s, BH snapshots within noise; removed.)
+    int spe = -1, spt = 0;   // past the budget: where the rest of the walk goes (entries, tasks)
+    int32_t wbud = bud;
     while (sp > 0) {
+        if (!PART && wbud > 0 && npops >= wbud && sp >= 2) {
+            spe = sp_alloc(sv, sp, spt);
+            if (spe >= 0) break;
+            wbud = 0;   // no room: walk on
+        }
         const int kb = sp > STACK / 2 ? 1 : (sp < 4 ? sp : 4);
         sp -= kb;
         stage_records(L, w, lane, sp, kb, qrec);
@@ -2204,7 +2388,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                 tm = msk_s & (__builtin_amdgcn_ballot_w64(__fma_rn(cdx, cdx, cdy * cdy) <= nd.rball) |
                               __builtin_amdgcn_ballot_w64(__fma_rn(dxm, dxm, dym * dym) <= nd.hmin));
             }
-            if (tm && ntt < TILE_CAP) {
+            if (!PART && tm && task && ntt == tcap) {   // a task's tile page is full (or none yet): the next one
+                if (page >= 0 && lane == 0) { sv.pg_n[page] = ntt; sv.pg_grp[page] = (int32_t)grp; }
+                int p = 0;
+                if (lane == 0) p = atomicAdd(&sv.ctl[SP_PAGES], 1);
+                p = __builtin_amdgcn_readfirstlane(p);
+                ntt = 0;
+                if (p < sv.pg_cap) {
+                    page = p;
+                    tdst = sv.pg_tiles + (int64_t)p * SP_PAGE;
+                    tcap = SP_PAGE;
+                } else {   // no page left: the lanes keep traversing (the reference's path; flagged)
+                    page = -1;
+                    tcap = 0;
+                    if (lane == 0) atomicOr(&sv.ctl[SP_OVF], 2);
+                }
+            }
+            if (tm && ntt < tcap) {
                 // The wave records (subtree, lanes) for tile_apply, or, when its
                 // list is full, the lanes keep traversing (the reference's path).
                 // The range holds whole equal-key runs, so either all of the
@@ -2213,7 +2413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
                 const int a = __builtin_amdgcn_readfirstlane(nd.first), b = __builtin_amdgcn_readfirstlane(nd.last);
                 if (lane == 0) {
                     TileTask tt; tt.ref = ref; tt.first = a; tt.last = b; tt.pad = nd.cnt; tt.mask = tm;
-                    mytt[ntt] = tt;
+                    tdst[ntt] = tt;
                 }
                 ++ntt;
                 ntilepts += b - a + 1;
@@ -2309,17 +2509,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
             }
         }
     }
-    if (valid) {
-        F[s] = make_double2(fx, fy);
-        Z[s] = zs;
+    if (!PART && spe >= 0) sp_write(sv, L, w, spe, spt, sp, (int32_t)grp);
+    if (!task) {
+        if (valid) {
+            F[s] = make_double2(fx, fy);
+            Z[s] = zs;
+        }
+        if (lane == 0) {
+            ttask_n[wid] = ntt;
+            tcost[wid] = ntilepts + 16 * ntt;
+            // (an add: the group's tasks add their pops too, possibly before this)
+            if (spill_on) atomicAdd(&wcost[wid], npops + (ntilepts >> 6));
+            else wcost[wid] = npops + (ntilepts >> 6);
+        }
+    } else {
+        if (page >= 0 && lane == 0) { sv.pg_n[page] = ntt; sv.pg_grp[page] = (int32_t)grp; }
+        if (valid && (fx != 0.0 || fy != 0.0 || zs != 0.0)) {
+            unsigned long long *a = sv.acc + 6 * s;
+            fxp_add(a, fx);
+            fxp_add(a + 2, fy);
+            fxp_add(a + 4, zs);
+        }
+        if (lane == 0) atomicAdd(&wcost[grp], npops + (ntilepts >> 6));
     }
-    if (lane == 0) {
-        ttask_n[wid] = ntt;
-        wcost[wid] = npops + (ntilepts >> 6);
-        tcost[wid] = ntilepts + 16 * ntt;
-    }
-    if (COST && bcost) {   // cost of this wave into its queries' 256-query buckets
-        // the wave's own run time (shader clock / 64; the slices only move work
+    if (COST && bcost) {   // cost of this walk into its queries' 256-query buckets
+        // the walk's own run time (shader clock / 64; the slices only move work
         // between ranks, every query's sums are unchanged)
         const unsigned long long c = ((unsigned long long)(clock64() - t_start) >> 6) + 1;
         if (cost_lab) {   // by label: an equal share into each query's label bucket
@@ -2331,7 +2545,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     }
     if (STATS && visits) {   // [0] reference-equivalent node evaluations, [3] wave-level pops,
                              // [4] wave-level tile points, [5] lane child evaluations, [6] wave
-                             // child slots, [7..9] heaviest wave ([1], [2]: tile_apply)
+                             // child slots, [7..9] heaviest wave ([1], [2]: tile_apply), [32] tasks run
         const unsigned long long tv = wave_sum(nvis), te = wave_sum(nevals);
         if (lane == 0) {
             atomicAdd(visits, tv);
@@ -2349,7 +2563,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
             atomicMax(visits + 16, ~0ull - w_start);
             atomicMax(visits + 17, w_end);
             atomicAdd(visits + 18, w_end - w_start);
+            if (task) atomicAdd(visits + 32, 1ull);
         }
+    }
+    // TASK: the next one of the level (never waiting for one to appear)
+    if (!TASK || !sp_next(sv, L, w, grp, tsp)) break;
     }
 }
 
@@ -2447,37 +2665,58 @@ __global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcos
 // coalesced dwordx4 load per lane, the next chunk prefetched into registers)
 // and read back as wave-uniform broadcasts.  Lanes whose bound holds are
 // counted for the next iteration's moment gate.
+// PAGE: the spill tasks' tile pages instead (one wave per page, its group's
+// 64 queries; moments evaluated in place; sums into the fixed-point
+// accumulators, see "Spill").
+template <bool PAGE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void tile_apply(
     const double2 *__restrict__ pos, const BHNode *__restrict__ nodes, const TileTask *__restrict__ ttask,
     const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
     int32_t *__restrict__ mom_flag, double mom_tol, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits,
-    const int32_t *__restrict__ torder, ChunkView cv) {
+    const int32_t *__restrict__ torder, ChunkView cv, const double *__restrict__ mom, SpillView sv) {
     __shared__ double2 tbuf[4][64];
     __shared__ int smark[4][64];
     __shared__ int2 srng[4][64];
     constexpr float LW_COST = 1.0f;   // lane-wise cost per point relative to a sweep slot (gathers, refills;
                                       // 1.6 before the lane-wise loop lost its accumulator copies, round 5)
     const int lane = lane_id(), w = threadIdx.x >> 6;
-    const int64_t blk = torder ? (int64_t)torder[blockIdx.x] : (int64_t)blockIdx.x;
-    const int64_t wid = blk * 4 + w;
-    int64_t qw = wid;   // chunks: slot wid = chunk c of C of traversal wave qw's tile list
-    int ch = 0, C = 1;
-    if (cv.slot_w) {
-        if (wid >= *cv.nslots) return;
-        qw = cv.slot_w[wid];
-        const int32_t v = cv.slot_c[wid];
-        ch = v & 0xffff;
-        C = v >> 16;
+    int64_t wid, qw;
+    int tb, nt;
+    const TileTask *mytt;
+    // PAGE: pages blockIdx.x * 4 + w, + 4 gridDim.x, ... (the loop's end below)
+    for (int64_t pit = (int64_t)blockIdx.x * 4 + w;; pit += (int64_t)gridDim.x * 4) {
+    if (PAGE) {   // page wid of the spill tasks
+        wid = pit;
+        if (wid >= (int64_t)min(sv.ctl[SP_PAGES], sv.pg_cap)) return;
+        qw = sv.pg_grp[wid];
+        mytt = sv.pg_tiles + wid * SP_PAGE;
+        tb = 0;
+        nt = sv.pg_n[wid];
+        if (nt == 0) return;
+    } else {
+        const int64_t blk = torder ? (int64_t)torder[blockIdx.x] : (int64_t)blockIdx.x;
+        wid = blk * 4 + w;
+        qw = wid;   // chunks: slot wid = chunk c of C of traversal wave qw's tile list
+        int ch = 0, C = 1;
+        if (cv.slot_w) {
+            if (wid >= *cv.nslots) return;
+            qw = cv.slot_w[wid];
+            const int32_t v = cv.slot_c[wid];
+            ch = v & 0xffff;
+            C = v >> 16;
+        }
+        if (g0 + qw * 64 >= g1) return;
+        mytt = ttask + qw * TILE_CAP;
+        const int ntw = ttask_n[qw];
+        tb = (int)((int64_t)ntw * ch / C);
+        nt = (int)((int64_t)ntw * (ch + 1) / C);
     }
-    if (g0 + qw * 64 >= g1) return;
     const int64_t kq = g0 + qw * 64 + lane;
     const bool valid = kq < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
     const int64_t e = cv.slot_w ? wid * 64 + lane : s;   // moment list / partial-sum entry
-    const int ntw = ttask_n[qw];
-    const int tb = (int)((int64_t)ntw * ch / C), nt = (int)((int64_t)ntw * (ch + 1) / C);
-    if (nt == tb) {
+    if (!PAGE && nt == tb) {
         if (valid) {
             mtask_n[e] = 0;
             if (cv.slot_w) { cv.Fp[e] = make_double2(0.0, 0.0); cv.Zp[e] = 0.0; }
@@ -2496,7 +2735,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     // steps (pair slots the wave issues) and this lane's useful pairs
     unsigned long long ps_steps[4] = {0, 0, 0, 0}, ps_pairs[4] = {0, 0, 0, 0};
     double2 *buf = tbuf[w];
-    const TileTask *mytt = ttask + qw * TILE_CAP;
     int masked_until = tb;   // tiles before this one take the masked sweep
     for (int t = tb; t < nt;) {
         const TileTask tt = mytt[t];
@@ -2689,13 +2927,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
         const int cnt = __builtin_amdgcn_readfirstlane(tt.pad);
         const bool mine = (tt.mask >> lane) & 1ull;
         bool usem = false;
-        if (mine && cnt >= MOM_MIN_POINTS && ntask < MOM_TASKS) {
+        if (mine && cnt >= MOM_MIN_POINTS && (PAGE || ntask < MOM_TASKS)) {
             const BHNode &nd = nodes[ref];
             if (moment_ok(nd.bx0, nd.bx1, nd.by0, nd.by1, qx, qy, mom_tol)) {
                 ++nwant;
                 if (mom_on) {
                     usem = true;
-                    mtask[e * MOM_TASKS + ntask++] = ref;
+                    if (PAGE) {   // evaluated here (no per-query list for pages)
+                        double cx, cy, R;
+                        box_centre(nd, cx, cy, R);
+                        moment_eval(mom + (int64_t)ref * MOM_K, qx - cx, qy - cy, fx, fy, zs);
+                        ++ntask;
+                    } else {
+                        mtask[e * MOM_TASKS + ntask++] = ref;
+                    }
                 }
             }
         }
@@ -2768,7 +3013,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             }
         }
     }
-    if (valid && cv.slot_w) {
+    if (PAGE) {
+        if (valid && (fx != 0.0 || fy != 0.0 || zs != 0.0)) {
+            unsigned long long *a = sv.acc + 6 * s;
+            fxp_add(a, fx);
+            fxp_add(a + 2, fy);
+            fxp_add(a + 4, zs);
+        }
+    } else if (valid && cv.slot_w) {
         mtask_n[e] = ntask;
         cv.Fp[e] = make_double2(fx, fy);
         cv.Zp[e] = zs;
@@ -2808,6 +3060,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             atomicMax(visits + 21, w_end);
             atomicAdd(visits + 22, w_end - w_start);
         }
+    }
+    if (!PAGE) break;
+    }
+}
+
+// F, Z of the queries of every group that spilled += their tasks' fixed-point
+// sums (then zeroed); thread 0 also empties the queue for the next traversal.
+__global__ void spill_combine(const int32_t *__restrict__ gflag, int32_t gen, unsigned long long *__restrict__ acc,
+                              int64_t g0, int64_t g1, const int32_t *__restrict__ qlist, double2 *__restrict__ F,
+                              double *__restrict__ Z, int32_t *__restrict__ ctl) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {   // the lists are empty for the next traversal
+        ctl[SP_PAGES] = 0;
+        for (int l = 1; l <= SP_LMAX; ++l) { ctl[sp_head(l)] = 0; ctl[sp_ttail(l)] = 0; ctl[sp_etail(l)] = 0; }
+    }
+    const int64_t k = g0 + i;
+    if (k >= g1 || gflag[i >> 6] != gen) return;
+    const int64_t s = qlist ? (int64_t)qlist[k] : k;
+    ulonglong2 *a = reinterpret_cast<ulonglong2 *>(acc + 6 * s);
+    const ulonglong2 vx = a[0], vy = a[1], vz = a[2];
+    if ((vx.x | vx.y | vy.x | vy.y | vz.x | vz.y) == 0ull) return;
+    const double2 f = F[s];
+    F[s] = make_double2(f.x + fxp_value(vx.x, vx.y), f.y + fxp_value(vy.x, vy.y));
+    Z[s] = Z[s] + fxp_value(vz.x, vz.y);
+    const ulonglong2 zero = make_ulonglong2(0ull, 0ull);
+    a[0] = zero; a[1] = zero; a[2] = zero;
+}
+
+// The next traversal's budgets from this one's costs (one workgroup): the
+// mean walk cost per group (pops + tile points / 64, the group's tasks
+// included; groups without a cost -- narrow ones before their selection --
+// left out), B0 = max(bmin, fac mean), B1 = max(8, ftask B0).
+__global__ __launch_bounds__(1024) void spill_budget(const int32_t *__restrict__ wcost, int64_t waves, double fac,
+                                                     double ftask, int32_t bmin, int32_t *__restrict__ ctl) {
+    __shared__ unsigned long long rs[16], rc[16];
+    const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    unsigned long long sum = 0, cnt = 0;
+    for (int64_t g = t; g < waves; g += 1024) {
+        const int32_t c = wcost[g];
+        if (c > 0) { sum += (unsigned long long)c; ++cnt; }
+    }
+    sum = wave_sum(sum);
+    cnt = wave_sum(cnt);
+    if (lane == 0) { rs[w] = sum; rc[w] = cnt; }
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long S = 0, C = 0;
+        for (int k = 0; k < 16; ++k) { S += rs[k]; C += rc[k]; }
+        const double mean = C ? (double)S / (double)C : 0.0;
+        const int32_t b0 = (int32_t)fmin(2e9, fmax((double)bmin, fac * mean));
+        ctl[SP_B0] = b0;
+        ctl[SP_B1] = (int32_t)fmax(8.0, ftask * (double)b0);
     }
 }
 
@@ -3150,7 +3454,46 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
     t.ncost = ws.get<int32_t>(pre + "ncost", (size_t)t.nar_hmax * NPARTS);
     t.nmtask = ws.get<int32_t>(pre + "nmtask", (size_t)t.nar_hmax * 64 * MOM_TASKS);
     t.nmtask_n = ws.get<int32_t>(pre + "nmtask_n", (size_t)t.nar_hmax * 64);
+    t.pre = pre;
+    t.sp_ctl = nullptr;   // spill buffers: on first use (bh_spill_alloc)
+    t.sp_gen = 0;
+    t.sp_waves = 0;
+    t.ran_spill = false;
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+// The spill buffers (see "Spill"): per level, stack entries and tasks for
+// max(16 per query group, 2^18) entries (far more than the budgets produce),
+// 64-tile pages for n / 4 + 16384 pages of task tiles, 48 B of accumulators
+// per point.
+static void bh_spill_alloc(tsne_ctx *ctx, BHTree &t) {
+    if (t.sp_ctl) return;
+    Workspace &ws = ctx->ws;
+    const std::string &pre = t.pre;
+    const int64_t n = t.n, qwaves = ceil_div(n, 64) + 4;
+    t.sp_cap = (int32_t)std::min<int64_t>(1 << 26, std::max<int64_t>(1 << 18, 16 * qwaves));
+    t.sp_pg_cap = (int32_t)std::min<int64_t>(1 << 24, n / 4 + (1 << 14));
+    t.sp_ctl = ws.get<int32_t>(pre + "sp_ctl", SP_NCTL);
+    t.sp_task = ws.get<int4>(pre + "sp_task", (size_t)SP_LMAX * t.sp_cap);
+    t.sp_ent = ws.get<uint4>(pre + "sp_ent", (size_t)SP_LMAX * t.sp_cap);
+    t.sp_gflag = ws.get<int32_t>(pre + "sp_gflag", t.tile_waves);
+    t.sp_acc = ws.get<unsigned long long>(pre + "sp_acc", 6 * (size_t)n);
+    t.sp_pg_tiles = ws.get<TileTask>(pre + "sp_pg_tiles", (size_t)t.sp_pg_cap * SP_PAGE);
+    t.sp_pg_grp = ws.get<int32_t>(pre + "sp_pg_grp", t.sp_pg_cap);
+    t.sp_pg_n = ws.get<int32_t>(pre + "sp_pg_n", t.sp_pg_cap);
+    hipStream_t st = ctx->stream;
+    TSNE_HIP(hipMemsetAsync(t.sp_ctl, 0, sizeof(int32_t) * SP_NCTL, st));
+    TSNE_HIP(hipMemsetAsync(t.sp_gflag, 0, sizeof(int32_t) * t.tile_waves, st));
+    TSNE_HIP(hipMemsetAsync(t.sp_acc, 0, sizeof(unsigned long long) * 6 * n, st));
+    t.sp_gen = 0;
+}
+
+int64_t bh_spill_counter(tsne_ctx *ctx, BHTree &t, bool flags) {
+    if (!t.sp_ctl) return 0;
+    int32_t c[SP_NCTL];
+    TSNE_HIP(hipMemcpyAsync(c, t.sp_ctl, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    return flags ? (int64_t)c[SP_OVF] : (int64_t)c[SP_TASKS];
 }
 
 int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t) {
@@ -3168,7 +3511,7 @@ BHTree &bh_single_tree(tsne_ctx *ctx, int64_t n) {
     // a single call is a function of its input alone unless the caller asked
     // for the previous call's costs (Options::reuse_costs): without costs the
     // traversal takes the 64-query layout everywhere
-    if (!ctx->opts.reuse_costs) t.sel_waves = 0;
+    if (!ctx->opts.reuse_costs) { t.sel_waves = 0; t.sp_waves = 0; }
     return t;
 }
 
@@ -3433,8 +3776,12 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // counters only when asked for: visits need every counter, the multi-GPU
     // cost buckets only the waves' run times
     const int mode = visits ? 2 : (bcost ? 1 : 0);
-    auto kern = plim ? (mode == 2 ? bh_traverse<2, true> : mode == 1 ? bh_traverse<1, true> : bh_traverse<0, true>)
-                     : (mode == 2 ? bh_traverse<2, false> : mode == 1 ? bh_traverse<1, false> : bh_traverse<0, false>);
+    auto kern = plim ? (mode == 2 ? bh_traverse<2, true, false> : mode == 1 ? bh_traverse<1, true, false>
+                                                                         : bh_traverse<0, true, false>)
+                     : (mode == 2 ? bh_traverse<2, false, false> : mode == 1 ? bh_traverse<1, false, false>
+                                                                           : bh_traverse<0, false, false>);
+    auto tkern = mode == 2 ? bh_traverse<2, false, true> : mode == 1 ? bh_traverse<1, false, true>
+                                                                     : bh_traverse<0, false, true>;
     const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     // heavy groups: selected after the previous traversal of the same query
@@ -3451,6 +3798,22 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         nv.nbn = (int32_t)ceil_div(t.nar_hmax * NPARTS, 4);
     }
     t.ran_narrow = narrow;
+    // work splitting of long walks (see "Spill"): budgets from the previous
+    // traversal of the same query count (spill_budget), or forced (tests)
+    const Options &o = ctx->opts;
+    const bool spill = !plim && (o.spill_force > 0 || (o.spill > 0.0 && t.sp_waves == waves));
+    SpillView sv;
+    if (spill) {
+        bh_spill_alloc(ctx, t);
+        ++t.sp_gen;
+        sv.ctl = t.sp_ctl; sv.task = t.sp_task; sv.ent = t.sp_ent; sv.gflag = t.sp_gflag; sv.acc = t.sp_acc;
+        sv.pg_tiles = t.sp_pg_tiles; sv.pg_grp = t.sp_pg_grp; sv.pg_n = t.sp_pg_n;
+        sv.cap = t.sp_cap; sv.pg_cap = t.sp_pg_cap; sv.gen = t.sp_gen;
+        sv.lin = 0;
+        sv.lout = 1;
+        sv.force = o.spill_force;
+    }
+    t.ran_spill = spill;
     const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
     if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
         TSNE_HIP(hipEventRecord(ctx->aux_ev[0], st));
@@ -3463,7 +3826,18 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
                        t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
-                       t.tcost, clab, nv, plim);
+                       t.tcost, clab, nv, plim, sv);
+    // the levels' tasks: drain launch l takes level l (one wave per slot),
+    // splitting into level l + 1; the last one without splits
+    const int levels = std::min(o.spill_drains, SP_LMAX);
+    for (int d = 1; spill && d <= levels; ++d) {
+        SpillView dv = sv;
+        dv.lin = d;
+        dv.lout = d < levels ? d + 1 : 0;
+        hipLaunchKernelGGL(tkern, dim3(std::max(1, ctx->cu_count * 8)), dim3(256), 0, st, t.pos, t.dupc, t.nodes,
+                           t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n,
+                           dF, dz, visits, bcost, t.wcost, t.tcost, clab, nv, plim, dv);
+    }
     // tile chunks of heavy waves (ChunkView): the single-workgroup plan while
     // the per-wave costs fit its LDS, else the multi-launch plan and block sort
     ChunkView cv;
@@ -3485,12 +3859,20 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     cv.slot_w = t.ch_slot_w; cv.slot_c = t.ch_slot_c; cv.nslots = t.ch_nslots;
     cv.Fp = t.ch_Fp; cv.Zp = t.ch_Zp;
-    hipLaunchKernelGGL(tile_apply, dim3(ceil_div(tslots, 4)), dim3(256), 0, st, t.pos, t.nodes, t.ttask, t.ttask_n,
-                       s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits, torder, cv);
+    hipLaunchKernelGGL(tile_apply<false>, dim3(ceil_div(tslots, 4)), dim3(256), 0, st, t.pos, t.nodes, t.ttask,
+                       t.ttask_n, s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits, torder, cv,
+                       t.mom, SpillView());
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(tslots * 64, 256)), dim3(256), 0, st, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
     hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.ch_Fp, t.ch_Zp, t.ch_C,
                        t.ch_slot0, s0, s1, qlist, dF, dz);
+    if (spill) {   // the tasks' tile pages, then their sums into F, Z
+        hipLaunchKernelGGL(tile_apply<true>, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.nodes,
+                           t.ttask, t.ttask_n, s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits,
+                           nullptr, ChunkView(), t.mom, sv);
+        hipLaunchKernelGGL(spill_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.sp_gflag, t.sp_gen,
+                           t.sp_acc, s0, s1, qlist, dF, dz, t.sp_ctl);
+    }
     // the narrow waves' own queries from here on (their F / Z entries are
     // disjoint from the 64-query waves' above, so the tiles did not wait for them)
     if (narrow) {
@@ -3507,6 +3889,15 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         t.sel_waves = waves;
     } else {
         t.sel_waves = 0;
+    }
+    // the next traversal's split budgets (of the same query count) from this one's costs
+    if (o.spill > 0.0 && o.spill_force == 0 && !plim) {
+        bh_spill_alloc(ctx, t);
+        hipLaunchKernelGGL(spill_budget, dim3(1), dim3(1024), 0, st, t.wcost, waves, o.spill, o.spill_task,
+                           (int32_t)o.spill_min, t.sp_ctl);
+        t.sp_waves = waves;
+    } else {
+        t.sp_waves = 0;
     }
     TSNE_LAUNCH_CHECK();
 }

@@ -175,6 +175,22 @@ struct BHTree {
     int64_t nar_hmax = 0;
     int64_t sel_waves = 0;       // query waves the current selection is for (0: none)
     bool ran_narrow = false;     // the last traversal used a selection
+    // work splitting of long traversals (bhtree.hip "Spill"): a walk past its
+    // pop budget hands its stack entries to the next level's task list, taken
+    // by drain launches; task sums go to per-query fixed-point accumulators
+    // (order-free, so the result does not depend on which wave ran which task)
+    int32_t *sp_ctl = nullptr;            // control words (levels' heads and tails, pages, budgets, flags)
+    int4 *sp_task = nullptr;              // per level: task -> {group, first entry, entries}
+    uint4 *sp_ent = nullptr;              // per level: stack entry -> {ref, 0, mask lo, mask hi}
+    int32_t *sp_gflag = nullptr;          // per 64-query group: generation of its last spill
+    unsigned long long *sp_acc = nullptr; // per sorted position: fx, fy, z as (lo, hi) pairs
+    TileTask *sp_pg_tiles = nullptr;      // task tile pages (64 tiles each)
+    int32_t *sp_pg_grp = nullptr, *sp_pg_n = nullptr;
+    int32_t sp_cap = 0, sp_pg_cap = 0;
+    int32_t sp_gen = 0;
+    int64_t sp_waves = 0;                 // query waves the budget words are for (0: none yet)
+    bool ran_spill = false;               // the last traversal split work
+    std::string pre;                      // the workspace prefix of this tree's buffers
 };
 
 // Allocate (from ctx->ws, buffers named pre + field) for n points.  One
@@ -220,6 +236,10 @@ void part_align(tsne_ctx *ctx, BHTree &t, const int64_t *cuts, int world, int ra
 void part_recut(tsne_ctx *ctx, const unsigned long long *cost, int world, int64_t n, int64_t *cuts);
 // This traversal's cost (sum over its waves of pops + tile points / 64) into *out.
 void part_cost(tsne_ctx *ctx, BHTree &t, int64_t waves, unsigned long long *out);
+// Spill counters of t (synchronises the stream): tasks split off over all its
+// traversals, or (flags) 1 a level's list full, 2 tile pages exhausted (those
+// walks went on unsplit / untiled: the same sums).
+int64_t bh_spill_counter(tsne_ctx *ctx, BHTree &t, bool flags);
 // Heavy groups the last traversal on t ran narrow (synchronises the stream).
 int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).

@@ -129,6 +129,11 @@ static const OptionField k_options[] = {
     {"knn_bf16", nullptr, &Options::knn_bf16, 0, 1},
     {"narrow", &Options::narrow, nullptr, 0.0, 1e6},
     {"reuse_costs", nullptr, &Options::reuse_costs, 0, 1},
+    {"spill", &Options::spill, nullptr, 0.0, 1e6},
+    {"spill_task", &Options::spill_task, nullptr, 0.0, 1e6},
+    {"spill_min", nullptr, &Options::spill_min, 1, 1 << 30},
+    {"spill_force", nullptr, &Options::spill_force, 0, 1 << 30},
+    {"spill_drains", nullptr, &Options::spill_drains, 1, 8},
     {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
     {"rep_stats", nullptr, &Options::rep_stats, 0, 1},
     {"loop_serial", nullptr, &Options::loop_serial, 0, 1},
@@ -389,6 +394,10 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         else if (k == "opt.narrow_groups") *value_out = opt_tree(ctx) ? bh_narrow_groups(ctx, *opt_tree(ctx)) : 0;
         else if (k == "bh.csort_oversized") *value_out = ctx->single_tree ? csort_oversized(ctx, ctx->single_tree->cs) : 0;
         else if (k == "opt.attract_kernel") *value_out = opt_attract_kernel(ctx);
+        else if (k == "bh.spill_tasks" || k == "bh.spill_flags")
+            *value_out = ctx->single_tree ? bh_spill_counter(ctx, *ctx->single_tree, k == "bh.spill_flags") : 0;
+        else if (k == "opt.spill_tasks" || k == "opt.spill_flags")
+            *value_out = opt_tree(ctx) ? bh_spill_counter(ctx, *opt_tree(ctx), k == "opt.spill_flags") : 0;
         else if (k.rfind("bh.", 0) == 0 && repulsion_stat(ctx, k, value_out)) {}
         else if (k == "comm.kind") *value_out = comm_counter(ctx, false);
         else if (k == "comm.calls") *value_out = comm_counter(ctx, true);

@@ -112,10 +112,12 @@ struct RcclComm : Comm {
     // rank has thrown).  Later calls report TSNE_ERR_COMM.
     void abort() override { g.abort(); }
     void run(const char *what, const std::function<ncclResult_t(ncclComm_t)> &op) {
-        ncclResult_t last = ncclSuccess;
-        const int rc = g.run([&](ncclComm_t c) { return last = op(c); });
+        const int rc = g.run([&](ncclComm_t c) { return op(c); });
         if (rc == -1) fail(TSNE_ERR_COMM, "RCCL communicator aborted (another rank failed)");
-        if (rc == -2) fail(TSNE_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(last == ncclSuccess ? ncclInternalError : last));
+        if (rc == -2) {   // the failing call's or the async poll's own code
+            const int e = g.error();
+            fail(TSNE_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(e > 0 ? (ncclResult_t)e : ncclInternalError));
+        }
     }
     void allreduce_f64(tsne_ctx *ctx, double *buf, size_t count) override {
         run("ncclAllReduce", [&](ncclComm_t c) { return ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, c, ctx->stream); });
@@ -447,16 +449,38 @@ void comm_init_group(const std::vector<tsne_ctx *> &subs, bool loopback) {
     ncclConfig_t cfg = nonblocking_config();
     int dev0 = 0;
     TSNE_HIP(hipGetDevice(&dev0));
-    nccl_check(ncclGroupStart(), "ncclGroupStart");
-    for (int r = 0; r < world; ++r) {
-        TSNE_HIP(hipSetDevice(subs[r]->device));
-        const ncclResult_t e = ncclCommInitRankConfig(&comms[r], world, uid, r, &cfg);
-        if (e != ncclSuccess && e != ncclInProgress) nccl_check(e, "ncclCommInitRankConfig");
+    // on any failure below: the caller's device back (the guard) and the
+    // communicators created so far aborted, not leaked
+    struct InitCleanup {
+        std::vector<ncclComm_t> &c;
+        bool done = false;
+        ~InitCleanup() {
+            if (done) return;
+            for (ncclComm_t x : c)
+                if (x) (void)ncclCommAbort(x);
+        }
+    } cleanup{comms};
+    {
+        DeviceGuard dg(dev0);
+        bool in_group = false;
+        try {
+            nccl_check(ncclGroupStart(), "ncclGroupStart");
+            in_group = true;
+            for (int r = 0; r < world; ++r) {
+                TSNE_HIP(hipSetDevice(subs[r]->device));
+                const ncclResult_t e = ncclCommInitRankConfig(&comms[r], world, uid, r, &cfg);
+                if (e != ncclSuccess && e != ncclInProgress) nccl_check(e, "ncclCommInitRankConfig");
+            }
+            in_group = false;
+            const ncclResult_t ge = ncclGroupEnd();
+            if (ge != ncclSuccess && ge != ncclInProgress) nccl_check(ge, "ncclGroupEnd");
+        } catch (...) {
+            if (in_group) (void)ncclGroupEnd();   // close the group before the aborts
+            throw;
+        }
     }
-    const ncclResult_t ge = ncclGroupEnd();
-    if (ge != ncclSuccess && ge != ncclInProgress) nccl_check(ge, "ncclGroupEnd");
-    TSNE_HIP(hipSetDevice(dev0));
     for (int r = 0; r < world; ++r) nccl_wait_init(comms[r], "ncclCommInitRankConfig");
+    cleanup.done = true;
     for (int r = 0; r < world; ++r) {
         comm_destroy(subs[r]);
         RcclComm *c = new RcclComm();

@@ -12,7 +12,12 @@
 //     exactly once; the owner checks `aborted` under `api` before every call,
 //     so no call ever reaches the library after the communicator was freed;
 //   * a poll that sees `aborted` fails with the caller's error instead of
-//     waiting on.
+//     waiting on;
+//   * a call or poll that reports a library error records it (`err`, under
+//     `api`): the communicator is then in an error state, so destroy() takes
+//     the abort path (NCCL's rule for an errored communicator) instead of the
+//     orderly finalize + destroy, and the caller's message names the async
+//     error itself rather than the enqueue's "in progress".
 // The backend B supplies the library calls; the header has no RCCL dependency
 // so that the protocol is tested on the CPU with a fake backend
 // (tests/test_comm_guard.py).
@@ -37,22 +42,30 @@ struct CommGuard {
     std::mutex api;
     std::atomic<bool> aborted{false};
     bool freed = false;   // under api
+    int err = 0;          // under api: the backend's error (-code) once a call or poll failed
 
-    // 0 ok; -1 aborted (by another thread); -2 library error
+    // 0 ok; -1 aborted (by another thread); -2 library error (error() names it)
     template <class F> int run(F &&op) {
         int rc;
         {
             std::lock_guard<std::mutex> lk(api);
             if (aborted.load()) return -1;
             rc = B::call(h, op);
+            if (rc < 0) err = -rc;
         }
         while (rc == 1) {
             std::this_thread::yield();
             std::lock_guard<std::mutex> lk(api);
             if (aborted.load()) return -1;
             rc = B::poll(h);
+            if (rc < 0) err = -rc;
         }
         return rc < 0 ? -2 : 0;
+    }
+    // the backend's error code of the last failed call or poll (0: none)
+    int error() {
+        std::lock_guard<std::mutex> lk(api);
+        return err;
     }
     // callable from any thread, any number of times
     void abort() {
@@ -67,7 +80,8 @@ struct CommGuard {
         std::lock_guard<std::mutex> lk(api);
         if (!freed) {
             freed = true;
-            B::destroy(h);
+            if (err) B::abort(h);   // an errored communicator is aborted, not finalized
+            else B::destroy(h);
         }
     }
 };

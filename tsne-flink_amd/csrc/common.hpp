@@ -194,6 +194,13 @@ struct Options {
                               // the optimizer runs its sharded code path through it (tests the transport)
     int reuse_costs = 0;      // single-call BH (tsne_gradient / tsne_repulsion): select narrow groups from the
                               // previous call's costs (results then depend on the call history at rounding level)
+    // BH work splitting (bhtree.hip "Spill"): a 64-query wave stops after spill x the previous
+    // traversal's mean wave cost (in record pops, >= spill_min) and hands its stack to idle waves as
+    // tasks, which split again after spill_task x that budget (0: off); spill_force > 0 sets both
+    // budgets to that many pops from the first traversal on (tests); spill_drains follow-up launches
+    // take the tasks left when the traversal's waves ended (the last one never splits)
+    double spill = 0.0, spill_task = 0.25;
+    int spill_min = 256, spill_force = 0, spill_drains = 2;
 };
 
 }  // namespace tsne

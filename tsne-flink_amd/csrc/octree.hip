@@ -1413,7 +1413,7 @@ void oct_alloc(tsne_ctx *ctx, OctTree &t, int64_t n, const std::string &pre) {
     t.meta = ws.get<int32_t>(pre + "meta", 4);
     t.bbox_blocks = (int)std::min<int64_t>(1024, std::max<int64_t>(1, ceil_div(n, 256)));
     t.bbox_part = ws.get<double>(pre + "bbox_part", 6 * (size_t)t.bbox_blocks);
-    t.W = ws.get<double>("oct.W", 1);
+    t.W = ws.get<double>(pre + "W", 1);
     size_t tb = 0;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, t.keys, t.keys_sorted, t.idx, t.idx_sorted, (int)n, 0,
                                                64, ctx->stream));

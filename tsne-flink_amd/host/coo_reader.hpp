@@ -31,5 +31,13 @@ CooTriples readCooFile(const std::string &path, int threads = 0);
 // Tsne.readInput: dense rows (id, x) in order of first appearance; a column
 // outside [0, dimension) throws std::out_of_range.
 std::vector<std::pair<int32_t, std::vector<double>>> cooToVectors(const CooTriples &t, int dimension);
+// Tsne.readInput straight into the kNN's dense form: the distinct ids sorted
+// ascending and X (ids.size() x dimension, row-major), x_i[j] the sum of row
+// i's values at column j in file order -- the rows of cooToVectors ordered by
+// id, without the per-row vectors and the serial passes (the file is parsed,
+// its ids marked and its values scattered by `threads` threads; cells that
+// occur more than once are re-summed in file order).
+void readInputDense(const std::string &path, int dimension, std::vector<int32_t> &ids, std::vector<double> &X,
+                    int threads = 0);
 
 }  // namespace tsne_flink

@@ -117,9 +117,23 @@ Csr TsneHelpers::kNearestNeighborsCsr(const Vectors &input, int32_t k, int32_t m
         return c;
     }
     std::vector<double> X;
+    std::vector<int32_t> ids;
     int32_t d = 0;
-    denseInput(input, c.ids, X, d);
+    denseInput(input, ids, X, d);
+    return kNearestNeighborsCsr(std::move(ids), X, d, k, metric, method, iterations, randomState);
+}
+
+Csr TsneHelpers::kNearestNeighborsCsr(std::vector<int32_t> ids, const std::vector<double> &X, int32_t d, int32_t k,
+                                      int32_t metric, const std::string &method, int32_t iterations,
+                                      int64_t randomState) {
+    Csr c;
+    c.ids = std::move(ids);
     const int64_t n = (int64_t)c.ids.size();
+    if (n < 2) {
+        c.row_ptr.assign(1, 0);
+        c.ids.clear();
+        return c;
+    }
     const int64_t kk = std::min<int64_t>(k, n - 1);
     c.col.resize((size_t)(n * kk));
     c.val.resize((size_t)(n * kk));

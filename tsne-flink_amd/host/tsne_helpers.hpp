@@ -86,6 +86,10 @@ class TsneHelpers {
     // knnMethod: "bruteforce" / "partition" (exact) or "project".
     Csr kNearestNeighborsCsr(const Vectors &input, int32_t k, int32_t metric, const std::string &method = "bruteforce",
                              int32_t iterations = 3, int64_t randomState = 0);
+    // the same on the input already dense: ids ascending, X ids.size() x d (readInputDense)
+    Csr kNearestNeighborsCsr(std::vector<int32_t> ids, const std::vector<double> &X, int32_t d, int32_t k,
+                             int32_t metric, const std::string &method = "bruteforce", int32_t iterations = 3,
+                             int64_t randomState = 0);
     Csr pairwiseAffinitiesCsr(const Csr &knn, double perplexity);
     Csr jointDistributionCsr(const Csr &affinities);
     void optimizeCsr(const Csr &P, WorkingSet &ws, double learningRate, int32_t iterations, int32_t metric,

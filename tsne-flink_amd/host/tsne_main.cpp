@@ -60,12 +60,6 @@ struct Params {
     long getLong(const std::string &k, long def) const { return has(k) ? (long)std::stod(getRequired(k)) : def; }
 };
 
-// Tsne.readInput (Tsne.scala:138-153): COO "i,j,v" lines -> dense vectors
-// (parallel mmap reader, coo_reader.cpp).
-Vectors readInput(const std::string &path, int dimension) {
-    return cooToVectors(readCooFile(path), dimension);
-}
-
 // Tsne.readDistanceMatrix (Tsne.scala:155-159): raw (i, j, d) triples.
 std::vector<Triple> readDistanceMatrix(const std::string &path) {
     const CooTriples t = readCooFile(path);
@@ -125,13 +119,16 @@ int main(int argc, char **argv) {
         if (inputDistanceMatrix) {
             knn = toCsr(readDistanceMatrix(inputPath));
         } else {
-            Vectors input = readInput(inputPath, inputDimension);
+            // Tsne.readInput's rows, ordered by id as the kNN takes them (readInputDense)
+            std::vector<int32_t> ids;
+            std::vector<double> X;
+            readInputDense(inputPath, inputDimension, ids, X);
             double t1 = now();
-            std::fprintf(stderr, "[tsne_hip] read %zu points in %.3f s\n", input.size(), t1 - t0);
+            std::fprintf(stderr, "[tsne_hip] read %zu points in %.3f s\n", ids.size(), t1 - t0);
             if (knnMethod != "bruteforce" && knnMethod != "partition" && knnMethod != "project")
                 throw std::invalid_argument("Knn method '" + metricName + "' not defined");  // Tsne.scala:78
-            knn = h.kNearestNeighborsCsr(input, (int32_t)neighbors, metric, knnMethod, (int32_t)knnIterations,
-                                         randomState);
+            knn = h.kNearestNeighborsCsr(std::move(ids), X, inputDimension, (int32_t)neighbors, metric, knnMethod,
+                                         (int32_t)knnIterations, randomState);
             std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", now() - t1);
         }
         double t2 = now();
