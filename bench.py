@@ -370,7 +370,7 @@ def main():
     attr_gbs = attr_bytes / (attr_ms * 1e-3) / 1e9 if attr_ms else None
     kinds = sorted({sa for (_, sa, _) in alog if sa in (0, 3)})
     attr_kernel = {0: "attract_rows<64,4,LOSS=false>", 1: "attract_tiles<LOSS=false>",
-                   2: "attract3<LOSS=false>"}.get(ctx.counter("opt.attract_kernel"), "?")
+                   2: "attract3<LOSS=false>", 3: "attract_tiles3<LOSS=false>"}.get(ctx.counter("opt.attract_kernel"), "?")
     knn_flops = 2.0 * (r1 - r0) * n * d
     knn_mode = "bf16x3" if ctx.get_option("knn_bf16") else "f32"
     upd_bytes = 64 * C * rows   # N*C*(5 reads + 3 writes)*8 B

@@ -137,6 +137,8 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             permutation);
  *   "root_tile" 1             root-tile shortcut of the small-embedding phase;
  *   "attract_tiles" 1         tiled attraction where the labels allow it;
+ *   "attract_tiles3" 0        3-D: the tiled attraction too (slower than the
+ *                             row kernel beside the octree traversal at C4);
  *   "attract_cfg" -1          its tile shape (-1 automatic, 0..3);
  *   "graph_order" 1           P's graph order as the initial labels;
  *   "relabel" -1              Morton relabels: -1 automatic, 0 never, 1 by
@@ -150,6 +152,15 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             selection reads the previous traversal's costs:
  *                             the optimizer's previous iteration, and for the
  *                             single-call operators only with
+ *   "spill" 0, "spill_task" 0.25, "spill_min" 256, "spill_force" 0,
+ *   "spill_drains" 2          BH work splitting (2-D): a walk past spill x the
+ *                             previous traversal's mean cost (>= spill_min
+ *                             record pops; spill_force: a fixed budget) hands
+ *                             the rest of its stack to task lists that
+ *                             spill_drains follow-up launches take, splitting
+ *                             again past spill_task x that budget; the sums are
+ *                             deterministic, equal to the unsplit walk to
+ *                             rounding (0: off, the default: slower at C3);
  *   "bh_split" 0              several ranks (2-D), 1: partition the Barnes-Hut
  *                             tree by ranges of its sorted points -- every rank
  *                             walks every query over the cells holding its own
@@ -213,7 +224,8 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *   "comm.kind"          the context's communicator: 0 none, 1 RCCL, 2 loopback,
  *                        3 caller callbacks; "comm.calls" collectives it issued;
  *   "opt.attract_kernel" the optimizer's attraction kernel: 0 attract_rows,
- *                        1 attract_tiles, 2 attract3 (3-D), -1 no optimizer;
+ *                        1 attract_tiles, 2 attract3 (3-D), 3 attract_tiles3
+ *                        (3-D, tiled), -1 no optimizer;
  *   "opt.csort_oversized_total"  the same summed over every build of the optimizer's tree;
  *   "bh.csort_oversized", "opt.csort_oversized"  buckets of the last coherent
  *                        Morton sort (csort.hpp) beyond its LDS capacity;

@@ -378,8 +378,12 @@ def test_c3_gmm_1m_full_size(ctx):
 def test_c4_sparse_cosine_3d_full_size(ctx):
     X = CF.c4()
     Xd = torch.from_numpy(X).cuda()
-    full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 150: 32}, grad_rows=250_000,
-                q0=77_777, stop=300, steps=(1, 120, 150, 300), name="C4")
+    # the whole schedule (round 6: past t = 300), the optimizer's own step
+    # checked in the late phase too (t = 650, 1000)
+    losses = full_config(ctx, Xd, X, 90, "cosine", 30.0, 0.5, 1000, 3, snaps={1: 16, 150: 32, 1000: 32},
+                         grad_rows=250_000, q0=77_777, steps=(1, 120, 150, 300, 650, 1000), name="C4")
+    assert sorted(losses) == list(range(10, 1001, 10))
+    assert all(np.isfinite(v) for v in losses.values())
 
 
 # ------------------------------------------------------------------- C5

@@ -122,6 +122,7 @@ static const OptionField k_options[] = {
     {"oct_layout_switch", &Options::oct_layout_switch, nullptr, 0, 1e6},
     {"root_tile", nullptr, &Options::root_tile, 0, 1},
     {"attract_tiles", nullptr, &Options::attract_tiles, 0, 1},
+    {"attract_tiles3", nullptr, &Options::attract_tiles3, 0, 1},
     {"attract_cfg", nullptr, &Options::attract_cfg, -1, 3},
     {"graph_order", nullptr, &Options::graph_order, 0, 1},
     {"relabel", nullptr, &Options::relabel, -1, 2},

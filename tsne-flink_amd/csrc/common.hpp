@@ -175,6 +175,8 @@ struct Options {
     int oct_records = 2;      // 3-D: octal records + the 64-query record traversal (1: the 8-query one; 0: the binary-node walk)
     int root_tile = 1;        // root-tile shortcut of the small-embedding phase
     int attract_tiles = 1;    // tiled attraction (attract_tiles) where the labels allow it
+    int attract_tiles3 = 0;   // 3-D: the tiled attraction (attract_tiles3) instead of attract3 (C4: 6.7 vs 3.7 ms
+                              // per launch beside the octree traversal; round 6)
     int attract_cfg = -1;     // its tile shape: -1 by rows per rank, else ATCfg0..3
     int graph_order = 1;      // P's graph order (components + BFS) as the initial labels
     int relabel = -1;         // -1 automatic, 0 never, 1 by the locality score, 2 always
@@ -285,7 +287,8 @@ void opt_profile(tsne_ctx *ctx, int enable, double *ms5, int64_t *visits);
 double opt_last_z(tsne_ctx *ctx);
 int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, double *ms, int32_t cap);
 void opt_destroy(tsne_ctx *ctx);
-int64_t opt_attract_kernel(tsne_ctx *ctx);   // the optimizer's attraction: 0 attract_rows, 1 attract_tiles, 2 attract3 (-1: none)
+int64_t opt_attract_kernel(tsne_ctx *ctx);   // the optimizer's attraction: 0 attract_rows, 1 attract_tiles, 2 attract3,
+                                              // 3 attract_tiles3 (-1: none)
 BHTree *opt_tree(tsne_ctx *ctx);   // the optimizer's 2-D tree (nullptr without one)
 
 // comm.cpp

@@ -117,6 +117,7 @@ struct OptState {
     // tiled attraction layout of the owned rows (attract_tiles), rebuilt with them
     bool at_on = false;
     int64_t at_nrb = 0, at_ncb = 0;
+    int64_t at_rbs = 0;       // rows per row block (<= the config's RB: the grid covers the CUs)
     int at_cfg = 0;
     bool morton_labels = false;   // the labels follow the embedding's Morton order (a relabel happened)
     ATile *at_tiles = nullptr;
@@ -405,6 +406,9 @@ using ATCfg0 = ATCfg<512, 5888, 1024>;    // 102 KB LDS
 using ATCfg1 = ATCfg<1024, 5888, 1024>;   // 110 KB
 using ATCfg2 = ATCfg<2048, 5888, 1024>;   // 126 KB
 using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
+// 3-D (attract_tiles3): 24-byte points, so a smaller window
+using ATCfg3D = ATCfg<2048, 4096, 1024>;   // 96 KB window + 48 KB accumulators
+using ATCfg3Ds = ATCfg<512, 4096, 1024>;   // 96 + 12 KB: a rank's share of the rows
 #ifndef AT_DIAG
 #define AT_DIAG 0   // 1 / 2: diagnostic builds of attract_tiles (timing only)
 #endif
@@ -418,15 +422,15 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
     const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
     const uint32_t *__restrict__ srow, int64_t rows, int64_t r0, int64_t n, const uint16_t *__restrict__ pk,
     const double *__restrict__ pv, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
-    int64_t xcd_chunk, double2 *__restrict__ attr, double *__restrict__ lpart) {
+    int64_t xcd_chunk, double2 *__restrict__ attr, double *__restrict__ lpart, int64_t rbs) {
     constexpr int RB = CF::RB, W = CF::W, NT = CF::NT, WAVES = CF::WAVES;
     __shared__ double2 win[W];
     __shared__ double2 acc[RB];
     __shared__ double sl[WAVES];
     const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
-    const int64_t b0 = rb * RB;
-    const int nr = (int)min((int64_t)RB, rows - b0);
+    const int64_t b0 = rb * rbs;   // rbs <= RB rows per block (build_attract_tiles)
+    const int nr = (int)min(rbs, rows - b0);
     const double2 *Y2 = reinterpret_cast<const double2 *>(Y);
     const double2 *Yrow = Y2 + r0 + b0;
     for (int i = tid; i < nr; i += NT) acc[i] = make_double2(0.0, 0.0);
@@ -548,11 +552,12 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
 // 1. key (row block * ncb + window) << rowbits | local row of every owned
 //    entry (wave per row), for a stable radix sort
 __global__ void at_keys(const int64_t *__restrict__ rpw, const int32_t *__restrict__ colw, int64_t rows, int64_t ncb,
-                        int rowbits, int64_t W, uint64_t *__restrict__ key, int32_t *__restrict__ idx) {
+                        int rowbits, int64_t rbs, int64_t W, uint64_t *__restrict__ key, int32_t *__restrict__ idx) {
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     if (r >= rows) return;
-    const uint64_t hi = (uint64_t)((r >> rowbits) * ncb);
-    const uint64_t lr = (uint64_t)(r & ((1 << rowbits) - 1));
+    const int64_t rb = r / rbs;   // row block of rbs (<= 2^rowbits) rows
+    const uint64_t hi = (uint64_t)(rb * ncb);
+    const uint64_t lr = (uint64_t)(r - rb * rbs);
     for (int64_t e = rpw[r] + lane_id(); e < rpw[r + 1]; e += 64) {
         key[e] = ((hi + (uint64_t)(colw[e] / W)) << rowbits) | lr;
         idx[e] = (int32_t)e;
@@ -1030,6 +1035,166 @@ __device__ __forceinline__ double qterm3(const double *a, const double *b) {
     return r;
 }
 
+// qterm3's q with x = 1 + metric returned too (the tiled 3-D attraction's
+// loss terms P ln(P Z x) need no division); the same arithmetic as qterm3.
+template <int MET>
+__device__ __forceinline__ double qforce3_t(const double *a, const double *b, double &x) {
+    double m;
+    if (MET == TSNE_METRIC_COSINE) {
+        double dt = 0.0, na = 0.0, nb = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            dt = __dadd_rn(dt, __dmul_rn(a[k], b[k]));
+            na = __dadd_rn(na, __dmul_rn(a[k], a[k]));
+            nb = __dadd_rn(nb, __dmul_rn(b[k], b[k]));
+        }
+        m = 1.0 - dt / (sqrt(na) * sqrt(nb));
+    } else {
+        double s2 = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            const double d = __dsub_rn(a[k], b[k]);
+            s2 = __dadd_rn(s2, __dmul_rn(d, d));
+        }
+        m = MET == TSNE_METRIC_EUCLIDEAN ? sqrt(s2) : s2;
+    }
+    x = 1.0 + m;
+    double r = __builtin_amdgcn_rcp(x);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    r = __fma_rn(r, __fma_rn(-x, r, 1.0), r);
+    return r;
+}
+
+// The tiled attraction in 3-D (round 6; the 2-D kernel attract_tiles above,
+// same layout and loop): per tile the window's W points (24 B each, copied
+// from Y as 16-byte pieces) and the row block's RB accumulators sit in LDS;
+// each row of a 64-row slice is one lane, summing its entries of the tile in
+// its own order with attract3's pair term (qterm3), then adding the sum to
+// its accumulator -- one fixed order per row, no atomics.  Replaces
+// attract3's Y_j gathers (24 B from a random line per entry: 0.03 of the
+// HBM roofline in the C4 loop) by LDS reads.
+template <class CF, bool LOSS, int MET>
+__global__ __launch_bounds__(CF::NT) void attract_tiles3(
+    const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
+    const uint32_t *__restrict__ srow, int64_t rows, int64_t r0, int64_t n, const uint16_t *__restrict__ pk,
+    const double *__restrict__ pv, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
+    int64_t xcd_chunk, double *__restrict__ attr, double *__restrict__ lpart, int64_t rbs) {
+    constexpr int RB = CF::RB, W = CF::W, NT = CF::NT, WAVES = CF::WAVES;
+    static_assert(W % 2 == 0, "window as 16-byte pieces (aligned)");
+    __shared__ double2 win2[3 * W / 2];
+    __shared__ double acc[3 * RB];
+    __shared__ double sl[WAVES];
+    const double *win = reinterpret_cast<const double *>(win2);
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t b0 = rb * rbs;   // rbs <= RB rows per block (build_attract_tiles)
+    const int nr = (int)min(rbs, rows - b0);
+    const double *Yrow = Y + 3 * (r0 + b0);
+    for (int i = tid; i < 3 * nr; i += NT) acc[i] = 0.0;
+    const double Z = LOSS ? scal[0] : 1.0;
+    double lsum = 0.0;
+    constexpr int WL = (3 * W / 2 + NT - 1) / NT;
+    const int t0 = rbt[rb], t1 = rbt[rb + 1];
+    for (int t = t0; t < t1; ++t) {
+        const ATile tl = tiles[t];
+        {   // the window's 3 wn doubles: 16-byte pieces (the odd last double of the last window alone)
+            const int64_t base = (int64_t)tl.cb * W;
+            const int wn = (int)min((int64_t)W, n - base);
+            const int np = 3 * wn / 2;
+            const double2 *src = reinterpret_cast<const double2 *>(Y + 3 * base);
+            double2 yv[WL];
+#pragma unroll
+            for (int k = 0; k < WL; ++k) yv[k] = src[min(tid + k * NT, np - 1)];
+#pragma unroll
+            for (int k = 0; k < WL; ++k) {
+                const int i = tid + k * NT;
+                if (i < np) win2[i] = yv[k];
+            }
+            if ((3 * wn) & 1) {
+                if (tid == 0) reinterpret_cast<double *>(win2)[3 * wn - 1] = Y[3 * (base + wn) - 1];
+            }
+        }
+        __syncthreads();
+        const int s0 = tl.s0, send = tl.s0 + tl.ns;
+        int s = s0 + w;
+        ASlice sd{};
+        uint32_t rl = 0;
+        if (s < send) {
+            sd = slices[s];
+            rl = srow[(int64_t)s * 64 + lane];
+        }
+        while (s < send) {
+            const int len = (int)(rl & ((1u << AT_LENBITS) - 1)), lrow = (int)(rl >> AT_LENBITS);
+            double yi[3] = {0.0, 0.0, 0.0};
+            if (len > 0) { yi[0] = Yrow[3 * lrow]; yi[1] = Yrow[3 * lrow + 1]; yi[2] = Yrow[3 * lrow + 2]; }
+            const int sn = s + WAVES;
+            ASlice sdn{};
+            uint32_t rln = 0;
+            double f0 = 0.0, f1 = 0.0, f2 = 0.0;
+            int64_t off = sd.base;
+            for (int k0 = 0; k0 < sd.width; k0 += AT_U) {
+                uint32_t cu[AT_U];
+                double vu[AT_U];
+#pragma unroll
+                for (int u = 0; u < AT_U; ++u) {
+                    const int k = k0 + u;
+                    cu[u] = 0;
+                    vu[u] = 0.0;
+                    if (k < len) { cu[u] = pk[off + lane]; vu[u] = pv[off + lane]; }
+                    off += __popcll(__ballot(len > k));
+                }
+                if (k0 == 0 && sn < send) {
+                    sdn = slices[sn];
+                    rln = srow[(int64_t)sn * 64 + lane];
+                }
+#pragma unroll
+                for (int u = 0; u < AT_U; ++u) {
+                    if (k0 + u < len) {
+                        const double yj[3] = {win[3 * cu[u]], win[3 * cu[u] + 1], win[3 * cu[u] + 2]};
+                        double x1m;
+                        const double q = qforce3_t<MET>(yi, yj, x1m);
+                        const double sc = __dmul_rn(vu[u], q);
+                        f0 = __fma_rn(sc, __dsub_rn(yi[0], yj[0]), f0);
+                        f1 = __fma_rn(sc, __dsub_rn(yi[1], yj[1]), f1);
+                        f2 = __fma_rn(sc, __dsub_rn(yi[2], yj[2]), f2);
+                        if (LOSS) {
+                            const double pij = __dmul_rn(vu[u], ex);
+                            lsum += pij * log_kl(pij * Z * x1m);
+                        }
+                    }
+                }
+            }
+            if (sd.wide) {   // one row over the 64 lanes: a fixed-order tree
+                f0 = wave_sum(f0);
+                f1 = wave_sum(f1);
+                f2 = wave_sum(f2);
+                if (lane == 0) {
+                    acc[3 * lrow] = __dadd_rn(acc[3 * lrow], f0);
+                    acc[3 * lrow + 1] = __dadd_rn(acc[3 * lrow + 1], f1);
+                    acc[3 * lrow + 2] = __dadd_rn(acc[3 * lrow + 2], f2);
+                }
+            } else if (len > 0) {
+                acc[3 * lrow] = __dadd_rn(acc[3 * lrow], f0);
+                acc[3 * lrow + 1] = __dadd_rn(acc[3 * lrow + 1], f1);
+                acc[3 * lrow + 2] = __dadd_rn(acc[3 * lrow + 2], f2);
+            }
+            s = sn;
+            sd = sdn;
+            rl = rln;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < 3 * nr; i += NT) attr[3 * b0 + i] = acc[i] * ex;
+    if (LOSS) {
+        lsum = wave_sum(lsum);
+        if (lane == 0) sl[w] = lsum;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int k = 0; k < WAVES; ++k) s += sl[k];
+            lpart[blockIdx.x] = s;
+        }
+    }
+}
+
 // One wave per row (grid-stride), lanes over the row's entries, then a
 // wave reduction: attr_i = sum_j ex P_ij q_ij (y_i - y_j); LOSS adds the KL
 // terms into one partial per block (TsneHelpers.scala:269-306).  A lane's
@@ -1161,6 +1326,33 @@ __global__ __launch_bounds__(256) void center3(const double *__restrict__ Ynew, 
 }
 
 static int64_t attract3_blocks(int64_t rows) { return std::max<int64_t>(1, std::min<int64_t>(8192, ceil_div(rows, 4))); }
+
+// attract_tiles3 over the tiled layout of the owned rows (3-D); returns the
+// workgroups (the loss partials)
+template <class CF, bool LOSS, int MET>
+static void attract_tiles3_c(hipStream_t st, const OptState *s, const double *Y, const double *scal, double ex,
+                             double *attr, double *lpart) {
+    const int64_t nb = s->at_nrb;
+    hipLaunchKernelGGL((attract_tiles3<CF, LOSS, MET>), dim3(nb), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt,
+                       s->at_slices, s->at_srow, s->L1 - s->L0, s->L0, s->n, s->at_pk, s->at_pv, Y, scal, ex,
+                       nb / NUM_XCD, attr, lpart, s->at_rbs);
+}
+template <bool LOSS, int MET>
+static void attract_tiles3_m(hipStream_t st, const OptState *s, const double *Y, const double *scal, double ex,
+                             double *attr, double *lpart) {
+    if (s->at_cfg == 4) attract_tiles3_c<ATCfg3D, LOSS, MET>(st, s, Y, scal, ex, attr, lpart);
+    else attract_tiles3_c<ATCfg3Ds, LOSS, MET>(st, s, Y, scal, ex, attr, lpart);
+}
+static int64_t attract_tiles3_launch(hipStream_t st, const OptState *s, const double *Y, const double *scal,
+                                     int metric, double ex, double *attr, double *lpart, bool loss) {
+#define TSNE_AT3(L, M) attract_tiles3_m<L, M>(st, s, Y, scal, ex, attr, lpart)
+    if (metric == TSNE_METRIC_EUCLIDEAN) { if (loss) TSNE_AT3(true, TSNE_METRIC_EUCLIDEAN); else TSNE_AT3(false, TSNE_METRIC_EUCLIDEAN); }
+    else if (metric == TSNE_METRIC_COSINE) { if (loss) TSNE_AT3(true, TSNE_METRIC_COSINE); else TSNE_AT3(false, TSNE_METRIC_COSINE); }
+    else { if (loss) TSNE_AT3(true, TSNE_METRIC_SQEUCLIDEAN); else TSNE_AT3(false, TSNE_METRIC_SQEUCLIDEAN); }
+#undef TSNE_AT3
+    TSNE_LAUNCH_CHECK();
+    return s->at_nrb;
+}
 
 static int64_t attract3_launch(hipStream_t st, const int64_t *rp, const int32_t *col, const double *val, int64_t r0,
                                int64_t r1, const double *Y, const double *scal, int metric, double ex, double *attr,
@@ -1451,8 +1643,10 @@ static void gather_working_set(tsne_ctx *ctx, OptState *s) {
     comm_allgatherv(ctx, s->gains[c], off.data());
 }
 
-// Tile configuration for `rows` owned rows (Options::attract_cfg 0..3 forces one)
-static int at_cfg(tsne_ctx *ctx, int64_t rows) {
+// Tile configuration for `rows` owned rows (Options::attract_cfg 0..3 forces one);
+// 3-D: 4 (ATCfg3D) when its row blocks cover the CUs, else 5 (ATCfg3Ds)
+static int at_cfg(tsne_ctx *ctx, int64_t rows, int C = 2) {
+    if (C == 3) return ceil_div(rows, (int64_t)ATCfg3D::RB) >= ctx->cu_count - ctx->cu_count / 16 ? 4 : 5;
     if (ctx->opts.attract_cfg >= 0) return ctx->opts.attract_cfg;
     for (int c = 3; c > 0; --c)
         if (ceil_div(rows, (int64_t)512 << c) >= ctx->cu_count - ctx->cu_count / 16) return c;
@@ -1476,16 +1670,23 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
     // embedding's Morton order, a row's Y_j are spatially local and
     // attract_rows' gathers hit the L2 (C3 loss launches: attract_rows 1.58
     // ms, attract_tiles 2.4 ms over t = 300..1000; in graph order 1.45 vs 1.11).
-    if (!on || rows <= 0 || s->morton_labels) return;
+    // 3-D only with Options::attract_tiles3 (measured slower than attract3 at C4)
+    if (!on || rows <= 0 || s->morton_labels || (s->C == 3 && !ctx->opts.attract_tiles3)) return;
     if (s->nnz / std::max<int64_t>(1, n) > 1024 && n * 16 <= (2 << 20)) return;
     int64_t m = 0;
     TSNE_HIP(hipMemcpyAsync(&m, s->rpw + rows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     TSNE_HIP(hipStreamSynchronize(st));
     if (m <= 0 || m >= (int64_t)INT32_MAX) return;
-    const int cfg = at_cfg(ctx, rows);
-    const int rowbits = cfg == 0 ? ATCfg0::ROWBITS : cfg == 1 ? ATCfg1::ROWBITS : cfg == 2 ? ATCfg2::ROWBITS : ATCfg3::ROWBITS;
-    const int64_t W = cfg == 0 ? ATCfg0::W : cfg == 1 ? ATCfg1::W : cfg == 2 ? ATCfg2::W : ATCfg3::W;
-    const int64_t nrb = ceil_div(rows, (int64_t)1 << rowbits), ncb = ceil_div(n, W);
+    const int cfg = at_cfg(ctx, rows, s->C);
+    const int rowbits = cfg == 0 ? ATCfg0::ROWBITS : cfg == 1 ? ATCfg1::ROWBITS : cfg == 2 ? ATCfg2::ROWBITS
+                      : cfg == 3 ? ATCfg3::ROWBITS : cfg == 4 ? ATCfg3D::ROWBITS : ATCfg3Ds::ROWBITS;
+    const int64_t W = cfg == 0 ? ATCfg0::W : cfg == 1 ? ATCfg1::W : cfg == 2 ? ATCfg2::W : cfg == 3 ? ATCfg3::W
+                    : cfg == 4 ? ATCfg3D::W : ATCfg3Ds::W;
+    // rows per block: the config's 2^rowbits, or fewer (a multiple of 64) so
+    // that the row blocks cover every CU (C3: 3968 rows, 253 blocks, instead
+    // of 245 blocks of 4096)
+    const int64_t rbs = std::min<int64_t>((int64_t)1 << rowbits, round_up(ceil_div(rows, (int64_t)ctx->cu_count), 64));
+    const int64_t nrb = ceil_div(rows, rbs), ncb = ceil_div(n, W);
     int bits = rowbits;
     for (uint64_t v = (uint64_t)(nrb * ncb - 1); v; v >>= 1) ++bits;
     uint64_t *key = ws.get<uint64_t>("opt.at.key", m), *key2 = ws.get<uint64_t>("opt.at.key2", m);
@@ -1503,8 +1704,8 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
         return h[0] + h[1];
     };
     // 1-2: entries sorted by (tile, local row), row order kept within a row
-    hipLaunchKernelGGL(at_keys, dim3(ceil_div(rows, 4)), dim3(256), 0, st, s->rpw, s->colw, rows, ncb, rowbits, W, key,
-                       idx);
+    hipLaunchKernelGGL(at_keys, dim3(ceil_div(rows, 4)), dim3(256), 0, st, s->rpw, s->colw, rows, ncb, rowbits, rbs, W,
+                       key, idx);
     size_t tb = 0;
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, idx, idx2, (int)m, 0, bits, st));
     TSNE_HIP(hipcub::DeviceRadixSort::SortPairs(ws.get<uint8_t>("opt.at.tmp", tb), tb, key, key2, idx, idx2, (int)m, 0,
@@ -1574,6 +1775,7 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
     }
     s->at_nrb = nrb;
     s->at_ncb = ncb;
+    s->at_rbs = rbs;
     s->at_cfg = cfg;
     s->at_on = true;
 }
@@ -1767,10 +1969,12 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
         TSNE_HIP(hipMemsetAsync(s->F3, 0, sizeof(double) * 3 * n, st));
     } else {
         bh_alloc(ctx, s->tree, n);
-        s->rpw = ws.get<int64_t>("opt.rpw", rows_cap + 1);
-        s->colw = ws.get<int32_t>("opt.colw", nnz + 1);
-        s->valw = ws.get<double>("opt.valw", nnz + 1);
-        // initial labels in P's graph order (Options::graph_order = 0: the original order)
+    }
+    s->rpw = ws.get<int64_t>("opt.rpw", rows_cap + 1);
+    s->colw = ws.get<int32_t>("opt.colw", nnz + 1);
+    s->valw = ws.get<double>("opt.valw", nnz + 1);
+    {   // initial labels in P's graph order (Options::graph_order = 0: the original order);
+        // in 3-D too since round 6 (attract3's Y_j gathers then hit the L2 as in 2-D)
         const bool gorder = ctx->opts.graph_order != 0;
         const bool dense_small = s->nnz / n > 1024 && n * 16 <= (2 << 20);   // see maybe_relabel
         if (gorder && n >= 2 && !(dense_small && !sharded(ctx))) {
@@ -1858,10 +2062,11 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
                 (double)(v[21] - (~0ull - v[20])) * 0.01, (double)v[19] * 0.01);
 }
 
-// One iteration of the 3-D (octree) optimizer: labels are the original
-// indices, rank r owns rows [L0, L1) of P0 and computes BH for exactly those
-// points (its query list in octree order); only Z, the loss and the updated
-// embedding cross ranks.
+// One iteration of the 3-D (octree) optimizer: labels are P's graph order
+// (set once at setup, as in 2-D; no Morton relabels), rank r owns labels
+// [L0, L1) -- its rows of P in labels (rpw / colw / valw) -- and computes BH
+// for exactly those points (its query list in octree order); only Z, the loss
+// and the updated embedding cross ranks.
 static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     hipStream_t st = ctx->stream;
     const tsne_params &p = s->p;
@@ -1872,7 +2077,9 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     const double mom = (t <= n1) ? p.initial_momentum : p.final_momentum;
     const bool want_loss = (t % 10 == 0);
     const int64_t n = s->n;
-    double *Y = s->Y[0];
+    const int c = s->cur;
+    double *Y = s->Y[c];
+    const int64_t *rpl = s->rpw - s->L0;   // this rank's rows by label (rpl[L0] = 0)
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[0], st));
     oct_build(ctx, s->otree, Y, p.theta, ex == 1.0);
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
@@ -1885,8 +2092,9 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
         TSNE_HIP(hipEventRecord(s->ev_y, st));
         TSNE_HIP(hipStreamWaitEvent(s->side, s->ev_y, 0));
         ctx->timers.begin("opt.attract", s->side);
-        blocks = attract3_launch(s->side, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr3,
-                                 s->part, false);
+        blocks = s->at_on ? attract_tiles3_launch(s->side, s, Y, s->scal, p.metric, ex, s->attr3, s->part, false)
+                          : attract3_launch(s->side, rpl, s->colw, s->valw, s->L0, s->L1, Y, s->scal, p.metric, ex,
+                                            s->attr3, s->part, false);
         ctx->timers.end("opt.attract", s->side);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     }
@@ -1903,8 +2111,9 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
         TSNE_HIP(hipStreamWaitEvent(st, s->ev_attr, 0));
     } else {
         ctx->timers.begin("opt.attract", st);
-        blocks = attract3_launch(st, s->rp0, s->col0, s->val0, s->L0, s->L1, Y, s->scal, p.metric, ex, s->attr3,
-                                 s->part, want_loss);
+        blocks = s->at_on ? attract_tiles3_launch(st, s, Y, s->scal, p.metric, ex, s->attr3, s->part, want_loss)
+                          : attract3_launch(st, rpl, s->colw, s->valw, s->L0, s->L1, Y, s->scal, p.metric, ex,
+                                            s->attr3, s->part, want_loss);
         ctx->timers.end("opt.attract", st);
     }
     s->log_attract(t, side ? 0 : 1);   // 0: beside the traversal (side stream); 1: loss launch alone after Z
@@ -1915,7 +2124,7 @@ static void opt_step3(tsne_ctx *ctx, OptState *s, int32_t t) {
     const bool fused_mean = !sharded(ctx);
     if (s->L1 > s->L0)
         hipLaunchKernelGGL(combine_update3<1>, dim3(ceil_div(s->L1 - s->L0, 256)), dim3(256), 0, st, s->L0, s->L1,
-                           s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[0], s->gains[0],
+                           s->attr3, s->otree.inv, s->F3, s->scal, Y, nullptr, s->Ynew, s->upd[c], s->gains[c],
                            p.min_gain, mom, p.learning_rate, fused_mean ? s->mpart : nullptr);
     TSNE_LAUNCH_CHECK();
     if (want_loss) record_loss(ctx, s, t, blocks);
@@ -2031,7 +2240,7 @@ static void attract_tiles_launch_c(hipStream_t st, const OptState *s, const Attr
     const int64_t nb = s->at_nrb;
     hipLaunchKernelGGL((attract_tiles<CF, LOSS, MET>), dim3(nb), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt,
                        s->at_slices, s->at_srow, a.r1 - a.r0, a.r0, s->n, s->at_pk, s->at_pv, a.Y, a.scal, a.ex,
-                       nb / NUM_XCD, a.attr, a.lpart);
+                       nb / NUM_XCD, a.attr, a.lpart, s->at_rbs);
 }
 template <bool LOSS, int MET>
 static void attract_tiles_launch_m(hipStream_t st, const OptState *s, const AttractArgs &a) {
@@ -2257,7 +2466,7 @@ int32_t opt_attract_log(tsne_ctx *ctx, int32_t *iters, int32_t *standalone, doub
 int64_t opt_attract_kernel(tsne_ctx *ctx) {
     OptState *s = ctx->opt;
     if (!s) return -1;
-    return s->C == 3 ? 2 : (s->at_on ? 1 : 0);
+    return s->C == 3 ? (s->at_on ? 3 : 2) : (s->at_on ? 1 : 0);
 }
 
 BHTree *opt_tree(tsne_ctx *ctx) {
