@@ -8,7 +8,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-B="python bench.py --no-cpu-baseline --trace 0 ${PMC_ARGS:-}"
+B="python bench.py --no-cpu-baseline --no-cli-e2e --trace 0 ${PMC_ARGS:-}"
 R='attract_tiles|combine_update|center2'
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$R" -d gpurun_out/pmc_fetch -o pmc \
   --output-format csv -- $B > gpurun_out/pmc_fetch.log 2>&1 || exit $?

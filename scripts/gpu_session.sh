@@ -58,7 +58,7 @@ if has bench; then
     case "$v" in -) ;; lib=*) lib="${v#lib=}" ;; *) opt="--option ${v//+/ --option }" ;; esac
     bi=$((${bi:-0}+1))
     echo "# $v" >> $O/bench.jsonl
-    TSNE_HIP_LIB="$lib" run 400 python bench.py --no-cpu-baseline $opt --detail-out $O/bench_detail_$bi.json >> $O/bench.jsonl 2>> $O/bench.err || exit $?
+    TSNE_HIP_LIB="$lib" run 400 python bench.py --no-cpu-baseline --no-cli-e2e $opt --detail-out $O/bench_detail_$bi.json >> $O/bench.jsonl 2>> $O/bench.err || exit $?
   done
 fi
 if has tests3d; then
@@ -76,7 +76,7 @@ if has bench4; then
   done
 fi
 if has ktrace; then
-  run 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o kt -- python bench.py --no-cpu-baseline --trace 0 ${KTRACE_ARGS:-} > $O/ktrace_bench.json 2> $O/ktrace.err || exit $?
+  run 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ktrace -o kt -- python bench.py --no-cpu-baseline --no-cli-e2e --trace 0 ${KTRACE_ARGS:-} > $O/ktrace_bench.json 2> $O/ktrace.err || exit $?
 fi
 if has tests_all; then
   tst 1100 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 --timeout-method thread \

@@ -205,6 +205,30 @@ def test_cli_end_to_end_on_gpu(tmp_path, method, nc, extra):
     assert loss.startswith("{") and "10=" in loss and "50=" in loss
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nc", [2, 3])
+def test_cli_device_chain_equals_host_chain(tmp_path, nc):
+    """The CLI's chain resident in HBM (device_pipeline.cpp, the default for
+    the exact kNN methods) against the TsneHelpers mirror's host round trips
+    between the operators (--hostChain): the same library operators on the
+    same data, so the same embedding and loss file."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    n, d = 700, 12
+    X = np.abs(rng.normal(size=(5, d)))[rng.integers(0, 5, n)] * 3 + rng.random((n, d))
+    lines = [f"{i + 3},{j},{float(X[i, j])!r}" for i in range(n) for j in range(d)]
+    (tmp_path / "in.csv").write_text("\n".join(lines) + "\n")
+    outs = []
+    for extra in ([], ["--hostChain"]):
+        r = run("--input", "in.csv", "--output", "out.csv", "--dimension", str(d), "--knnMethod", "bruteforce",
+                "--perplexity", "20", "--iterations", "120", "--nComponents", str(nc), "--theta", "0.5",
+                "--loss", "loss.txt", *extra, cwd=tmp_path)
+        assert r.returncode == 0, r.stderr
+        outs.append(((tmp_path / "out.csv").read_text(), (tmp_path / "loss.txt").read_text()))
+    assert outs[0][0].splitlines()[0].startswith("3,")
+    assert outs[0] == outs[1]
+
+
 DENSE_HARNESS = r'''
 #include <algorithm>
 #include <cstdio>
@@ -262,3 +286,42 @@ def test_read_input_dense_equals_reference_rows(tmp_path, case):
                            str(PKG / "host" / "coo_reader.cpp"), "-o", str(exe)])
     r = subprocess.run([str(exe), str(f), str(d), "4"], capture_output=True, text=True)
     assert r.returncode == 0 and r.stdout.strip() == str(n), (r.returncode, r.stdout, r.stderr)
+
+
+PARSE_HARNESS = r'''
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include "coo_reader.hpp"
+using namespace tsne_flink;
+// each value token parsed by parseCoo must be strtod's double, bit for bit
+int main() {
+    const char *vals[] = {"1.5", "+1.5", "-0.0", "0", "4.9e-324", "1e-330", "1.7976931348623157E308", "1e400",
+                          "-1e400", "2.2250738585072011e-308", "0x1.8p1", "3.141592653589793238462643383279",
+                          "12345678901234567890", ".5", "5.", "-.25e-3", "1E+2", "0.1"};
+    std::string buf;
+    for (size_t k = 0; k < sizeof(vals) / sizeof(vals[0]); ++k) buf += std::to_string(k) + ",0," + vals[k] + "\n";
+    CooTriples t = parseCoo(buf.data(), buf.size(), 1);
+    if (t.v.size() != sizeof(vals) / sizeof(vals[0])) return 1;
+    for (size_t k = 0; k < t.v.size(); ++k) {
+        const double w = std::strtod(vals[k], nullptr);
+        if (std::memcmp(&w, &t.v[k], sizeof(double)) != 0) { std::printf("mismatch %s\n", vals[k]); return 2; }
+    }
+    std::printf("ok\n");
+    return 0;
+}
+'''
+
+
+def test_coo_values_parse_as_strtod(tmp_path):
+    """The reader's value parser (from_chars, strtod for the rest) gives the
+    correctly rounded doubles Double.parseDouble / strtod give, edge formats
+    included (sign, subnormals, overflow, hex, long mantissas)."""
+    src = tmp_path / "p.cpp"
+    src.write_text(PARSE_HARNESS)
+    exe = tmp_path / "p"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-pthread", f"-I{PKG / 'host'}", str(src),
+                           str(PKG / "host" / "coo_reader.cpp"), "-o", str(exe)])
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", (r.returncode, r.stdout, r.stderr)

@@ -1701,16 +1701,23 @@ struct NarrowView {
 constexpr int32_t REF_FORCED = 1 << 30;
 constexpr int PART_LEVEL = 10;
 
-// The traversal kernels' state (LDS per 4-wave block): KB records per batch
+// The traversal kernels' state (LDS per WPB-wave block): KB records per batch
 // (4 in the 64-query layout, NKP in the narrow one).
-template <int KB>
+template <int KB, int WPB = 4>
 struct TravLDS_T {
-    QRec srec[4][KB];            // first: the record fields' LDS offsets fit the ds_read2 immediates
-    int32_t sref[4][STACK];
-    uint64_t smask[4][STACK];
-    int32_t bref[4][KB];         // the batch's refs (its masks ride in the records' lmask)
+    QRec srec[WPB][KB];          // first: the record fields' LDS offsets fit the ds_read2 immediates
+    int32_t sref[WPB][STACK];
+    uint64_t smask[WPB][STACK];
+    int32_t bref[WPB][KB];       // the batch's refs (its masks ride in the records' lmask)
 };
-using TravLDS = TravLDS_T<4>;
+// Waves per block of the 64-query traversal (a block holds its LDS and wave
+// slots until its last wave ends; 2 instead of 4: C3 loop 5.03 / 5.02 vs
+// 5.03 / 5.04 s, t = 450 snapshot span 13.6 vs 13.5 ms -- not the limiter,
+// round 6)
+#ifndef TRAV_WPB
+#define TRAV_WPB 4
+#endif
+using TravLDS = TravLDS_T<4, TRAV_WPB>;
 using NarrowLDS = TravLDS_T<(NKP > 4 ? NKP : 4)>;
 
 // Stage the records of stack entries [sp, sp + k) of wave w into LDS (one
@@ -2197,7 +2204,7 @@ __device__ __forceinline__ void sp_write(const SpillView &sv, LDS &L, int w, int
 // whose waves take tasks while the queue has any (see "Spill" above) -- a
 // kernel of its own, so that the 64-query walk keeps its registers.
 template <int MODE, bool PART, bool TASK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void bh_traverse(
+__global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8))) void bh_traverse(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, TileTask *__restrict__ ttask, int32_t *__restrict__ ttask_n,
     const int32_t *__restrict__ meta, int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0,
@@ -2211,7 +2218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void b
     __shared__ TravLDS L;
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
-    const int64_t wid = (int64_t)blockIdx.x * 4 + w;   // query slots g0 + 64 wid .. + 63, tile list wid
+    const int64_t wid = (int64_t)blockIdx.x * TRAV_WPB + w;   // query slots g0 + 64 wid .. + 63, tile list wid
     const bool spill_on = !PART && sv.lout != 0;
     int32_t bud = 0;   // pops after which a walk splits (0: never)
     if (spill_on) bud = sv.force > 0 ? sv.force : sv.ctl[TASK ? SP_B1 : SP_B0];
@@ -3782,7 +3789,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                                                                            : bh_traverse<0, false, false>);
     auto tkern = mode == 2 ? bh_traverse<2, false, true> : mode == 1 ? bh_traverse<1, false, true>
                                                                      : bh_traverse<0, false, true>;
-    const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, 4);
+    const int64_t waves = ceil_div(s1 - s0, 64), nblocks = ceil_div(waves, TRAV_WPB);
     TSNE_REQUIRE(waves <= t.tile_waves, "tile task lists sized for fewer queries");
     // heavy groups: selected after the previous traversal of the same query
     // count from its costs (narrow_select at the end of this function, so
@@ -3824,7 +3831,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                            t.tcost, clab, nv);
         TSNE_HIP(hipEventRecord(ctx->aux_ev[1], ctx->aux_stream));
     }
-    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(256), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
+    hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * TRAV_WPB), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
                        t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
                        t.tcost, clab, nv, plim, sv);
     // the levels' tasks: drain launch l takes level l (one wave per slot),
@@ -3834,7 +3841,8 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         SpillView dv = sv;
         dv.lin = d;
         dv.lout = d < levels ? d + 1 : 0;
-        hipLaunchKernelGGL(tkern, dim3(std::max(1, ctx->cu_count * 8)), dim3(256), 0, st, t.pos, t.dupc, t.nodes,
+        hipLaunchKernelGGL(tkern, dim3(std::max(1, ctx->cu_count * 32 / TRAV_WPB)), dim3(64 * TRAV_WPB), 0, st, t.pos,
+                           t.dupc, t.nodes,
                            t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n,
                            dF, dz, visits, bcost, t.wcost, t.tcost, clab, nv, plim, dv);
     }

@@ -49,6 +49,7 @@ int32_t getMetric(const std::string &name);
 class TsneHelpers {
   public:
     explicit TsneHelpers(int device = 0);
+    tsne_ctx *context() const { return ctx_; }   // the handle its calls run on
     ~TsneHelpers();
     TsneHelpers(const TsneHelpers &) = delete;
     TsneHelpers &operator=(const TsneHelpers &) = delete;

@@ -8,7 +8,11 @@
 //            [--randomState 0] [--neighbors 3*perplexity] [--initialMomentum 0.5]
 //            [--finalMomentum 0.8] [--theta 0.25] [--loss loss.txt | --lossFile loss.txt]
 //            [--knnIterations 3] [--knnBlocks P] [--inputDistanceMatrix] [--executionPlan]
-//            [--device 0]
+//            [--device 0] [--hostChain]
+// The exact kNN methods run kNN -> affinities -> joint -> optimize resident
+// in HBM (device_pipeline.hpp); --hostChain (and --knnMethod project, the
+// distance-matrix input) take the TsneHelpers mirror, whose operators pass
+// host CSR between them as the reference's operators pass DataSets.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -19,10 +23,12 @@
 #include <map>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
 #include "coo_reader.hpp"
+#include "device_pipeline.hpp"
 #include "tsne_helpers.hpp"
 
 using namespace tsne_flink;
@@ -113,9 +119,22 @@ int main(int argc, char **argv) {
         const int32_t metric = getMetric(metricName);  // IllegalArgumentException before any work
         TsneHelpers h(device);
         double t0 = now();
+        WorkingSet ws;
+        std::map<int32_t, double> loss;
+        tsne_params prm;
+        tsne_params_default(&prm);
+        prm.n_components = (int32_t)nComponents;
+        prm.metric = metric;
+        prm.learning_rate = learningRate;
+        prm.iterations = (int32_t)iterations;
+        prm.early_exaggeration = earlyExaggeration;
+        prm.initial_momentum = initialMomentum;
+        prm.final_momentum = finalMomentum;
+        prm.theta = theta;
         // P as CSR over the sorted point ids; the kNN methods keep that form
         // from the GPU's output on (no 10^8-element triple vectors)
         Csr knn;
+        bool done = false;
         if (inputDistanceMatrix) {
             knn = toCsr(readDistanceMatrix(inputPath));
         } else {
@@ -127,42 +146,71 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "[tsne_hip] read %zu points in %.3f s\n", ids.size(), t1 - t0);
             if (knnMethod != "bruteforce" && knnMethod != "partition" && knnMethod != "project")
                 throw std::invalid_argument("Knn method '" + metricName + "' not defined");  // Tsne.scala:78
-            knn = h.kNearestNeighborsCsr(std::move(ids), X, inputDimension, (int32_t)neighbors, metric, knnMethod,
-                                         (int32_t)knnIterations, randomState);
-            std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", now() - t1);
-        }
-        double t2 = now();
-        Csr P = h.jointDistributionCsr(h.pairwiseAffinitiesCsr(knn, perplexity));
-        {   // the working set's rows are P's non-empty rows (points without an entry drop out)
-            bool all = true;
-            for (size_t i = 0; i + 1 < P.row_ptr.size(); ++i) all = all && P.row_ptr[i + 1] > P.row_ptr[i];
-            if (!all) {
-                const std::vector<Triple> t = fromCsr(P);
-                std::vector<int32_t> ids;
-                for (const auto &e : t)
-                    if (ids.empty() || e.i != ids.back()) ids.push_back(e.i);
-                P = toCsr(t, &ids);
+            if (knnMethod != "project" && ids.size() >= 2 && !parameters.has("hostChain")) {
+                // the exact kNN methods: the whole chain resident in HBM (device_pipeline.hpp);
+                // --hostChain runs the TsneHelpers mirror's host round trips instead
+                DeviceRun run = runOnDevice(h.context(), X, (int64_t)ids.size(), inputDimension, (int32_t)neighbors,
+                                            perplexity, prm, randomState);
+                std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", run.t_knn);
+                std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %lld)\n", run.t_aff,
+                             (long long)run.nnz);
+                std::fprintf(stderr, "[tsne_hip] %ld iterations in %.3f s\n", iterations, run.t_loop);
+                ws.ids = std::move(ids);
+                ws.n_components = (int32_t)nComponents;
+                ws.y = std::move(run.y);
+                loss = std::move(run.loss);
+                done = true;
+            } else {
+                knn = h.kNearestNeighborsCsr(std::move(ids), X, inputDimension, (int32_t)neighbors, metric, knnMethod,
+                                             (int32_t)knnIterations, randomState);
+                std::fprintf(stderr, "[tsne_hip] kNN in %.3f s\n", now() - t1);
             }
         }
-        std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %zu)\n", now() - t2, P.val.size());
-        WorkingSet ws = h.initWorkingSet(P.ids, (int32_t)nComponents, randomState);
-        std::map<int32_t, double> loss;
-        double t3 = now();
-        h.optimizeCsr(P, ws, learningRate, (int32_t)iterations, metric, earlyExaggeration, initialMomentum,
-                      finalMomentum, theta, &loss);
-        std::fprintf(stderr, "[tsne_hip] %ld iterations in %.3f s\n", iterations, now() - t3);
+        if (!done) {
+            double t2 = now();
+            Csr P = h.jointDistributionCsr(h.pairwiseAffinitiesCsr(knn, perplexity));
+            {   // the working set's rows are P's non-empty rows (points without an entry drop out)
+                bool all = true;
+                for (size_t i = 0; i + 1 < P.row_ptr.size(); ++i) all = all && P.row_ptr[i + 1] > P.row_ptr[i];
+                if (!all) {
+                    const std::vector<Triple> t = fromCsr(P);
+                    std::vector<int32_t> ids;
+                    for (const auto &e : t)
+                        if (ids.empty() || e.i != ids.back()) ids.push_back(e.i);
+                    P = toCsr(t, &ids);
+                }
+            }
+            std::fprintf(stderr, "[tsne_hip] affinities + joint in %.3f s (nnz %zu)\n", now() - t2, P.val.size());
+            ws = h.initWorkingSet(P.ids, (int32_t)nComponents, randomState);
+            double t3 = now();
+            h.optimizeCsr(P, ws, learningRate, (int32_t)iterations, metric, earlyExaggeration, initialMomentum,
+                          finalMomentum, theta, &loss);
+            std::fprintf(stderr, "[tsne_hip] %ld iterations in %.3f s\n", iterations, now() - t3);
+        }
 
         {   // result.map(x => (x._1, x._2(0), x._2(1))).writeAsCsv (Tsne.scala:86);
-            // the 3-D extension appends the third component
+            // the 3-D extension appends the third component.  Rows formatted
+            // by parallel chunks (java.lang.Double.toString each), written in order.
+            const size_t nc = (size_t)ws.n_components, rows = ws.ids.size();
+            const int T = (int)std::max<size_t>(1, std::min<size_t>(16, rows / 4096));
+            std::vector<std::string> part((size_t)T);
+            std::vector<std::thread> pool;
+            for (int t = 0; t < T; ++t)
+                pool.emplace_back([&, t] {
+                    std::string &o = part[(size_t)t];
+                    for (size_t r = rows * t / T; r < rows * (t + 1) / T; ++r) {
+                        o += std::to_string(ws.ids[r]);
+                        for (size_t k = 0; k < std::min<size_t>(nc, 3); ++k) {
+                            o += ',';
+                            o += javaDouble(ws.y[nc * r + k]);
+                        }
+                        o += '\n';
+                    }
+                });
+            for (auto &th : pool) th.join();
             FILE *f = std::fopen(outputPath.c_str(), "w");
             if (!f) throw std::runtime_error("cannot write " + outputPath);
-            const size_t nc = (size_t)ws.n_components;
-            for (size_t r = 0; r < ws.ids.size(); ++r) {
-                std::fprintf(f, "%d", ws.ids[r]);
-                for (size_t k = 0; k < std::min<size_t>(nc, 3); ++k)
-                    std::fprintf(f, ",%s", javaDouble(ws.y[nc * r + k]).c_str());
-                std::fprintf(f, "\n");
-            }
+            for (const std::string &o : part) std::fwrite(o.data(), 1, o.size(), f);
             std::fclose(f);
         }
         std::ofstream lf(lossFile);  // Tsne.scala:99-101
