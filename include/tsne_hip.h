@@ -216,6 +216,8 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *   "bh.wave_ticks_max", "bh.wave_ticks_sum", "bh.span_ticks"  (rep_stats) the
  *                        traversal waves' longest and summed run time and
  *                        the grid's span, in 100 MHz ticks (both layouts);
+ *   "bh.tile_ticks_max", "bh.tile_ticks_sum", "bh.tile_span_ticks"  (rep_stats)
+ *                        the same for tile_apply's waves;
  *   "bh.dense_pairs", "bh.moment_evals", "bh.tile_steps0".."bh.tile_steps3",
  *   "bh.tile_pairs0".."bh.tile_pairs3"  (rep_stats) exact-sum work: pair terms,
  *                        moment evaluations, and per dense path of tile_apply

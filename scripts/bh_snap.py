@@ -69,7 +69,8 @@ def main():
                 ctx.set_option("rep_stats", 1)
                 ctx.dev_repulsion(Y, a.theta, F, z)
                 for k in ("pops", "child_slots", "tile_points", "visits", "wave_ticks_max", "wave_ticks_sum",
-                          "span_ticks", "dense_pairs", "moment_evals") + tuple(f"tile_{w}{j}" for j in range(4)
+                          "span_ticks", "dense_pairs", "moment_evals", "tile_ticks_max", "tile_ticks_sum",
+                          "tile_span_ticks") + tuple(f"tile_{w}{j}" for j in range(4)
                                                                               for w in ("steps", "pairs")):
                     rec[k] = ctx.counter("bh." + k)
                 ctx.set_option("rep_stats", 0)

@@ -1555,7 +1555,9 @@ bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) 
     // points, wave child slots, reference-equivalent evaluations
     const int at = name == "bh.pops" ? 3 : name == "bh.tile_points" ? 4 : name == "bh.child_slots" ? 6
                  : name == "bh.visits" ? 0 : name == "bh.wave_ticks_max" ? 15 : name == "bh.wave_ticks_sum" ? 18
-                 : name == "bh.span_ticks" ? 17 : name == "bh.dense_pairs" ? 2 : name == "bh.moment_evals" ? 1 : -1;
+                 : name == "bh.span_ticks" ? 17 : name == "bh.dense_pairs" ? 2 : name == "bh.moment_evals" ? 1
+                 : name == "bh.tile_ticks_max" ? 19 : name == "bh.tile_ticks_sum" ? 22 : name == "bh.tile_span_ticks" ? 21
+                 : -1;
     // tile_apply's dense paths k = 0..3 (lane-wise, packed, query-major, staged
     // sweep): "bh.tile_steps<k>" wave steps issued, "bh.tile_pairs<k>" useful lane pairs
     int atk = at;
@@ -1568,7 +1570,8 @@ bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) 
                             ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     // span: last wave end - first wave start ([16] holds ~first start), 100 MHz ticks
-    *value_out = atk == 17 ? (int64_t)(v[17] - (~0ull - v[16])) : (int64_t)v[atk];
+    *value_out = atk == 17 ? (int64_t)(v[17] - (~0ull - v[16])) : atk == 21 ? (int64_t)(v[21] - (~0ull - v[20]))
+                                                                              : (int64_t)v[atk];
     return true;
 }
 
