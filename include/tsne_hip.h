@@ -161,6 +161,22 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             again past spill_task x that budget; the sums are
  *                             deterministic, equal to the unsplit walk to
  *                             rounding (0: off, the default: slower at C3);
+ *   "tile_stream" 0, "tile_stream_max" 0, "tile_stream_frac" 1,
+ *   "tile_stream_wait" 48, "tile_stream_gate" 1, "trav_prio" 0
+ *                             BH tile streaming (2-D, one rank): tile_stream
+ *                             workgroups per CU (<= 8), on a stream of their
+ *                             own and (gate 1) dispatched once every traversal
+ *                             block has started, sum the finished traversal
+ *                             waves' tile lists of cost (points + 16 per task)
+ *                             <= tile_stream_max (0: tile_stream_frac x the
+ *                             previous tile plan's chunk unit) while the
+ *                             traversal's last waves run, leaving after
+ *                             tile_stream_wait polls (~0.4 us each) without a
+ *                             list; the slot path sums the rest.  Deterministic;
+ *                             tile_stream_max <= 4095: the bits of 0 (off, the
+ *                             default: measured slower at C3).
+ *                             trav_prio 1-3: the 64-query traversal's waves at
+ *                             that issue priority (no measured effect);
  *   "bh_split" 0              several ranks (2-D), 1: partition the Barnes-Hut
  *                             tree by ranges of its sorted points -- every rank
  *                             walks every query over the cells holding its own
@@ -235,7 +251,9 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *                        "spill"), summed over every traversal of the tree;
  *   "bh.spill_flags", "opt.spill_flags"  1 a task list full, 2 task tile pages
  *                        exhausted (those walks went on unsplit / untiled: the
- *                        same sums, but their split points then depend on timing). */
+ *                        same sums, but their split points then depend on timing);
+ *   "bh.stream_lists", "opt.stream_lists"  tile lists the streaming consumers
+ *                        summed (option "tile_stream"), over every traversal. */
 int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);
 
 /* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls

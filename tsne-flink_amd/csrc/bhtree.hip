@@ -1213,7 +1213,8 @@ __global__ void chunk_total(const int32_t *__restrict__ tcost, int64_t waves, un
     if (lane_id() == 0 && ws) atomicAdd(total, ws);
 }
 __global__ void chunk_parts(const int32_t *__restrict__ tcost, const unsigned long long *__restrict__ total,
-                            int64_t waves, int32_t *__restrict__ Cw) {
+                            int64_t waves, int32_t *__restrict__ Cw, const int32_t *__restrict__ claims, int32_t gen,
+                            int32_t *__restrict__ wout, double frac) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w > waves) return;
     if (w == waves) { Cw[w] = 0; return; }
@@ -1221,7 +1222,11 @@ __global__ void chunk_parts(const int32_t *__restrict__ tcost, const unsigned lo
     // inside the slot capacity (waves + waves / 2 + 64, bh_alloc)
     const unsigned long long W = (unsigned long long)max<int64_t>(waves, 1);
     const long long target = max((long long)CHUNK_MIN, (long long)((2 * (*total) + W - 1) / W));
-    Cw[w] = 1 + (int32_t)min((long long)(CHUNK_MAX - 1), (long long)max(tcost[w], 0) / target);
+    if (wout && w == 0) *wout = (int32_t)min(2.0e9, frac * (double)target);
+    // (tile streaming: a handed-over list is one chunk, whichever path sums it)
+    Cw[w] = claims && (claims[w] >> 2) == gen ? 1
+                                              : 1 + (int32_t)min((long long)(CHUNK_MAX - 1),
+                                                                 (long long)max(tcost[w], 0) / target);
 }
 __global__ void chunk_fill(int32_t *__restrict__ Cw, int32_t *__restrict__ slot0,
                            const int32_t *__restrict__ tcost, int64_t waves, int32_t *__restrict__ slot_w,
@@ -1285,7 +1290,9 @@ __device__ __forceinline__ int32_t wave_bucket_add(int32_t *hist, int key, bool 
 __global__ __launch_bounds__(1024) void tile_plan(const int32_t *__restrict__ tcost, int64_t waves, int64_t slots_max,
                                                   int32_t *__restrict__ Cw, int32_t *__restrict__ slot0,
                                                   int32_t *__restrict__ slot_w, int32_t *__restrict__ slot_c,
-                                                  int32_t *__restrict__ nslots, int32_t *__restrict__ torder) {
+                                                  int32_t *__restrict__ nslots, int32_t *__restrict__ torder,
+                                                  const int32_t *__restrict__ claims, int32_t gen,
+                                                  int32_t *__restrict__ wout, double frac) {
     __shared__ int32_t bc[PLAN_BLOCKS_MAX];
     __shared__ int32_t tc[PLAN_WAVES_MAX];
     __shared__ unsigned long long red[16];
@@ -1311,9 +1318,12 @@ __global__ __launch_bounds__(1024) void tile_plan(const int32_t *__restrict__ tc
     // ceil(2 total / waves): the extra chunks sum to <= waves / 2 (bh_alloc's slot capacity)
     const unsigned long long Wd = (unsigned long long)max<int64_t>(waves, 1);
     const long long target = max((long long)CHUNK_MIN, (long long)((2 * total + Wd - 1) / Wd));
+    // (tile streaming: a handed-over list is one chunk, whichever path sums it)
     auto chunks = [&](int64_t v) {
+        if (claims && (claims[v] >> 2) == gen) return 1;
         return 1 + (int32_t)min((long long)(CHUNK_MAX - 1), (long long)tc[v] / target);
     };
+    if (wout && t == 0) *wout = (int32_t)min(2.0e9, frac * (double)target);
     // this thread's contiguous run of waves and its slot count
     const int64_t per = (waves + 1023) / 1024, v0 = min(waves, t * per), v1 = min(waves, v0 + per);
     int32_t loc = 0;
@@ -2086,6 +2096,73 @@ struct SpillView {
     int32_t force = 0;  // > 0: both budgets this many pops
 };
 
+// ---- Tile streaming (option tile_stream, round 6)
+// The 64-query traversal's tail -- its last, heavy waves finishing one by one
+// -- leaves wave slots idle, while tile_apply's work waits for the whole grid.
+// With streaming, a traversal wave whose list is short enough (st_streamed:
+// tile cost <= maxcost, so the slot path would not chunk it) hands it over
+// when it ends: its list stored, an agent-scope release, then the item
+// gen << 32 | wave at items[tail++].  tile_apply<2>, a persistent grid of
+// tile_stream workgroups per CU on a stream of its own, dispatched once every
+// traversal block has started (hipStreamWaitValue32 on ST_STARTED, which the
+// blocks count; tile_stream_gate 0: at once), takes items in order (head++);
+// it waits a bounded while for a claimed item to appear and otherwise leaves.
+// A list goes to whichever path claims its wave first (claims[wave]: gen << 2
+// | 1 the slot path, | 2 a consumer; compare-and-swap), so a list published
+// after the consumers left is summed by the slot path.  A consumer sums a list
+// as the slot path does a one-chunk wave -- D (the dense terms, the same
+// loops) into per-item partials and the moment list -- and stream_finish,
+// after the traversal's launch and the consumers, adds M (the moment terms in
+// list order, from 0) and then F += D + M, as moment_apply and chunk_combine
+// would: the same bits, whichever path took a list and when.  Handed-over
+// words are read through the vector path after the acquire (it does not
+// invalidate the scalar cache).  Nothing waits on a later launch, so no
+// consumer can hold resources another stream's kernel needs to finish.
+constexpr int ST_STARTED = 0, ST_TAIL = 1, ST_HEAD = 2, ST_CUM = 9, ST_W = 10;
+constexpr int ST_RESET = 8;     // words [0, 8) zeroed after every call (ST_CUM accumulates;
+                                // ST_W: the streaming threshold the last tile plan set)
+constexpr int ST_Q0 = 16;       // the claims (one word per wave slot) from word 16 on, then the items (8 B each)
+
+#ifndef TSNE_ST_TRAV
+#define TSNE_ST_TRAV 1   // 0: the traversal's hand-over hooks compiled out (A/B of their cost only)
+#endif
+struct StreamView {
+    int32_t *ctl = nullptr;             // ST_* words, then the claims, then the items
+    int32_t gen = 0;                    // this call's generation (never 0)
+    int32_t maxcost = 0;                // > 0: streamed when the tile cost (points + 16 per task) <= maxcost;
+                                        // 0: <= ctl[ST_W] (the previous plan's chunk unit x tile_stream_frac)
+    int32_t cap = 0;                    // wave slots the claims and items have room for
+    int32_t total = 0;                  // traversal wave slots of this call (blocks x TRAV_WPB)
+    int32_t fence = 1;                  // 0: no release before an item (timing experiments only: stale)
+    int32_t prio = 0;                   // the 64-query traversal waves' issue priority (s_setprio; option trav_prio)
+    int32_t wait = 48;                  // polls (s_sleep 16 each, ~0.4 us) a consumer waits for a claimed item
+};
+__device__ __forceinline__ int32_t *st_claims(int32_t *ctl) { return ctl + ST_Q0; }
+__device__ __forceinline__ unsigned long long *st_items(int32_t *ctl, int32_t cap) {
+    return reinterpret_cast<unsigned long long *>(ctl + ST_Q0 + ((cap + 1) & ~1));
+}
+// A wave's claim word: gen << 2 when its list was handed over this call,
+// | 1 once the slot path, | 2 once a consumer took it.  Claim for `who`: the
+// owner (`who` itself for a list that was not handed over: the slot path's).
+__device__ __forceinline__ int32_t st_claim(int32_t *claims, int64_t w, int32_t gen, int32_t who) {
+    int32_t v = __hip_atomic_load(&claims[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        if ((v >> 2) != gen) return who;
+        if (v & 3) return v & 3;
+        if (__hip_atomic_compare_exchange_strong(&claims[w], &v, (gen << 2) | who, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return who;
+    }
+}
+
+// A load through the vector path: handed-over bytes read after the acquire
+// must not come from the scalar cache, which the acquire does not invalidate
+// (a wave-uniform address would otherwise make it an s_load).
+template <class T> __device__ __forceinline__ T vec_load(const T *p) {
+    asm volatile("" : "+v"(p));
+    return *p;
+}
+
 // a += v as fixed point: X = v 2^64 truncated toward zero (|v| < 2^31), kept
 // as two words that add without carries, so both atomics are independent
 // (no returned value to wait for): a[0] += the low 32 bits of X (unsigned,
@@ -2211,8 +2288,15 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
     int64_t g1, const int32_t *__restrict__ qlist, int32_t virt, double2 *__restrict__ F, double *__restrict__ Z,
     unsigned long long *__restrict__ visits, unsigned long long *__restrict__ bcost, int32_t *__restrict__ wcost,
     int32_t *__restrict__ tcost, const int32_t *__restrict__ cost_lab, NarrowView nv, int32_t *__restrict__ plim,
-    SpillView sv) {
+    SpillView sv, StreamView stv) {
     constexpr bool STATS = MODE == 2, COST = MODE >= 1;
+    if (!PART && !TASK && stv.prio > 0) {   // issue priority over the waves beside it (option trav_prio)
+        if (stv.prio == 1) __builtin_amdgcn_s_setprio(1);
+        else if (stv.prio == 2) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(3);
+    }
+    // tile streaming (see "Tile streaming"): every block counts its start
+    if (TSNE_ST_TRAV && !PART && !TASK && stv.ctl && threadIdx.x == 0) atomicAdd(&stv.ctl[ST_STARTED], 1);
     // tree partition: this rank's sorted positions [plo, phi) (plim[2]: stack overflow flag)
     const int32_t plo = PART ? plim[0] : 0, phi = PART ? plim[1] : INT32_MAX;
     __shared__ TravLDS L;
@@ -2529,6 +2613,21 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
             if (spill_on) atomicAdd(&wcost[wid], npops + (ntilepts >> 6));
             else wcost[wid] = npops + (ntilepts >> 6);
         }
+        if (TSNE_ST_TRAV && !PART && stv.ctl && ntt > 0 &&
+            ntilepts + 16 * ntt <= (stv.maxcost > 0 ? stv.maxcost : stv.ctl[ST_W])) {
+            // hand the list to the streaming consumers: every store of this
+            // wave done, its claim word, an agent-scope release, then the item
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                __hip_atomic_store(st_claims(stv.ctl) + wid, stv.gen << 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (stv.fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int32_t k = atomicAdd(&stv.ctl[ST_TAIL], 1);
+                __hip_atomic_store(st_items(stv.ctl, stv.cap) + k,
+                                   ((unsigned long long)(uint32_t)stv.gen << 32) | (unsigned long long)wid,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     } else {
         if (page >= 0 && lane == 0) { sv.pg_n[page] = ntt; sv.pg_grp[page] = (int32_t)grp; }
         if (valid && (fx != 0.0 || fy != 0.0 || zs != 0.0)) {
@@ -2672,16 +2771,21 @@ __global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcos
 // coalesced dwordx4 load per lane, the next chunk prefetched into registers)
 // and read back as wave-uniform broadcasts.  Lanes whose bound holds are
 // counted for the next iteration's moment gate.
-// PAGE: the spill tasks' tile pages instead (one wave per page, its group's
-// 64 queries; moments evaluated in place; sums into the fixed-point
-// accumulators, see "Spill").
-template <bool PAGE>
+// MODE 1 (PAGE): the spill tasks' tile pages instead (one wave per page, its
+// group's 64 queries; moments evaluated in place; sums into the fixed-point
+// accumulators, see "Spill").  MODE 2 (STREAM): the streaming consumer (see
+// "Tile streaming"): persistent waves taking the handed-over lists, moments
+// recorded per consumer lane and evaluated after its tiles, F += D + M.  MODE 0 skips the
+// streamed waves' lists (st_streamed: their list length and tile cost).
+template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void tile_apply(
     const double2 *__restrict__ pos, const BHNode *__restrict__ nodes, const TileTask *__restrict__ ttask,
     const int32_t *__restrict__ ttask_n, int64_t g0, int64_t g1, const int32_t *__restrict__ qlist,
     int32_t *__restrict__ mom_flag, double mom_tol, int32_t *__restrict__ mtask, int32_t *__restrict__ mtask_n,
     double2 *__restrict__ F, double *__restrict__ Z, unsigned long long *__restrict__ visits,
-    const int32_t *__restrict__ torder, ChunkView cv, const double *__restrict__ mom, SpillView sv) {
+    const int32_t *__restrict__ torder, ChunkView cv, const double *__restrict__ mom, SpillView sv,
+    StreamView stv, const int32_t *__restrict__ tcost) {
+    constexpr bool PAGE = MODE == 1, STREAM = MODE == 2;
     __shared__ double2 tbuf[4][64];
     __shared__ int smark[4][64];
     __shared__ int2 srng[4][64];
@@ -2701,6 +2805,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
         tb = 0;
         nt = sv.pg_n[wid];
         if (nt == 0) return;
+    } else if (STREAM) {   // the next handed-over list (see "Tile streaming")
+        int32_t k = 0;
+        if (lane == 0) k = atomicAdd(&stv.ctl[ST_HEAD], 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        int64_t got = -1;
+        if (k < stv.total) {
+            for (int poll = 0; poll < stv.wait; ++poll) {
+                unsigned long long v = 0;
+                if (lane == 0)
+                    v = __hip_atomic_load(st_items(stv.ctl, stv.cap) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t vhi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+                const uint32_t vlo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+                if (vhi == (uint32_t)stv.gen) { got = vlo; break; }
+                __builtin_amdgcn_s_sleep(16);
+            }
+        }
+        if (got < 0) return;   // nothing more for now: the slot path takes what comes later
+        int32_t own = 0;
+        if (lane == 0) own = st_claim(st_claims(stv.ctl), got, stv.gen, 2);
+        if (__builtin_amdgcn_readfirstlane(own) != 2) continue;   // the slot path has it
+        // the producer's release pairs with this acquire: its list, F and Z fresh
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wid = k;   // entries k x 64 + lane of the consumers' partial sums and moment lists
+        qw = got;
+        mytt = ttask + qw * TILE_CAP;
+        tb = 0;
+        nt = vec_load(ttask_n + qw);
+        if (lane == 0) atomicAdd(&stv.ctl[ST_CUM], 1);
     } else {
         const int64_t blk = torder ? (int64_t)torder[blockIdx.x] : (int64_t)blockIdx.x;
         wid = blk * 4 + w;
@@ -2715,15 +2848,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
         }
         if (g0 + qw * 64 >= g1) return;
         mytt = ttask + qw * TILE_CAP;
-        const int ntw = ttask_n[qw];
+        // (a list a streaming consumer claimed first: nothing here, zero partials)
+        int ntw = ttask_n[qw];
+        if (stv.ctl) {
+            int32_t own = 0;
+            if (lane == 0) own = st_claim(st_claims(stv.ctl), qw, stv.gen, 1);
+            if (__builtin_amdgcn_readfirstlane(own) == 2) ntw = 0;
+        }
         tb = (int)((int64_t)ntw * ch / C);
         nt = (int)((int64_t)ntw * (ch + 1) / C);
     }
     const int64_t kq = g0 + qw * 64 + lane;
     const bool valid = kq < g1;
     const int64_t s = valid ? (qlist ? (int64_t)qlist[kq] : kq) : -1;
-    const int64_t e = cv.slot_w ? wid * 64 + lane : s;   // moment list / partial-sum entry
-    if (!PAGE && nt == tb) {
+    const int64_t e = STREAM || cv.slot_w ? wid * 64 + lane : s;   // moment list / partial-sum entry
+    if (MODE == 0 && nt == tb) {
         if (valid) {
             mtask_n[e] = 0;
             if (cv.slot_w) { cv.Fp[e] = make_double2(0.0, 0.0); cv.Zp[e] = 0.0; }
@@ -2744,7 +2883,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
     double2 *buf = tbuf[w];
     int masked_until = tb;   // tiles before this one take the masked sweep
     for (int t = tb; t < nt;) {
-        const TileTask tt = mytt[t];
+        const TileTask tt = STREAM ? vec_load(mytt + t) : mytt[t];
         if (t >= masked_until && tt.last - tt.first + 1 < MOM_MIN_POINTS) {
             // Lane-wise window: the run of <= 64 consecutive small tiles
             // starting at t.  Each lane walks only the points of ITS tiles
@@ -3027,7 +3166,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             fxp_add(a + 2, fy);
             fxp_add(a + 4, zs);
         }
-    } else if (valid && cv.slot_w) {
+    } else if (valid && (STREAM || cv.slot_w)) {   // STREAM: item entries (stream_finish adds them)
         mtask_n[e] = ntask;
         cv.Fp[e] = make_double2(fx, fy);
         cv.Zp[e] = zs;
@@ -3068,7 +3207,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             atomicAdd(visits + 22, w_end - w_start);
         }
     }
-    if (!PAGE) break;
+    if (MODE == 0) break;
+    }
+}
+
+// Tile streaming's last step (see "Tile streaming"), on the consumers' stream
+// after them: per handed-over list's query, moment_apply's terms M over its
+// moment list, then F += D + M as moment_apply + chunk_combine would for a
+// one-chunk wave (Fp = D; Fp += M if any; F += 0 + Fp if nonzero): the same bits.
+__global__ __launch_bounds__(256) void stream_finish(const double2 *__restrict__ pos, const BHNode *__restrict__ nodes,
+                                                     const double *__restrict__ mom, int32_t *__restrict__ ctl,
+                                                     const int32_t *__restrict__ mtask,
+                                                     const int32_t *__restrict__ mtask_n, const double2 *__restrict__ Dp,
+                                                     const double *__restrict__ Dz, int64_t g0, int64_t g1,
+                                                     double2 *__restrict__ F, double *__restrict__ Z, int32_t cap,
+                                                     int32_t gen) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = i >> 6;
+    if (k >= ctl[ST_TAIL]) return;
+    const int64_t w = (int64_t)(uint32_t)st_items(ctl, cap)[k];
+    if (st_claims(ctl)[w] != ((gen << 2) | 2)) return;   // summed by the slot path
+    const int64_t s = g0 + w * 64 + (i & 63);
+    if (s >= g1) return;
+    double2 d = Dp[i];
+    double dz = Dz[i];
+    const int nt = mtask_n[i];
+    if (nt > 0) {
+        const double2 qp = pos[s];
+        double fx = 0.0, fy = 0.0, zs = 0.0;
+        for (int t = 0; t < nt; ++t) {
+            const int node = mtask[i * MOM_TASKS + t];
+            double cx, cy, R;
+            box_centre(nodes[node], cx, cy, R);
+            moment_eval(mom + (int64_t)node * MOM_K, qp.x - cx, qp.y - cy, fx, fy, zs);
+        }
+        d = make_double2(d.x + fx, d.y + fy);
+        dz = dz + zs;
+    }
+    const double sx = 0.0 + d.x, sy = 0.0 + d.y, sz = 0.0 + dz;
+    if (sx != 0.0 || sy != 0.0 || sz != 0.0) {
+        const double2 f = F[s];
+        F[s] = make_double2(f.x + sx, f.y + sy);
+        Z[s] = Z[s] + sz;
     }
 }
 
@@ -3495,6 +3675,41 @@ static void bh_spill_alloc(tsne_ctx *ctx, BHTree &t) {
     t.sp_gen = 0;
 }
 
+// Tile streaming: control words, one item and one flag per traversal wave;
+// the consumers' stream and events on the context.
+static void bh_stream_alloc(tsne_ctx *ctx, BHTree &t) {
+    if (!ctx->st_stream) {
+        TSNE_HIP(hipStreamCreateWithFlags(&ctx->st_stream, hipStreamNonBlocking));
+        for (auto &e : ctx->st_ev) TSNE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    Workspace &ws = ctx->ws;
+    // control words, the claims, the items; kept (with ST_W, the threshold
+    // the last plan set) while the tree keeps its size
+    const size_t words = ST_Q0 + 3 * (size_t)t.tile_waves + 2;
+    int32_t *c = ws.get<int32_t>(t.pre + "st_ctl", words);
+    const bool fresh = c != t.st_ctl || t.st_words != words;
+    t.st_ctl = c;
+    t.st_words = words;
+    // per item (<= one per traversal wave slot) and lane: partial sums D and moment lists
+    const size_t ent = (size_t)(ceil_div(t.n, 64) + TRAV_WPB) * 64;
+    t.st_Dp = ws.get<double2>(t.pre + "st_Dp", ent);
+    t.st_Dz = ws.get<double>(t.pre + "st_Dz", ent);
+    t.st_mtask_n = ws.get<int32_t>(t.pre + "st_mtask_n", ent);
+    t.st_mtask = ws.get<int32_t>(t.pre + "st_mtask", ent * MOM_TASKS);
+    if (fresh) {
+        TSNE_HIP(hipMemsetAsync(t.st_ctl, 0, sizeof(int32_t) * words, ctx->stream));
+        t.st_gen = 0;
+    }
+}
+
+int64_t bh_stream_counter(tsne_ctx *ctx, BHTree &t) {
+    if (!t.st_ctl) return 0;
+    int32_t c[ST_Q0];
+    TSNE_HIP(hipMemcpyAsync(c, t.st_ctl, sizeof(c), hipMemcpyDeviceToHost, ctx->stream));
+    TSNE_HIP(hipStreamSynchronize(ctx->stream));
+    return (int64_t)c[ST_CUM];
+}
+
 int64_t bh_spill_counter(tsne_ctx *ctx, BHTree &t, bool flags) {
     if (!t.sp_ctl) return 0;
     int32_t c[SP_NCTL];
@@ -3821,6 +4036,33 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         sv.force = o.spill_force;
     }
     t.ran_spill = spill;
+    // tile streaming (see "Tile streaming"): one rank's own queries only (a
+    // rank's list, a tree partition and spill keep the slot path)
+    StreamView stv;
+    const bool stream = o.tile_stream > 0 && !plim && !spill && !qlist;
+    const int cblocks = std::max(1, ctx->cu_count * o.tile_stream);
+    if (stream) {
+        bh_stream_alloc(ctx, t);
+        stv.ctl = t.st_ctl;
+        stv.gen = ++t.st_gen;
+        if (t.st_gen >= (1 << 29)) t.st_gen = 1;   // (claims hold gen << 2; 0: never claimed)
+        stv.gen = t.st_gen;
+        stv.maxcost = o.tile_stream_max;
+        stv.wait = o.tile_stream_wait;
+        stv.total = (int32_t)(nblocks * TRAV_WPB);
+        stv.cap = (int32_t)t.tile_waves;
+        stv.fence = o.tile_stream_fence;
+        // ungated, the consumers' stream starts behind everything before the
+        // traversal (gated, the traversal's start implies that; and no marker
+        // goes between the build and the traversal on this stream, which lets
+        // the side stream's attraction reach the CUs first)
+        if (!o.tile_stream_gate) {
+            TSNE_HIP(hipEventRecord(ctx->st_ev[0], st));
+            TSNE_HIP(hipStreamWaitEvent(ctx->st_stream, ctx->st_ev[0], 0));
+        }
+    }
+    t.ran_stream = stream;
+    stv.prio = o.trav_prio;   // (also without streaming)
     const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
     if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
         TSNE_HIP(hipEventRecord(ctx->aux_ev[0], st));
@@ -3833,7 +4075,29 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     hipLaunchKernelGGL(kern, dim3(nblocks), dim3(64 * TRAV_WPB), 0, st, t.pos, t.dupc, t.nodes, t.qrec, t.ttask, t.ttask_n,
                        t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n, dF, dz, visits, bcost, t.wcost,
-                       t.tcost, clab, nv, plim, sv);
+                       t.tcost, clab, nv, plim, sv, stv);
+    if (stream) {   // the consumers beside the traversal, then their moments and sums into F, Z
+        // (tile_stream_gate: dispatched once every traversal block has started,
+        // so that they take the slots its tail frees, not slots its blocks need)
+        if (o.tile_stream_gate)
+            TSNE_HIP(hipStreamWaitValue32(ctx->st_stream, t.st_ctl + ST_STARTED, (uint32_t)nblocks,
+                                          hipStreamWaitValueGte, 0xffffffffu));
+        ChunkView scv;
+        scv.Fp = t.st_Dp;
+        scv.Zp = t.st_Dz;
+        hipLaunchKernelGGL(tile_apply<2>, dim3(cblocks), dim3(256), 0, ctx->st_stream, t.pos, t.nodes, t.ttask,
+                           t.ttask_n, s0, s1, qlist, t.mom_flag, mom_tol, t.st_mtask, t.st_mtask_n, dF, dz, visits,
+                           nullptr, scv, t.mom, SpillView(), stv, t.tcost);
+        // (F, Z of the traversal itself: read after its launch has ended)
+        TSNE_HIP(hipEventRecord(ctx->st_ev[2], st));
+        TSNE_HIP(hipStreamWaitEvent(ctx->st_stream, ctx->st_ev[2], 0));
+        hipLaunchKernelGGL(stream_finish, dim3(ceil_div((int64_t)stv.total * 64, 256)), dim3(256), 0, ctx->st_stream,
+                           t.pos, t.nodes, t.mom, t.st_ctl, t.st_mtask, t.st_mtask_n, t.st_Dp, t.st_Dz, s0, s1,
+                           dF, dz, stv.cap, stv.gen);
+        // the per-call words zeroed for the next call (after the traversal and the consumers)
+        TSNE_HIP(hipMemsetAsync(t.st_ctl, 0, sizeof(int32_t) * ST_RESET, ctx->st_stream));
+        TSNE_HIP(hipEventRecord(ctx->st_ev[1], ctx->st_stream));
+    }
     // the levels' tasks: drain launch l takes level l (one wave per slot),
     // splitting into level l + 1; the last one without splits
     const int levels = std::min(o.spill_drains, SP_LMAX);
@@ -3844,7 +4108,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         hipLaunchKernelGGL(tkern, dim3(std::max(1, ctx->cu_count * 32 / TRAV_WPB)), dim3(64 * TRAV_WPB), 0, st, t.pos,
                            t.dupc, t.nodes,
                            t.qrec, t.ttask, t.ttask_n, t.meta, t.mom_flag, mom_tol, theta, s0, s1, qlist, (int32_t)t.n,
-                           dF, dz, visits, bcost, t.wcost, t.tcost, clab, nv, plim, dv);
+                           dF, dz, visits, bcost, t.wcost, t.tcost, clab, nv, plim, dv, StreamView());
     }
     // tile chunks of heavy waves (ChunkView): the single-workgroup plan while
     // the per-wave costs fit its LDS, else the multi-launch plan and block sort
@@ -3853,12 +4117,15 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     const int32_t *torder = t.torder;
     if (waves <= PLAN_WAVES_MAX && ceil_div(tslots, 4) <= PLAN_BLOCKS_MAX) {
         hipLaunchKernelGGL(tile_plan, dim3(1), dim3(1024), 0, st, t.tcost, waves, tslots, t.ch_C, t.ch_slot0,
-                           t.ch_slot_w, t.ch_slot_c, t.ch_nslots, t.torder);
+                           t.ch_slot_w, t.ch_slot_c, t.ch_nslots, t.torder, stream ? t.st_ctl + ST_Q0 : nullptr,
+                           stv.gen, stream ? t.st_ctl + ST_W : nullptr, o.tile_stream_frac);
     } else {
         const int64_t wb = ceil_div(waves + 1, 256);
         TSNE_HIP(hipMemsetAsync(t.ch_total, 0, sizeof(unsigned long long), st));
         hipLaunchKernelGGL(chunk_total, dim3(wb), dim3(256), 0, st, t.tcost, waves, t.ch_total);
-        hipLaunchKernelGGL(chunk_parts, dim3(wb), dim3(256), 0, st, t.tcost, t.ch_total, waves, t.ch_C);
+        hipLaunchKernelGGL(chunk_parts, dim3(wb), dim3(256), 0, st, t.tcost, t.ch_total, waves, t.ch_C,
+                           stream ? t.st_ctl + ST_Q0 : nullptr, stv.gen, stream ? t.st_ctl + ST_W : nullptr,
+                           o.tile_stream_frac);
         size_t tb = t.ch_scan_bytes;
         TSNE_HIP(hipcub::DeviceScan::ExclusiveSum(t.ch_scan_tmp, tb, t.ch_C, t.ch_slot0, (int)(waves + 1), st));
         hipLaunchKernelGGL(chunk_fill, dim3(wb), dim3(256), 0, st, t.ch_C, t.ch_slot0, t.tcost, waves, t.ch_slot_w,
@@ -3867,17 +4134,17 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     cv.slot_w = t.ch_slot_w; cv.slot_c = t.ch_slot_c; cv.nslots = t.ch_nslots;
     cv.Fp = t.ch_Fp; cv.Zp = t.ch_Zp;
-    hipLaunchKernelGGL(tile_apply<false>, dim3(ceil_div(tslots, 4)), dim3(256), 0, st, t.pos, t.nodes, t.ttask,
+    hipLaunchKernelGGL(tile_apply<0>, dim3(ceil_div(tslots, 4)), dim3(256), 0, st, t.pos, t.nodes, t.ttask,
                        t.ttask_n, s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits, torder, cv,
-                       t.mom, SpillView());
+                       t.mom, SpillView(), stv, t.tcost);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(tslots * 64, 256)), dim3(256), 0, st, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
     hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.ch_Fp, t.ch_Zp, t.ch_C,
                        t.ch_slot0, s0, s1, qlist, dF, dz);
     if (spill) {   // the tasks' tile pages, then their sums into F, Z
-        hipLaunchKernelGGL(tile_apply<true>, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.nodes,
+        hipLaunchKernelGGL(tile_apply<1>, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.nodes,
                            t.ttask, t.ttask_n, s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits,
-                           nullptr, ChunkView(), t.mom, sv);
+                           nullptr, ChunkView(), t.mom, sv, StreamView(), t.tcost);
         hipLaunchKernelGGL(spill_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.sp_gflag, t.sp_gen,
                            t.sp_acc, s0, s1, qlist, dF, dz, t.sp_ctl);
     }
@@ -3907,6 +4174,9 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     } else {
         t.sp_waves = 0;
     }
+    // the streamed lists' sums are in F, Z (and the control words zeroed)
+    // before anything after this call reads them
+    if (stream) TSNE_HIP(hipStreamWaitEvent(st, ctx->st_ev[1], 0));
     TSNE_LAUNCH_CHECK();
 }
 

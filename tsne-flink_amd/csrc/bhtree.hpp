@@ -190,6 +190,14 @@ struct BHTree {
     int32_t sp_gen = 0;
     int64_t sp_waves = 0;                 // query waves the budget words are for (0: none yet)
     bool ran_spill = false;               // the last traversal split work
+    // tile streaming (option tile_stream; bhtree.hip "Tile streaming")
+    int32_t *st_ctl = nullptr;            // ST_* control words (zero between calls), then the items
+    double2 *st_Dp = nullptr;             // per item x 64: the consumers' dense sums (F part)
+    double *st_Dz = nullptr;              // per item x 64: (z part)
+    int32_t *st_mtask = nullptr, *st_mtask_n = nullptr;   // per item x 64: moment lists
+    int32_t st_gen = 0;
+    size_t st_words = 0;
+    bool ran_stream = false;              // the last traversal streamed its lists
     std::string pre;                      // the workspace prefix of this tree's buffers
 };
 
@@ -240,6 +248,8 @@ void part_cost(tsne_ctx *ctx, BHTree &t, int64_t waves, unsigned long long *out)
 // traversals, or (flags) 1 a level's list full, 2 tile pages exhausted (those
 // walks went on unsplit / untiled: the same sums).
 int64_t bh_spill_counter(tsne_ctx *ctx, BHTree &t, bool flags);
+// tile streaming: the lists the consumers summed over every call of the tree
+int64_t bh_stream_counter(tsne_ctx *ctx, BHTree &t);
 // Heavy groups the last traversal on t ran narrow (synchronises the stream).
 int64_t bh_narrow_groups(tsne_ctx *ctx, BHTree &t);
 // Cut [0, n) into world slices of equal bucket cost -> bounds[0..world] (device).

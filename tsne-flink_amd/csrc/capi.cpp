@@ -135,6 +135,13 @@ static const OptionField k_options[] = {
     {"spill_min", nullptr, &Options::spill_min, 1, 1 << 30},
     {"spill_force", nullptr, &Options::spill_force, 0, 1 << 30},
     {"spill_drains", nullptr, &Options::spill_drains, 1, 8},
+    {"tile_stream", nullptr, &Options::tile_stream, 0, 8},
+    {"tile_stream_max", nullptr, &Options::tile_stream_max, -1, 1 << 30},
+    {"tile_stream_frac", &Options::tile_stream_frac, nullptr, 0.0, 64.0},
+    {"tile_stream_fence", nullptr, &Options::tile_stream_fence, 0, 1},
+    {"tile_stream_gate", nullptr, &Options::tile_stream_gate, 0, 1},
+    {"trav_prio", nullptr, &Options::trav_prio, 0, 3},
+    {"tile_stream_wait", nullptr, &Options::tile_stream_wait, 1, 1 << 20},
     {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
     {"rep_stats", nullptr, &Options::rep_stats, 0, 1},
     {"loop_serial", nullptr, &Options::loop_serial, 0, 1},
@@ -346,6 +353,10 @@ int tsne_ctx_destroy(tsne_ctx *ctx) {
         if (ctx->aux_stream) (void)hipStreamDestroy(ctx->aux_stream);
         for (auto &e : ctx->aux_ev)
             if (e) (void)hipEventDestroy(e);
+        if (ctx->st_stream) (void)hipStreamSynchronize(ctx->st_stream);
+        if (ctx->st_stream) (void)hipStreamDestroy(ctx->st_stream);
+        for (auto &e : ctx->st_ev)
+            if (e) (void)hipEventDestroy(e);
     });
     delete ctx;
     return rc;
@@ -399,6 +410,10 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
             *value_out = ctx->single_tree ? bh_spill_counter(ctx, *ctx->single_tree, k == "bh.spill_flags") : 0;
         else if (k == "opt.spill_tasks" || k == "opt.spill_flags")
             *value_out = opt_tree(ctx) ? bh_spill_counter(ctx, *opt_tree(ctx), k == "opt.spill_flags") : 0;
+        else if (k == "bh.stream_lists")
+            *value_out = ctx->single_tree ? bh_stream_counter(ctx, *ctx->single_tree) : 0;
+        else if (k == "opt.stream_lists")
+            *value_out = opt_tree(ctx) ? bh_stream_counter(ctx, *opt_tree(ctx)) : 0;
         else if (k.rfind("bh.", 0) == 0 && repulsion_stat(ctx, k, value_out)) {}
         else if (k == "comm.kind") *value_out = comm_counter(ctx, false);
         else if (k == "comm.calls") *value_out = comm_counter(ctx, true);

@@ -203,6 +203,18 @@ struct Options {
     // take the tasks left when the traversal's waves ended (the last one never splits)
     double spill = 0.0, spill_task = 0.25;
     int spill_min = 256, spill_force = 0, spill_drains = 2;
+    // tile streaming (2-D BH, one rank): tile_stream > 0 launches that many
+    // consumer workgroups per CU on their own stream beside the traversal;
+    // they sum the tile lists of traversal waves
+    // whose tile cost is <= tile_stream_max while the traversal's last waves
+    // run (4095: only lists the slot path would not chunk, so the sums are
+    // bit-identical to tile_stream 0)
+    int tile_stream = 0, tile_stream_max = 0;
+    double tile_stream_frac = 1.0;   // tile_stream_max 0: streamed up to this x the previous plan's chunk unit
+    int tile_stream_fence = 1;   // 0: timing experiment only (no release before a hand-over: stale reads)
+    int tile_stream_wait = 48;   // polls (~0.4 us each) a consumer waits for the next list before it leaves
+    int trav_prio = 0;           // 1-3: the 64-query BH traversal's waves at that issue priority (s_setprio)
+    int tile_stream_gate = 1;    // 1: the consumers wait (on the device) until every traversal block has started
 };
 
 }  // namespace tsne
@@ -213,6 +225,9 @@ struct tsne_ctx {
     bool own_stream = false;
     hipStream_t aux_stream = nullptr;   // second stream of one operator (the narrow BH waves)
     hipEvent_t aux_ev[2] = {nullptr, nullptr};
+    // third stream: the tile-streaming consumers (created on first use)
+    hipStream_t st_stream = nullptr;
+    hipEvent_t st_ev[3] = {nullptr, nullptr, nullptr};
     int rank = 0, world = 1;
     tsne::Comm *comm = nullptr;
     tsne::Workspace ws;
