@@ -119,6 +119,7 @@ def max_over_ranks(x, world):
 
 def trace_entry(ctx, t, rows, Y, n):
     ms_t, vis_t = ctx.dev_opt_profile(0)
+    ctx.synchronize()   # Y (dev_opt_sync) is written on the context's stream
     per_wave = max(1, rows / 64)
     return {"t": t, "tree_ms": ms_t[0], "bh_ms": ms_t[1], "exchange_ms": ms_t[2],
             "attract_ms": ms_t[3], "update_ms": ms_t[4],
@@ -132,6 +133,7 @@ def trace_entry(ctx, t, rows, Y, n):
             "heaviest_wave_vs_mean": vis_t[7] / max(1e-9, (vis_t[3] + vis_t[4] / 16) / per_wave),
             "max_wave_pops": vis_t[8], "max_wave_dense_points": vis_t[9],
             "narrow_groups": ctx.counter("opt.narrow_groups"),
+            "wave_mhz": ctx.counter("opt.wave_mhz"),
             "extent": (Y[:n].max(0).values - Y[:n].min(0).values).max().item()}
 
 
@@ -161,6 +163,7 @@ def setup_c3(ctx, a, dev, world, rank, r0, r1, metric="sqeuclidean"):
     rp_local = torch.arange(0, (r1 - r0) * kk + 1, kk, dtype=torch.int64, device=dev)
     p = torch.empty_like(dist)
     ctx.dev_affinities(rp_local, dist, r1 - r0, a.perplexity, p)
+    ctx.synchronize()   # the context's outputs before torch reads them (its stream is its own: api.py _fence)
     chunk = -(-n // world)
     if world > 1:   # full conditional graph on every rank for the symmetrisation
         pad = chunk - (r1 - r0)
@@ -322,6 +325,7 @@ def main():
     losses = ctx.dev_opt_losses()
     csort_over = ctx.counter("opt.csort_oversized_total") if C == 2 else None   # the timed run's sorts
     ctx.dev_opt_sync()   # the working set back to the caller's buffers (collective), timed with the D2H
+    ctx.synchronize()    # (written on the context's stream)
     Y_final = Y[:n].cpu().numpy() if rank == 0 else None   # noqa: F841 (the D2H of the result, timed)
     t_out = time.perf_counter() - t0
     alog = ctx.dev_opt_attract_log()
@@ -350,6 +354,8 @@ def main():
                 torch.cuda.synchronize()
                 snaps[t] = Y[:n].cpu().numpy().copy()
             if rank == 0 and t in dumps:
+                ctx.synchronize()   # the sync's write-back is on the context's stream (before round 6's fix
+                # the dump raced it and held the previous sync point's Y: DESIGN.md 6)
                 os.makedirs(a.dump_dir, exist_ok=True)
                 np.save(os.path.join(a.dump_dir, f"Y_t{t}.npy"), Y[:n].cpu().numpy())
         torch.cuda.synchronize()

@@ -70,7 +70,8 @@ def main():
                 ctx.dev_repulsion(Y, a.theta, F, z)
                 for k in ("pops", "child_slots", "tile_points", "visits", "wave_ticks_max", "wave_ticks_sum",
                           "span_ticks", "dense_pairs", "moment_evals", "tile_ticks_max", "tile_ticks_sum",
-                          "tile_span_ticks") + tuple(f"tile_{w}{j}" for j in range(4)
+                          "tile_span_ticks", "slow_wave_ticks", "slow_wave_pops", "slow_wave_ties",
+                          "slow_wave_tile_points", "slow_wave_slots", "wave_mhz") + tuple(f"tile_{w}{j}" for j in range(4)
                                                                               for w in ("steps", "pairs")):
                     rec[k] = ctx.counter("bh." + k)
                 ctx.set_option("rep_stats", 0)

@@ -2027,6 +2027,7 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
             atomicMax(visits + 16, ~0ull - w_start);
             atomicMax(visits + 17, w_end);
             atomicAdd(visits + 18, w_end - w_start);
+            atomicAdd(visits + 37, (unsigned long long)(clock64() - t_start));   // shader cycles (wave_mhz)
             atomicMax(visits + 31, w_end - w_start);   // longest narrow wave
         }
     }
@@ -2332,6 +2333,7 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
     const int ndup = valid ? dupc[s] : 0;   // exact duplicates of the query (itself included)
     double fx = 0.0, fy = 0.0, zs = 0.0;
     unsigned long long nvis = 0, nevals = 0, wpops = 0, wtile = 0, wslots = 0;   // STATS only
+    unsigned long long wtie = 0;                                               // STATS: key-tie points walked
     unsigned long long wfull = 0, wpart = 0;                                   // STATS only
     int sp = 0;
     int ntt = 0;
@@ -2591,6 +2593,7 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
                         }
                     } else if (kind == QK_TIE) {
                         const BHNode &tn = nodes[__builtin_amdgcn_readfirstlane(nd.cref[c])];
+                        if (STATS) wtie += (unsigned long long)(tn.last - tn.first + 1);
                         for (int p = tn.first; p <= tn.last; ++p) {
                             const double2 pp = pos[p];
                             if (act) { if (STATS) ++nvis; leaf_force(qx, qy, pp.x, pp.y, fx, fy, zs); }
@@ -2670,6 +2673,13 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
             atomicMax(visits + 17, w_end);
             atomicAdd(visits + 18, w_end - w_start);
             if (task) atomicAdd(visits + 32, 1ull);
+            atomicAdd(visits + 37, (unsigned long long)(clock64() - t_start));   // shader cycles (wave_mhz)
+            // the slowest wave's own counts (ticks << 24 | count: the max keeps that wave's)
+            const unsigned long long tk = min(w_end - w_start, (1ull << 40) - 1) << 24, cm = (1ull << 24) - 1;
+            atomicMax(visits + 33, tk | min(wpops, cm));
+            atomicMax(visits + 34, tk | min(wtie, cm));
+            atomicMax(visits + 35, tk | min(wtile, cm));
+            atomicMax(visits + 36, tk | min(wslots, cm));
         }
     }
     // TASK: the next one of the level (never waiting for one to appear)

@@ -80,6 +80,10 @@ __host__ __device__ inline double qacc_open(double ch, double inv_theta) {
     return (1.0 + ch * inv_theta * (1.0 - QACC_MARGIN)) * (1.0 - 1e-15);
 }
 
+// counters of the BH kernels' STATS blocks (visits arrays: bh_traverse,
+// tile_apply; repulsion_stat names them)
+constexpr int VIS_N = 48;
+
 struct BHTree {
     int64_t n = 0;           // points (queries)
     // device arrays (ctx workspace)

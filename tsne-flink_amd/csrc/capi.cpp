@@ -141,6 +141,8 @@ static const OptionField k_options[] = {
     {"tile_stream_fence", nullptr, &Options::tile_stream_fence, 0, 1},
     {"tile_stream_gate", nullptr, &Options::tile_stream_gate, 0, 1},
     {"trav_prio", nullptr, &Options::trav_prio, 0, 3},
+    {"attract_serial_t0", nullptr, &Options::attract_serial_t0, 0, 1 << 30},
+    {"attract_serial_t1", nullptr, &Options::attract_serial_t1, -1, 1 << 30},
     {"tile_stream_wait", nullptr, &Options::tile_stream_wait, 1, 1 << 20},
     {"comm_world1", nullptr, &Options::comm_world1, 0, 1},
     {"rep_stats", nullptr, &Options::rep_stats, 0, 1},
@@ -404,6 +406,7 @@ int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out) {
         const std::string k = name;
         if (k == "bh.narrow_groups") *value_out = ctx->single_tree ? bh_narrow_groups(ctx, *ctx->single_tree) : 0;
         else if (k == "opt.narrow_groups") *value_out = opt_tree(ctx) ? bh_narrow_groups(ctx, *opt_tree(ctx)) : 0;
+        else if (k == "opt.wave_mhz") *value_out = opt_wave_mhz(ctx);
         else if (k == "bh.csort_oversized") *value_out = ctx->single_tree ? csort_oversized(ctx, ctx->single_tree->cs) : 0;
         else if (k == "opt.attract_kernel") *value_out = opt_attract_kernel(ctx);
         else if (k == "bh.spill_tasks" || k == "bh.spill_flags")

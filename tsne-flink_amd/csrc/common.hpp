@@ -213,6 +213,7 @@ struct Options {
     double tile_stream_frac = 1.0;   // tile_stream_max 0: streamed up to this x the previous plan's chunk unit
     int tile_stream_fence = 1;   // 0: timing experiment only (no release before a hand-over: stale reads)
     int tile_stream_wait = 48;   // polls (~0.4 us each) a consumer waits for the next list before it leaves
+    int attract_serial_t0 = 0, attract_serial_t1 = -1;   // 2-D: the attraction after BH for t in [t0, t1] (A/B)
     int trav_prio = 0;           // 1-3: the 64-query BH traversal's waves at that issue priority (s_setprio)
     int tile_stream_gate = 1;    // 1: the consumers wait (on the device) until every traversal block has started
 };
@@ -286,6 +287,7 @@ void gradient_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_c
 // "bh.pops" / "bh.child_slots" / "bh.tile_points" / "bh.visits" of the last 2-D
 // repulsion_device call with Options::rep_stats; false for other names.
 bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out);
+int64_t opt_wave_mhz(tsne_ctx *ctx);   // the last traced 2-D traversal's waves' shader clock (MHz), 0 if none
 void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, double theta, double *dF,
                       double *dz);
 void gradient3_device(tsne_ctx *ctx, const int64_t *d_row_ptr, const int32_t *d_col, const double *d_P, int64_t n,

@@ -128,6 +128,7 @@ struct OptState {
     double *at_pv = nullptr;
     double last_ms[5] = {0, 0, 0, 0, 0};
     int64_t last_visits[10] = {};
+    int64_t last_mhz = 0;   // the traced traversal's waves' shader clock (MHz)
     // tree partition (Options::bh_split, several ranks, 2-D): cuts of the sorted
     // points (world + 1), this rank's aligned [lo, hi) + overflow flag, the
     // ranks' traversal costs (all-reduced), F in label order (reduce-scatter)
@@ -1534,8 +1535,8 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
         bh_build(ctx, t, dY, theta, nullptr, root_tile_enabled(ctx));
         unsigned long long *vis = nullptr;   // Options::rep_stats: the counting traversal
         if (ctx->opts.rep_stats) {
-            vis = ctx->ws.get<unsigned long long>("rep.visits", 32);
-            TSNE_HIP(hipMemsetAsync(vis, 0, sizeof(unsigned long long) * 32, st));
+            vis = ctx->ws.get<unsigned long long>("rep.visits", VIS_N);
+            TSNE_HIP(hipMemsetAsync(vis, 0, sizeof(unsigned long long) * VIS_N, st));
         }
         bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, vis);
         inv = t.inv;
@@ -1550,6 +1551,8 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
     TSNE_LAUNCH_CHECK();
 }
 
+int64_t opt_wave_mhz(tsne_ctx *ctx) { return ctx->opt ? ctx->opt->last_mhz : 0; }
+
 bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) {
     // indices of bh_traverse's counters (its STATS block): wave pops, tile
     // points, wave child slots, reference-equivalent evaluations
@@ -1557,21 +1560,26 @@ bool repulsion_stat(tsne_ctx *ctx, const std::string &name, int64_t *value_out) 
                  : name == "bh.visits" ? 0 : name == "bh.wave_ticks_max" ? 15 : name == "bh.wave_ticks_sum" ? 18
                  : name == "bh.span_ticks" ? 17 : name == "bh.dense_pairs" ? 2 : name == "bh.moment_evals" ? 1
                  : name == "bh.tile_ticks_max" ? 19 : name == "bh.tile_ticks_sum" ? 22 : name == "bh.tile_span_ticks" ? 21
-                 : -1;
+                 : name == "bh.slow_wave_ticks" ? 33 : name == "bh.slow_wave_pops" ? 33 : name == "bh.slow_wave_ties" ? 34
+                 : name == "bh.slow_wave_tile_points" ? 35 : name == "bh.slow_wave_slots" ? 36
+                 : name == "bh.wave_mhz" ? 37 : -1;
     // tile_apply's dense paths k = 0..3 (lane-wise, packed, query-major, staged
     // sweep): "bh.tile_steps<k>" wave steps issued, "bh.tile_pairs<k>" useful lane pairs
     int atk = at;
     if (at < 0 && name.size() == 14 && name.compare(0, 13, "bh.tile_steps") == 0) atk = 24 + 2 * (name[13] - '0');
     if (at < 0 && name.size() == 14 && name.compare(0, 13, "bh.tile_pairs") == 0) atk = 25 + 2 * (name[13] - '0');
-    if (atk < 0 || atk > 31) return false;
+    if (atk < 0 || atk >= VIS_N) return false;
     TSNE_REQUIRE(ctx->opts.rep_stats && ctx->ws.has("rep.visits"), "counter '" + name + "' needs option rep_stats");
-    unsigned long long v[32];
-    TSNE_HIP(hipMemcpyAsync(v, ctx->ws.get<unsigned long long>("rep.visits", 32), sizeof(v), hipMemcpyDeviceToHost,
+    unsigned long long v[VIS_N];
+    TSNE_HIP(hipMemcpyAsync(v, ctx->ws.get<unsigned long long>("rep.visits", VIS_N), sizeof(v), hipMemcpyDeviceToHost,
                             ctx->stream));
     TSNE_HIP(hipStreamSynchronize(ctx->stream));
     // span: last wave end - first wave start ([16] holds ~first start), 100 MHz ticks
     *value_out = atk == 17 ? (int64_t)(v[17] - (~0ull - v[16])) : atk == 21 ? (int64_t)(v[21] - (~0ull - v[20]))
                                                                               : (int64_t)v[atk];
+    if (atk == 37) *value_out = v[18] ? (int64_t)(100.0 * (double)v[37] / (double)v[18]) : 0;
+    if (atk >= 33 && atk <= 36)   // (ticks << 24 | count) of the slowest wave
+        *value_out = name == "bh.slow_wave_ticks" ? (int64_t)(v[atk] >> 24) : (int64_t)(v[atk] & ((1ull << 24) - 1));
     return true;
 }
 
@@ -1939,7 +1947,7 @@ void opt_setup(tsne_ctx *ctx, const tsne_params *p, const int64_t *d_row_ptr, co
     s->loss_slots = std::max(1, p->iterations / 10 + 1);
     s->loss = ws.get<double>("opt.loss", s->loss_slots);
     s->loss_written.assign(s->loss_slots, 0);
-    s->visits = ws.get<unsigned long long>("opt.visits", 32);
+    s->visits = ws.get<unsigned long long>("opt.visits", VIS_N);
     if (sharded(ctx)) {
         const int64_t nb = ceil_div(n, 256);
         if (C == 2) {
@@ -2045,9 +2053,11 @@ static void finish_profile(tsne_ctx *ctx, OptState *s, int32_t t) {
         for (int k = 0; k < 10; ++k) s->last_visits[k] = 0;
         return;
     }
-    unsigned long long v[32] = {};
+    unsigned long long v[VIS_N] = {};
     TSNE_HIP(hipMemcpy(v, s->visits, sizeof(v), hipMemcpyDeviceToHost));
     for (int k = 0; k < 10; ++k) s->last_visits[k] = (int64_t)v[k];
+    // the traversal waves' shader clock: their cycles over their 100 MHz wall ticks
+    s->last_mhz = v[18] ? (int64_t)(100.0 * (double)v[37] / (double)v[18]) : 0;
     const bool dbg = debug_tiles();   // tile_apply diagnostics
     if (dbg)
         fprintf(stderr, "[tiles] t=%d tasks=%llu dense_pts=%llu momchk=%llu moment_evals=%llu dense_pairs=%llu "
@@ -2296,7 +2306,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     const int64_t n = s->n;
     double *Y = s->Y[s->cur];
     if (s->profile) {
-        TSNE_HIP(hipMemsetAsync(s->visits, 0, 32 * sizeof(unsigned long long), st));
+        TSNE_HIP(hipMemsetAsync(s->visits, 0, VIS_N * sizeof(unsigned long long), st));
         TSNE_HIP(hipEventRecord(s->ev[0], st));
     }
     // attraction over this rank's rows (row pointer local to L0)
@@ -2323,6 +2333,9 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
         s->log_attract(t, want_loss ? 2 : 0);
         TSNE_HIP(hipEventRecord(s->ev_attr, s->side));
     };
+    // (attract_serial_t0 <= t <= attract_serial_t1: the attraction alone on
+    // this stream after the BH kernels instead -- an A/B of the overlap's cost)
+    const bool serial_at = t >= ctx->opts.attract_serial_t0 && t <= ctx->opts.attract_serial_t1 && !rt_phase;
     if (rt_phase) side_attract();
     // 1. tree (identical on every rank)
     // insertion rows = original indices; the root-tile shortcut while the
@@ -2331,7 +2344,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     // amplify any difference fastest there), the late one after
     bh_build(ctx, s->tree, Y, p.theta, s->orig[s->cur], root_tile_enabled(ctx), bh_near_tol(ctx, ex == 1.0));
     if (sharded(ctx)) comm_mark(ctx, s->tree.root_tile ? "tree_rt" : "tree");
-    if (!rt_phase) side_attract();
+    if (!rt_phase && !serial_at) side_attract();
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[1], st));
     // 2. repulsion for this rank's points: all of them, or its query list
     // (its labels' sorted positions, ascending: the waves stay Morton-local);
@@ -2355,6 +2368,7 @@ void opt_step(tsne_ctx *ctx, int32_t t) {
     } else {
         bh_repulsion(ctx, s->tree, p.theta, 0, n, s->F, s->z, s->profile ? s->visits : nullptr);
     }
+    if (serial_at) side_attract();   // (the side stream waits for everything above)
     if (s->profile) TSNE_HIP(hipEventRecord(s->ev[2], st));
     // 3. Z (TsneHelpers.scala:266): the only per-iteration all-reduce
     reduce_Z(ctx, s, s->z, split);
