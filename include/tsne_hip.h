@@ -256,6 +256,12 @@ int tsne_ctx_loop_profile(tsne_ctx *ctx, char *buf, int64_t cap, int64_t *len_ou
  *                        summed (option "tile_stream"), over every traversal. */
 int tsne_ctx_counter(tsne_ctx *ctx, const char *name, int64_t *value_out);
 
+/* Diagnostics (option "wave_log" with "rep_stats"): the last counting
+ * repulsion call's BH waves as (start, end << 2 | kind) pairs in 100 MHz wall
+ * ticks, kind 0 64-query traversal, 1 narrow, 2 tile_apply; up to cap pairs
+ * copied to out, *count = the pairs logged (<= 2^17). */
+int tsne_debug_wave_log(tsne_ctx *ctx, uint64_t *out, int64_t cap, int64_t *count);
+
 /* Multi-GPU, one process per GPU over RCCL.  Rank 0 calls
  * tsne_comm_unique_id and ships the bytes to the other ranks out of band
  * (torch.distributed / MPI / a file); every rank then calls

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--theta", type=float, default=0.5)
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE", help="tsne_ctx_set_option")
+    ap.add_argument("--wavelog", default="", help="with --stats: save each snapshot's BH wave timeline "
+                    "(start, end, kind; option wave_log) to <wavelog>_<snapshot>.npz")
     ap.add_argument("--stats", action="store_true",
                     help="after the timed calls, one call of the counting traversal (option rep_stats): "
                          "wave pops, child slots, tile points (2-D)")
@@ -67,7 +69,15 @@ def main():
                 rec["spill_flags"] = ctx.counter("bh.spill_flags")
             if a.stats and Y.shape[1] == 2 and ctx_has_option(ctx, "rep_stats"):
                 ctx.set_option("rep_stats", 1)
+                if a.wavelog:
+                    ctx.set_option("wave_log", 1)
                 ctx.dev_repulsion(Y, a.theta, F, z)
+                if a.wavelog:
+                    ctx.synchronize()
+                    t0w, t1w, kw = ctx.debug_wave_log()
+                    np.savez(f"{a.wavelog}_{os.path.basename(path).replace('.npy', '')}.npz", start=t0w, end=t1w,
+                             kind=kw)
+                    ctx.set_option("wave_log", 0)
                 for k in ("pops", "child_slots", "tile_points", "visits", "wave_ticks_max", "wave_ticks_sum",
                           "span_ticks", "dense_pairs", "moment_evals", "tile_ticks_max", "tile_ticks_sum",
                           "tile_span_ticks", "slow_wave_ticks", "slow_wave_pops", "slow_wave_ties",

@@ -1691,7 +1691,21 @@ struct NarrowView {
     int32_t *mtask_n = nullptr;
     const int32_t *nflag = nullptr;    // per group: heavy slot + 1, or 0 (the 64-query layout)
     int32_t nbn = 0;                   // workgroups of the narrow part of the grid (hmax x NPARTS / 4)
+    unsigned long long *wlog = nullptr;   // STATS + option wave_log: per-wave timeline (wave_log_put)
 };
+
+// Option wave_log (counting calls only): every traversal / narrow / tile wave
+// appends (start, end << 2 | kind) in 100 MHz wall ticks; wlog[0] counts.
+constexpr int64_t WAVE_LOG_CAP = 1 << 17;
+__device__ __forceinline__ void wave_log_put(unsigned long long *wlog, unsigned long long t0, unsigned long long t1,
+                                             int kind) {
+    if (!wlog) return;
+    const unsigned long long k = atomicAdd(wlog, 1ull);
+    if (k < (unsigned long long)WAVE_LOG_CAP) {
+        wlog[1 + 2 * k] = t0;
+        wlog[2 + 2 * k] = (t1 << 2) | (unsigned long long)kind;
+    }
+}
 
 // Tree partition (several ranks, bh_repulsion with `plim`): rank r owns the
 // sorted positions [lo, hi) and walks every query over the cells that hold
@@ -2029,6 +2043,7 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
             atomicAdd(visits + 18, w_end - w_start);
             atomicAdd(visits + 37, (unsigned long long)(clock64() - t_start));   // shader cycles (wave_mhz)
             atomicMax(visits + 31, w_end - w_start);   // longest narrow wave
+            wave_log_put(nv.wlog, w_start, w_end, 1);
         }
     }
 }
@@ -2037,7 +2052,12 @@ __device__ void narrow_wave(NarrowLDS &L, const double2 *__restrict__ pos, const
 // heavy count.  A kernel of its own (its ~78 VGPRs would cost the 64-query
 // layout's 8 waves per SIMD), launched on a second stream beside bh_traverse.
 template <int MODE>
-__global__ __launch_bounds__(256) void bh_traverse_narrow(
+#ifdef NARROW_WPE   // A/B builds: the narrow waves' occupancy bound (waves per SIMD)
+#define NARROW_ATTR __attribute__((amdgpu_waves_per_eu(NARROW_WPE)))
+#else
+#define NARROW_ATTR
+#endif
+__global__ __launch_bounds__(256) NARROW_ATTR void bh_traverse_narrow(
     const double2 *__restrict__ pos, const int32_t *__restrict__ dupc, const BHNode *__restrict__ nodes,
     const QRec *__restrict__ qrec, int32_t *__restrict__ ttask_n, const int32_t *__restrict__ meta,
     int32_t *__restrict__ mom_flag, double mom_tol, double theta, int64_t g0, int64_t g1,
@@ -2137,6 +2157,7 @@ struct StreamView {
     int32_t fence = 1;                  // 0: no release before an item (timing experiments only: stale)
     int32_t prio = 0;                   // the 64-query traversal waves' issue priority (s_setprio; option trav_prio)
     int32_t wait = 48;                  // polls (s_sleep 16 each, ~0.4 us) a consumer waits for a claimed item
+    unsigned long long *wlog = nullptr; // the wave timeline (tile_apply's waves; see NarrowView::wlog)
 };
 __device__ __forceinline__ int32_t *st_claims(int32_t *ctl) { return ctl + ST_Q0; }
 __device__ __forceinline__ unsigned long long *st_items(int32_t *ctl, int32_t cap) {
@@ -2674,6 +2695,7 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
             atomicAdd(visits + 18, w_end - w_start);
             if (task) atomicAdd(visits + 32, 1ull);
             atomicAdd(visits + 37, (unsigned long long)(clock64() - t_start));   // shader cycles (wave_mhz)
+            if (!TASK) wave_log_put(nv.wlog, w_start, w_end, 0);
             // the slowest wave's own counts (ticks << 24 | count: the max keeps that wave's)
             const unsigned long long tk = min(w_end - w_start, (1ull << 40) - 1) << 24, cm = (1ull << 24) - 1;
             atomicMax(visits + 33, tk | min(wpops, cm));
@@ -3215,6 +3237,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void t
             atomicMax(visits + 20, ~0ull - w_start);
             atomicMax(visits + 21, w_end);
             atomicAdd(visits + 22, w_end - w_start);
+            if (MODE == 0) wave_log_put(stv.wlog, w_start, w_end, 2);
         }
     }
     if (MODE == 0) break;
@@ -4021,6 +4044,9 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // that nothing delays this traversal's dispatch behind the tree build);
     // none on a tree's first traversal or with Options::narrow = 0
     NarrowView nv;
+    unsigned long long *wlog = visits && ctx->opts.wave_log ? ctx->ws.get<unsigned long long>("rep.wavelog", 1 + 2 * WAVE_LOG_CAP)
+                                                             : nullptr;
+    nv.wlog = wlog;
     const double nfac = ctx->opts.narrow;
     // (not with a tree partition: every rank walks all queries, the 64-query grid fills the chip)
     const bool narrow = nfac > 0.0 && t.sel_waves == waves && !plim;
@@ -4073,6 +4099,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     t.ran_stream = stream;
     stv.prio = o.trav_prio;   // (also without streaming)
+    stv.wlog = wlog;
     const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
     if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
         TSNE_HIP(hipEventRecord(ctx->aux_ev[0], st));

@@ -141,6 +141,7 @@ static const OptionField k_options[] = {
     {"tile_stream_fence", nullptr, &Options::tile_stream_fence, 0, 1},
     {"tile_stream_gate", nullptr, &Options::tile_stream_gate, 0, 1},
     {"trav_prio", nullptr, &Options::trav_prio, 0, 3},
+    {"wave_log", nullptr, &Options::wave_log, 0, 1},
     {"attract_serial_t0", nullptr, &Options::attract_serial_t0, 0, 1 << 30},
     {"attract_serial_t1", nullptr, &Options::attract_serial_t1, -1, 1 << 30},
     {"tile_stream_wait", nullptr, &Options::tile_stream_wait, 1, 1 << 20},
@@ -394,6 +395,27 @@ int tsne_ctx_set_option(tsne_ctx *ctx, const char *key, double value) {
         set_option(o, key, value);
         ctx->opts = o;
         for (tsne_ctx *c : ctx->group) c->opts = o;
+    });
+}
+
+int tsne_debug_wave_log(tsne_ctx *ctx, uint64_t *out, int64_t cap, int64_t *count) {
+    return guard([&] {
+        check_ctx(ctx);
+        TSNE_REQUIRE(count != nullptr && (out != nullptr || cap == 0) && cap >= 0, "bad output buffer");
+        DeviceGuard g(ctx->device);
+        *count = 0;
+        if (!ctx->ws.has("rep.wavelog")) return;
+        const unsigned long long *d = ctx->ws.get<unsigned long long>("rep.wavelog", 1);
+        uint64_t n = 0;
+        TSNE_HIP(hipMemcpyAsync(&n, d, 8, hipMemcpyDeviceToHost, ctx->stream));
+        TSNE_HIP(hipStreamSynchronize(ctx->stream));
+        n = std::min<uint64_t>(n, (uint64_t)(1 << 17));
+        *count = (int64_t)n;
+        const uint64_t m = std::min<uint64_t>(n, (uint64_t)cap);
+        if (m) {
+            TSNE_HIP(hipMemcpyAsync(out, d + 1, 16 * m, hipMemcpyDeviceToHost, ctx->stream));
+            TSNE_HIP(hipStreamSynchronize(ctx->stream));
+        }
     });
 }
 

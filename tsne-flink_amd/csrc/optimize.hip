@@ -1537,6 +1537,8 @@ void repulsion_device(tsne_ctx *ctx, const double *dY, int64_t n, int32_t c, dou
         if (ctx->opts.rep_stats) {
             vis = ctx->ws.get<unsigned long long>("rep.visits", VIS_N);
             TSNE_HIP(hipMemsetAsync(vis, 0, sizeof(unsigned long long) * VIS_N, st));
+            if (ctx->opts.wave_log)   // (the log's count; bh_repulsion takes the buffer)
+                TSNE_HIP(hipMemsetAsync(ctx->ws.get<unsigned long long>("rep.wavelog", 1), 0, 8, st));
         }
         bh_repulsion(ctx, t, theta, 0, n, reinterpret_cast<double2 *>(Fs), zs, vis);
         inv = t.inv;

@@ -84,6 +84,7 @@ SIGNATURES = {
     "tsne_ctx_get_option": (C.c_int, [P, C.c_char_p, PD]),
     "tsne_hip_versions": (C.c_int, [PI32, PI32]),
     "tsne_ctx_counter": (C.c_int, [P, C.c_char_p, PI64]),
+    "tsne_debug_wave_log": (C.c_int, [P, P, I64, PI64]),
     "tsne_ctx_loop_profile": (C.c_int, [P, C.c_char_p, I64, PI64]),
 }
 

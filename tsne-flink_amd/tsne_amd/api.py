@@ -185,6 +185,17 @@ class Context:
     def synchronize(self):
         check(lib().tsne_ctx_synchronize(self._h))
 
+    def debug_wave_log(self):
+        """(start, end, kind) per BH wave of the last counting call (options
+        wave_log + rep_stats), 100 MHz ticks; kind 0 traversal, 1 narrow, 2 tile."""
+        import numpy as np
+        n = C.c_int64()
+        check(lib().tsne_debug_wave_log(self._h, None, C.c_int64(0), C.byref(n)))
+        buf = np.zeros(2 * max(1, n.value), dtype=np.uint64)
+        check(lib().tsne_debug_wave_log(self._h, buf.ctypes.data_as(C.c_void_p), C.c_int64(n.value), C.byref(n)))
+        buf = buf[:2 * n.value].reshape(-1, 2)
+        return buf[:, 0], buf[:, 1] >> np.uint64(2), (buf[:, 1] & np.uint64(3)).astype(np.int32)
+
     # ---- host operators (TsneHelpers names)
     def kNearestNeighbors(self, X, k, metric="sqeuclidean", q0=0, q1=None):
         """TsneHelpers.scala:41-59 -> (idx[nq, kk] int32, dist[nq, kk] f64)."""
