@@ -138,3 +138,15 @@ def test_optimizer_stream():
     assert np.abs(Yc - Ya).max() <= 1e-6 * np.abs(Ya).max()
     for t in la:
         assert abs(lc[t] - la[t]) <= 1e-7 * abs(la[t]), t
+
+
+@pytest.mark.parametrize("front", [0.5, 1.0, 2.0])
+def test_trav_front_order_bit_identical(front):
+    """trav_front: the 64-query workgroups dispatched heavy-first (the order
+    made with the narrow selection from the previous call's costs): every wave
+    sums its own queries, so F and z keep their bits."""
+    Y = clustered(40_000, 7)
+    base = {"reuse_costs": 1}
+    F0, z0, _ = run(Y, 0.5, base, calls=3)
+    F1, z1, _ = run(Y, 0.5, dict(base, trav_front=front), calls=3)
+    assert np.array_equal(F1, F0) and np.array_equal(z1, z0)

@@ -2158,6 +2158,7 @@ struct StreamView {
     int32_t prio = 0;                   // the 64-query traversal waves' issue priority (s_setprio; option trav_prio)
     int32_t wait = 48;                  // polls (s_sleep 16 each, ~0.4 us) a consumer waits for a claimed item
     unsigned long long *wlog = nullptr; // the wave timeline (tile_apply's waves; see NarrowView::wlog)
+    const int32_t *border = nullptr;    // the 64-query traversal's workgroup order (trav_front), or identity
 };
 __device__ __forceinline__ int32_t *st_claims(int32_t *ctl) { return ctl + ST_Q0; }
 __device__ __forceinline__ unsigned long long *st_items(int32_t *ctl, int32_t cap) {
@@ -2324,7 +2325,9 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
     __shared__ TravLDS L;
     const int lane = lane_id(), w = threadIdx.x >> 6;
     const double th_lo = theta * (1.0 - 1e-14), th_hi = theta * (1.0 + 1e-14);
-    const int64_t wid = (int64_t)blockIdx.x * TRAV_WPB + w;   // query slots g0 + 64 wid .. + 63, tile list wid
+    // (option trav_front: the previous traversal's heavy workgroups first)
+    const int64_t blk = !PART && !TASK && stv.border ? (int64_t)stv.border[blockIdx.x] : (int64_t)blockIdx.x;
+    const int64_t wid = blk * TRAV_WPB + w;   // query slots g0 + 64 wid .. + 63, tile list wid
     const bool spill_on = !PART && sv.lout != 0;
     int32_t bud = 0;   // pops after which a walk splits (0: never)
     if (spill_on) bud = sv.force > 0 ? sv.force : sv.ctl[TASK ? SP_B1 : SP_B0];
@@ -2723,7 +2726,8 @@ constexpr int32_t NARROW_MIN = 32;
 __global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcost, int64_t waves,
                                                       int32_t *__restrict__ nflag, const int32_t *__restrict__ ncost,
                                                       int32_t *__restrict__ hlist, int32_t *__restrict__ hcount,
-                                                      int64_t hmax, double fac, int64_t hfill) {
+                                                      int64_t hmax, double fac, int64_t hfill,
+                                                      int32_t *__restrict__ border, double ffac) {
     __shared__ unsigned long long red[16];
     __shared__ int32_t wtot[16];
     __shared__ int32_t hist[PLAN_BUCKETS];
@@ -2792,6 +2796,40 @@ __global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcos
         __syncthreads();
     }
     if (t == 0) *hcount = (int32_t)min<int64_t>(base, hmax);
+    if (!border) return;
+    // The next traversal's block order (option trav_front): the 64-query
+    // workgroups whose heaviest wave (narrow groups excluded: they leave at
+    // once) cost >= ffac x the mean first, then the rest, each in Morton order
+    __syncthreads();
+    const int64_t nb = (waves + TRAV_WPB - 1) / TRAV_WPB;
+    const double fthr = ffac * (double)sthr / fmax(fac, 1e-300);   // sthr = fac x mean (or NARROW_MIN)
+    int32_t pos = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
+            const int64_t b = b0 + t;
+            bool in = false;
+            if (b < nb) {
+                int32_t c = 0;
+                for (int k = 0; k < TRAV_WPB; ++k) {
+                    const int64_t g = b * TRAV_WPB + k;
+                    if (g < waves && nflag[g] == 0) c = max(c, wcost[g]);
+                }
+                const bool heavy = (double)c >= fthr;
+                in = pass == 0 ? heavy : !heavy;
+            }
+            const uint64_t m = __ballot(in);
+            if (lane == 0) wtot[w] = (int32_t)__popcll(m);
+            __syncthreads();
+            int32_t off = pos, tot = 0;
+            for (int j = 0; j < 16; ++j) {
+                if (j < w) off += wtot[j];
+                tot += wtot[j];
+            }
+            if (in) border[off + (int32_t)__popcll(m & lanemask_lt())] = (int32_t)b;
+            pos += tot;
+            __syncthreads();
+        }
+    }
 }
 
 // The traversal waves' tiles, in recording order: one wave per traversal
@@ -3766,7 +3804,7 @@ BHTree &bh_single_tree(tsne_ctx *ctx, int64_t n) {
     // a single call is a function of its input alone unless the caller asked
     // for the previous call's costs (Options::reuse_costs): without costs the
     // traversal takes the 64-query layout everywhere
-    if (!ctx->opts.reuse_costs) { t.sel_waves = 0; t.sp_waves = 0; }
+    if (!ctx->opts.reuse_costs) { t.sel_waves = 0; t.sp_waves = 0; t.front_waves = 0; }
     return t;
 }
 
@@ -4099,6 +4137,7 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     }
     t.ran_stream = stream;
     stv.prio = o.trav_prio;   // (also without streaming)
+    if (o.trav_front > 0.0 && narrow && t.front_waves == waves) stv.border = t.trav_order;
     stv.wlog = wlog;
     const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
     if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
@@ -4196,11 +4235,16 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     // the next traversal's heavy groups (of the same query count) from this one's costs
     if (nfac > 0.0 && !plim) {
         if (!narrow) TSNE_HIP(hipMemsetAsync(t.nflag, 0, sizeof(int32_t) * waves, st));   // no stale slots
+        const bool front = o.trav_front > 0.0;
+        if (front) t.trav_order = ctx->ws.get<int32_t>(t.pre + "trav_order", ceil_div(t.tile_waves, TRAV_WPB) + 1);
         hipLaunchKernelGGL(narrow_select, dim3(1), dim3(1024), 0, st, t.wcost, waves, t.nflag, t.ncost, t.hlist,
-                           t.hcount, t.nar_hmax, nfac, std::min<int64_t>(t.nar_hmax, narrow_fill(ctx, waves)));
+                           t.hcount, t.nar_hmax, nfac, std::min<int64_t>(t.nar_hmax, narrow_fill(ctx, waves)),
+                           front ? t.trav_order : nullptr, o.trav_front);
         t.sel_waves = waves;
+        t.front_waves = front ? waves : 0;
     } else {
         t.sel_waves = 0;
+        t.front_waves = 0;
     }
     // the next traversal's split budgets (of the same query count) from this one's costs
     if (o.spill > 0.0 && o.spill_force == 0 && !plim) {

@@ -201,6 +201,8 @@ struct BHTree {
     int32_t *st_mtask = nullptr, *st_mtask_n = nullptr;   // per item x 64: moment lists
     int32_t st_gen = 0;
     size_t st_words = 0;
+    int32_t *trav_order = nullptr;        // option trav_front: the next traversal's workgroup order
+    int64_t front_waves = 0;              // query waves that order is for (0: none)
     bool ran_stream = false;              // the last traversal streamed its lists
     std::string pre;                      // the workspace prefix of this tree's buffers
 };

@@ -215,6 +215,8 @@ struct Options {
     int tile_stream_wait = 48;   // polls (~0.4 us each) a consumer waits for the next list before it leaves
     int attract_serial_t0 = 0, attract_serial_t1 = -1;   // 2-D: the attraction after BH for t in [t0, t1] (A/B)
     int wave_log = 0;            // with rep_stats: the counting call logs every BH wave's start / end (tsne_debug_wave_log)
+    double trav_front = 0.0;     // > 0: the 64-query traversal's workgroups whose heaviest wave cost >= this x the
+                                 // previous traversal's mean first (the order made with the narrow selection)
     int trav_prio = 0;           // 1-3: the 64-query BH traversal's waves at that issue priority (s_setprio)
     int tile_stream_gate = 1;    // 1: the consumers wait (on the device) until every traversal block has started
 };
