@@ -177,6 +177,17 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             default: measured slower at C3).
  *                             trav_prio 1-3: the 64-query traversal's waves at
  *                             that issue priority (no measured effect);
+ *   "trav_front" 0             > 0: the 64-query traversal's workgroups whose
+ *                             heaviest wave cost >= this x the previous
+ *                             traversal's mean are dispatched first (the order
+ *                             is made with the narrow selection; same sums; no
+ *                             measured gain);
+ *   "attract_serial_t0" 0, "attract_serial_t1" -1
+ *                             2-D optimizer: for t in [t0, t1] the attraction
+ *                             runs after the BH kernels instead of beside them
+ *                             (an A/B of the overlap; slower);
+ *   "wave_log" 0               with "rep_stats": the counting call logs every
+ *                             BH wave's start and end (tsne_debug_wave_log);
  *   "bh_split" 0              several ranks (2-D), 1: partition the Barnes-Hut
  *                             tree by ranges of its sorted points -- every rank
  *                             walks every query over the cells holding its own
