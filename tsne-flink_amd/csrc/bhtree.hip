@@ -2154,7 +2154,6 @@ struct StreamView {
                                         // 0: <= ctl[ST_W] (the previous plan's chunk unit x tile_stream_frac)
     int32_t cap = 0;                    // wave slots the claims and items have room for
     int32_t total = 0;                  // traversal wave slots of this call (blocks x TRAV_WPB)
-    int32_t fence = 1;                  // 0: no release before an item (timing experiments only: stale)
     int32_t prio = 0;                   // the 64-query traversal waves' issue priority (s_setprio; option trav_prio)
     int32_t wait = 48;                  // polls (s_sleep 16 each, ~0.4 us) a consumer waits for a claimed item
     unsigned long long *wlog = nullptr; // the wave timeline (tile_apply's waves; see NarrowView::wlog)
@@ -2647,7 +2646,7 @@ __global__ __launch_bounds__(64 * TRAV_WPB) __attribute__((amdgpu_waves_per_eu(8
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) {
                 __hip_atomic_store(st_claims(stv.ctl) + wid, stv.gen << 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (stv.fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const int32_t k = atomicAdd(&stv.ctl[ST_TAIL], 1);
                 __hip_atomic_store(st_items(stv.ctl, stv.cap) + k,
@@ -4125,7 +4124,6 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
         stv.wait = o.tile_stream_wait;
         stv.total = (int32_t)(nblocks * TRAV_WPB);
         stv.cap = (int32_t)t.tile_waves;
-        stv.fence = o.tile_stream_fence;
         // ungated, the consumers' stream starts behind everything before the
         // traversal (gated, the traversal's start implies that; and no marker
         // goes between the build and the traversal on this stream, which lets

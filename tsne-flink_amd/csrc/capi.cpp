@@ -138,7 +138,6 @@ static const OptionField k_options[] = {
     {"tile_stream", nullptr, &Options::tile_stream, 0, 8},
     {"tile_stream_max", nullptr, &Options::tile_stream_max, -1, 1 << 30},
     {"tile_stream_frac", &Options::tile_stream_frac, nullptr, 0.0, 64.0},
-    {"tile_stream_fence", nullptr, &Options::tile_stream_fence, 0, 1},
     {"tile_stream_gate", nullptr, &Options::tile_stream_gate, 0, 1},
     {"trav_prio", nullptr, &Options::trav_prio, 0, 3},
     {"trav_front", &Options::trav_front, nullptr, 0.0, 1e6},

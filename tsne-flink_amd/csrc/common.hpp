@@ -211,7 +211,6 @@ struct Options {
     // bit-identical to tile_stream 0)
     int tile_stream = 0, tile_stream_max = 0;
     double tile_stream_frac = 1.0;   // tile_stream_max 0: streamed up to this x the previous plan's chunk unit
-    int tile_stream_fence = 1;   // 0: timing experiment only (no release before a hand-over: stale reads)
     int tile_stream_wait = 48;   // polls (~0.4 us each) a consumer waits for the next list before it leaves
     int attract_serial_t0 = 0, attract_serial_t1 = -1;   // 2-D: the attraction after BH for t in [t0, t1] (A/B)
     int wave_log = 0;            // with rep_stats: the counting call logs every BH wave's start / end (tsne_debug_wave_log)
