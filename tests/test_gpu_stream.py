@@ -150,3 +150,40 @@ def test_trav_front_order_bit_identical(front):
     F0, z0, _ = run(Y, 0.5, base, calls=3)
     F1, z1, _ = run(Y, 0.5, dict(base, trav_front=front), calls=3)
     assert np.array_equal(F1, F0) and np.array_equal(z1, z0)
+
+
+@pytest.mark.parametrize("front", [0.8, 1.5])
+def test_trav_front_cur_bit_identical(front):
+    """trav_front_cur: the dispatch order predicted from the points' previous
+    costs through this build's Morton order (made on the second stream during
+    the build): F and z keep their bits, single calls and the optimizer."""
+    Y = clustered(40_000, 9)
+    base = {"reuse_costs": 1}
+    F0, z0, _ = run(Y, 0.5, base, calls=3)
+    F1, z1, _ = run(Y, 0.5, dict(base, trav_front_cur=front), calls=3)
+    assert np.array_equal(F1, F0) and np.array_equal(z1, z0)
+    from test_gpu_parity import random_problem
+    n = 6000
+    rp, col, val = random_problem(n, 30, seed=29)
+    Y0 = np.random.default_rng(5).normal(size=(n, 2)) * 1e-4
+    p = default_params(iterations=150, theta=0.5)
+    dev = torch.device("cuda", 0)
+    Pd = tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (rp, col, val))
+
+    def go(o):
+        with T.Context(0) as c:
+            c.set_option("root_tile", 0)
+            for k, v in o.items():
+                c.set_option(k, v)
+            Yd = torch.from_numpy(Y0.copy()).to(dev)
+            u, g = torch.zeros_like(Yd), torch.ones_like(Yd)
+            c.dev_opt_setup(p, *Pd, n, Yd, u, g)
+            for t in range(1, p.iterations + 1):
+                c.dev_opt_step(t)
+            c.dev_opt_sync()
+            c.synchronize()
+            return Yd.cpu().numpy(), c.dev_opt_losses()
+
+    Ya, la = go({})
+    Yb, lb = go({"trav_front_cur": front})
+    assert np.array_equal(Ya, Yb) and la == lb

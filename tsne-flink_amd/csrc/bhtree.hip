@@ -222,8 +222,16 @@ __global__ void count_in_root(const uint64_t *__restrict__ ks, int64_t n, int32_
 }
 
 __global__ void gather_sorted(const double *__restrict__ Y, const int32_t *__restrict__ idx_sorted,
-                              int64_t n, double2 *__restrict__ pos, int32_t *__restrict__ inv) {
+                              int64_t n, double2 *__restrict__ pos, int32_t *__restrict__ inv,
+                              const int32_t *__restrict__ pcost, int32_t *__restrict__ pred) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // (option trav_front_cur: each new 64-query wave's predicted cost, the
+    // largest previous cost of its points -- lanes = the wave's queries)
+    if (pred) {
+        const int32_t c = s < n ? pcost[idx_sorted[s]] : 0;
+        const int32_t m = wave_max(c);
+        if (lane_id() == 0 && s < n) pred[s >> 6] = m;
+    }
     if (s >= n) return;
     int32_t i = idx_sorted[s];
     const double x = Y[2 * i], y = Y[2 * i + 1];
@@ -1386,9 +1394,15 @@ __global__ __launch_bounds__(1024) void tile_plan(const int32_t *__restrict__ tc
 // F, Z of each query += its chunks' partial sums, in chunk order
 __global__ void chunk_combine(const double2 *__restrict__ Fp, const double *__restrict__ Zp,
                               const int32_t *__restrict__ Cw, const int32_t *__restrict__ slot0, int64_t g0, int64_t g1,
-                              const int32_t *__restrict__ qlist, double2 *__restrict__ F, double *__restrict__ Z) {
+                              const int32_t *__restrict__ qlist, double2 *__restrict__ F, double *__restrict__ Z,
+                              int32_t *__restrict__ pcost, const int32_t *__restrict__ idx_sorted,
+                              const int32_t *__restrict__ wcost, const int32_t *__restrict__ nflag) {
     const int64_t k = g0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= g1) return;
+    if (pcost) {   // option trav_front_cur: the point's wave cost (a narrow group's: heavy)
+        const int64_t wq = (k - g0) >> 6;
+        pcost[idx_sorted[k]] = nflag && nflag[wq] ? (1 << 29) : wcost[wq];
+    }
     const int64_t w = (k - g0) >> 6, lane = (k - g0) & 63;
     const int64_t s = qlist ? (int64_t)qlist[k] : k;
     const int64_t b = (int64_t)slot0[w] * 64 + lane;
@@ -2831,6 +2845,61 @@ __global__ __launch_bounds__(1024) void narrow_select(int32_t *__restrict__ wcos
     }
 }
 
+// Option trav_front_cur: the traversal's workgroup order from this build's
+// predicted wave costs (gather_sorted): workgroups whose heaviest predicted
+// 64-query wave (narrow groups excluded) is >= ffac x the mean first, the rest
+// after, each in Morton order.  One workgroup, on the second stream during the build.
+__global__ __launch_bounds__(1024) void trav_order_cur(const int32_t *__restrict__ pred,
+                                                       const int32_t *__restrict__ nflag, int64_t waves, double ffac,
+                                                       int32_t *__restrict__ border) {
+    __shared__ unsigned long long red[16];
+    __shared__ int32_t wtot[16];
+    __shared__ double sthr;
+    const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    unsigned long long acc = 0, cnt = 0;
+    for (int64_t g = t; g < waves; g += 1024)
+        if (!(nflag && nflag[g])) { acc += (unsigned long long)max(pred[g], 0); ++cnt; }
+    acc = wave_sum(acc);
+    cnt = wave_sum(cnt);
+    if (lane == 0) { red[w] = acc; wtot[w] = (int32_t)cnt; }
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long a = 0, c = 0;
+        for (int j = 0; j < 16; ++j) { a += red[j]; c += (unsigned long long)wtot[j]; }
+        sthr = ffac * (double)a / (double)max(1ull, c);
+    }
+    __syncthreads();
+    const double thr = sthr;
+    const int64_t nb = (waves + TRAV_WPB - 1) / TRAV_WPB;
+    int32_t pos = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
+            const int64_t b = b0 + t;
+            bool in = false;
+            if (b < nb) {
+                int32_t c = 0;
+                for (int k = 0; k < TRAV_WPB; ++k) {
+                    const int64_t g = b * TRAV_WPB + k;
+                    if (g < waves && !(nflag && nflag[g])) c = max(c, pred[g]);
+                }
+                const bool heavy = c > 0 && (double)c >= thr;
+                in = pass == 0 ? heavy : !heavy;
+            }
+            const uint64_t m = __ballot(in);
+            __syncthreads();
+            if (lane == 0) wtot[w] = (int32_t)__popcll(m);
+            __syncthreads();
+            int32_t off = pos, tot = 0;
+            for (int j = 0; j < 16; ++j) {
+                if (j < w) off += wtot[j];
+                tot += wtot[j];
+            }
+            if (in) border[off + (int32_t)__popcll(m & lanemask_lt())] = (int32_t)b;
+            pos += tot;
+        }
+    }
+}
+
 // The traversal waves' tiles, in recording order: one wave per traversal
 // wave (same 64 queries).  For every (subtree, lanes) task each lane of the
 // mask takes the subtree's exact leaf sum either from its moments -- when the
@@ -3713,6 +3782,8 @@ void bh_alloc(tsne_ctx *ctx, BHTree &t, int64_t n, const std::string &pre) {
     t.nmtask_n = ws.get<int32_t>(pre + "nmtask_n", (size_t)t.nar_hmax * 64);
     t.pre = pre;
     t.sp_ctl = nullptr;   // spill buffers: on first use (bh_spill_alloc)
+    t.pcost_valid = false;   // (trav_front_cur: no previous costs for this size)
+    t.order_ready = false;
     t.sp_gen = 0;
     t.sp_waves = 0;
     t.ran_spill = false;
@@ -4010,7 +4081,21 @@ void bh_build(tsne_ctx *ctx, BHTree &t, const double *dY, double theta, const in
     }
     t.cs_primed = true;
     hipLaunchKernelGGL(count_in_root, dim3(1), dim3(64), 0, st, t.keys_sorted, n, t.meta);
-    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv);
+    // (trav_front_cur: predictions from the previous traversal's per-point costs,
+    // the order made on the second stream while the build goes on)
+    const bool cur_order = ctx->opts.trav_front_cur > 0.0 && t.pcost_valid && t.sel_waves == ceil_div(n, 64);
+    hipLaunchKernelGGL(gather_sorted, dim3(ceil_div(n, 256)), dim3(256), 0, st, dY, t.idx_sorted, n, t.pos, t.inv,
+                       cur_order ? t.pcost : nullptr, cur_order ? t.pred : nullptr);
+    t.order_ready = false;
+    if (cur_order) {
+        TSNE_HIP(hipEventRecord(ctx->aux_ev[0], st));
+        TSNE_HIP(hipStreamWaitEvent(ctx->aux_stream, ctx->aux_ev[0], 0));
+        hipLaunchKernelGGL(trav_order_cur, dim3(1), dim3(1024), 0, ctx->aux_stream, t.pred, t.nflag, ceil_div(n, 64),
+                           ctx->opts.trav_front_cur, t.trav_order);
+        if (!t.ord_ev) TSNE_HIP(hipEventCreateWithFlags(&t.ord_ev, hipEventDisableTiming));
+        TSNE_HIP(hipEventRecord(t.ord_ev, ctx->aux_stream));
+        t.order_ready = true;
+    }
     hipLaunchKernelGGL(dup_count, dim3(ceil_div(n, 256)), dim3(256), 0, st, t.pos, t.keys_sorted, n, t.dupc, t.vid,
                        t.dflag);
     if (++t.gen <= 0) {   // wrapped: clear the marks once
@@ -4136,6 +4221,10 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
     t.ran_stream = stream;
     stv.prio = o.trav_prio;   // (also without streaming)
     if (o.trav_front > 0.0 && narrow && t.front_waves == waves) stv.border = t.trav_order;
+    if (t.order_ready && narrow && !plim && !qlist && s0 == 0 && waves == ceil_div(t.n, 64)) {
+        TSNE_HIP(hipStreamWaitEvent(st, t.ord_ev, 0));   // (done long before: made during the build)
+        stv.border = t.trav_order;
+    }
     stv.wlog = wlog;
     const int32_t *clab = cost_by_label ? t.idx_sorted : nullptr;
     if (narrow) {   // the narrow waves on the second stream, beside the 64-query grid
@@ -4213,8 +4302,16 @@ void bh_repulsion(tsne_ctx *ctx, BHTree &t, double theta, int64_t s0, int64_t s1
                        t.mom, SpillView(), stv, t.tcost);
     hipLaunchKernelGGL(moment_apply, dim3(ceil_div(tslots * 64, 256)), dim3(256), 0, st, t.pos, t.nodes, t.mom,
                        t.mtask, t.mtask_n, s0, s1, qlist, dF, dz, cv);
+    const bool keep_pcost = o.trav_front_cur > 0.0 && !plim && !qlist && s0 == 0 && s1 == t.n;
+    if (keep_pcost) {
+        t.pcost = ctx->ws.get<int32_t>(t.pre + "pcost", (size_t)t.n);
+        t.pred = ctx->ws.get<int32_t>(t.pre + "pred", (size_t)ceil_div(t.n, 64) + 1);
+        t.trav_order = ctx->ws.get<int32_t>(t.pre + "trav_order", ceil_div(t.tile_waves, TRAV_WPB) + 1);
+    }
     hipLaunchKernelGGL(chunk_combine, dim3(ceil_div(s1 - s0, 256)), dim3(256), 0, st, t.ch_Fp, t.ch_Zp, t.ch_C,
-                       t.ch_slot0, s0, s1, qlist, dF, dz);
+                       t.ch_slot0, s0, s1, qlist, dF, dz, keep_pcost ? t.pcost : nullptr, t.idx_sorted, t.wcost,
+                       narrow ? t.nflag : nullptr);
+    t.pcost_valid = keep_pcost;
     if (spill) {   // the tasks' tile pages, then their sums into F, Z
         hipLaunchKernelGGL(tile_apply<1>, dim3(std::max(1, ctx->cu_count * 4)), dim3(256), 0, st, t.pos, t.nodes,
                            t.ttask, t.ttask_n, s0, s1, qlist, t.mom_flag, mom_tol, t.mtask, t.mtask_n, dF, dz, visits,

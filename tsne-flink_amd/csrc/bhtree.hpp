@@ -203,6 +203,11 @@ struct BHTree {
     size_t st_words = 0;
     int32_t *trav_order = nullptr;        // option trav_front: the next traversal's workgroup order
     int64_t front_waves = 0;              // query waves that order is for (0: none)
+    // option trav_front_cur: per point (Y row) the previous traversal's wave
+    // cost, per new wave its prediction, the order event
+    int32_t *pcost = nullptr, *pred = nullptr;
+    bool pcost_valid = false, order_ready = false;
+    hipEvent_t ord_ev = nullptr;
     bool ran_stream = false;              // the last traversal streamed its lists
     std::string pre;                      // the workspace prefix of this tree's buffers
 };

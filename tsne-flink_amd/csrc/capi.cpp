@@ -141,6 +141,7 @@ static const OptionField k_options[] = {
     {"tile_stream_gate", nullptr, &Options::tile_stream_gate, 0, 1},
     {"trav_prio", nullptr, &Options::trav_prio, 0, 3},
     {"trav_front", &Options::trav_front, nullptr, 0.0, 1e6},
+    {"trav_front_cur", &Options::trav_front_cur, nullptr, 0.0, 1e6},
     {"wave_log", nullptr, &Options::wave_log, 0, 1},
     {"attract_serial_t0", nullptr, &Options::attract_serial_t0, 0, 1 << 30},
     {"attract_serial_t1", nullptr, &Options::attract_serial_t1, -1, 1 << 30},

@@ -216,6 +216,8 @@ struct Options {
     int wave_log = 0;            // with rep_stats: the counting call logs every BH wave's start / end (tsne_debug_wave_log)
     double trav_front = 0.0;     // > 0: the 64-query traversal's workgroups whose heaviest wave cost >= this x the
                                  // previous traversal's mean first (the order made with the narrow selection)
+    double trav_front_cur = 0.0; // > 0: as trav_front, the order predicted from the points' previous costs
+                                 // through this build's Morton order (made during the build, second stream)
     int trav_prio = 0;           // 1-3: the 64-query BH traversal's waves at that issue priority (s_setprio)
     int tile_stream_gate = 1;    // 1: the consumers wait (on the device) until every traversal block has started
 };
