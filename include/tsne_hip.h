@@ -182,6 +182,9 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             traversal's mean are dispatched first (the order
  *                             is made with the narrow selection; same sums; no
  *                             measured gain);
+ *   "trav_front_cur" 0         > 0: as trav_front with the order predicted from
+ *                             each point's previous cost through the current
+ *                             Morton order (made during the build; slower);
  *   "attract_serial_t0" 0, "attract_serial_t1" -1
  *                             2-D optimizer: for t in [t0, t1] the attraction
  *                             runs after the BH kernels instead of beside them
