@@ -140,6 +140,11 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *   "attract_tiles3" 0        3-D: the tiled attraction too (slower than the
  *                             row kernel beside the octree traversal at C4);
  *   "attract_cfg" -1          its tile shape (-1 automatic, 0..3);
+ *   "attract_pipe" 0          2-D tiled attraction: 0 attract_tiles; 1..5 the
+ *                             pipelined kernel (entries of the next 1 or 2
+ *                             slices in flight; identical results);
+ *   "attract_dyn" 1           attract_tiles: the waves claim a tile's slices
+ *                             instead of taking every 16th (identical results);
  *   "graph_order" 1           P's graph order as the initial labels;
  *   "relabel" -1              Morton relabels: -1 automatic, 0 never, 1 by
  *                             locality score, 2 always;

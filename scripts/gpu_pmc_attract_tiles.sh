@@ -11,5 +11,5 @@ for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   k=$((k+1))
   timeout -s KILL 240 rocprofv3 --pmc $ctrs --kernel-include-regex 'attract_(rows|tiles)' \
     -d gpurun_out/pmc_at$k -o pmc --output-format csv -- \
-    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --trace 0 ${PMC_ARGS:-} > gpurun_out/pmc_at$k.log 2>&1 || exit $?
+    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-cli-e2e --trace 0 ${PMC_ARGS:-} > gpurun_out/pmc_at$k.log 2>&1 || exit $?
 done

@@ -4,7 +4,7 @@
 #   mksnaps     bench.py --dump-y 250,450,650 into /tmp/snaps (the snapshots the snap steps read)
 #   snap        bh_snap.py on snaps/Y_t{250,450,650}.npy per SNAP_VARS entry ("-" = defaults, else KEY=VALUE;
 #               SNAP_ARGS: more bh_snap arguments, e.g. --stats)
-#   tests_narrow / tests_spill / tests_stream / tests3d / tests_all   GPU test subsets / the whole -m gpu suite
+#   tests_narrow / tests_spill / tests_stream / tests_attr / tests3d / tests_all   GPU test subsets / the whole -m gpu suite
 #   bench / bench4   bench.py (C3 / C4) per BENCH_VARS / BENCH4_VARS entry ("K1=V1+K2=V2": two options)
 #   ktrace      rocprofv3 --kernel-trace --stats of the default bench (KTRACE_ARGS)
 #   smoke       __graft_entry__.smoke()
@@ -50,6 +50,10 @@ fi
 if has tests_stream; then
   tst 600 python -u -m pytest tests/test_gpu_stream.py -v -p no:cacheprovider \
       --timeout 300 --timeout-method thread > $O/tests_stream.log 2>&1 || exit $?
+fi
+if has tests_attr; then
+  tst 600 python -u -m pytest tests/test_gpu_parity.py -v -p no:cacheprovider -k "tiled_attraction" \
+      --timeout 300 --timeout-method thread > $O/tests_attr.log 2>&1 || exit $?
 fi
 if has tests_multi; then
   tst 900 python -u -m pytest tests/test_gpu_multi.py -v -p no:cacheprovider \

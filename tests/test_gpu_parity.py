@@ -493,7 +493,7 @@ def test_tiled_attraction_every_config():
     Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
     lo = O.optimize(rp, col, val, Yo, uo, go, learning_rate=200.0, iterations=10, theta=0.0, threads=8)
     for opt in ({"attract_cfg": 0}, {"attract_cfg": 1}, {"attract_cfg": 2}, {"attract_cfg": 3},
-                {"attract_tiles": 0}):
+                {"attract_cfg": 0, "attract_dyn": 0}, {"attract_cfg": 2, "attract_dyn": 0}, {"attract_tiles": 0}):
         with T.Context(0) as c:
             for k, v in opt.items():
                 c.set_option(k, v)
@@ -501,6 +501,36 @@ def test_tiled_attraction_every_config():
             lg = c.optimize(rp, col, val, Yg, ug, gg, default_params(iterations=10, theta=0.0, learning_rate=200.0))
         assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max(), opt
         assert abs(lg[10] - lo[10]) <= 1e-9 * abs(lo[10]), opt
+
+
+def test_tiled_attraction_pipe_identical():
+    """The pipelined tiled attraction ("attract_pipe" 1..5: the next 1..3
+    slices' entries in flight while a wave sums the current one; non-loss
+    launches) and attract_tiles with claimed slices ("attract_dyn" 1, loss
+    launches too) return the same bits as attract_tiles over 10 iterations of a P
+    with hub rows (wide slices, rows past the pipelined steps), at the
+    4096-row configuration the pipeline is built for; and the oracle's
+    embedding within 1e-9."""
+    n = 12000
+    rp, col, val = hub_problem(n)
+    Y0 = np.random.default_rng(75).normal(size=(n, 2)) * 5.0
+    Yo, uo, go = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+    lo = O.optimize(rp, col, val, Yo, uo, go, learning_rate=200.0, iterations=10, theta=0.0, threads=8)
+    ref = None
+    for pipe, dyn in [(0, 0), (0, 1)] + [(k, 0) for k in range(1, 6)]:
+        with T.Context(0) as c:
+            c.set_option("attract_cfg", 3)
+            c.set_option("attract_pipe", pipe)
+            c.set_option("attract_dyn", dyn)
+            Yg, ug, gg = Y0.copy(), np.zeros_like(Y0), np.ones_like(Y0)
+            lg = c.optimize(rp, col, val, Yg, ug, gg, default_params(iterations=10, theta=0.0, learning_rate=200.0))
+        if ref is None:
+            ref = (Yg, ug, gg, lg)
+        else:
+            assert np.array_equal(Yg, ref[0]) and np.array_equal(ug, ref[1]) and np.array_equal(gg, ref[2]), pipe
+            assert lg == ref[3], pipe
+        assert np.abs(Yg - Yo).max() <= 1e-9 * np.abs(Yo).max(), pipe
+        assert abs(lg[10] - lo[10]) <= 1e-9 * abs(lo[10]), pipe
 
 
 def _relabel_run(relabel):

@@ -124,6 +124,8 @@ static const OptionField k_options[] = {
     {"attract_tiles", nullptr, &Options::attract_tiles, 0, 1},
     {"attract_tiles3", nullptr, &Options::attract_tiles3, 0, 1},
     {"attract_cfg", nullptr, &Options::attract_cfg, -1, 3},
+    {"attract_pipe", nullptr, &Options::attract_pipe, 0, 5},
+    {"attract_dyn", nullptr, &Options::attract_dyn, 0, 1},
     {"graph_order", nullptr, &Options::graph_order, 0, 1},
     {"relabel", nullptr, &Options::relabel, -1, 2},
     {"recut", nullptr, &Options::recut, 0, 1},

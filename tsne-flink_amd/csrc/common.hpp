@@ -178,6 +178,8 @@ struct Options {
     int attract_tiles3 = 0;   // 3-D: the tiled attraction (attract_tiles3) instead of attract3 (C4: 6.7 vs 3.7 ms
                               // per launch beside the octree traversal; round 6)
     int attract_cfg = -1;     // its tile shape: -1 by rows per rank, else ATCfg0..3
+    int attract_pipe = 0;     // 2-D tiled attraction: 0 attract_tiles, 1..5 attract_tiles_pipe shapes (round 6)
+    int attract_dyn = 1;      // attract_tiles: a tile's slices claimed by the waves (round 6; same sums)
     int graph_order = 1;      // P's graph order (components + BFS) as the initial labels
     int relabel = -1;         // -1 automatic, 0 never, 1 by the locality score, 2 always
     int recut = 0;            // several ranks on the tiled layout: re-cut by BH cost instead of relabels

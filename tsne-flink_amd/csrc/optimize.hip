@@ -119,6 +119,8 @@ struct OptState {
     int64_t at_nrb = 0, at_ncb = 0;
     int64_t at_rbs = 0;       // rows per row block (<= the config's RB: the grid covers the CUs)
     int at_cfg = 0;
+    int at_pipe = 0;   // Options::attract_pipe when the layout was built
+    int at_dyn = 0;    // Options::attract_dyn
     bool morton_labels = false;   // the labels follow the embedding's Morton order (a relabel happened)
     ATile *at_tiles = nullptr;
     int32_t *at_rbt = nullptr;
@@ -416,9 +418,43 @@ using ATCfg3Ds = ATCfg<512, 4096, 1024>;   // 96 + 12 KB: a rank's share of the 
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
 
+constexpr uint32_t AT_OOB = 0x80000000u;   // >= the descriptors' range: reads 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t at_rsrc(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, 0x7ffffff0, 0x00020000);
+}
+// the tile window into LDS: all loads before the first store, every store
+// unconditional (indices past the window clamped onto its last point, whose
+// writers all hold the same value), so no load can sink into a branch
+template <int WN, int NT>
+__device__ __forceinline__ void at_window_regs(double2 (&yv)[(WN + NT - 1) / NT], const double2 *src, int wn, int tid) {
+#pragma unroll
+    for (int k = 0; k < (WN + NT - 1) / NT; ++k) yv[k] = src[min(tid + k * NT, wn - 1)];
+}
+template <int WN, int NT>
+__device__ __forceinline__ void at_window_store(double2 *win, const double2 (&yv)[(WN + NT - 1) / NT], int tid) {
+#pragma unroll
+    for (int k = 0; k < (WN + NT - 1) / NT; ++k) win[min(tid + k * NT, WN - 1)] = yv[k];
+}
+
+// A wave's next slice of the current tile: an LDS counter per tile parity
+// (lane 0's atomic, broadcast)
+__device__ __forceinline__ int at_claim(int *c) {
+    int v = 0;
+    if (lane_id() == 0) v = atomicAdd(c, 1);
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
 // One workgroup per row block (owned rows [b0, b0 + RB) of [0, rows), label
 // r0 + local row); XCD-chunked block order.  attr / lpart as attract_rows.
-template <class CF, bool LOSS, int MET>
+// DYN (Options::attract_dyn, round 6): a tile's slices are claimed by the
+// waves from a counter instead of dealt round-robin.  The slices come sorted
+// by descending width, so round-robin gives wave 0 the widest of every 16 and
+// the other waves wait for it at the tile's barrier (PMC: waves wait 58 % of
+// their lifetime, 22 % on their own loads).  Every row has one slice per tile
+// and the tiles keep their order, so each accumulator receives the same terms
+// in the same order: the sums are bit-identical either way.
+template <class CF, bool LOSS, int MET, bool DYN = false>
 __global__ __launch_bounds__(CF::NT) void attract_tiles(
     const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
     const uint32_t *__restrict__ srow, int64_t rows, int64_t r0, int64_t n, const uint16_t *__restrict__ pk,
@@ -428,6 +464,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
     __shared__ double2 win[W];
     __shared__ double2 acc[RB];
     __shared__ double sl[WAVES];
+    __shared__ int claim[2];
     const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
     const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
     const int64_t b0 = rb * rbs;   // rbs <= RB rows per block (build_attract_tiles)
@@ -435,6 +472,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
     const double2 *Y2 = reinterpret_cast<const double2 *>(Y);
     const double2 *Yrow = Y2 + r0 + b0;
     for (int i = tid; i < nr; i += NT) acc[i] = make_double2(0.0, 0.0);
+    if (DYN && tid < 2) claim[tid] = 0;
     const double Z = LOSS ? scal[0] : 1.0;
     double lsum = 0.0;
     constexpr int WL = (W + NT - 1) / NT;
@@ -442,22 +480,19 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
     for (int t = t0; t < t1; ++t) {
         const ATile tl = tiles[t];
         {   // the tile's window: all of a thread's loads in flight before its LDS stores
+            // (round 6: unconditional stores; with `if (i < wn)` the compiler sank each
+            // load into its store's branch and the copy took WL dependent round trips)
             const int64_t base = (int64_t)tl.cb * W;
-            const int wn = (int)min((int64_t)W, n - base);
             double2 yv[WL];
-#pragma unroll
-            for (int k = 0; k < WL; ++k) yv[k] = Y2[base + min(tid + k * NT, wn - 1)];
-#pragma unroll
-            for (int k = 0; k < WL; ++k) {
-                const int i = tid + k * NT;
-                if (i < wn) win[i] = yv[k];
-            }
+            at_window_regs<W, NT>(yv, Y2 + base, (int)min((int64_t)W, n - base), tid);
+            at_window_store<W, NT>(win, yv, tid);
         }
         __syncthreads();
         const int s0 = tl.s0, send = tl.s0 + tl.ns;
-        // the wave's slices s0 + w, s0 + w + WAVES, ...; the next slice's record
-        // and lane word are fetched during the current one
-        int s = s0 + w;
+        // the wave's slices s0 + w, s0 + w + WAVES, ... (DYN: claimed); the next
+        // slice's record and lane word are fetched during the current one
+        if (DYN && tid == 0) claim[(t + 1) & 1] = 0;   // the next tile's counter: its last claim was before this barrier
+        int s = DYN ? s0 + at_claim(&claim[t & 1]) : s0 + w;
         ASlice sd{};
         uint32_t rl = 0;
         if (s < send) {
@@ -468,7 +503,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
             const int len = (int)(rl & ((1u << AT_LENBITS) - 1)), lrow = (int)(rl >> AT_LENBITS);
             double2 yi = make_double2(0.0, 0.0);
             if (len > 0) yi = Yrow[lrow];
-            const int sn = s + WAVES;
+            const int sn = DYN ? s0 + at_claim(&claim[t & 1]) : s + WAVES;
             ASlice sdn{};
             uint32_t rln = 0;
             double fx = 0.0, fy = 0.0;
@@ -547,9 +582,254 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
     }
 }
 
+// ---- attract_tiles, pipelined (Options::attract_pipe, round 6)
+// attract_tiles' ISA waits once per slice for ALL of that slice's loads (its
+// entries and the next slice's prefetched record alike: the entry loads sit in
+// exec-masked branches, so the compiler's wait counts fall back to vmcnt(0)),
+// and nothing is in flight while the slice is summed; each tile's window
+// copy also ran as WL dependent load -> wait -> store round trips (the loads
+// were sunk into the stores' branches).  Here a wave has the entries of its
+// next D slices in flight while it sums the current one, the slice records
+// 2D ahead, and the next tile's window is loaded into registers during the
+// current tile (WPF).  Every slice issues the same instructions: the entry
+// loads are buffer loads whose lanes past their row's entries address out of
+// range (0, no memory request), so the compiler's wait counts stay exact.
+// A slice wider than U steps loads and sums its remaining steps in place.
+// Each lane sums its row's entries in the same order as attract_tiles, so the
+// results are bit-identical.
+// The wave's cursor over the row block's tiles (tile t, slice s < send;
+// t == t1: none)
+struct ATCur {
+    int t, s, send;
+};
+// ring R (records and lane words, 2D + 1 slices ahead) and ring E (entries
+// of the first U steps and y_i, D slices ahead)
+struct ATRSlot {
+    uint32_t lo;   // the slice record as loaded (every lane the same address):
+    int2 wd;       // first entry (< 2^31: build_attract_tiles), width, wide
+    uint32_t rl;   // lane word: local row << AT_LENBITS | entries
+    ATCur c;
+};
+template <int U>
+struct ATESlot {
+    uint16_t cu[U];   // widened where summed: a widening here waits for the load
+    double vu[U];
+    double2 yi;
+    int base, width, wide, rU;   // wave-uniform; rU: entries of the first U steps
+};
+constexpr int AT_RU = 4;   // steps past U: loaded and summed 4 at a time
+
+// the wave's first slice in tiles t.. (scalar loads: every value wave-uniform)
+__device__ __forceinline__ ATCur atp_first(const ATile *__restrict__ tiles, int t, int t1, int w) {
+    ATCur c{__builtin_amdgcn_readfirstlane(t), 0, 0};
+    for (; c.t < t1; c.t = __builtin_amdgcn_readfirstlane(c.t + 1)) {
+        const int s0 = __builtin_amdgcn_readfirstlane(tiles[c.t].s0);
+        const int ns = __builtin_amdgcn_readfirstlane(tiles[c.t].ns);
+        c.s = s0 + w;
+        c.send = s0 + ns;
+        if (c.s < c.send) break;
+    }
+    return c;
+}
+template <int WAVES>
+__device__ __forceinline__ ATCur atp_next(const ATile *__restrict__ tiles, const ATCur &c, int t1, int w) {
+    if (c.t >= t1) return c;
+    ATCur d = c;
+    d.s += WAVES;
+    return d.s < d.send ? d : atp_first(tiles, c.t + 1, t1, w);
+}
+// ring R's loads: unconditional, so that every step issues the same
+// instructions (past the wave's last slice a dummy slice's, whose entries are
+// loaded but never summed); nothing consumes them until the entries' issue
+// (a select on the lane word here would wait for it at once).  The record
+// goes through buffer loads: vector memory, counted in order with the rest
+// (scalar loads share their counter with the LDS reads of the sums).
+__device__ __forceinline__ void atp_issue_rec(ATRSlot &x, const ASlice *__restrict__ slices,
+                                              const uint32_t *__restrict__ srow, int t1, int sdummy, int lane) {
+    const int s = x.c.t < t1 ? x.c.s : sdummy;
+    const __amdgpu_buffer_rsrc_t rr = at_rsrc(slices + s);
+    x.lo = __builtin_amdgcn_raw_buffer_load_b32(rr, 0u, 0, 0);   // base (low word)
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    const u2v wd = __builtin_amdgcn_raw_buffer_load_b64(rr, 8u, 0, 0);
+    x.wd = make_int2((int)wd.x, (int)wd.y);
+    x.rl = srow[(int64_t)s * 64 + lane];
+}
+template <int U>
+__device__ __forceinline__ void atp_issue_entries(const ATRSlot &x, ATESlot<U> &e, const uint16_t *__restrict__ pk,
+                                                  const double *__restrict__ pv, const double2 *__restrict__ Yrow,
+                                                  int lane) {
+    e.base = __builtin_amdgcn_readfirstlane((int)x.lo);
+    e.width = __builtin_amdgcn_readfirstlane(x.wd.x);
+    e.wide = __builtin_amdgcn_readfirstlane(x.wd.y);
+    const int len = (int)(x.rl & ((1u << AT_LENBITS) - 1)), lrow = (int)(x.rl >> AT_LENBITS);
+    const __amdgpu_buffer_rsrc_t rk = at_rsrc(pk + e.base), rv = at_rsrc(pv + e.base);
+    int r = 0;   // wave-uniform: the step's first entry, relative to base
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const bool act = len > u;
+        const uint32_t o = (uint32_t)(r + lane);
+        e.cu[u] = __builtin_amdgcn_raw_buffer_load_b16(rk, act ? 2u * o : AT_OOB, 0, 0);
+        typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+        const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rv, act ? 8u * o : AT_OOB, 0, 0);
+        e.vu[u] = __longlong_as_double((long long)(((uint64_t)v.y << 32) | v.x));
+        r += __popcll(__ballot(act));
+    }
+    e.rU = r;
+    e.yi = Yrow[lrow];   // lrow = 0 for a lane without a row: a valid point
+}
+template <bool LOSS, int MET>
+__device__ __forceinline__ void atp_term(const double2 *win, double2 yi, uint32_t c, double v, double ex, double Z,
+                                         double &fx, double &fy, double &lsum) {
+    const double2 yj = win[c];
+    const double dx = __dsub_rn(yi.x, yj.x), dy = __dsub_rn(yi.y, yj.y);
+    double x1m;
+    const double q = qforce_t<MET>(yi.x, yi.y, yj.x, yj.y, dx, dy, x1m);
+    const double sc = __dmul_rn(v, q);
+    fx = __fma_rn(sc, dx, fx);
+    fy = __fma_rn(sc, dy, fy);
+    if (LOSS) {
+        const double pij = __dmul_rn(v, ex);
+        lsum += pij * log_kl(pij * Z * x1m);
+    }
+}
+// a slice's sums into its rows' accumulators (steps past U loaded in place)
+template <int U, bool LOSS, int MET>
+__device__ __forceinline__ void atp_sum(const ATRSlot &x, const ATESlot<U> &e, const double2 *win, double2 *acc,
+                                        const uint16_t *__restrict__ pk, const double *__restrict__ pv, double ex,
+                                        double Z, int lane, double &lsum) {
+    const int len = (int)(x.rl & ((1u << AT_LENBITS) - 1)), lrow = (int)(x.rl >> AT_LENBITS);
+    double fx = 0.0, fy = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (u < len) atp_term<LOSS, MET>(win, e.yi, e.cu[u], e.vu[u], ex, Z, fx, fy, lsum);
+    if (e.width > U) {
+        int64_t off = (int64_t)e.base + e.rU;
+        for (int k0 = U; k0 < e.width; k0 += AT_RU) {
+            uint32_t cu[AT_RU];
+            double vu[AT_RU];
+#pragma unroll
+            for (int u = 0; u < AT_RU; ++u) {
+                const int k = k0 + u;
+                cu[u] = 0;
+                vu[u] = 0.0;
+                if (k < len) { cu[u] = pk[off + lane]; vu[u] = pv[off + lane]; }
+                off += __popcll(__ballot(len > k));
+            }
+#pragma unroll
+            for (int u = 0; u < AT_RU; ++u)
+                if (k0 + u < len) atp_term<LOSS, MET>(win, e.yi, cu[u], vu[u], ex, Z, fx, fy, lsum);
+        }
+        // vmcnt(0): the remainder's loads are consumed in exec-masked branches,
+        // so past this block the compiler would count them as outstanding and
+        // make every later step wait for nearly everything in flight
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    if (e.wide) {   // one row over the 64 lanes: a fixed-order tree
+        fx = wave_sum(fx);
+        fy = wave_sum(fy);
+        if (lane == 0) {
+            const double2 o = acc[lrow];
+            acc[lrow] = make_double2(__dadd_rn(o.x, fx), __dadd_rn(o.y, fy));
+        }
+    } else if (len > 0) {
+        const double2 o = acc[lrow];
+        acc[lrow] = make_double2(__dadd_rn(o.x, fx), __dadd_rn(o.y, fy));
+    }
+}
+// tile t's window into LDS, then the barrier (every wave has left the previous one)
+template <int W, int NT>
+__device__ __forceinline__ void atp_tile_begin(double2 *win, const ATile *__restrict__ tiles, const double2 *Y2,
+                                               int64_t n, int t, int tid) {
+    const int64_t nb = (int64_t)__builtin_amdgcn_readfirstlane(tiles[t].cb) * W;
+    double2 yv[(W + NT - 1) / NT];
+    at_window_regs<W, NT>(yv, Y2 + nb, (int)min((int64_t)W, n - nb), tid);
+    at_window_store<W, NT>(win, yv, tid);
+    __syncthreads();
+}
+
+template <class CF, int D, int U, bool LOSS, int MET>
+__global__ __launch_bounds__(CF::NT) void attract_tiles_pipe(
+    const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
+    const uint32_t *__restrict__ srow, int64_t rows, int64_t r0, int64_t n, const uint16_t *__restrict__ pk,
+    const double *__restrict__ pv, const double *__restrict__ Y, const double *__restrict__ scal, double ex,
+    int64_t xcd_chunk, double2 *__restrict__ attr, double *__restrict__ lpart, int64_t rbs) {
+    constexpr int RB = CF::RB, W = CF::W, NT = CF::NT, WAVES = CF::WAVES;
+    constexpr int NE = D + 1, NR = 2 * (D + 1);   // the step loop is unrolled over NR
+    static_assert(D >= 1 && D <= 3 && U >= 1, "pipeline shape");
+    __shared__ double2 win[W];
+    __shared__ double2 acc[RB];
+    __shared__ double sl[WAVES];
+    const int tid = threadIdx.x, lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform for the compiler
+    const int64_t rb = xcd_chunk > 0 ? xcd_block_chunked(blockIdx.x, gridDim.x, xcd_chunk) : (int64_t)blockIdx.x;
+    const int64_t b0 = rb * rbs;
+    const int nr = (int)min(rbs, rows - b0);
+    const double2 *Y2 = reinterpret_cast<const double2 *>(Y);
+    const double2 *Yrow = Y2 + r0 + b0;
+    for (int i = tid; i < nr; i += NT) acc[i] = make_double2(0.0, 0.0);
+    const double Z = LOSS ? scal[0] : 1.0;
+    double lsum = 0.0;
+    const int t0 = __builtin_amdgcn_readfirstlane(rbt[rb]), t1 = __builtin_amdgcn_readfirstlane(rbt[rb + 1]);
+    if (t0 < t1) {
+        const int sdummy = __builtin_amdgcn_readfirstlane(tiles[t0].s0);   // a valid slice for "no slice"
+        ATRSlot R[NR];
+        ATESlot<U> E[NE];
+        // prologue: slices 0 .. 2D: records; 0 .. D-1: entries, issued in the
+        // steps' own order (entries of j, then the record of j + D + 1), so
+        // that the compiler's outstanding-load counts agree at the loop head
+        R[0].c = atp_first(tiles, t0, t1, w);
+#pragma unroll
+        for (int j = 1; j <= 2 * D; ++j) R[j].c = atp_next<WAVES>(tiles, R[j - 1].c, t1, w);
+#pragma unroll
+        for (int j = 0; j <= D; ++j) atp_issue_rec(R[j], slices, srow, t1, sdummy, lane);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            atp_issue_entries<U>(R[j], E[j], pk, pv, Yrow, lane);
+            atp_issue_rec(R[j + D + 1], slices, srow, t1, sdummy, lane);
+        }
+        int tcur = t0;
+        atp_tile_begin<W, NT>(win, tiles, Y2, n, t0, tid);
+        // Rounds of NR steps; every step issues its loads whether or not its
+        // slice exists (past the wave's last slice: dummies), only the sum is
+        // conditional -- a step skipped as a whole would make the compiler
+        // count fewer loads after each outstanding one and wait for nearly all
+        do {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {   // the step of slice i, r = i mod NR
+                const bool live = R[r].c.t < t1;
+                while (live && tcur != R[r].c.t) {   // the wave's next slice is in a later tile
+                    __syncthreads();
+                    tcur = __builtin_amdgcn_readfirstlane(tcur + 1);
+                    atp_tile_begin<W, NT>(win, tiles, Y2, n, tcur, tid);
+                }
+                atp_issue_entries<U>(R[(r + D) % NR], E[(r + D) % NE], pk, pv, Yrow, lane);   // slice i + D
+                if (live) atp_sum<U, LOSS, MET>(R[r], E[r % NE], win, acc, pk, pv, ex, Z, lane, lsum);
+                // slice i - 1's record slot is free: slice i + 2D + 1
+                R[(r + NR - 1) % NR].c = atp_next<WAVES>(tiles, R[(r + 2 * D) % NR].c, t1, w);
+                atp_issue_rec(R[(r + NR - 1) % NR], slices, srow, t1, sdummy, lane);
+            }
+        } while (R[0].c.t < t1);
+        while (tcur + 1 < t1) {   // the barriers of the tiles this wave has no slice in
+            __syncthreads();
+            tcur = __builtin_amdgcn_readfirstlane(tcur + 1);
+            atp_tile_begin<W, NT>(win, tiles, Y2, n, tcur, tid);
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < nr; i += NT) attr[b0 + i] = make_double2(acc[i].x * ex, acc[i].y * ex);
+    if (LOSS) {
+        lsum = wave_sum(lsum);
+        if (lane == 0) sl[tid >> 6] = lsum;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int k = 0; k < WAVES; ++k) s += sl[k];
+            lpart[blockIdx.x] = s;
+        }
+    }
+}
+
 // ---- tile layout build (at every relabel; see build_attract_tiles)
-// 1. key (row block * ncb + window) << rowbits | local row of every owned
-//    entry (wave per row), for a stable radix sort
 // 1. key (row block * ncb + window) << rowbits | local row of every owned
 //    entry (wave per row), for a stable radix sort
 __global__ void at_keys(const int64_t *__restrict__ rpw, const int32_t *__restrict__ colw, int64_t rows, int64_t ncb,
@@ -1790,6 +2070,8 @@ static void build_attract_tiles(tsne_ctx *ctx, OptState *s) {
     s->at_ncb = ncb;
     s->at_rbs = rbs;
     s->at_cfg = cfg;
+    s->at_pipe = ctx->opts.attract_pipe;
+    s->at_dyn = ctx->opts.attract_dyn;
     s->at_on = true;
 }
 
@@ -2253,9 +2535,23 @@ static void maybe_relabel(tsne_ctx *ctx, OptState *s) {
 template <class CF, bool LOSS, int MET>
 static void attract_tiles_launch_c(hipStream_t st, const OptState *s, const AttractArgs &a) {
     const int64_t nb = s->at_nrb;
-    hipLaunchKernelGGL((attract_tiles<CF, LOSS, MET>), dim3(nb), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt,
-                       s->at_slices, s->at_srow, a.r1 - a.r0, a.r0, s->n, s->at_pk, s->at_pv, a.Y, a.scal, a.ex,
-                       nb / NUM_XCD, a.attr, a.lpart, s->at_rbs);
+#define TSNE_ATP(K)                                                                                            \
+    hipLaunchKernelGGL(K, dim3(nb), dim3(CF::NT), 0, st, s->at_tiles, s->at_rbt, s->at_slices, s->at_srow,    \
+                       a.r1 - a.r0, a.r0, s->n, s->at_pk, s->at_pv, a.Y, a.scal, a.ex, nb / NUM_XCD, a.attr, \
+                       a.lpart, s->at_rbs)
+    if constexpr (CF::RB == 4096 && !LOSS) {
+        switch (s->at_pipe) {
+            case 1: TSNE_ATP((attract_tiles_pipe<CF, 1, 6, LOSS, MET>)); return;
+            case 2: TSNE_ATP((attract_tiles_pipe<CF, 1, 8, LOSS, MET>)); return;
+            case 3: TSNE_ATP((attract_tiles_pipe<CF, 2, 4, LOSS, MET>)); return;
+            case 4: TSNE_ATP((attract_tiles_pipe<CF, 2, 6, LOSS, MET>)); return;
+            case 5: TSNE_ATP((attract_tiles_pipe<CF, 3, 4, LOSS, MET>)); return;
+            default: break;
+        }
+    }
+    if (s->at_dyn) TSNE_ATP((attract_tiles<CF, LOSS, MET, true>));
+    else TSNE_ATP((attract_tiles<CF, LOSS, MET, false>));
+#undef TSNE_ATP
 }
 template <bool LOSS, int MET>
 static void attract_tiles_launch_m(hipStream_t st, const OptState *s, const AttractArgs &a) {
