@@ -47,8 +47,8 @@ METRIC = "t-SNE iterations/sec + end-to-end sec at N=1M×128 on 1/2/4/8 MI355X; 
 FP32_MFMA_PEAK_TF = 157.3
 BF16_MFMA_PEAK_TF = 2500.0   # dense (MI355X_MICROARCH.md); the kNN filter's bf16x3 passes run 3 bf16 MFMAs per product
 HBM_PEAK_GBS = 8000.0
-PMC_ATTRACT = "r06_s_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
-PMC_BH = "r06_s_bh_valu.json"
+PMC_ATTRACT = "r06_ar_attract_traffic.json"   # committed PMC summaries the line quotes (see main)
+PMC_BH = "r06_ar_bh_valu.json"
 UPDATE_KERNELS = ("combine_update", "center2")   # update + centre kernels in the PMC summary
 
 
