@@ -144,7 +144,8 @@ int tsne_ctx_synchronize(tsne_ctx *ctx);
  *                             pipelined kernel (entries of the next 1 or 2
  *                             slices in flight; identical results);
  *   "attract_dyn" 1           attract_tiles: the waves claim a tile's slices
- *                             instead of taking every 16th (identical results);
+ *                             instead of taking every 16th (non-loss launches;
+ *                             identical results);
  *   "graph_order" 1           P's graph order as the initial labels;
  *   "relabel" -1              Morton relabels: -1 automatic, 0 never, 1 by
  *                             locality score, 2 always;

@@ -506,8 +506,8 @@ def test_tiled_attraction_every_config():
 def test_tiled_attraction_pipe_identical():
     """The pipelined tiled attraction ("attract_pipe" 1..5: the next 1..3
     slices' entries in flight while a wave sums the current one; non-loss
-    launches) and attract_tiles with claimed slices ("attract_dyn" 1, loss
-    launches too) return the same bits as attract_tiles over 10 iterations of a P
+    launches) and attract_tiles with claimed slices ("attract_dyn" 1, non-loss
+    launches) return the same bits as attract_tiles over 10 iterations of a P
     with hub rows (wide slices, rows past the pipelined steps), at the
     4096-row configuration the pipeline is built for; and the oracle's
     embedding within 1e-9."""

@@ -453,7 +453,9 @@ __device__ __forceinline__ int at_claim(int *c) {
 // the other waves wait for it at the tile's barrier (PMC: waves wait 58 % of
 // their lifetime, 22 % on their own loads).  Every row has one slice per tile
 // and the tiles keep their order, so each accumulator receives the same terms
-// in the same order: the sums are bit-identical either way.
+// in the same order: the sums are bit-identical either way.  (Not for the
+// loss: a wave's partial would sum whichever slices it claimed, so loss
+// launches keep the round-robin deal.)
 template <class CF, bool LOSS, int MET, bool DYN = false>
 __global__ __launch_bounds__(CF::NT) void attract_tiles(
     const ATile *__restrict__ tiles, const int32_t *__restrict__ rbt, const ASlice *__restrict__ slices,
@@ -2549,7 +2551,9 @@ static void attract_tiles_launch_c(hipStream_t st, const OptState *s, const Attr
             default: break;
         }
     }
-    if (s->at_dyn) TSNE_ATP((attract_tiles<CF, LOSS, MET, true>));
+    // loss launches deal the slices round-robin: a wave's loss partial sums the
+    // slices it ran, so claimed slices would make the loss's rounding vary
+    if (s->at_dyn && !LOSS) TSNE_ATP((attract_tiles<CF, LOSS, MET, true>));
     else TSNE_ATP((attract_tiles<CF, LOSS, MET, false>));
 #undef TSNE_ATP
 }
