@@ -413,7 +413,7 @@ using ATCfg3 = ATCfg<4096, 5888, 1024>;   // 156 KB
 using ATCfg3D = ATCfg<2048, 4096, 1024>;   // 96 KB window + 48 KB accumulators
 using ATCfg3Ds = ATCfg<512, 4096, 1024>;   // 96 + 12 KB: a rank's share of the rows
 #ifndef AT_DIAG
-#define AT_DIAG 0   // 1 / 2: diagnostic builds of attract_tiles (timing only)
+#define AT_DIAG 0   // 1 / 2 / 3: diagnostic builds of attract_tiles (timing only; see DESIGN.md 6, rounds 5 and 6)
 #endif
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
@@ -481,6 +481,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
     const int t0 = rbt[rb], t1 = rbt[rb + 1];
     for (int t = t0; t < t1; ++t) {
         const ATile tl = tiles[t];
+#if AT_DIAG != 3
         {   // the tile's window: all of a thread's loads in flight before its LDS stores
             // (round 6: unconditional stores; with `if (i < wn)` the compiler sank each
             // load into its store's branch and the copy took WL dependent round trips)
@@ -489,6 +490,7 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
             at_window_regs<W, NT>(yv, Y2 + base, (int)min((int64_t)W, n - base), tid);
             at_window_store<W, NT>(win, yv, tid);
         }
+#endif
         __syncthreads();
         const int s0 = tl.s0, send = tl.s0 + tl.ns;
         // the wave's slices s0 + w, s0 + w + WAVES, ... (DYN: claimed); the next
@@ -504,7 +506,9 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
         while (s < send) {
             const int len = (int)(rl & ((1u << AT_LENBITS) - 1)), lrow = (int)(rl >> AT_LENBITS);
             double2 yi = make_double2(0.0, 0.0);
+#if AT_DIAG != 3
             if (len > 0) yi = Yrow[lrow];
+#endif
             const int sn = DYN ? s0 + at_claim(&claim[t & 1]) : s + WAVES;
             ASlice sdn{};
             uint32_t rln = 0;
@@ -531,7 +535,8 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
                 }
 #pragma unroll
                 for (int u = 0; u < AT_U; ++u) {
-#if AT_DIAG == 1   // diagnostic build: loads only, no window reads or pair terms
+#if AT_DIAG == 1 || AT_DIAG == 3   // diagnostic builds: loads only, no window reads or pair terms
+                                    // (3: no window copy or Y_i either -- the entry stream's own rate)
                     if (k0 + u < len) { fx += vu[u]; fy += (double)cu[u]; }
                     continue;
 #endif
