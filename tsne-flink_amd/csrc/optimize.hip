@@ -416,6 +416,9 @@ using ATCfg3Ds = ATCfg<512, 4096, 1024>;   // 96 + 12 KB: a rank's share of the 
 #define AT_DIAG 0   // 1 / 2 / 3: diagnostic builds of attract_tiles (timing only; see DESIGN.md 6, rounds 5 and 6)
 #endif
 constexpr int AT_U = 12;          // jagged steps whose loads are issued together
+#ifndef AT_NT
+#define AT_NT 1   // attract_tiles' entry loads nontemporal (round 6)
+#endif
 constexpr int AT_LENBITS = 20;    // slice lane word: local row << 20 | entries in the tile
 
 constexpr uint32_t AT_OOB = 0x80000000u;   // >= the descriptors' range: reads 0
@@ -524,6 +527,11 @@ __global__ __launch_bounds__(CF::NT) void attract_tiles(
                     vu[u] = 0.0;
 #if AT_DIAG == 2   // diagnostic build: no entry loads
                     if (k < len) { cu[u] = (uint32_t)((lane * 97 + k * 31) % W); vu[u] = 1e-9; }
+#elif AT_NT   // entries read once per launch (1.6 GB at C3, past the Infinity Cache): nontemporal
+                    if (k < len) {
+                        cu[u] = __builtin_nontemporal_load(pk + off + lane);
+                        vu[u] = __builtin_nontemporal_load(pv + off + lane);
+                    }
 #else
                     if (k < len) { cu[u] = pk[off + lane]; vu[u] = pv[off + lane]; }
 #endif
