@@ -415,7 +415,10 @@ using ATCfg3Ds = ATCfg<512, 4096, 1024>;   // 96 + 12 KB: a rank's share of the 
 #ifndef AT_DIAG
 #define AT_DIAG 0   // 1 / 2 / 3: diagnostic builds of attract_tiles (timing only; see DESIGN.md 6, rounds 5 and 6)
 #endif
-constexpr int AT_U = 12;          // jagged steps whose loads are issued together
+#ifndef AT_UNROLL
+#define AT_UNROLL 12
+#endif
+constexpr int AT_U = AT_UNROLL;   // jagged steps whose loads are issued together
 #ifndef AT_NT
 #define AT_NT 1   // attract_tiles' entry loads nontemporal (round 6)
 #endif
